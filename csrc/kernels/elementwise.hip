@@ -1,0 +1,344 @@
+// Elementwise / layout / reduction / embedding / loss kernels for gfx950
+// (SURVEY §2.4.b K1, K2, K7, K8, K17, K18). Every kernel is 16-B vectorized and
+// grid-stride (Guideline 13: scalar bf16 loads cost 2-2.5x on CDNA).
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float gelu_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+// Counter-based hash RNG (deterministic; backward regenerates the mask).
+__device__ __forceinline__ float uhash(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.f / 16777216.f);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  long n8 = n / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float4 a = reinterpret_cast<const float4*>(x)[2 * i], b = reinterpret_cast<const float4*>(x)[2 * i + 1];
+    float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    store8(y + i * 8, f);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) y[n8 * 8 + threadIdx.x] = f2bf(x[n8 * 8 + threadIdx.x]);
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long n) {
+  long n8 = n / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(x + i * 8, f);
+    reinterpret_cast<float4*>(y)[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
+    reinterpret_cast<float4*>(y)[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) y[n8 * 8 + threadIdx.x] = bf2f(x[n8 * 8 + threadIdx.x]);
+}
+
+// NCHW f32 image batch -> NHWC bf16 with channels zero-padded to Cp (input pipeline on device)
+__global__ void nchw_to_nhwc_pad_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int HW,
+                                        int Cp) {
+  long total = (long)N * HW;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long n = i / HW, s = i % HW;
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        int c = c0 + j;
+        f[j] = c < C ? x[(n * C + c) * HW + s] : 0.f;
+      }
+      store8(y + i * Cp + c0, f);
+    }
+  }
+}
+
+// Filter KRSC (f32 master or bf16) -> bf16 CRSK (the dgrad operand layout).
+__global__ void filter_krsc_to_crsk_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ o, int K, int RS,
+                                           int C) {
+  long total = (long)K * RS * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    // i indexes the OUTPUT [c][rs][k] so writes are contiguous
+    int k = (int)(i % K);
+    long t = i / K;
+    int rs = (int)(t % RS);
+    int c = (int)(t / RS);
+    o[i] = w[((long)k * RS + rs) * C + c];
+  }
+}
+
+__global__ void add_bf16_kernel(const bf16_t* a, const bf16_t* b, bf16_t* y, long n8, float alpha, float beta) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float fa[8], fb[8];
+    load8(a + i * 8, fa);
+    load8(b + i * 8, fb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fa[j] = alpha * fa[j] + beta * fb[j];
+    store8(y + i * 8, fa);
+  }
+}
+
+// act: 1 relu, 2 gelu. fwd: y = act(x); bwd: dx = dy * act'(x)
+__global__ void act_kernel(const bf16_t* x, const bf16_t* dy, bf16_t* y, long n8, int act, int bwd) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8], g[8];
+    load8(x + i * 8, f);
+    if (bwd) load8(dy + i * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!bwd) f[j] = act == 1 ? fmaxf(f[j], 0.f) : gelu_f(f[j]);
+      else f[j] = g[j] * (act == 1 ? (f[j] > 0.f ? 1.f : 0.f) : gelu_grad(f[j]));
+    }
+    store8(y + i * 8, f);
+  }
+}
+
+// dropout: y = x * mask / keep ; mask regenerated from (seed, index)
+__global__ void dropout_kernel(const bf16_t* x, bf16_t* y, long n8, float keep, uint64_t seed) {
+  const float inv = 1.f / keep;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(x + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = uhash(seed, i * 8 + j) < keep ? f[j] * inv : 0.f;
+    store8(y + i * 8, f);
+  }
+}
+
+// Column sum of a bf16 [M][N] matrix into f32 [N] (BiasAddGrad); N % 8 == 0
+__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, long M, int N,
+                                                     float* __restrict__ out) {
+  const int cols8 = N / 8;
+  const int TPR = cols8 < 256 ? cols8 : 256, RPB = 256 / TPR;
+  const int t = threadIdx.x;
+  if (t >= TPR * RPB) return;
+  for (int cc = t % TPR; cc < cols8; cc += TPR) {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (long r = (long)blockIdx.x * RPB + t / TPR; r < M; r += (long)gridDim.x * RPB) {
+      float f[8];
+      load8(x + r * N + cc * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(out + cc * 8 + j, s[j]);
+  }
+}
+
+// Embedding lookup: out[t] = table[idx[t]] (+ table2[idx2[t]]) (+ table3[idx3[t]]), bf16 rows, D % 8 == 0
+__global__ void embed_fwd_kernel(const bf16_t* __restrict__ t1, const long* __restrict__ i1,
+                                 const bf16_t* __restrict__ t2, const long* __restrict__ i2,
+                                 const bf16_t* __restrict__ t3, const long* __restrict__ i3, bf16_t* __restrict__ out,
+                                 long T, int D, int pos_mod) {
+  const int d8 = D / 8;
+  long total = T * d8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i / d8;
+    int c = (int)(i % d8) * 8;
+    float f[8];
+    load8(t1 + i1[t] * D + c, f);
+    if (t2) {
+      float g[8];
+      long r = i2 ? i2[t] : (t % pos_mod);
+      load8(t2 + r * D + c, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += g[j];
+    }
+    if (t3) {
+      float g[8];
+      long r = i3 ? i3[t] : 0;
+      load8(t3 + r * D + c, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += g[j];
+    }
+    store8(out + t * D + c, f);
+  }
+}
+
+// Embedding gradient: dtable[idx[t]] += dy[t] (f32 atomics; each wave-instruction covers contiguous row bytes)
+__global__ void embed_bwd_kernel(const bf16_t* __restrict__ dy, const long* __restrict__ idx, float* __restrict__ dt,
+                                 long T, int D, int pos_mod) {
+  long total = T * (long)D;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i / D;
+    int c = (int)(i % D);
+    long r = idx ? idx[t] : (t % pos_mod);
+    atomicAdd(dt + r * D + c, bf2f(dy[i]));
+  }
+}
+
+// Fused softmax cross-entropy over rows (logits f32 or bf16), int64 labels.
+// loss[r] = logsumexp(x) - x[label]; dlogits = (softmax - onehot) * gscale (written in the fwd pass).
+// label < 0 => ignored row (loss 0, grad 0). label_smoothing eps spreads eps/V over all classes.
+__global__ void __launch_bounds__(256) softmax_ce_kernel(const void* __restrict__ logits, int in_f32,
+                                                         const long* __restrict__ labels, float* __restrict__ loss,
+                                                         void* __restrict__ dlogits, int grad_f32, int V,
+                                                         float gscale, float smooth) {
+  __shared__ float red[16];
+  const long r = blockIdx.x;
+  const float* xf = in_f32 ? reinterpret_cast<const float*>(logits) + r * V : nullptr;
+  const bf16_t* xb = in_f32 ? nullptr : reinterpret_cast<const bf16_t*>(logits) + r * V;
+  auto ld = [&](int i) { return xf ? xf[i] : bf2f(xb[i]); };
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) m = fmaxf(m, ld(i));
+  m = block_max(m, red);
+  float s = 0.f, sx = 0.f;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    float v = ld(i);
+    s += __expf(v - m);
+    sx += v;
+  }
+  s = block_sum(s, red);
+  sx = block_sum(sx, red);
+  const long lab = labels[r];
+  const float lse = m + __logf(s);
+  if (threadIdx.x == 0) {
+    float l = 0.f;
+    if (lab >= 0) {
+      float xl = ld((int)lab);
+      l = (1.f - smooth) * (lse - xl) + smooth * (lse - sx / V);
+    }
+    loss[r] = l;
+  }
+  if (!dlogits) return;
+  const float inv = 1.f / s;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    float p = __expf(ld(i) - m) * inv;
+    float tgt = (i == lab ? 1.f - smooth : 0.f) + smooth / V;
+    float gval = lab >= 0 ? (p - tgt) * gscale : 0.f;
+    if (grad_f32) reinterpret_cast<float*>(dlogits)[r * V + i] = gval;
+    else reinterpret_cast<bf16_t*>(dlogits)[r * V + i] = f2bf(gval);
+  }
+}
+
+// Row softmax over bf16 scores with scale and optional causal mask (attention probabilities).
+// rows are [batch][Sq] with row length Sk; causal: col > (row % Sq) + (Sk - Sq) masked.
+__global__ void __launch_bounds__(256) softmax_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                          int Sq, int Sk, float scale, int causal,
+                                                          const float* __restrict__ add_mask) {
+  __shared__ float red[16];
+  const long r = blockIdx.x;
+  const int qi = (int)(r % Sq);
+  const long bidx = r / Sq;
+  const bf16_t* xr = x + r * Sk;
+  const int lim = causal ? qi + (Sk - Sq) : Sk - 1;
+  const float* am = add_mask ? add_mask + bidx * Sk : nullptr;  // [batch][Sk] additive mask
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < Sk; i += blockDim.x) {
+    float v = i <= lim ? bf2f(xr[i]) * scale + (am ? am[i] : 0.f) : -INFINITY;
+    m = fmaxf(m, v);
+  }
+  m = block_max(m, red);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < Sk; i += blockDim.x) {
+    float v = i <= lim ? bf2f(xr[i]) * scale + (am ? am[i] : 0.f) : -INFINITY;
+    s += v == -INFINITY ? 0.f : __expf(v - m);
+  }
+  s = block_sum(s, red);
+  const float inv = s > 0.f ? 1.f / s : 0.f;
+  for (int i = threadIdx.x; i < Sk; i += blockDim.x) {
+    float v = i <= lim ? bf2f(xr[i]) * scale + (am ? am[i] : 0.f) : -INFINITY;
+    y[r * Sk + i] = f2bf(v == -INFINITY ? 0.f : __expf(v - m) * inv);
+  }
+}
+
+// dx = scale * y * (dy - sum(dy*y))
+__global__ void __launch_bounds__(256) softmax_bwd_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dy,
+                                                          bf16_t* __restrict__ dx, int Sk, float scale) {
+  __shared__ float red[16];
+  const long r = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < Sk; i += blockDim.x) s += bf2f(y[r * Sk + i]) * bf2f(dy[r * Sk + i]);
+  s = block_sum(s, red);
+  for (int i = threadIdx.x; i < Sk; i += blockDim.x) {
+    float yv = bf2f(y[r * Sk + i]);
+    dx[r * Sk + i] = f2bf(scale * yv * (bf2f(dy[r * Sk + i]) - s));
+  }
+}
+
+}  // namespace
+
+#define GRID(n) dim3(stream_grid((n), 256)), dim3(256), 0, (hipStream_t)stream
+
+DTF_API int dtf_cast_f32_bf16(const float* x, void* y, long n, void* stream) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, GRID(n / 8 + 1), x, (bf16_t*)y, n);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_cast_bf16_f32(const void* x, float* y, long n, void* stream) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, GRID(n / 8 + 1), (const bf16_t*)x, y, n);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_nchw_to_nhwc_pad(const float* x, void* y, int N, int C, int HW, int Cp, void* stream) {
+  if (Cp & 7) return -1;
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel, GRID((long)N * HW), x, (bf16_t*)y, N, C, HW, Cp);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_filter_to_crsk(const void* w, void* o, int K, int RS, int C, void* stream) {
+  hipLaunchKernelGGL(filter_krsc_to_crsk_kernel, GRID((long)K * RS * C), (const bf16_t*)w, (bf16_t*)o, K, RS, C);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_add_bf16(const void* a, const void* b, void* y, long n, float alpha, float beta, void* stream) {
+  if (n & 7) return -1;
+  hipLaunchKernelGGL(add_bf16_kernel, GRID(n / 8), (const bf16_t*)a, (const bf16_t*)b, (bf16_t*)y, n / 8, alpha,
+                     beta);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_act(const void* x, const void* dy, void* y, long n, int act, int bwd, void* stream) {
+  if (n & 7) return -1;
+  hipLaunchKernelGGL(act_kernel, GRID(n / 8), (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)y, n / 8, act, bwd);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_dropout(const void* x, void* y, long n, float keep, unsigned long long seed, void* stream) {
+  if (n & 7) return -1;
+  hipLaunchKernelGGL(dropout_kernel, GRID(n / 8), (const bf16_t*)x, (bf16_t*)y, n / 8, keep, (uint64_t)seed);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_colsum(const void* x, long M, int N, float* out, int accumulate, void* stream) {
+  if (N & 7) return -1;
+  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, (hipStream_t)stream);
+  int cols8 = N / 8, TPR = cols8 < 256 ? cols8 : 256, RPB = 256 / TPR;
+  long blocks = (M + RPB * 32L - 1) / (RPB * 32L);
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(colsum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, M, N, out);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_embed_fwd(const void* t1, const long* i1, const void* t2, const long* i2, const void* t3,
+                          const long* i3, void* out, long T, int D, int pos_mod, void* stream) {
+  if (D & 7) return -1;
+  hipLaunchKernelGGL(embed_fwd_kernel, GRID(T * (D / 8)), (const bf16_t*)t1, i1, (const bf16_t*)t2, i2,
+                     (const bf16_t*)t3, i3, (bf16_t*)out, T, D, pos_mod < 1 ? 1 : pos_mod);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_embed_bwd(const void* dy, const long* idx, float* dt, long T, int D, int pos_mod, void* stream) {
+  hipLaunchKernelGGL(embed_bwd_kernel, GRID(T * D), (const bf16_t*)dy, idx, dt, T, D, pos_mod < 1 ? 1 : pos_mod);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_softmax_ce(const void* logits, int in_f32, const long* labels, float* loss, void* dlogits,
+                           int grad_f32, long rows, int V, float gscale, float smooth, void* stream) {
+  hipLaunchKernelGGL(softmax_ce_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, logits, in_f32, labels, loss,
+                     dlogits, grad_f32, V, gscale, smooth);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_softmax_fwd(const void* x, void* y, long rows, int Sq, int Sk, float scale, int causal,
+                            const float* add_mask, void* stream) {
+  hipLaunchKernelGGL(softmax_fwd_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     (bf16_t*)y, Sq, Sk, scale, causal, add_mask);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_softmax_bwd(const void* y, const void* dy, void* dx, long rows, int Sk, float scale, void* stream) {
+  hipLaunchKernelGGL(softmax_bwd_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)y,
+                     (const bf16_t*)dy, (bf16_t*)dx, Sk, scale);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,373 @@
+// FusedBatchNorm (NHWC, training + inference) and LayerNorm for gfx950.
+//
+// TF's FusedBatchNormV3 / FusedBatchNormGradV3 and LayerNorm equivalents
+// (SURVEY §2.4.b K5/K6). Layout is channels-last [M = N*H*W][C], bf16 I/O,
+// f32 statistics. The forward statistics are normally produced for free by the
+// conv epilogue (gemm.hip `stats`), so the standalone path here is:
+//   bn_stats (only when no conv produced them) -> bn_finalize (per channel,
+//   also updates running stats TF-style) -> bn_apply (scale/shift [+res] [+relu]).
+// Backward: bn_bwd_reduce (sum dz, sum dz*xhat with the ReLU mask applied
+//   on the fly) -> bn_bwd_finalize -> bn_bwd_apply (dx, optional dz for the
+//   residual branch). All passes are 16-B vectorized, grid-stride, one atomic
+//   per (block, channel).
+#include "common.h"
+
+namespace {
+
+// Column-reduction geometry: TPR threads per row (8 channels each), RPB rows per pass.
+struct ColGeo {
+  int cols8, TPR, RPB;
+};
+__host__ __device__ inline ColGeo colgeo(int C) {
+  ColGeo g;
+  g.cols8 = C / 8;
+  g.TPR = g.cols8 < 256 ? g.cols8 : 256;
+  g.RPB = 256 / g.TPR;
+  return g;
+}
+
+__global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
+                                                       float* __restrict__ stats) {
+  ColGeo g = colgeo(C);
+  const int t = threadIdx.x;
+  if (t >= g.TPR * g.RPB) return;
+  const int rsub = t / g.TPR;
+  for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
+    float s[8] = {0}, q[8] = {0};
+    for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
+      float f[8];
+      load8(x + r * C + cc * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(stats + cc * 8 + j, s[j]);
+      atomicAdd(stats + C + cc * 8 + j, q[j]);
+    }
+  }
+}
+
+// Per-channel: mean/var from sums; scale = gamma*invstd, shift = beta - mean*scale.
+// Running stats follow Keras BatchNormalization: r = r*momentum + batch*(1-momentum),
+// with the unbiased variance, as TF's FusedBatchNormV3 does.
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* running_mean, float* running_var,
+                                   long M, int C, float momentum, float eps, float* __restrict__ scale,
+                                   float* __restrict__ shift, float* __restrict__ mean_out,
+                                   float* __restrict__ invstd_out) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float mean = stats[c] / (float)M;
+  float var = fmaxf(stats[C + c] / (float)M - mean * mean, 0.f);
+  float inv = rsqrtf(var + eps);
+  float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale[c] = gm * inv;
+  shift[c] = bt - mean * gm * inv;
+  if (mean_out) mean_out[c] = mean;
+  if (invstd_out) invstd_out[c] = inv;
+  if (running_mean) {
+    float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    running_mean[c] = running_mean[c] * momentum + mean * (1.f - momentum);
+    running_var[c] = running_var[c] * momentum + unb * (1.f - momentum);
+  }
+}
+
+// Inference: scale/shift from running statistics.
+__global__ void bn_infer_coeff_kernel(const float* gamma, const float* beta, const float* rmean,
+                                      const float* rvar, int C, float eps, float* scale, float* shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float inv = rsqrtf(rvar[c] + eps);
+  float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale[c] = gm * inv;
+  shift[c] = bt - rmean[c] * gm * inv;
+}
+
+__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+                                                       long n8, int C, int relu) {
+  const int c8 = C / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c8) * 8;
+    float f[8], r[8];
+    load8(x + i * 8, f);
+    if (res) load8(res + i * 8, r);
+    float4 s0 = *reinterpret_cast<const float4*>(scale + c), s1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j] * sc[j] + sh[j];
+      if (res) v += r[j];
+      if (relu) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    store8(y + i * 8, f);
+  }
+}
+
+// Backward reduce: dz = dy * (y > 0 if relu-mask given); sums: [0,C) sum dz, [C,2C) sum dz*xhat
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
+                                                            const bf16_t* __restrict__ ymask,
+                                                            const bf16_t* __restrict__ x,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, long M, int C,
+                                                            float* __restrict__ sums) {
+  ColGeo g = colgeo(C);
+  const int t = threadIdx.x;
+  if (t >= g.TPR * g.RPB) return;
+  const int rsub = t / g.TPR;
+  for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
+    float mu[8], is[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[cc * 8 + j]; is[j] = invstd[cc * 8 + j]; }
+    float s[8] = {0}, q[8] = {0};
+    for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
+      float d[8], xv[8];
+      load8(dy + r * C + cc * 8, d);
+      load8(x + r * C + cc * 8, xv);
+      if (ymask) {
+        uint4 mv = *reinterpret_cast<const uint4*>(ymask + r * C + cc * 8);
+        uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // bf16 > 0  <=>  sign bit clear and value bits non-zero
+          uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+          if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
+          if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += d[j];
+        q[j] += d[j] * (xv[j] - mu[j]) * is[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(sums + cc * 8 + j, s[j]);
+      atomicAdd(sums + C + cc * 8 + j, q[j]);
+    }
+  }
+}
+
+// dgamma = sum dz*xhat, dbeta = sum dz; coefficients for the apply pass:
+//   dx = k1 * (dz - k2 - xhat * k3)   with k1 = gamma*invstd, k2 = sum_dz/M, k3 = sum_dzxhat/M
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ gamma,
+                                       const float* __restrict__ invstd, long M, int C, float* dgamma,
+                                       float* dbeta, int accumulate, float* __restrict__ coef) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sdz = sums[c], sdx = sums[C + c];
+  if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + sdx;
+  if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + sdz;
+  float gm = gamma ? gamma[c] : 1.f;
+  coef[c] = gm * invstd[c];
+  coef[C + c] = sdz / (float)M;
+  coef[2 * C + c] = sdx / (float)M;
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
+                                                           const bf16_t* __restrict__ ymask,
+                                                           const bf16_t* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ coef, long n8, int C,
+                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out) {
+  const int c8 = C / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c8) * 8;
+    float d[8], xv[8];
+    load8(dy + i * 8, d);
+    load8(x + i * 8, xv);
+    if (ymask) {
+      uint4 mv = *reinterpret_cast<const uint4*>(ymask + i * 8);
+      uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+        if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
+        if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
+      }
+      if (dz_out) store8(dz_out + i * 8, d);
+    }
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float xh = (xv[j] - mean[c + j]) * invstd[c + j];
+      o[j] = coef[c + j] * (d[j] - coef[C + c + j] - xh * coef[2 * C + c + j]);
+    }
+    store8(dx + i * 8, o);
+  }
+}
+
+// ---------------- LayerNorm: one wave per row, D % 8 == 0 ----------------
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, bf16_t* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     long M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + row * D;
+  const int d8 = D / 8;
+  float s = 0.f, q = 0.f;
+  for (int c = lane; c < d8; c += 64) {
+    float f[8];
+    load8(xr + c * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += f[j];
+  }
+  s = wave_sum(s);
+  const float mu = s / D;
+  for (int c = lane; c < d8; c += 64) {
+    float f[8];
+    load8(xr + c * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { float t = f[j] - mu; q += t * t; }
+  }
+  q = wave_sum(q);
+  const float rs = rsqrtf(q / D + eps);
+  if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+  for (int c = lane; c < d8; c += 64) {
+    float f[8];
+    load8(xr + c * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (f[j] - mu) * rs * gamma[c * 8 + j] + beta[c * 8 + j];
+    store8(y + row * D + c * 8, f);
+  }
+}
+
+// dx = rstd * (g*dy - mean(g*dy) - xhat*mean(g*dy*xhat)); dgamma/dbeta partials per block -> atomics
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, bf16_t* __restrict__ dx,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                     long M, int D, int rows_per_block) {
+  extern __shared__ float sred[];  // [2][D] block partials
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) sred[i] = 0.f;
+  __syncthreads();
+  const int d8 = D / 8;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  for (long row = r0 + w; row < min(M, r0 + rows_per_block); row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float a = 0.f, b = 0.f;
+    for (int c = lane; c < d8; c += 64) {
+      float f[8], g[8];
+      load8(x + row * D + c * 8, f);
+      load8(dy + row * D + c * 8, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float xh = (f[j] - mu) * rs;
+        float gd = g[j] * gamma[c * 8 + j];
+        a += gd;
+        b += gd * xh;
+        atomicAdd(&sred[c * 8 + j], g[j] * xh);
+        atomicAdd(&sred[D + c * 8 + j], g[j]);
+      }
+    }
+    a = wave_sum(a) / D;
+    b = wave_sum(b) / D;
+    for (int c = lane; c < d8; c += 64) {
+      float f[8], g[8], o[8];
+      load8(x + row * D + c * 8, f);
+      load8(dy + row * D + c * 8, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float xh = (f[j] - mu) * rs;
+        o[j] = rs * (g[j] * gamma[c * 8 + j] - a - xh * b);
+      }
+      store8(dx + row * D + c * 8, o);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    atomicAdd(dgamma + i, sred[i]);
+    atomicAdd(dbeta + i, sred[D + i]);
+  }
+}
+
+int red_grid(long M, int C) {
+  ColGeo g = colgeo(C);
+  long rows_per_thread = 32;
+  long blocks = (M + (long)g.RPB * rows_per_thread - 1) / ((long)g.RPB * rows_per_thread);
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+}  // namespace
+
+DTF_API int dtf_bn_stats(const void* x, long M, int C, float* stats, int zero, void* stream) {
+  if (C & 7) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  if (zero) (void)hipMemsetAsync(stats, 0, sizeof(float) * 2 * C, st);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(red_grid(M, C)), dim3(256), 0, st, (const bf16_t*)x, M, C, stats);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_bn_finalize(const float* stats, const float* gamma, const float* beta, float* running_mean,
+                            float* running_var, long M, int C, float momentum, float eps, float* scale,
+                            float* shift, float* mean_out, float* invstd_out, void* stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, gamma, beta,
+                     running_mean, running_var, M, C, momentum, eps, scale, shift, mean_out, invstd_out);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_bn_infer_coeff(const float* gamma, const float* beta, const float* rmean, const float* rvar, int C,
+                               float eps, float* scale, float* shift, void* stream) {
+  hipLaunchKernelGGL(bn_infer_coeff_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, gamma, beta,
+                     rmean, rvar, C, eps, scale, shift);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, const void* res, void* y, long M,
+                         int C, int relu, void* stream) {
+  if (C & 7) return -1;
+  long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, n8, C, relu);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* x, const float* mean, const float* invstd,
+                       const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma, float* dbeta,
+                       int accumulate, float* work /* 5*C floats */, void* stream) {
+  if (C & 7) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  float* sums = work;
+  float* coef = work + 2 * C;
+  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, st);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(red_grid(M, C)), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)ymask, (const bf16_t*)x, mean, invstd, M, C, sums);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, gamma, invstd, M, C,
+                     dgamma, dbeta, accumulate, coef);
+  long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)ymask, (const bf16_t*)x, mean, invstd, coef, n8, C, (bf16_t*)dx,
+                     (bf16_t*)dz_out);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
+                              float* rstd, long M, int D, float eps, void* stream) {
+  if (D & 7) return -1;
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, gamma,
+                     beta, (bf16_t*)y, mean, rstd, M, D, eps);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
+                              void* dx, float* dgamma, float* dbeta, long M, int D, void* stream) {
+  if (D & 7) return -1;
+  int rpb = 64;
+  size_t sh = sizeof(float) * 2 * D;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(cdiv(M, rpb)), dim3(256), sh, (hipStream_t)stream, (const bf16_t*)dy,
+                     (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, dgamma, dbeta, M, D, rpb);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,124 @@
+"""ctypes bindings to the in-tree native libraries.
+
+The HIP kernel library is a plain C ABI (``extern "C"``) shared object: every
+entry point takes raw device pointers, sizes and the ``hipStream_t`` of the
+caller (PyTorch's current stream), so launches are capturable into a
+hipGraph and ordered with the framework's own streams. Nothing here
+falls back silently: on a machine with a GPU, a missing or stale library is an
+error (``require_kernels``); CPU tensors take the reference (torch) path in
+``ops`` explicitly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+_lock = threading.Lock()
+_kern = None
+_rt = None
+
+P, I, L, F, U = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_ulonglong
+
+_KERNEL_SIGS = {
+    "dtf_gemm": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, L, L, L, F, F, I, I, I, I, P],
+    "dtf_conv_fwd": [P, P, P, P, P] + [I] * 15 + [I, I, I, P],
+    "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P],
+    "dtf_conv_wgrad": [P, P, P] + [I] * 15 + [I, I, I, P],
+    "dtf_bn_stats": [P, L, I, P, I, P],
+    "dtf_bn_finalize": [P, P, P, P, P, L, I, F, F, P, P, P, P, P],
+    "dtf_bn_infer_coeff": [P, P, P, P, I, F, P, P, P],
+    "dtf_bn_apply": [P, P, P, P, P, L, I, I, P],
+    "dtf_bn_bwd": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, P],
+    "dtf_layernorm_fwd": [P, P, P, P, P, P, L, I, F, P],
+    "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, I, P],
+    "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
+    "dtf_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
+    "dtf_gap_fwd": [P, P, I, I, I, I, P],
+    "dtf_gap_bwd": [P, I, P, I, I, I, P],
+    "dtf_optim_apply": [I, P, P, P, P, P, L, F, F, F, F, F, F, F, I, I, P, P, P],
+    "dtf_sumsq": [P, L, P, I, P],
+    "dtf_cast_f32_bf16": [P, P, L, P],
+    "dtf_cast_bf16_f32": [P, P, L, P],
+    "dtf_nchw_to_nhwc_pad": [P, P, I, I, I, I, P],
+    "dtf_filter_to_crsk": [P, P, I, I, I, P],
+    "dtf_add_bf16": [P, P, P, L, F, F, P],
+    "dtf_act": [P, P, P, L, I, I, P],
+    "dtf_dropout": [P, P, L, F, U, P],
+    "dtf_colsum": [P, L, I, P, I, P],
+    "dtf_embed_fwd": [P, P, P, P, P, P, P, L, I, I, P],
+    "dtf_embed_bwd": [P, P, P, L, I, I, P],
+    "dtf_softmax_ce": [P, I, P, P, P, I, L, I, F, F, P],
+    "dtf_softmax_fwd": [P, P, L, I, I, F, I, P, P],
+    "dtf_softmax_bwd": [P, P, P, L, I, F, P],
+    "dtf_attn_fwd": [P, P, P, P, P, I, I, I, I, I, I, F, I, P],
+    "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P],
+    "dtf_gemm_fp8": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, P],
+    "dtf_quant_fp8": [P, P, L, P, P, I, P],
+}
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def _load(path):
+    # torch must be imported first so its HIP runtime (same soname) is the one bound.
+    import torch  # noqa: F401
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+def kernels_available() -> bool:
+    return os.path.exists(os.path.join(_LIBDIR, "libdtf_kernels.so"))
+
+
+def kernels():
+    """Return the loaded kernel library (raises NativeMissing if it is not built)."""
+    global _kern
+    if _kern is not None:
+        return _kern
+    with _lock:
+        if _kern is not None:
+            return _kern
+        path = os.path.join(_LIBDIR, "libdtf_kernels.so")
+        if not os.path.exists(path):
+            raise NativeMissing(
+                f"{path} is missing: run `python -m distributed_tensorflow_amd._build` (hipcc, gfx950)")
+        lib = _load(path)
+        for name, sig in _KERNEL_SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = sig
+            fn.restype = ctypes.c_int
+        _kern = lib
+        return lib
+
+
+def runtime():
+    """Return the host C++ runtime library (checkpoint IO, KV store, PS transport...)."""
+    global _rt
+    if _rt is not None:
+        return _rt
+    with _lock:
+        if _rt is not None:
+            return _rt
+        path = os.path.join(_LIBDIR, "libdtf_runtime.so")
+        if not os.path.exists(path):
+            from . import _build
+            _build.build_runtime(verbose=False)
+        lib = ctypes.CDLL(path)
+        from . import _runtime_sigs
+        _runtime_sigs.declare(lib)
+        _rt = lib
+        return lib
+
+
+def call(name, *args):
+    """Invoke a kernel entry point; raise on a non-zero status."""
+    fn = getattr(kernels(), name)
+    rc = fn(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
+    return rc

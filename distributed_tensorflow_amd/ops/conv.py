@@ -1,0 +1,191 @@
+"""NHWC Conv2D (+ fused FusedBatchNorm / residual / ReLU) on the gfx950 implicit-GEMM kernel.
+
+Activations are channels-last ``[N, H, W, C]`` bf16; filters are stored KRSC
+(``[out, kh, kw, in]``) as f32 master variables with a bf16 compute shadow.
+The training-mode BatchNorm statistics are produced by the conv epilogue
+(per-column sum / sum^2 f32 atomics) so the forward BN costs one apply pass
+instead of three (SURVEY §2.4.b K4/K5, §7.4 hard part 1).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._util import BF16, F32, bf16_shadow, call, crsk_shadow, on_gpu, ptr, stream
+
+
+def out_size(h, k, s, p, d=1):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def same_pads(h, k, s, d=1):
+    """TF 'SAME' padding (pad_top, pad_total) for one spatial dim."""
+    out = (h + s - 1) // s
+    total = max((out - 1) * s + (k - 1) * d + 1 - h, 0)
+    return total // 2, total
+
+
+def _geom(x, w, stride, pad, dil):
+    N, H, W, C = x.shape
+    K, R, S, C2 = w.shape
+    assert C == C2, f"channel mismatch {C} vs {C2}"
+    sh, sw = stride
+    ph, pw = pad
+    dh, dw = dil
+    P = out_size(H, R, sh, ph, dh)
+    Q = out_size(W, S, sw, pw, dw)
+    return N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw
+
+
+def conv_fwd_raw(x, w16, g, stats=None, bias=None, act=0):
+    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
+    y = torch.empty((N, P, Q, K), dtype=BF16, device=x.device)
+    call("dtf_conv_fwd", ptr(x), ptr(w16), ptr(y), ptr(bias), ptr(stats), N, H, W, C, K, R, S, P, Q, sh, sw, ph,
+         pw, dh, dw, int(act), 0, -1, stream())
+    return y
+
+
+def conv_dgrad_raw(dy, w_master, g):
+    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
+    wc = crsk_shadow(w_master, K, R * S, C)
+    dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device)
+    call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0.0,
+         -1, stream())
+    return dx
+
+
+def conv_wgrad_raw(x, dy, g):
+    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
+    dw_ = torch.empty((K, R, S, C), dtype=F32, device=x.device)
+    call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw_), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0, -1,
+         stream())
+    return dw_
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dil, act):
+        x = x.contiguous()
+        g = _geom(x, w, stride, pad, dil)
+        y = conv_fwd_raw(x, bf16_shadow(w), g, bias=b, act=act)
+        ctx.save_for_backward(x, w, y if act else None)
+        ctx.g = g
+        ctx.act = act
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dy = dy.to(BF16).contiguous()
+        if ctx.act == 1:
+            dz = torch.empty_like(dy)
+            call("dtf_act", ptr(y), ptr(dy), ptr(dz), dz.numel(), 1, 1, stream())  # relu'(y) == relu'(pre)
+            dy = dz
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad_raw(dy, w, ctx.g)
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad_raw(x, dy, ctx.g)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.empty(dy.shape[-1], dtype=F32, device=dy.device)
+            call("dtf_colsum", ptr(dy), dy.numel() // dy.shape[-1], dy.shape[-1], ptr(db), 0, stream())
+        return dx, dw, db, None, None, None, None
+
+
+def _ref_conv(x, w, b, stride, pad, dil):
+    y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).to(w.dtype), w.permute(0, 3, 1, 2), b, stride=stride,
+                                   padding=pad, dilation=dil)
+    return y.permute(0, 2, 3, 1)
+
+
+def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), act=0):
+    """NHWC conv; w is KRSC. Explicit symmetric padding (use same_pads for TF SAME)."""
+    stride, pad, dil = tuple(stride), tuple(pad), tuple(dil)
+    if on_gpu(x):
+        return _ConvFn.apply(x.to(BF16), w, b, stride, pad, dil, act)
+    y = _ref_conv(x, w, b, stride, pad, dil)
+    return torch.relu(y) if act == 1 else y
+
+
+class _ConvBNFn(torch.autograd.Function):
+    """y = [relu]( BN_train(conv(x, w)) [+ residual] ) with batch statistics from the conv epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, res, rmean, rvar, stride, pad, dil, relu, momentum, eps, training):
+        x = x.contiguous()
+        g = _geom(x, w, stride, pad, dil)
+        N, H, W, C, K, R, S, P, Q = g[:9]
+        M = N * P * Q
+        dev = x.device
+        work = torch.empty(6 * K, dtype=F32, device=dev)  # stats(2K) scale shift mean invstd
+        stats, scale, shift, mean, invstd = work[:2 * K], work[2 * K:3 * K], work[3 * K:4 * K], work[4 * K:5 * K], \
+            work[5 * K:]
+        if training:
+            stats.zero_()
+            yc = conv_fwd_raw(x, bf16_shadow(w), g, stats=stats)
+            call("dtf_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, K, float(momentum),
+                 float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
+        else:
+            yc = conv_fwd_raw(x, bf16_shadow(w), g)
+            call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
+                 ptr(shift), stream())
+        out = torch.empty_like(yc)
+        if res is not None:
+            res = res.contiguous()
+        call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), stream())
+        ctx.save_for_backward(x, w, gamma, yc, out if relu else None, mean, invstd)
+        ctx.g = g
+        ctx.relu = relu
+        ctx.has_res = res is not None
+        ctx.training = training
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, gamma, yc, out, mean, invstd = ctx.saved_tensors
+        g = ctx.g
+        K = g[4]
+        M = yc.numel() // K
+        dout = dout.to(BF16).contiguous()
+        dyc = torch.empty_like(yc)
+        dres = torch.empty_like(yc) if (ctx.has_res and ctx.relu) else None
+        dgamma = torch.empty(K, dtype=F32, device=yc.device)
+        dbeta = torch.empty(K, dtype=F32, device=yc.device)
+        work = torch.empty(5 * K, dtype=F32, device=yc.device)
+        call("dtf_bn_bwd", ptr(dout), ptr(out), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K, ptr(dyc),
+             ptr(dres), ptr(dgamma), ptr(dbeta), 0, ptr(work), stream())
+        if ctx.has_res and not ctx.relu:
+            dres = dout
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad_raw(dyc, w, g)
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad_raw(x, dyc, g)
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+
+
+def conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1), relu=True, residual=None,
+            momentum=0.9, eps=1e-5, training=True):
+    """Fused Conv2D -> FusedBatchNorm -> (+residual) -> ReLU, NHWC."""
+    stride, pad, dil = tuple(stride), tuple(pad), tuple(dil)
+    if on_gpu(x):
+        return _ConvBNFn.apply(x.to(BF16), w, gamma, beta, residual, rmean, rvar, stride, pad, dil, bool(relu),
+                               float(momentum), float(eps), bool(training))
+    y = _ref_conv(x, w, None, stride, pad, dil)
+    from .norm import batch_norm_ref
+    y = batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training)
+    if residual is not None:
+        y = y + residual.to(y.dtype)
+    return torch.relu(y) if relu else y
+
+
+def image_to_nhwc_bf16(x_nchw, cpad=8):
+    """Device-side input pipeline step: f32 NCHW images -> bf16 NHWC, channels padded to `cpad`."""
+    N, C, H, W = x_nchw.shape
+    if on_gpu(x_nchw):
+        y = torch.empty((N, H, W, cpad), dtype=BF16, device=x_nchw.device)
+        call("dtf_nchw_to_nhwc_pad", ptr(x_nchw.contiguous()), ptr(y), N, C, H * W, cpad, stream())
+        return y
+    y = torch.zeros((N, H, W, cpad), dtype=x_nchw.dtype)
+    y[..., :C] = x_nchw.permute(0, 2, 3, 1)
+    return y

@@ -1,0 +1,164 @@
+"""MatMul / Dense (Linear) / batched matmul on the gfx950 MFMA GEMM (csrc/kernels/gemm.hip).
+
+TF's MatMul + BiasAdd (+ activation) and their gradients.
+On GPU every product runs on the hand-written MFMA kernel; on CPU the same
+function evaluates the f32 reference so the API works device-agnostically.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._util import BF16, F32, bf16_shadow, call, on_gpu, ptr, stream
+
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+_ACTS = {None: 0, "linear": 0, "relu": 1, "gelu": 2}
+
+
+def act_code(act):
+    if isinstance(act, int):
+        return act
+    return _ACTS[act]
+
+
+def gemm(a, b, *, a_kouter=False, b_kouter=False, out=None, out_dtype=BF16, bias=None, act=0, alpha=1.0,
+         beta=0.0, stats=None, aux=None, splitk=0, tile=-1):
+    """C[m,n] = alpha * sum_k A(m,k) B(n,k) + beta*C  (+bias[n], act).
+
+    A is [M,K] (or [K,M] if a_kouter), B is [N,K] (or [K,N] if b_kouter); 2-D or
+    batched 3-D (leading batch dim). bf16 inputs; C bf16 or f32.
+    """
+    assert a.dtype == BF16 and b.dtype == BF16, "gemm operands must be bf16"
+    batched = a.dim() == 3
+    if batched:
+        bt = a.shape[0]
+        M, K = (a.shape[2], a.shape[1]) if a_kouter else (a.shape[1], a.shape[2])
+        N = b.shape[2] if b_kouter else b.shape[1]
+    else:
+        bt = 1
+        M, K = (a.shape[1], a.shape[0]) if a_kouter else (a.shape[0], a.shape[1])
+        N = b.shape[1] if b_kouter else b.shape[0]
+    if out is None:
+        shape = (bt, M, N) if batched else (M, N)
+        out = (torch.zeros if beta != 0 else torch.empty)(shape, dtype=out_dtype, device=a.device)
+    lda = a.stride(-2)
+    ldb = b.stride(-2)
+    ldc = out.stride(-2)
+    sA = a.stride(0) if batched else 0
+    sB = b.stride(0) if batched else 0
+    sC = out.stride(0) if batched else 0
+    call("dtf_gemm", ptr(a), ptr(b), ptr(out), ptr(aux), ptr(bias), ptr(stats), M, N, K, lda, ldb, ldc,
+         int(a_kouter), int(b_kouter), bt, sA, sB, sC, float(alpha), float(beta), int(act),
+         int(out.dtype == F32), int(splitk), int(tile), stream())
+    return out
+
+
+def colsum(x2d, out=None, accumulate=False):
+    """BiasAddGrad: column sums of a bf16 [M,N] matrix into f32 [N]."""
+    M, N = x2d.shape
+    if out is None:
+        out = torch.empty(N, dtype=F32, device=x2d.device)
+    call("dtf_colsum", ptr(x2d), M, N, ptr(out), int(accumulate), stream())
+    return out
+
+
+def _act_ref(x, act):
+    if act == ACT_RELU:
+        return torch.relu(x)
+    if act == ACT_GELU:
+        return torch.nn.functional.gelu(x, approximate="tanh")
+    return x
+
+
+class _DenseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        # x: [..., in] bf16 ; w: [out, in] f32 master ; b: [out] f32 or None
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        w16 = bf16_shadow(w)
+        pre = torch.empty((x2.shape[0], w.shape[0]), dtype=BF16, device=x.device) if act else None
+        y = gemm(x2, w16, bias=b, act=act, aux=pre)
+        ctx.save_for_backward(x2, w, pre)
+        ctx.act = act
+        ctx.has_b = b is not None
+        ctx.shp = shp
+        return y.reshape(*shp[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, pre = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0])
+        if dy2.dtype != BF16:
+            dy2 = dy2.to(BF16)
+        dy2 = dy2.contiguous()
+        if ctx.act:
+            dz = torch.empty_like(dy2)
+            call("dtf_act", ptr(pre), ptr(dy2), ptr(dz), dz.numel(), ctx.act, 1, stream())
+        else:
+            dz = dy2
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            # dx[t,i] = sum_o dz[t,o] W[o,i]  -> B stored [K=out][N=in] (k-outer)
+            dx = gemm(dz, bf16_shadow(w), b_kouter=True).reshape(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            # dW[o,i] = sum_t dz[t,o] x[t,i]  -> both operands k-outer, f32 out
+            dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = colsum(dz)
+        return dx, dw, db, None
+
+
+def dense(x, w, b=None, act=None):
+    """y = act(x @ w^T + b); w is [out, in] (f32 master variable)."""
+    a = act_code(act)
+    if on_gpu(x):
+        if x.dtype != BF16:
+            x = x.to(BF16)
+        return _DenseFn.apply(x, w, b, a)
+    y = torch.nn.functional.linear(x.to(w.dtype), w, b)
+    return _act_ref(y, a)
+
+
+class _BMMFn(torch.autograd.Function):
+    """Batched C = A @ B^T (nt=True) or A @ B (nt=False) for bf16 [b, m, k] tensors."""
+
+    @staticmethod
+    def forward(ctx, a, b, nt, alpha):
+        a = a.contiguous()
+        b = b.contiguous()
+        ctx.save_for_backward(a, b)
+        ctx.nt = nt
+        ctx.alpha = alpha
+        return gemm(a, b, b_kouter=not nt, alpha=alpha)
+
+    @staticmethod
+    def backward(ctx, dc):
+        a, b = ctx.saved_tensors
+        dc = dc.to(BF16).contiguous()
+        al = ctx.alpha
+        if ctx.nt:  # C = A B^T : dA = dC B ; dB = dC^T A
+            da = gemm(dc, b, b_kouter=True, alpha=al)
+            db = gemm(dc, a, a_kouter=True, b_kouter=True, alpha=al)
+        else:  # C = A B : dA = dC B^T ; dB = A^T dC
+            da = gemm(dc, b, alpha=al)
+            db = gemm(a, dc, a_kouter=True, b_kouter=True, alpha=al)
+        return da, db, None, None
+
+
+def bmm(a, b, transpose_b=False, alpha=1.0):
+    if on_gpu(a):
+        return _BMMFn.apply(a.to(BF16), b.to(BF16), bool(transpose_b), float(alpha))
+    bb = b.transpose(-1, -2) if transpose_b else b
+    return alpha * torch.matmul(a, bb)
+
+
+def matmul(a, b, transpose_a=False, transpose_b=False):
+    """tf.linalg.matmul-like entry point (2-D or batched)."""
+    if transpose_a:
+        a = a.transpose(-1, -2)
+    if a.dim() == 2 and b.dim() == 2:
+        return bmm(a.unsqueeze(0), b.unsqueeze(0), transpose_b=transpose_b)[0] if on_gpu(a) else (
+            a @ (b.transpose(-1, -2) if transpose_b else b))
+    return bmm(a, b, transpose_b=transpose_b)

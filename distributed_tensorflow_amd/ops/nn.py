@@ -1,0 +1,274 @@
+"""Pooling, activations, dropout, embeddings, softmax / cross-entropy ops
+(csrc/kernels/pool.hip, elementwise.hip) with CPU references."""
+from __future__ import annotations
+
+import torch
+
+from ._util import BF16, F32, call, on_gpu, ptr, stream
+from .conv import out_size
+
+
+# ------------------------------------------------------------------ pooling
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        P, Q = out_size(H, k[0], s[0], p[0]), out_size(W, k[1], s[1], p[1])
+        y = torch.empty((N, P, Q, C), dtype=BF16, device=x.device)
+        arg = torch.empty((N, P, Q, C), dtype=torch.uint8, device=x.device)
+        call("dtf_maxpool_fwd", ptr(x), ptr(y), ptr(arg), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+             stream())
+        ctx.save_for_backward(arg)
+        ctx.geo = (N, H, W, C, P, Q, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, H, W, C, P, Q, k, s, p = ctx.geo
+        dy = dy.to(BF16).contiguous()
+        dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device)
+        call("dtf_maxpool_bwd", ptr(dy), ptr(arg), ptr(dx), N, H, W, C, P, Q, k[0], k[1], s[0], s[1], p[0], p[1],
+             stream())
+        return dx, None, None, None
+
+
+def max_pool2d(x, ksize=(3, 3), strides=(2, 2), pad=(1, 1)):
+    ksize, strides, pad = tuple(ksize), tuple(strides), tuple(pad)
+    if on_gpu(x) and x.shape[-1] % 8 == 0:
+        return _MaxPoolFn.apply(x.to(BF16), ksize, strides, pad)
+    y = torch.nn.functional.max_pool2d(x.permute(0, 3, 1, 2), ksize, strides, pad)
+    return y.permute(0, 2, 3, 1)
+
+
+class _GAPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        y = torch.empty((N, C), dtype=BF16, device=x.device)
+        call("dtf_gap_fwd", ptr(x), ptr(y), N, H * W, C, 0, stream())
+        ctx.geo = (N, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.geo
+        dy = dy.contiguous()
+        dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device)
+        call("dtf_gap_bwd", ptr(dy), int(dy.dtype == F32), ptr(dx), N, H * W, C, stream())
+        return dx
+
+
+def global_avg_pool(x):
+    if on_gpu(x) and x.shape[-1] % 8 == 0:
+        return _GAPFn.apply(x.to(BF16))
+    return x.mean(dim=(1, 2))
+
+
+# ------------------------------------------------------------------ activations
+class _ActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        call("dtf_act", ptr(x), None, ptr(y), x.numel(), act, 0, stream())
+        ctx.save_for_backward(x)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.to(BF16).contiguous()
+        dx = torch.empty_like(x)
+        call("dtf_act", ptr(x), ptr(dy), ptr(dx), x.numel(), ctx.act, 1, stream())
+        return dx, None
+
+
+def relu(x):
+    if on_gpu(x) and x.dtype == BF16 and x.numel() % 8 == 0:
+        return _ActFn.apply(x, 1)
+    return torch.relu(x)
+
+
+def gelu(x):
+    if on_gpu(x) and x.dtype == BF16 and x.numel() % 8 == 0:
+        return _ActFn.apply(x, 2)
+    return torch.nn.functional.gelu(x, approximate="tanh")
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, keep, seed):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        call("dtf_dropout", ptr(x), ptr(y), x.numel(), float(keep), int(seed), stream())
+        ctx.keep, ctx.seed = keep, seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.to(BF16).contiguous()
+        dx = torch.empty_like(dy)
+        call("dtf_dropout", ptr(dy), ptr(dx), dy.numel(), float(ctx.keep), int(ctx.seed), stream())
+        return dx, None, None
+
+
+_seed_counter = [0x5EED]
+
+
+def dropout(x, rate, training=True, seed=None):
+    if not training or rate <= 0.0:
+        return x
+    keep = 1.0 - rate
+    if on_gpu(x) and x.dtype == BF16 and x.numel() % 8 == 0:
+        if seed is None:
+            _seed_counter[0] += 1
+            seed = _seed_counter[0] * 0x9E3779B1
+        return _DropoutFn.apply(x, keep, seed & 0xFFFFFFFFFFFFFFFF)
+    return torch.nn.functional.dropout(x, rate, True)
+
+
+def add(a, b):
+    if on_gpu(a) and a.dtype == BF16 and b.dtype == BF16 and a.numel() % 8 == 0 and a.shape == b.shape:
+        return _AddFn.apply(a, b)
+    return a + b
+
+
+class _AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        y = torch.empty_like(a)
+        call("dtf_add_bf16", ptr(a), ptr(b), ptr(y), a.numel(), 1.0, 1.0, stream())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+# ------------------------------------------------------------------ embeddings
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, table, pos_table, type_ids, type_table, seq_len):
+        ids = ids.contiguous().long()
+        T = ids.numel()
+        D = table.shape[1]
+        from ._util import bf16_shadow
+        t16 = bf16_shadow(table)
+        p16 = bf16_shadow(pos_table) if pos_table is not None else None
+        y16 = bf16_shadow(type_table) if type_table is not None else None
+        tid = type_ids.contiguous().long() if type_ids is not None else None
+        out = torch.empty((T, D), dtype=BF16, device=ids.device)
+        call("dtf_embed_fwd", ptr(t16), ptr(ids), ptr(p16), None, ptr(y16), ptr(tid), ptr(out), T, D, int(seq_len),
+             stream())
+        ctx.save_for_backward(ids, tid)
+        ctx.shapes = (table.shape, None if pos_table is None else pos_table.shape,
+                      None if type_table is None else type_table.shape, seq_len)
+        return out.reshape(*ids.shape, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, tid = ctx.saved_tensors
+        tshape, pshape, yshape, seq_len = ctx.shapes
+        dy = dy.to(BF16).contiguous()
+        T = ids.numel()
+        D = tshape[1]
+        dt = torch.zeros(tshape, dtype=F32, device=dy.device)
+        call("dtf_embed_bwd", ptr(dy), ptr(ids), ptr(dt), T, D, 1, stream())
+        dp = dy_ = None
+        if pshape is not None:
+            dp = torch.zeros(pshape, dtype=F32, device=dy.device)
+            call("dtf_embed_bwd", ptr(dy), None, ptr(dp), T, D, int(seq_len), stream())
+        if yshape is not None:
+            dy_ = torch.zeros(yshape, dtype=F32, device=dy.device)
+            if tid is not None:
+                call("dtf_embed_bwd", ptr(dy), ptr(tid), ptr(dy_), T, D, 1, stream())
+            else:
+                call("dtf_embed_bwd", ptr(dy), None, ptr(dy_), T, D, 1, stream())
+        return None, dt, dp, None, dy_, None
+
+
+def embedding(ids, table, pos_table=None, type_ids=None, type_table=None):
+    """out[..., :] = table[ids] (+ pos_table[position]) (+ type_table[type_ids]); positions = last axis index."""
+    seq_len = ids.shape[-1]
+    if on_gpu(ids) and table.shape[1] % 8 == 0:
+        return _EmbedFn.apply(ids, table, pos_table, type_ids, type_table, seq_len)
+    out = table[ids.long()]
+    if pos_table is not None:
+        out = out + pos_table[:seq_len]
+    if type_table is not None:
+        out = out + (type_table[type_ids.long()] if type_ids is not None else type_table[0])
+    return out
+
+
+# ------------------------------------------------------------------ softmax / losses
+class _SoftmaxCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, smooth):
+        logits = logits.contiguous()
+        V = logits.shape[-1]
+        rows = logits.numel() // V
+        loss = torch.empty(rows, dtype=F32, device=logits.device)
+        dl = torch.empty_like(logits)
+        call("dtf_softmax_ce", ptr(logits), int(logits.dtype == F32), ptr(labels.contiguous().long()), ptr(loss),
+             ptr(dl), int(dl.dtype == F32), rows, V, 1.0, float(smooth), stream())
+        ctx.save_for_backward(dl)
+        return loss.reshape(logits.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, dloss):
+        (dl,) = ctx.saved_tensors
+        g = dloss.reshape(-1, 1).to(dl.dtype)
+        V = dl.shape[-1]
+        return (dl.reshape(-1, V) * g).reshape(dl.shape), None, None
+
+
+def sparse_softmax_cross_entropy(logits, labels, label_smoothing=0.0):
+    """Per-example loss of tf.nn.sparse_softmax_cross_entropy_with_logits (fused fwd+grad kernel)."""
+    if on_gpu(logits):
+        return _SoftmaxCEFn.apply(logits, labels, float(label_smoothing))
+    return torch.nn.functional.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), labels.reshape(-1).long(),
+                                             reduction="none", label_smoothing=label_smoothing,
+                                             ignore_index=-100).reshape(labels.shape)
+
+
+class _SoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, scale, causal, add_mask):
+        x = x.contiguous()
+        Sq, Sk = x.shape[-2], x.shape[-1]
+        rows = x.numel() // Sk
+        y = torch.empty_like(x)
+        call("dtf_softmax_fwd", ptr(x), ptr(y), rows, Sq, Sk, float(scale), int(causal), ptr(add_mask), stream())
+        ctx.save_for_backward(y)
+        ctx.scale = scale
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.to(BF16).contiguous()
+        Sk = y.shape[-1]
+        dx = torch.empty_like(y)
+        call("dtf_softmax_bwd", ptr(y), ptr(dy), ptr(dx), y.numel() // Sk, Sk, float(ctx.scale), stream())
+        return dx, None, None, None
+
+
+def softmax(x, scale=1.0, causal=False, add_mask=None):
+    """Row softmax(scale*x + mask) over the last axis.
+
+    add_mask: optional f32 additive mask of shape [prod(x.shape[:-2]), Sk] (one row per score matrix)."""
+    if on_gpu(x) and x.dtype == BF16:
+        return _SoftmaxFn.apply(x, float(scale), bool(causal), add_mask)
+    z = x.float() * scale
+    if causal:
+        Sq, Sk = z.shape[-2], z.shape[-1]
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=z.device).tril(Sk - Sq)
+        z = z.masked_fill(~m, float("-inf"))
+    if add_mask is not None:
+        z = z + add_mask.reshape(*z.shape[:-2], 1, z.shape[-1])
+    return torch.softmax(z, dim=-1).to(x.dtype)

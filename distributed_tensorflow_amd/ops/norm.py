@@ -1,0 +1,118 @@
+"""FusedBatchNorm (NHWC) and LayerNorm ops (csrc/kernels/norm.hip), with CPU references."""
+from __future__ import annotations
+
+import torch
+
+from ._util import BF16, F32, call, on_gpu, ptr, stream
+
+
+def batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training):
+    """f32 reference of training/inference BN over all but the last (channel) axis."""
+    yf = y.float()
+    red = tuple(range(yf.dim() - 1))
+    if training:
+        mean = yf.mean(dim=red)
+        var = yf.var(dim=red, unbiased=False)
+        if rmean is not None:
+            n = yf.numel() // yf.shape[-1]
+            with torch.no_grad():
+                rmean.mul_(momentum).add_(mean.detach() * (1 - momentum))
+                rvar.mul_(momentum).add_(var.detach() * (n / max(n - 1, 1)) * (1 - momentum))
+    else:
+        mean, var = rmean, rvar
+    out = (yf - mean) * torch.rsqrt(var + eps)
+    if gamma is not None:
+        out = out * gamma
+    if beta is not None:
+        out = out + beta
+    return out
+
+
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, rmean, rvar, relu, momentum, eps, training):
+        x = x.contiguous()
+        C = x.shape[-1]
+        M = x.numel() // C
+        work = torch.empty(6 * C, dtype=F32, device=x.device)
+        stats, scale, shift, mean, invstd = work[:2 * C], work[2 * C:3 * C], work[3 * C:4 * C], work[4 * C:5 * C], \
+            work[5 * C:]
+        if training:
+            call("dtf_bn_stats", ptr(x), M, C, ptr(stats), 1, stream())
+            call("dtf_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, C, float(momentum),
+                 float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
+        else:
+            call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), C, float(eps), ptr(scale),
+                 ptr(shift), stream())
+        out = torch.empty_like(x)
+        if res is not None:
+            res = res.to(BF16).contiguous()
+        call("dtf_bn_apply", ptr(x), ptr(scale), ptr(shift), ptr(res), ptr(out), M, C, int(relu), stream())
+        ctx.save_for_backward(x, gamma, out if relu else None, mean, invstd)
+        ctx.relu = relu
+        ctx.has_res = res is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, gamma, out, mean, invstd = ctx.saved_tensors
+        C = x.shape[-1]
+        M = x.numel() // C
+        dout = dout.to(BF16).contiguous()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if (ctx.has_res and ctx.relu) else None
+        dgamma = torch.empty(C, dtype=F32, device=x.device)
+        dbeta = torch.empty(C, dtype=F32, device=x.device)
+        work = torch.empty(5 * C, dtype=F32, device=x.device)
+        call("dtf_bn_bwd", ptr(dout), ptr(out), ptr(x), ptr(mean), ptr(invstd), ptr(gamma), M, C, ptr(dx), ptr(dres),
+             ptr(dgamma), ptr(dbeta), 0, ptr(work), stream())
+        if ctx.has_res and not ctx.relu:
+            dres = dout
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+def batch_norm(x, gamma, beta, rmean, rvar, training=True, momentum=0.99, eps=1e-3, relu=False, residual=None):
+    """Channels-last FusedBatchNorm (+ optional residual add and ReLU)."""
+    if on_gpu(x) and x.shape[-1] % 8 == 0:
+        return _BNFn.apply(x.to(BF16), gamma, beta, residual, rmean, rvar, bool(relu), float(momentum), float(eps),
+                           bool(training))
+    y = batch_norm_ref(x, gamma, beta, rmean, rvar, momentum, eps, training)
+    if residual is not None:
+        y = y + residual.float()
+    y = torch.relu(y) if relu else y
+    return y.to(x.dtype) if x.is_floating_point() else y
+
+
+class _LNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x = x.contiguous()
+        D = x.shape[-1]
+        M = x.numel() // D
+        y = torch.empty_like(x)
+        mean = torch.empty(M, dtype=F32, device=x.device)
+        rstd = torch.empty(M, dtype=F32, device=x.device)
+        call("dtf_layernorm_fwd", ptr(x), ptr(gamma), ptr(beta), ptr(y), ptr(mean), ptr(rstd), M, D, float(eps),
+             stream())
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        D = x.shape[-1]
+        M = x.numel() // D
+        dy = dy.to(BF16).contiguous()
+        dx = torch.empty_like(x)
+        dg = torch.zeros(D, dtype=F32, device=x.device)
+        db = torch.zeros(D, dtype=F32, device=x.device)
+        call("dtf_layernorm_bwd", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(dg), ptr(db), M, D,
+             stream())
+        return dx, dg, db, None
+
+
+def layer_norm(x, gamma, beta, eps=1e-5):
+    if on_gpu(x) and x.shape[-1] % 8 == 0:
+        return _LNFn.apply(x.to(BF16), gamma, beta, float(eps))
+    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), gamma, beta, eps).to(
+        x.dtype if x.is_floating_point() else torch.float32)
