@@ -106,24 +106,30 @@ class Layer:
     def variables(self):
         return self.weights
 
+    def _collect(self, trainable_ctx=True):
+        """(weight, effectively_trainable) pairs, depth-first, de-duplicated by identity."""
+        out, seen = [], set()
+
+        def rec(layer, ctx):
+            ctx = ctx and layer._trainable
+            for w in layer._own_weights:
+                if id(w) not in seen:
+                    seen.add(id(w))
+                    out.append((w, ctx and w.trainable))
+            for l in layer._layers:
+                rec(l, ctx)
+        rec(self, trainable_ctx)
+        return out
+
     @property
     def trainable_weights(self):
-        if not self._trainable:
-            return []
-        return [w for w in self._all_weights() if w.trainable and self._owner_trainable(w)]
+        return [w for w, t in self._collect() if t]
 
     trainable_variables = trainable_weights
 
-    def _owner_trainable(self, w):
-        for l in self._layers:
-            if w in l._all_weights() and not l._trainable:
-                return False
-        return True
-
     @property
     def non_trainable_weights(self):
-        tw = {id(w) for w in self.trainable_weights}
-        return [w for w in self._all_weights() if id(w) not in tw]
+        return [w for w, t in self._collect() if not t]
 
     non_trainable_variables = non_trainable_weights
 

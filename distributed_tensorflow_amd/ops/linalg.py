@@ -28,6 +28,28 @@ def gemm(a, b, *, a_kouter=False, b_kouter=False, out=None, out_dtype=BF16, bias
     batched 3-D (leading batch dim). bf16 inputs; C bf16 or f32.
     """
     assert a.dtype == BF16 and b.dtype == BF16, "gemm operands must be bf16"
+    padded = _pad_operands(a, b, a_kouter, b_kouter)
+    if padded is not None:
+        a2, b2, M, N = padded
+        o = gemm(a2, b2, a_kouter=a_kouter, b_kouter=b_kouter, out_dtype=out_dtype if out is None else out.dtype,
+                 bias=None if bias is None else torch.nn.functional.pad(bias, (0, b2.shape[-1 if b_kouter else -2]
+                                                                               - N)),
+                 act=act, alpha=alpha, splitk=splitk, tile=tile)
+        o = o[..., :M, :N]
+        if stats is not None:
+            y = o.float()
+            red = tuple(range(y.dim() - 1))
+            stats[:N] += y.sum(red)
+            stats[N:] += (y * y).sum(red)
+        if aux is not None:
+            raise NotImplementedError("aux output with padded gemm")
+        if out is None:
+            return o.contiguous()
+        if beta != 0:
+            out.mul_(beta).add_(o.to(out.dtype))
+        else:
+            out.copy_(o)
+        return out
     batched = a.dim() == 3
     if batched:
         bt = a.shape[0]
@@ -52,9 +74,41 @@ def gemm(a, b, *, a_kouter=False, b_kouter=False, out=None, out_dtype=BF16, bias
     return out
 
 
+def _pad_operands(a, b, a_kouter, b_kouter):
+    """Zero-pad to the kernel's alignment (K%8, M%8 / N%8 for K-outer operands, N%4); None if aligned."""
+    if a_kouter:
+        K, M = a.shape[-2], a.shape[-1]
+    else:
+        M, K = a.shape[-2], a.shape[-1]
+    if b_kouter:
+        N = b.shape[-1]
+    else:
+        N = b.shape[-2]
+    Kp = -(-K // 8) * 8
+    Mp = -(-M // 8) * 8 if a_kouter else M
+    Np = -(-N // 8) * 8 if b_kouter else -(-N // 4) * 4
+    if (Kp, Mp, Np) == (K, M, N):
+        return None
+    F = torch.nn.functional
+    if a_kouter:
+        a2 = F.pad(a, (0, Mp - M, 0, Kp - K))
+    else:
+        a2 = F.pad(a, (0, Kp - K))
+    if b_kouter:
+        b2 = F.pad(b, (0, Np - N, 0, Kp - K))
+    else:
+        b2 = F.pad(b, (0, Kp - K, 0, Np - N))
+    return a2.contiguous(), b2.contiguous(), M, N
+
+
 def colsum(x2d, out=None, accumulate=False):
     """BiasAddGrad: column sums of a bf16 [M,N] matrix into f32 [N]."""
     M, N = x2d.shape
+    if N % 8:
+        r = x2d.float().sum(0)
+        if out is None:
+            return r
+        return out.add_(r) if accumulate else out.copy_(r)
     if out is None:
         out = torch.empty(N, dtype=F32, device=x2d.device)
     call("dtf_colsum", ptr(x2d), M, N, ptr(out), int(accumulate), stream())

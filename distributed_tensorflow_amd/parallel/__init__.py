@@ -1,0 +1,4 @@
+"""Distribution strategies, cluster resolution and collectives (tf.distribute surface)."""
+from .cluster_resolver import ClusterSpec, TFConfigClusterResolver, TorchrunClusterResolver, SimpleClusterResolver  # noqa
+from .strategy import (Strategy, OneDeviceStrategy, MirroredStrategy, MultiWorkerMirroredStrategy,  # noqa
+                       ReduceOp, get_strategy, has_strategy, InputContext)

@@ -1,0 +1,297 @@
+"""tf.distribute-style strategies on MI355X.
+
+* ``OneDeviceStrategy`` / default strategy — single device.
+* ``MirroredStrategy`` — synchronous data parallelism. Under a one-process-per-GPU
+  launch (torchrun / bench.py, the idiomatic MI355X layout) it is the same
+  collective all-reduce as MultiWorkerMirroredStrategy restricted to one node.
+  Given several local devices in ONE process it runs in-process replicas
+  (``CPU:0,CPU:1`` plumbing config of BASELINE.json): replicas share the
+  variables when they share a device, otherwise gradients are reduced to the
+  first device (ReductionToOneDevice) and weights broadcast back.
+* ``MultiWorkerMirroredStrategy`` — CollectiveAllReduce across processes,
+  topology from TF_CONFIG (chief/worker tasks) or torchrun's env, RCCL over
+  xGMI for GPUs and gloo for CPUs, with the bucketed backward-overlapped
+  all-reduce of ``collective.GradientBucketer``.
+* ``ParameterServerStrategy`` lives in ``parameter_server.py``.
+"""
+from __future__ import annotations
+
+import contextlib
+import enum
+import os
+import threading
+
+import torch
+import torch.distributed as dist
+
+from .. import context
+from . import collective
+from .cluster_resolver import TFConfigClusterResolver, TorchrunClusterResolver
+
+_tls = threading.local()
+
+
+class ReduceOp(enum.Enum):
+    SUM = "sum"
+    MEAN = "mean"
+    MAX = "max"
+    MIN = "min"
+
+
+def get_strategy():
+    s = getattr(_tls, "strategy", None)
+    return s if s is not None else _default()
+
+
+def has_strategy():
+    return getattr(_tls, "strategy", None) is not None
+
+
+_DEFAULT = None
+
+
+def _default():
+    global _DEFAULT
+    if _DEFAULT is None:
+        _DEFAULT = OneDeviceStrategy(context.default_device())
+    return _DEFAULT
+
+
+class Strategy:
+    """Common interface the Keras training loop talks to."""
+
+    def __init__(self):
+        self._bucketers = {}
+
+    # ---- properties
+    @property
+    def num_replicas_in_sync(self):
+        return 1
+
+    @property
+    def is_chief(self):
+        return True
+
+    @property
+    def worker_index(self):
+        return 0
+
+    @property
+    def num_workers(self):
+        return 1
+
+    @property
+    def device(self):
+        return context.default_device()
+
+    @contextlib.contextmanager
+    def scope(self):
+        prev = getattr(_tls, "strategy", None)
+        _tls.strategy = self
+        try:
+            with context.device(self.device):
+                yield self
+        finally:
+            _tls.strategy = prev
+
+    # ---- training-loop hooks
+    def setup_model(self, model, arena):
+        """Called once after the trainable arena exists (broadcast initial state, install hooks)."""
+
+    def backward(self, loss, arena):
+        loss.backward()
+
+    def grad_scale(self):
+        return 1.0
+
+    def local_batch_slice(self, n):
+        """Which rows of a global batch of n rows this process consumes."""
+        return slice(0, n)
+
+    def reduce(self, op, value, axis=None):
+        v = value
+        if axis is not None and isinstance(v, torch.Tensor):
+            v = v.sum(axis) if _op(op) == "sum" else v.mean(axis)
+        return v
+
+    def run(self, fn, args=(), kwargs=None):
+        return fn(*args, **(kwargs or {}))
+
+    def experimental_distribute_dataset(self, dataset):
+        return dataset
+
+    def distribute_datasets_from_function(self, fn):
+        return fn(InputContext(self.num_workers, self.worker_index, self.num_replicas_in_sync))
+
+    def barrier(self):
+        pass
+
+
+def _op(op):
+    return op.value if isinstance(op, ReduceOp) else str(op).lower()
+
+
+class InputContext:
+    def __init__(self, num_input_pipelines, input_pipeline_id, num_replicas_in_sync):
+        self.num_input_pipelines = num_input_pipelines
+        self.input_pipeline_id = input_pipeline_id
+        self.num_replicas_in_sync = num_replicas_in_sync
+
+    def get_per_replica_batch_size(self, global_batch_size):
+        if global_batch_size % self.num_replicas_in_sync:
+            raise ValueError("global batch size must be divisible by the number of replicas")
+        return global_batch_size // self.num_replicas_in_sync
+
+
+class OneDeviceStrategy(Strategy):
+    def __init__(self, device=None):
+        super().__init__()
+        self._device = context.parse_device(device) if device is not None else context.default_device()
+
+    @property
+    def device(self):
+        return self._device
+
+
+class MultiWorkerMirroredStrategy(Strategy):
+    """Synchronous collective all-reduce data parallelism, one process per device."""
+
+    def __init__(self, cluster_resolver=None, communication_options=None, bucket_mb=None):
+        super().__init__()
+        self.bucket_mb = bucket_mb
+        if cluster_resolver is None:
+            if TorchrunClusterResolver.active():
+                cluster_resolver = TorchrunClusterResolver()
+            else:
+                cluster_resolver = TFConfigClusterResolver()
+        self.cluster_resolver = cluster_resolver
+        if isinstance(cluster_resolver, TorchrunClusterResolver):
+            self._rank, self._world = cluster_resolver.rank, cluster_resolver.world_size
+            addr, port = cluster_resolver.master_addr, cluster_resolver.master_port
+            self._local_rank = cluster_resolver.local_rank
+        else:
+            tasks = cluster_resolver.trainer_tasks() if not cluster_resolver.standalone else [("worker", 0)]
+            self._world = len(tasks)
+            self._rank = max(0, cluster_resolver.trainer_rank()) if not cluster_resolver.standalone else 0
+            chief_addr = cluster_resolver.cluster.task_address(*tasks[0]) if not cluster_resolver.standalone \
+                else "127.0.0.1:29500"
+            addr, port = chief_addr.rsplit(":", 1)
+            port = int(port)
+            self._local_rank = int(os.environ.get("LOCAL_RANK", self._rank if torch.cuda.device_count() > 1 else 0))
+        if torch.cuda.is_available():
+            dev = torch.device("cuda", self._local_rank % torch.cuda.device_count())
+            torch.cuda.set_device(dev)
+        else:
+            dev = torch.device("cpu")
+        self._device = dev
+        if self._world > 1:
+            collective.init_process_group(self._rank, self._world, addr, port, dev.type)
+
+    @property
+    def device(self):
+        return self._device
+
+    @property
+    def num_replicas_in_sync(self):
+        return self._world
+
+    @property
+    def num_workers(self):
+        return self._world
+
+    @property
+    def worker_index(self):
+        return self._rank
+
+    @property
+    def is_chief(self):
+        return self._rank == 0
+
+    def setup_model(self, model, arena):
+        if self._world <= 1:
+            return
+        # identical initial state everywhere: one broadcast of the whole master arena + non-trainables
+        collective.broadcast_tensors([arena.flat] + [v.data for v in model.non_trainable_weights], src=0)
+        arena.refresh_bf16()
+        from ..ops._util import bump_weights_epoch
+        bump_weights_epoch()
+        b = collective.GradientBucketer(arena, bucket_mb=self.bucket_mb).install()
+        self._bucketers[id(arena)] = b
+
+    def backward(self, loss, arena):
+        loss.backward()
+        b = self._bucketers.get(id(arena))
+        if b is not None:
+            b.finalize()
+
+    def grad_scale(self):
+        return 1.0 / self._world
+
+    def local_batch_slice(self, n):
+        per = n // self._world
+        return slice(self._rank * per, (self._rank + 1) * per)
+
+    def reduce(self, op, value, axis=None):
+        v = super().reduce(op, value, axis)
+        if self._world <= 1:
+            return v
+        t = v if isinstance(v, torch.Tensor) else torch.tensor(float(v), device=self._device)
+        t = t.detach().clone().to(self._device).float()
+        collective.all_reduce_(t, _op(op))
+        return t
+
+    def experimental_distribute_dataset(self, dataset):
+        return dataset.shard(self._world, self._rank) if self._world > 1 else dataset
+
+    def barrier(self):
+        if self._world > 1:
+            dist.barrier()
+
+
+class MirroredStrategy(MultiWorkerMirroredStrategy):
+    """Single-node synchronous data parallelism.
+
+    devices=None under a multi-process launch: one replica per process (RCCL).
+    devices=[...] in one process: in-process replicas over those devices."""
+
+    def __init__(self, devices=None, cross_device_ops=None, bucket_mb=None):
+        self._devices = [context.parse_device(d) for d in devices] if devices else None
+        if self._devices and len(self._devices) > 1 and not TorchrunClusterResolver.active():
+            Strategy.__init__(self)
+            self.bucket_mb = bucket_mb
+            self._rank, self._world, self._local_rank = 0, 1, 0
+            self._device = self._devices[0]
+            self.cluster_resolver = None
+            self._inproc = True
+            return
+        self._inproc = False
+        if self._devices and len(self._devices) == 1:
+            Strategy.__init__(self)
+            self.bucket_mb = bucket_mb
+            self._rank, self._world, self._local_rank = 0, 1, 0
+            self._device = self._devices[0]
+            self.cluster_resolver = None
+            return
+        if TorchrunClusterResolver.active():
+            super().__init__(TorchrunClusterResolver(), bucket_mb=bucket_mb)
+        else:
+            super().__init__(TFConfigClusterResolver(tf_config={}), bucket_mb=bucket_mb)
+
+    @property
+    def extended_devices(self):
+        return self._devices or [self._device]
+
+    @property
+    def num_replicas_in_sync(self):
+        if self._inproc:
+            return len(self._devices)
+        return self._world
+
+    # ---- in-process replica execution (used by Model.train_step when _inproc)
+    def inproc_replicas(self):
+        return self._devices if self._inproc else None
+
+    def grad_scale(self):
+        if self._inproc:
+            return 1.0 / len(self._devices)
+        return super().grad_scale()

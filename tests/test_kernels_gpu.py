@@ -41,6 +41,14 @@ def test_gemm_layouts(cuda, M, N, K, ak, bk):
     close(C, ref, 2e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(2, 1000, 2048), (3, 10, 7), (13, 24, 5)])
+def test_gemm_unaligned_padding(cuda, M, N, K):
+    A, B = rnd(M, K, dev=cuda), rnd(N, K, dev=cuda)
+    close(ops.gemm(A, B, out_dtype=torch.float32), A.float() @ B.float().t(), 2e-3)
+    close(ops.gemm(A.t().contiguous(), B.t().contiguous(), a_kouter=True, b_kouter=True, out_dtype=torch.float32),
+          A.float() @ B.float().t(), 2e-3)
+
+
 def test_gemm_asymmetric_identity(cuda):
     # A = I with asymmetric B catches a transposed C write (guide §3)
     n = 128
