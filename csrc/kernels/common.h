@@ -114,3 +114,10 @@ static inline int stream_grid(long work_items, int block) {
   if (g < 1) g = 1;
   return (int)g;
 }
+
+// Sum groups of `sg` consecutive rows of a [rows][W] f32 matrix (row stride `stride` elements).
+// Group g's sum is written either into its first row (in place, leaders at stride sg*stride) or,
+// when `out` is given (single group), into out (+= when accumulate). grid = (ceil(W/256), ngroups).
+__global__ void __launch_bounds__(256) dtf_group_rows_kernel(float* __restrict__ rows, long stride, int nrows,
+                                                             int sg, long W, float* __restrict__ out,
+                                                             int accumulate);

@@ -25,6 +25,7 @@
 //  * Fused epilogue: alpha/beta, bias, ReLU/GELU, pre-activation side output,
 //    per-column sum/sum^2 (BatchNorm statistics) and split-K f32 atomics.
 #include "common.h"
+#include <algorithm>
 #include <type_traits>
 
 namespace dtf {
@@ -61,6 +62,7 @@ struct GemmArgs {
   int act;              // 0 none, 1 relu, 2 gelu(tanh)
   int out_f32;          // C is float
   int atomic_out;       // atomicAdd into float C (split-K / accumulate)
+  long slab;            // >0: split-K partials go to slab (blockIdx.z) of this many elements (plain stores)
   ConvGeom g;
 };
 
@@ -298,7 +300,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
-  if (kbeg >= kend && a.atomic_out) return;
+  if (kbeg >= kend && a.atomic_out) return;  // (slab mode writes zeros for empty splits)
 
   const bf16_t* Ap = a.A + (long)bz * a.sA;
   const bf16_t* Bp = a.B + (long)bz * a.sB;
@@ -357,7 +359,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   }
 
   // ---- epilogue: lane owns row m = ..+(lane&15), cols n = ..+(lane>>4)*4 + r ----
-  const long cbase = (long)bz * a.sC;
+  const long cbase = a.slab > 0 ? (long)z * a.slab : (long)bz * a.sC;
   float csum[TN][4], csq[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j)
@@ -428,7 +430,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     }
   }
   if (a.stats) {
-    // reduce over the 16 rows held by lanes with equal (lane>>4), then one atomic per column
+    // Deterministic BN statistics: reduce the 16 rows of a lane group by shuffles, the WM wave rows of
+    // the tile through LDS, then write ONE partial row per M-tile: stats[tile_m][0,N) = sum,
+    // stats[tile_m][N,2N) = sum of squares (bn_finalize sums the tiles_m rows). No atomics.
+    float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
 #pragma unroll
@@ -436,15 +441,65 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
         float s = csum[j][r], q = csq[j][r];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
-        const int n = n0 + wn * WTN + j * 16 + (lane >> 4) * 4 + r;
-        if ((lane & 15) == 0 && n < a.N) {
-          atomicAdd(a.stats + n, s);
-          atomicAdd(a.stats + a.N + n, q);
+        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4 + r;
+        if ((lane & 15) == 0) {
+          red[wm * BN + nl] = s;
+          red[WM * BN + wm * BN + nl] = q;
         }
       }
     }
+    __syncthreads();
+    float* prow = a.stats + (long)tile_m * 2 * a.N;
+    for (int nl = threadIdx.x; nl < BN; nl += NT) {
+      const int n = n0 + nl;
+      if (n >= a.N) continue;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) { s += red[w * BN + nl]; q += red[WM * BN + w * BN + nl]; }
+      prow[n] = s;
+      prow[a.N + n] = q;
+    }
   }
 }
+
+}  // namespace dtf
+
+// Deterministic grouped row sums (split-K slabs, BN partial rows): see common.h.
+__global__ void __launch_bounds__(256) dtf_group_rows_kernel(float* __restrict__ rows, long stride, int nrows,
+                                                             int sg, long W, float* __restrict__ out,
+                                                             int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W) return;
+  const int r0 = blockIdx.y * sg;
+  const int r1 = min(nrows, r0 + sg);
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r) acc += rows[(long)r * stride + i];
+  if (out) out[i] = accumulate ? out[i] + acc : acc;
+  else rows[(long)r0 * stride + i] = acc;
+}
+
+// Two-level deterministic reduction of `nrows` rows into out (or into row 0 if out == nullptr).
+// Returns nothing; stream-ordered.
+DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int gx = (int)((W + 255) / 256);
+  long s = stride;
+  int n = nrows;
+  // stage 1: enough groups to fill the chip, each summing sg rows into its leader row
+  while (n > 8 && gx < 2048) {
+    int groups = (int)std::min<long>(n, std::max<long>(1, 1024 / gx));
+    int sg = std::max(8, (n + groups - 1) / groups);
+    groups = (n + sg - 1) / sg;
+    hipLaunchKernelGGL(dtf_group_rows_kernel, dim3(gx, groups), dim3(256), 0, st, rows, s, n, sg, W,
+                       (float*)nullptr, 0);
+    s *= sg;
+    n = groups;
+    if (n <= 8) break;
+  }
+  hipLaunchKernelGGL(dtf_group_rows_kernel, dim3(gx, 1), dim3(256), 0, st, rows, s, n, n, W, out, accumulate);
+}
+
+namespace dtf {
 
 // ---------------------------------------------------------------------------
 // host side
@@ -504,9 +559,10 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int P
 
 static int choose_splitk(long M, long N, long K, int tile_m, int tile_n, long batch) {
   long tiles = (long)cdiv(M, tile_m) * cdiv(N, tile_n) * batch;
-  if (tiles >= 512 || K <= 512) return 1;
-  long want = (1024 + tiles - 1) / tiles;
-  long maxs = K / 256;  // keep >= 256 of K per split
+  if (tiles >= 256 || K <= 1024) return 1;
+  long want = (512 + tiles - 1) / tiles;
+  if (want > 256) want = 256;
+  long maxs = K / 512;  // keep >= 512 of K per split
   if (want > maxs) want = maxs;
   return want < 1 ? 1 : (int)want;
 }
@@ -517,10 +573,11 @@ using namespace dtf;
 
 // Generic (batched) GEMM: C[b][m][n] = alpha * sum_k A(m,k) B(n,k) + beta*C (+bias, act)
 //   a_kouter: A stored [K][M] (ld=lda) instead of [M][K]; b_kouter: B stored [K][N] instead of [N][K].
+// stats (optional): per-M-tile partial rows [tiles_m][2N] (capacity ceil(M/64) rows); *stat_rows = tiles_m.
 DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const float* bias, float* stats,
-                     int M, int N, int K, long lda, long ldb, long ldc, int a_kouter, int b_kouter,
+                     int* stat_rows, int M, int N, int K, long lda, long ldb, long ldc, int a_kouter, int b_kouter,
                      int batch, long sA, long sB, long sC, float alpha, float beta, int act, int out_f32,
-                     int splitk, int tile, void* stream) {
+                     int splitk, int tile, float* ws, long ws_elems, void* stream) {
   if ((N & 3) || (K & 7) || M <= 0 || N <= 0) return -1;
   if (a_kouter && (M & 7)) return -2;
   if (b_kouter && (N & 7)) return -3;
@@ -534,21 +591,39 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
                                 ? choose_splitk(M, N, K, 128, 128, a.batch) : 1;
   a.splitk = splitk;
   a.kchunk = ((K + splitk - 1) / splitk + BK - 1) / BK * BK;
-  a.atomic_out = splitk > 1;
-  if (a.atomic_out) {
-    // split-K accumulates with f32 atomics: C must be dense f32 and is zeroed first when beta == 0
-    if (!out_f32 || ldc != N || (a.batch > 1 && sC != (long)M * N)) return -4;
-    if (beta == 0.f) hipMemsetAsync(C, 0, (size_t)a.batch * M * N * 4, (hipStream_t)stream);
-    else if (beta != 1.f) return -6;
+  if (splitk > 1) {
+    // split-K: per-split f32 slabs + deterministic reduce (C = alpha*AB + beta*C, beta in {0,1})
+    const long mn = (long)a.batch * M * N;
+    if (!out_f32 || ldc != N || (a.batch > 1 && sC != (long)M * N) || (beta != 0.f && beta != 1.f)) return -4;
+    if (ws == nullptr || ws_elems < 2 * mn) {
+      a.splitk = splitk = 1;
+      a.kchunk = (K + BK - 1) / BK * BK;
+    } else {
+      if ((long)splitk * mn > ws_elems) splitk = (int)(ws_elems / mn);
+      a.splitk = splitk;
+      a.kchunk = ((K + splitk - 1) / splitk + BK - 1) / BK * BK;
+      a.C = ws;
+      a.slab = (long)M * N;  // z = batch*splitk + split -> slab index
+      a.beta = 0.f;
+      dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
+      // slabs are [batch][splitk][M*N]: reduce each batch separately
+      for (int b = 0; b < a.batch; ++b)
+        dtf_sum_rows(ws + (long)b * splitk * M * N, (long)M * N, splitk, (long)M * N, (float*)C + (long)b * M * N,
+                     beta != 0.f ? 1 : 0, stream);
+      return (int)hipGetLastError();
+    }
   }
+  if (stats && (a.batch > 1 || a.splitk > 1)) return -7;
   dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
+  if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();
 }
 
 // NHWC conv forward: Y[N,P,Q,K] = X[N,H,W,C] * W[K,R,S,C] (+bias, act, BN stats of Y)
-DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int N, int H,
-                         int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh,
-                         int dw, int act, int out_f32, int tile, void* stream) {
+// stats (optional): BN partial rows [tiles_m][2K] (capacity ceil(N*P*Q/64) rows); *stat_rows = tiles_m.
+DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
+                         int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
+                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream) {
   if ((C & 7) || (K & 3)) return -1;
   GemmArgs a{};
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
@@ -559,6 +634,7 @@ DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bi
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   dispatch(a, pointwise ? OP_KCONTIG : OP_IM2COL, OP_KCONTIG, tile, (hipStream_t)stream);
+  if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();
 }
 
@@ -584,22 +660,33 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
 //   = sum_{n,p,q} dY[n,p,q,k] * X[n, p*sh-ph+r*dh, q*sw-pw+s*dw, c]
 DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int accumulate,
-                           int splitk, int tile, void* stream) {
+                           int splitk, int tile, float* ws, long ws_elems, void* stream) {
   if ((C & 7) || (K & 7)) return -1;
+  hipStream_t st = (hipStream_t)stream;
   GemmArgs a{};
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
-  a.A = (const bf16_t*)dY; a.B = (const bf16_t*)X; a.C = dW;
+  a.A = (const bf16_t*)dY; a.B = (const bf16_t*)X;
   a.M = K; a.N = R * S * C; a.K = N * P * Q;
   a.lda = K; a.ldb = C; a.ldc = (long)R * S * C;
   a.batch = 1;
   a.alpha = 1.f; a.beta = 0.f; a.act = 0; a.out_f32 = 1;
+  const long mn = (long)a.M * a.N;
   if (splitk <= 0) splitk = choose_splitk(a.M, a.N, a.K, 128, 128, 1);
+  if (ws == nullptr || ws_elems < mn * 2) splitk = 1;
+  else if ((long)splitk * mn > ws_elems) splitk = (int)(ws_elems / mn);
   if (splitk < 1) splitk = 1;
   a.splitk = splitk;
   a.kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;
-  a.atomic_out = 1;
-  if (!accumulate) hipMemsetAsync(dW, 0, (size_t)a.M * a.N * 4, (hipStream_t)stream);
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
-  dispatch(a, OP_KOUTER, pointwise ? OP_KOUTER : OP_WGRADX, tile, (hipStream_t)stream);
+  if (splitk == 1) {
+    a.C = dW;
+    a.beta = accumulate ? 1.f : 0.f;
+    dispatch(a, OP_KOUTER, pointwise ? OP_KOUTER : OP_WGRADX, tile, st);
+    return (int)hipGetLastError();
+  }
+  a.C = ws;
+  a.slab = mn;
+  dispatch(a, OP_KOUTER, pointwise ? OP_KOUTER : OP_WGRADX, tile, st);
+  dtf_sum_rows(ws, mn, splitk, mn, dW, accumulate, st);
   return (int)hipGetLastError();
 }

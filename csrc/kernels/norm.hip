@@ -8,8 +8,8 @@
 //   also updates running stats TF-style) -> bn_apply (scale/shift [+res] [+relu]).
 // Backward: bn_bwd_reduce (sum dz, sum dz*xhat with the ReLU mask applied
 //   on the fly) -> bn_bwd_finalize -> bn_bwd_apply (dx, optional dz for the
-//   residual branch). All passes are 16-B vectorized, grid-stride, one atomic
-//   per (block, channel).
+//   residual branch). All passes are 16-B vectorized and grid-stride; reductions
+//   write one partial row per block (no same-address atomics: deterministic).
 #include "common.h"
 
 namespace {
@@ -26,40 +26,78 @@ __host__ __device__ inline ColGeo colgeo(int C) {
   return g;
 }
 
-__global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
-                                                       float* __restrict__ stats) {
-  ColGeo g = colgeo(C);
+// Block-level column reduction of per-thread 8-channel partial sums -> one partial row per block.
+// s/q: this thread's sums for channels [cc*8, cc*8+8); rows of the block with equal cc are combined in LDS.
+__device__ __forceinline__ void block_col_partials(float (&s)[8], float (&q)[8], int cc0, int TPR, int RPB, int C,
+                                                   float* __restrict__ part_row, float* red) {
   const int t = threadIdx.x;
-  if (t >= g.TPR * g.RPB) return;
-  const int rsub = t / g.TPR;
-  for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
-    float s[8] = {0}, q[8] = {0};
-    for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
-      float f[8];
-      load8(x + r * C + cc * 8, f);
+  const bool act = t < TPR * RPB;
+  __syncthreads();
+  if (act) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+    for (int j = 0; j < 8; ++j) { red[t * 8 + j] = s[j]; red[2048 + t * 8 + j] = q[j]; }
+  }
+  __syncthreads();
+  for (int o = t; o < TPR * 8; o += blockDim.x) {
+    const int c = cc0 * 8 + o;
+    if (c >= C) continue;
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < RPB; ++r) {
+      a += red[(r * TPR + (o >> 3)) * 8 + (o & 7)];
+      b += red[2048 + (r * TPR + (o >> 3)) * 8 + (o & 7)];
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      atomicAdd(stats + cc * 8 + j, s[j]);
-      atomicAdd(stats + C + cc * 8 + j, q[j]);
-    }
+    part_row[c] = a;
+    part_row[C + c] = b;
   }
 }
 
-// Per-channel: mean/var from sums; scale = gamma*invstd, shift = beta - mean*scale.
+// Standalone BN statistics: partial [gridDim.x][2C] rows (no atomics; summed by bn_finalize).
+__global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
+                                                       float* __restrict__ part) {
+  __shared__ float red[4096];
+  ColGeo g = colgeo(C);
+  const int t = threadIdx.x;
+  const int rsub = t / g.TPR;
+  for (int cc0 = 0; cc0 < g.cols8; cc0 += g.TPR) {
+    const int cc = cc0 + t % g.TPR;
+    float s[8] = {0}, q[8] = {0};
+    if (t < g.TPR * g.RPB && cc < g.cols8) {
+      for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
+        float f[8];
+        load8(x + r * C + cc * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] += f[j] * f[j]; }
+      }
+    }
+    block_col_partials(s, q, cc0, g.TPR, g.RPB, C, part + (long)blockIdx.x * 2 * C, red);
+  }
+}
+
+// Per-channel: sum T partial rows, mean/var, scale = gamma*invstd, shift = beta - mean*scale.
 // Running stats follow Keras BatchNormalization: r = r*momentum + batch*(1-momentum),
 // with the unbiased variance, as TF's FusedBatchNormV3 does.
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* running_mean, float* running_var,
-                                   long M, int C, float momentum, float eps, float* __restrict__ scale,
-                                   float* __restrict__ shift, float* __restrict__ mean_out,
-                                   float* __restrict__ invstd_out) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float mean = stats[c] / (float)M;
-  float var = fmaxf(stats[C + c] / (float)M - mean * mean, 0.f);
+// grid: ceil(C/64) blocks of 256 threads (4 row-groups x 64 channels).
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int T,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, long M, int C, float momentum,
+                                                          float eps, float* __restrict__ scale,
+                                                          float* __restrict__ shift, float* __restrict__ mean_out,
+                                                          float* __restrict__ invstd_out) {
+  __shared__ float red[2][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float a = 0.f, b = 0.f;
+  if (c < C)
+    for (int r = grp; r < T; r += 4) { a += part[(long)r * 2 * C + c]; b += part[(long)r * 2 * C + C + c]; }
+  red[0][grp][cl] = a;
+  red[1][grp][cl] = b;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  a = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  b = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  float mean = a / (float)M;
+  float var = fmaxf(b / (float)M - mean * mean, 0.f);
   float inv = rsqrtf(var + eps);
   float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
   scale[c] = gm * inv;
@@ -109,59 +147,70 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// Backward reduce: dz = dy * (y > 0 if relu-mask given); sums: [0,C) sum dz, [C,2C) sum dz*xhat
+// Backward reduce: dz = dy * (y > 0 if relu-mask given); partial rows [gridDim.x][2C]:
+// [0,C) sum dz, [C,2C) sum dz*xhat. No atomics; bn_bwd_finalize sums the rows.
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
                                                             const bf16_t* __restrict__ ymask,
                                                             const bf16_t* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long M, int C,
-                                                            float* __restrict__ sums) {
+                                                            float* __restrict__ part) {
+  __shared__ float red[4096];
   ColGeo g = colgeo(C);
   const int t = threadIdx.x;
-  if (t >= g.TPR * g.RPB) return;
   const int rsub = t / g.TPR;
-  for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
-    float mu[8], is[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { mu[j] = mean[cc * 8 + j]; is[j] = invstd[cc * 8 + j]; }
+  for (int cc0 = 0; cc0 < g.cols8; cc0 += g.TPR) {
+    const int cc = cc0 + t % g.TPR;
     float s[8] = {0}, q[8] = {0};
-    for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
-      float d[8], xv[8];
-      load8(dy + r * C + cc * 8, d);
-      load8(x + r * C + cc * 8, xv);
-      if (ymask) {
-        uint4 mv = *reinterpret_cast<const uint4*>(ymask + r * C + cc * 8);
-        uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+    if (t < g.TPR * g.RPB && cc < g.cols8) {
+      float mu[8], is[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          // bf16 > 0  <=>  sign bit clear and value bits non-zero
-          uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
-          if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
-          if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
+      for (int j = 0; j < 8; ++j) { mu[j] = mean[cc * 8 + j]; is[j] = invstd[cc * 8 + j]; }
+      for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
+        float d[8], xv[8];
+        load8(dy + r * C + cc * 8, d);
+        load8(x + r * C + cc * 8, xv);
+        if (ymask) {
+          uint4 mv = *reinterpret_cast<const uint4*>(ymask + r * C + cc * 8);
+          uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            // bf16 > 0  <=>  sign bit clear and value bits non-zero
+            uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+            if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
+            if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += d[j];
+          q[j] += d[j] * (xv[j] - mu[j]) * is[j];
         }
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s[j] += d[j];
-        q[j] += d[j] * (xv[j] - mu[j]) * is[j];
-      }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      atomicAdd(sums + cc * 8 + j, s[j]);
-      atomicAdd(sums + C + cc * 8 + j, q[j]);
-    }
+    block_col_partials(s, q, cc0, g.TPR, g.RPB, C, part + (long)blockIdx.x * 2 * C, red);
   }
 }
 
-// dgamma = sum dz*xhat, dbeta = sum dz; coefficients for the apply pass:
+// Sum T partial rows; dgamma = sum dz*xhat, dbeta = sum dz; coefficients for the apply pass:
 //   dx = k1 * (dz - k2 - xhat * k3)   with k1 = gamma*invstd, k2 = sum_dz/M, k3 = sum_dzxhat/M
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ gamma,
-                                       const float* __restrict__ invstd, long M, int C, float* dgamma,
-                                       float* dbeta, int accumulate, float* __restrict__ coef) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float sdz = sums[c], sdx = sums[C + c];
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int T,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ invstd, long M, int C,
+                                                              float* dgamma, float* dbeta, int accumulate,
+                                                              float* __restrict__ coef) {
+  __shared__ float red[2][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float a = 0.f, b = 0.f;
+  if (c < C)
+    for (int r = grp; r < T; r += 4) { a += part[(long)r * 2 * C + c]; b += part[(long)r * 2 * C + C + c]; }
+  red[0][grp][cl] = a;
+  red[1][grp][cl] = b;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  float sdz = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  float sdx = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + sdx;
   if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + sdz;
   float gm = gamma ? gamma[c] : 1.f;
@@ -297,24 +346,32 @@ int red_grid(long M, int C) {
   long rows_per_thread = 32;
   long blocks = (M + (long)g.RPB * rows_per_thread - 1) / ((long)g.RPB * rows_per_thread);
   if (blocks > 1024) blocks = 1024;
+  if (blocks < 256 && M >= 256L * g.RPB) blocks = 256;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
 }
 
 }  // namespace
 
-DTF_API int dtf_bn_stats(const void* x, long M, int C, float* stats, int zero, void* stream) {
+// Statistics of x: writes G partial rows into `part` (capacity >= 1024*2*C floats), returns G via *rows.
+DTF_API int dtf_bn_stats(const void* x, long M, int C, float* part, int* rows, void* stream) {
   if (C & 7) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  if (zero) (void)hipMemsetAsync(stats, 0, sizeof(float) * 2 * C, st);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(red_grid(M, C)), dim3(256), 0, st, (const bf16_t*)x, M, C, stats);
+  int G = red_grid(M, C);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(G), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, M, C, part);
+  *rows = G;
   return (int)hipGetLastError();
 }
 
-DTF_API int dtf_bn_finalize(const float* stats, const float* gamma, const float* beta, float* running_mean,
+DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream);
+
+DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float* beta, float* running_mean,
                             float* running_var, long M, int C, float momentum, float eps, float* scale,
                             float* shift, float* mean_out, float* invstd_out, void* stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, gamma, beta,
+  if (T > 1) {  // collapse the T partial rows in parallel (deterministic), then finalize one row
+    dtf_sum_rows(part, 2L * C, T, 2L * C, nullptr, 0, stream);
+    T = 1;
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, T, gamma, beta,
                      running_mean, running_var, M, C, momentum, eps, scale, shift, mean_out, invstd_out);
   return (int)hipGetLastError();
 }
@@ -335,17 +392,19 @@ DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, 
   return (int)hipGetLastError();
 }
 
+// work: (2*1024 + 3) * C floats (partials + coefficients)
 DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* x, const float* mean, const float* invstd,
                        const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma, float* dbeta,
-                       int accumulate, float* work /* 5*C floats */, void* stream) {
+                       int accumulate, float* work, void* stream) {
   if (C & 7) return -1;
   hipStream_t st = (hipStream_t)stream;
-  float* sums = work;
-  float* coef = work + 2 * C;
-  (void)hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, st);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(red_grid(M, C)), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)ymask, (const bf16_t*)x, mean, invstd, M, C, sums);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, gamma, invstd, M, C,
+  float* coef = work;
+  float* part = work + 3 * C;
+  int G = red_grid(M, C);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
+                     (const bf16_t*)x, mean, invstd, M, C, part);
+  dtf_sum_rows(part, 2L * C, G, 2L * C, nullptr, 0, stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, 1, gamma, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);
   long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)dy,

@@ -16,6 +16,33 @@ def ptr(t):
     return t.data_ptr()
 
 
+class IntOut:
+    """A C int the native side can write (passed as its address)."""
+
+    def __init__(self):
+        import ctypes
+        self._v = ctypes.c_int(0)
+        self.addr = ctypes.addressof(self._v)
+
+    @property
+    def value(self):
+        return self._v.value
+
+
+_WS = {}
+WS_ELEMS = 32 << 20  # 128 MiB of f32 split-K slabs per device
+
+
+def workspace(device, nelem=WS_ELEMS):
+    """Persistent per-device f32 scratch (split-K slabs). Stream-ordered reuse only."""
+    key = (device.type, device.index)
+    w = _WS.get(key)
+    if w is None or w.numel() < nelem:
+        w = torch.empty(nelem, dtype=torch.float32, device=device)
+        _WS[key] = w
+    return w
+
+
 def stream():
     return torch.cuda.current_stream().cuda_stream
 

@@ -3,14 +3,15 @@
 Activations are channels-last ``[N, H, W, C]`` bf16; filters are stored KRSC
 (``[out, kh, kw, in]``) as f32 master variables with a bf16 compute shadow.
 The training-mode BatchNorm statistics are produced by the conv epilogue
-(per-column sum / sum^2 f32 atomics) so the forward BN costs one apply pass
+(per-M-tile partial sum / sum^2 rows, reduced deterministically by bn_finalize)
+so the forward BN costs one apply pass
 instead of three (SURVEY §2.4.b K4/K5, §7.4 hard part 1).
 """
 from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, bf16_shadow, call, crsk_shadow, on_gpu, ptr, stream
+from ._util import BF16, F32, IntOut, bf16_shadow, call, crsk_shadow, on_gpu, ptr, stream, workspace
 
 
 def out_size(h, k, s, p, d=1):
@@ -36,11 +37,18 @@ def _geom(x, w, stride, pad, dil):
     return N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw
 
 
-def conv_fwd_raw(x, w16, g, stats=None, bias=None, act=0):
+def conv_fwd_raw(x, w16, g, stats=False, bias=None, act=0):
+    """Returns y, or (y, partials, rows) when stats: BN partial sums, one [2K] row per M-tile."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     y = torch.empty((N, P, Q, K), dtype=BF16, device=x.device)
-    call("dtf_conv_fwd", ptr(x), ptr(w16), ptr(y), ptr(bias), ptr(stats), N, H, W, C, K, R, S, P, Q, sh, sw, ph,
-         pw, dh, dw, int(act), 0, -1, stream())
+    part = rows = None
+    if stats:
+        part = torch.empty(((N * P * Q + 63) // 64) * 2 * K, dtype=F32, device=x.device)
+        rows = IntOut()
+    call("dtf_conv_fwd", ptr(x), ptr(w16), ptr(y), ptr(bias), ptr(part), rows.addr if rows else None, N, H, W, C,
+         K, R, S, P, Q, sh, sw, ph, pw, dh, dw, int(act), 0, -1, stream())
+    if stats:
+        return y, part, rows.value
     return y
 
 
@@ -56,8 +64,9 @@ def conv_dgrad_raw(dy, w_master, g):
 def conv_wgrad_raw(x, dy, g):
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     dw_ = torch.empty((K, R, S, C), dtype=F32, device=x.device)
+    ws = workspace(x.device)
     call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw_), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0, -1,
-         stream())
+         ptr(ws), ws.numel(), stream())
     return dw_
 
 
@@ -117,14 +126,12 @@ class _ConvBNFn(torch.autograd.Function):
         N, H, W, C, K, R, S, P, Q = g[:9]
         M = N * P * Q
         dev = x.device
-        work = torch.empty(6 * K, dtype=F32, device=dev)  # stats(2K) scale shift mean invstd
-        stats, scale, shift, mean, invstd = work[:2 * K], work[2 * K:3 * K], work[3 * K:4 * K], work[4 * K:5 * K], \
-            work[5 * K:]
+        work = torch.empty(4 * K, dtype=F32, device=dev)  # scale shift mean invstd
+        scale, shift, mean, invstd = work[:K], work[K:2 * K], work[2 * K:3 * K], work[3 * K:]
         if training:
-            stats.zero_()
-            yc = conv_fwd_raw(x, bf16_shadow(w), g, stats=stats)
-            call("dtf_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, K, float(momentum),
-                 float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
+            yc, part, rows = conv_fwd_raw(x, bf16_shadow(w), g, stats=True)
+            call("dtf_bn_finalize", ptr(part), rows, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, K,
+                 float(momentum), float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
         else:
             yc = conv_fwd_raw(x, bf16_shadow(w), g)
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
@@ -151,7 +158,7 @@ class _ConvBNFn(torch.autograd.Function):
         dres = torch.empty_like(yc) if (ctx.has_res and ctx.relu) else None
         dgamma = torch.empty(K, dtype=F32, device=yc.device)
         dbeta = torch.empty(K, dtype=F32, device=yc.device)
-        work = torch.empty(5 * K, dtype=F32, device=yc.device)
+        work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
         call("dtf_bn_bwd", ptr(dout), ptr(out), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K, ptr(dyc),
              ptr(dres), ptr(dgamma), ptr(dbeta), 0, ptr(work), stream())
         if ctx.has_res and not ctx.relu:

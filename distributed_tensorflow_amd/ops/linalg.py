@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, bf16_shadow, call, on_gpu, ptr, stream
+from ._util import BF16, F32, IntOut, bf16_shadow, call, on_gpu, ptr, stream, workspace
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 _ACTS = {None: 0, "linear": 0, "relu": 1, "gelu": 2}
@@ -68,9 +68,17 @@ def gemm(a, b, *, a_kouter=False, b_kouter=False, out=None, out_dtype=BF16, bias
     sA = a.stride(0) if batched else 0
     sB = b.stride(0) if batched else 0
     sC = out.stride(0) if batched else 0
-    call("dtf_gemm", ptr(a), ptr(b), ptr(out), ptr(aux), ptr(bias), ptr(stats), M, N, K, lda, ldb, ldc,
-         int(a_kouter), int(b_kouter), bt, sA, sB, sC, float(alpha), float(beta), int(act),
-         int(out.dtype == F32), int(splitk), int(tile), stream())
+    part = rows = None
+    ws = workspace(a.device) if out.dtype == F32 else None
+    if stats is not None:  # kernel writes per-M-tile partial rows; reduce them here
+        part = torch.empty(((M + 63) // 64) * 2 * N, dtype=F32, device=a.device)
+        rows = IntOut()
+        splitk = 1
+    call("dtf_gemm", ptr(a), ptr(b), ptr(out), ptr(aux), ptr(bias), ptr(part), rows.addr if rows else None, M, N, K,
+         lda, ldb, ldc, int(a_kouter), int(b_kouter), bt, sA, sB, sC, float(alpha), float(beta), int(act),
+         int(out.dtype == F32), int(splitk), int(tile), ptr(ws), ws.numel() if ws is not None else 0, stream())
+    if stats is not None:
+        stats += part[:rows.value * 2 * N].view(rows.value, 2 * N).sum(0)
     return out
 
 

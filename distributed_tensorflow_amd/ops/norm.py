@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, call, on_gpu, ptr, stream
+from ._util import BF16, F32, IntOut, call, on_gpu, ptr, stream
 
 
 def batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training):
@@ -34,13 +34,14 @@ class _BNFn(torch.autograd.Function):
         x = x.contiguous()
         C = x.shape[-1]
         M = x.numel() // C
-        work = torch.empty(6 * C, dtype=F32, device=x.device)
-        stats, scale, shift, mean, invstd = work[:2 * C], work[2 * C:3 * C], work[3 * C:4 * C], work[4 * C:5 * C], \
-            work[5 * C:]
+        work = torch.empty(4 * C, dtype=F32, device=x.device)
+        scale, shift, mean, invstd = work[:C], work[C:2 * C], work[2 * C:3 * C], work[3 * C:]
         if training:
-            call("dtf_bn_stats", ptr(x), M, C, ptr(stats), 1, stream())
-            call("dtf_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, C, float(momentum),
-                 float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
+            part = torch.empty(1024 * 2 * C, dtype=F32, device=x.device)
+            rows = IntOut()
+            call("dtf_bn_stats", ptr(x), M, C, ptr(part), rows.addr, stream())
+            call("dtf_bn_finalize", ptr(part), rows.value, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, C,
+                 float(momentum), float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
         else:
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), C, float(eps), ptr(scale),
                  ptr(shift), stream())
@@ -63,7 +64,7 @@ class _BNFn(torch.autograd.Function):
         dres = torch.empty_like(x) if (ctx.has_res and ctx.relu) else None
         dgamma = torch.empty(C, dtype=F32, device=x.device)
         dbeta = torch.empty(C, dtype=F32, device=x.device)
-        work = torch.empty(5 * C, dtype=F32, device=x.device)
+        work = torch.empty((2 * 1024 + 3) * C, dtype=F32, device=x.device)
         call("dtf_bn_bwd", ptr(dout), ptr(out), ptr(x), ptr(mean), ptr(invstd), ptr(gamma), M, C, ptr(dx), ptr(dres),
              ptr(dgamma), ptr(dbeta), 0, ptr(work), stream())
         if ctx.has_res and not ctx.relu:
