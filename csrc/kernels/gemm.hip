@@ -472,10 +472,30 @@ __global__ void __launch_bounds__(256) dtf_group_rows_kernel(float* __restrict__
   if (i >= W) return;
   const int r0 = blockIdx.y * sg;
   const int r1 = min(nrows, r0 + sg);
-  float acc = 0.f;
-  for (int r = r0; r < r1; ++r) acc += rows[(long)r * stride + i];
+  float a8[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // independent chains: the loads stay in flight
+  int r = r0;
+  for (; r + 8 <= r1; r += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a8[u] += rows[(long)(r + u) * stride + i];
+  }
+  for (; r < r1; ++r) a8[0] += rows[(long)r * stride + i];
+  const float acc = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
   if (out) out[i] = accumulate ? out[i] + acc : acc;
   else rows[(long)r0 * stride + i] = acc;
+}
+
+// One launch: sum groups of rows into leader rows so that <= target leaders remain; returns their count
+// and (via out_stride) their row stride.
+DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int target, long* out_stride,
+                                void* stream) {
+  *out_stride = stride;
+  if (nrows <= target) return nrows;
+  const int sg = (nrows + target - 1) / target;
+  const int groups = (nrows + sg - 1) / sg;
+  hipLaunchKernelGGL(dtf_group_rows_kernel, dim3((unsigned)((W + 255) / 256), groups), dim3(256), 0,
+                     (hipStream_t)stream, rows, stride, nrows, sg, W, (float*)nullptr, 0);
+  *out_stride = stride * sg;
+  return groups;
 }
 
 // Two-level deterministic reduction of `nrows` rows into out (or into row 0 if out == nullptr).

@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
 // Running stats follow Keras BatchNormalization: r = r*momentum + batch*(1-momentum),
 // with the unbiased variance, as TF's FusedBatchNormV3 does.
 // grid: ceil(C/64) blocks of 256 threads (4 row-groups x 64 channels).
-__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int T,
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int T, long rs,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
                                                           float* running_var, long M, int C, float momentum,
@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   const int c = blockIdx.x * 64 + cl;
   float a = 0.f, b = 0.f;
   if (c < C)
-    for (int r = grp; r < T; r += 4) { a += part[(long)r * 2 * C + c]; b += part[(long)r * 2 * C + C + c]; }
+    for (int r = grp; r < T; r += 4) { a += part[(long)r * rs + c]; b += part[(long)r * rs + C + c]; }
   red[0][grp][cl] = a;
   red[1][grp][cl] = b;
   __syncthreads();
@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
 
 // Sum T partial rows; dgamma = sum dz*xhat, dbeta = sum dz; coefficients for the apply pass:
 //   dx = k1 * (dz - k2 - xhat * k3)   with k1 = gamma*invstd, k2 = sum_dz/M, k3 = sum_dzxhat/M
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int T,
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int T, long rs,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ invstd, long M, int C,
                                                               float* dgamma, float* dbeta, int accumulate,
@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   const int c = blockIdx.x * 64 + cl;
   float a = 0.f, b = 0.f;
   if (c < C)
-    for (int r = grp; r < T; r += 4) { a += part[(long)r * 2 * C + c]; b += part[(long)r * 2 * C + C + c]; }
+    for (int r = grp; r < T; r += 4) { a += part[(long)r * rs + c]; b += part[(long)r * rs + C + c]; }
   red[0][grp][cl] = a;
   red[1][grp][cl] = b;
   __syncthreads();
@@ -363,15 +363,16 @@ DTF_API int dtf_bn_stats(const void* x, long M, int C, float* part, int* rows, v
 }
 
 DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream);
+DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int target, long* out_stride,
+                                void* stream);
 
 DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float* beta, float* running_mean,
                             float* running_var, long M, int C, float momentum, float eps, float* scale,
                             float* shift, float* mean_out, float* invstd_out, void* stream) {
-  if (T > 1) {  // collapse the T partial rows in parallel (deterministic), then finalize one row
-    dtf_sum_rows(part, 2L * C, T, 2L * C, nullptr, 0, stream);
-    T = 1;
-  }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, T, gamma, beta,
+  long rs = 2L * C;
+  T = dtf_group_rows_once(part, rs, T, 2L * C, 32, &rs, stream);  // <= 32 leader rows, one launch
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, T, rs, gamma,
+                     beta,
                      running_mean, running_var, M, C, momentum, eps, scale, shift, mean_out, invstd_out);
   return (int)hipGetLastError();
 }
@@ -403,8 +404,9 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* x, const f
   int G = red_grid(M, C);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
                      (const bf16_t*)x, mean, invstd, M, C, part);
-  dtf_sum_rows(part, 2L * C, G, 2L * C, nullptr, 0, stream);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, 1, gamma, invstd, M, C,
+  long rs = 2L * C;
+  int T = dtf_group_rows_once(part, rs, G, 2L * C, 32, &rs, stream);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);
   long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)dy,
