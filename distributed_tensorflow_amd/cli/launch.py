@@ -1,0 +1,113 @@
+"""Local cluster launcher: the reference runbook (README.md:9-27) as one command.
+
+    python -m distributed_tensorflow_amd.cli.launch --ps 1 --workers 1 --chief 1 \
+        [--gpus 0,1,...] -- python -m distributed_tensorflow_amd.cli.train --optimizer=adam
+
+Every task gets its own process, a free 127.0.0.1 port and a ``TF_CONFIG`` naming the whole
+cluster (chief job ``master``, like the reference). With ``--gpus`` the chief/worker tasks get
+one GPU each through ``HIP_VISIBLE_DEVICES`` (PS tasks too when ``--ps_gpus``), otherwise
+``HIP_VISIBLE_DEVICES=''`` (the README runs everything on CPU). Exit code: the first non-zero
+task exit code, else 0. Output lines are prefixed with the task name.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import threading
+
+
+def free_ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def make_cluster(num_ps, num_workers, num_chief, chief_job="master"):
+    ports = free_ports(num_ps + num_workers + num_chief)
+    it = iter(ports)
+    cluster = {}
+    if num_ps:
+        cluster["ps"] = [f"127.0.0.1:{next(it)}" for _ in range(num_ps)]
+    if num_workers:
+        cluster["worker"] = [f"127.0.0.1:{next(it)}" for _ in range(num_workers)]
+    if num_chief:
+        cluster[chief_job] = [f"127.0.0.1:{next(it)}" for _ in range(num_chief)]
+    return cluster
+
+
+def _pump(prefix, stream, out):
+    for line in iter(stream.readline, b""):
+        out.write(f"[{prefix}] {line.decode(errors='replace')}")
+        out.flush()
+
+
+def launch(cmd, num_ps=1, num_workers=1, num_chief=1, gpus=None, ps_gpus=False, chief_job="master", env=None,
+           timeout=None, log=sys.stdout):
+    cluster = make_cluster(num_ps, num_workers, num_chief, chief_job)
+    tasks = [("ps", i) for i in range(num_ps)] + [(chief_job, i) for i in range(num_chief)] + \
+            [("worker", i) for i in range(num_workers)]
+    gpu_list = [g for g in (gpus.split(",") if gpus else []) if g != ""]
+    procs = []
+    gi = 0
+    for t, i in tasks:
+        e = dict(os.environ, **(env or {}))
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
+        e["TF_CONFIG"] = json.dumps({"cluster": cluster, "task": {"type": t, "index": i}})
+        e["DTF_ROLE"] = f"{t}{i}"
+        if gpu_list and (t != "ps" or ps_gpus):
+            e["HIP_VISIBLE_DEVICES"] = gpu_list[gi % len(gpu_list)]
+            gi += 1
+        else:
+            e["HIP_VISIBLE_DEVICES"] = ""
+            e["CUDA_VISIBLE_DEVICES"] = ""
+        p = subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        th = threading.Thread(target=_pump, args=(f"{t}{i}", p.stdout, log), daemon=True)
+        th.start()
+        procs.append((t, i, p, th))
+    rc = 0
+    try:
+        for t, i, p, th in procs:
+            r = p.wait(timeout=timeout)
+            th.join(timeout=5)
+            if r != 0 and rc == 0:
+                rc = r
+    except subprocess.TimeoutExpired:
+        rc = 124
+    finally:
+        for t, i, p, th in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc, cluster
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser("dtf-launch")
+    ap.add_argument("--ps", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--chief", type=int, default=1)
+    ap.add_argument("--chief_job", default="master")
+    ap.add_argument("--gpus", default=None)
+    ap.add_argument("--ps_gpus", action="store_true")
+    ap.add_argument("--timeout", type=float, default=None)
+    ap.add_argument("cmd", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
+    if not cmd:
+        cmd = [sys.executable, "-m", "distributed_tensorflow_amd.cli.train"]
+    rc, _ = launch(cmd, a.ps, a.workers, a.chief, a.gpus, a.ps_gpus, a.chief_job, timeout=a.timeout)
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

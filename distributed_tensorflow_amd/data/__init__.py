@@ -239,9 +239,9 @@ def _stack(items):
 # ---------------------------------------------------------------- synthetic data
 def reference_linear_data(seed=None, n=100):
     """The reference's regression data: x = linspace(-1,1,100), y = 2x + 10 + 0.33 N(0,1)."""
-    rng = np.random.default_rng(seed) if seed is not None else np.random
+    rng = np.random.RandomState(seed) if seed is not None else np.random
     x = np.linspace(-1, 1, n)
-    y = 2 * x + rng.standard_normal(x.shape) * 0.33 + 10
+    y = 2 * x + rng.randn(*x.shape) * 0.33 + 10
     return x.astype(np.float32), y.astype(np.float32)
 
 

@@ -40,6 +40,11 @@ def _pair(v):
 class Layer:
     """Base layer: weight creation, sublayer tracking, lazy build on first call."""
 
+    def __new__(cls, *args, **kwargs):
+        obj = super().__new__(cls)
+        object.__setattr__(obj, "_init_args", (args, dict(kwargs)))  # for SavedModel re-construction
+        return obj
+
     def __init__(self, name=None, trainable=True, dtype=None, **kwargs):
         object.__setattr__(self, "_layers", [])
         object.__setattr__(self, "_own_weights", [])
@@ -150,6 +155,7 @@ class Layer:
             with context.device(context.current_device()):
                 self.build(shape)
             self.built = True
+            object.__setattr__(self, "_build_input_shape", shape)
         return self.call(inputs, *args, **kwargs)
 
     def get_config(self):

@@ -149,8 +149,7 @@ class Model(Layer):
         loss = self.compute_loss(x, y, y_pred, sw)
         arena = self._ensure_arena()
         strat.backward(loss, arena)
-        self.optimizer.set_grad_scale(strat.grad_scale())
-        self.optimizer.apply_arena(arena, zero_grad=True)
+        strat.apply_gradients(self.optimizer, arena)
         return self._update_metrics(loss, y, y_pred)
 
     def _update_metrics(self, loss, y, y_pred):

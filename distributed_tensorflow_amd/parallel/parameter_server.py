@@ -1,0 +1,425 @@
+"""ParameterServerStrategy: asynchronous between-graph data parallelism with variables on PS tasks.
+
+This is the reference's only parallelism mode (reference trainer/task.py:111-142, 232-236):
+TF_CONFIG names ``ps`` / ``worker`` / ``master`` tasks; ``replica_device_setter`` places every
+variable round-robin on the PS tasks; every worker runs its own training loop, pulling the
+variables and pushing gradients each step with no synchronisation between workers (async SGD);
+the optimizer's apply ops run on the PS.
+
+MI355X-first realisation:
+  * each PS task owns a contiguous f32 shard arena in its GPU's HBM (CPU if no GPU) plus optimizer
+    slot arenas, and applies every pushed gradient with ONE fused optimizer launch over the shard;
+  * the data plane is the native transport (csrc/runtime/ps_transport.cc): one PULL and one PUSH
+    per PS per step, packed buffers (the per-variable RPCs of TF's Send/Recv become one message);
+  * the control plane is the native KV store hosted by the chief: variable spec publication,
+    chief-initialises / others-wait readiness (Supervisor semantics), the async ``global_step``
+    counter, and the auto-stop done counter (reference auto_stop_ps/task.py:127-150) — PS tasks
+    exit once every trainer has reported done. The chief reports done only AFTER it has pulled
+    the final variables and exported (fixes the reference's export race).
+Partitioners: ``round_robin`` (replica_device_setter order, reference behaviour) or
+``balanced`` (greedy by size, like TF's min-size partitioning).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import threading
+import time
+
+import numpy as np
+import torch
+
+from .. import _native, context
+from .._runtime_sigs import err
+from ..variables import ParamArena, Variable
+from .cluster_resolver import TFConfigClusterResolver
+from .kv import KVClient, KVServer
+from .strategy import Strategy
+
+ASSIGN = 1
+GRAD = 0
+
+
+def _host_port(addr):
+    h, p = addr.rsplit(":", 1)
+    return (h if h not in ("", "localhost") else "127.0.0.1"), int(p)
+
+
+def kv_address(resolver):
+    tasks = resolver.trainer_tasks()
+    if not tasks:
+        raise ValueError("cluster has no chief/worker task to host the coordination service")
+    return _host_port(resolver.cluster.task_address(*tasks[0]))
+
+
+def partition(sizes, num_ps, mode="round_robin"):
+    """Variable index -> PS index."""
+    if num_ps <= 0:
+        raise ValueError("no ps tasks")
+    if mode == "round_robin":
+        return [i % num_ps for i in range(len(sizes))]
+    if mode == "balanced":
+        load = [0] * num_ps
+        out = [0] * len(sizes)
+        for i in sorted(range(len(sizes)), key=lambda i: -sizes[i]):
+            p = min(range(num_ps), key=lambda j: load[j])
+            out[i] = p
+            load[p] += sizes[i]
+        return out
+    raise ValueError(mode)
+
+
+class PSClient:
+    def __init__(self, host, port, timeout_s=600):
+        self.lib = _native.runtime()
+        self.h = self.lib.dtfrt_ps_connect(host.encode(), int(port), int(timeout_s * 1000))
+        if not self.h:
+            raise ConnectionError(err(self.lib))
+        self._ver = ctypes.c_uint64()
+
+    def pull(self, var, host_tensor):
+        rc = self.lib.dtfrt_ps_pull(self.h, var, 0, host_tensor.data_ptr(), host_tensor.numel() * 4,
+                                    ctypes.addressof(self._ver))
+        if rc:
+            raise ConnectionError(err(self.lib))
+        return self._ver.value
+
+    def push(self, var, host_tensor):
+        rc = self.lib.dtfrt_ps_push(self.h, var, 0, host_tensor.data_ptr(), host_tensor.numel() * 4,
+                                    ctypes.addressof(self._ver))
+        if rc:
+            raise ConnectionError(err(self.lib))
+        return self._ver.value
+
+    def close(self):
+        if self.h:
+            self.lib.dtfrt_ps_close(self.h)
+            self.h = None
+
+
+# ---------------------------------------------------------------------------- PS task
+class ParameterServer:
+    """The PS task's daemon: serves pulls from a host mirror, applies pushed gradients in HBM."""
+
+    def __init__(self, resolver=None, device=None, kv_timeout_s=900, slot_sync_every=50):
+        self.r = resolver or TFConfigClusterResolver()
+        if not self.r.is_ps:
+            raise ValueError("ParameterServer must run in a 'ps' task")
+        self.index = self.r.task_id
+        self.num_ps = self.r.cluster.num_tasks("ps")
+        self.num_trainers = len(self.r.trainer_tasks())
+        host, port = _host_port(self.r.cluster.task_address("ps", self.index))
+        self.lib = _native.runtime()
+        bound = ctypes.c_int()
+        self.srv = self.lib.dtfrt_ps_server_start(b"0.0.0.0", port, ctypes.addressof(bound))
+        if not self.srv:
+            raise OSError(err(self.lib))
+        self.port = bound.value
+        self.device = context.parse_device(device) if device is not None else context.default_device()
+        kh, kp = kv_address(self.r)
+        self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
+        self.slot_sync_every = slot_sync_every
+        self.applies = 0
+
+    def _build(self):
+        spec = self.kv.get_json("ps/spec")
+        mine = [v for v in spec["vars"] if v["ps"] == self.index]
+        self.names = [v["name"] for v in mine]
+        with context.device(self.device):
+            self.vars = [Variable(torch.zeros(v["shape"], dtype=torch.float32), name=v["name"],
+                                  device=self.device) for v in mine]
+        from ..keras import optimizers as O
+        oc = spec["optimizer"]
+        self.opt = O.Optimizer.__new__(O.Optimizer)
+        O.Optimizer.__init__(self.opt, oc["learning_rate"], name=oc.get("name"), **oc["hyper"])
+        self.opt.kind = oc["kind"]
+        self.numel = sum(int(np.prod(v["shape"])) if v["shape"] else 1 for v in mine)
+        if not self.vars:
+            self.arena = None
+            self.mirror = torch.zeros(1, dtype=torch.float32)
+            self.pidx = None
+        else:
+            self.arena = ParamArena(self.vars, device=self.device, with_bf16=False)
+            self.opt.build(self.vars)
+            self.arena = self.opt.arena_for(self.vars)
+            idx = []
+            for v, o in zip(self.arena.variables, self.arena.offsets):
+                idx.append(torch.arange(o, o + v.numel()))
+            self.pidx = torch.cat(idx).to(self.device)
+            self.mirror = torch.zeros(self.numel, dtype=torch.float32)
+            if torch.cuda.is_available() and self.device.type == "cuda":
+                self.mirror = self.mirror.pin_memory()
+        nb = self.mirror.numel() * 4
+        self.lib.dtfrt_ps_register(self.srv, GRAD, self.mirror.data_ptr(), nb)
+        self.lib.dtfrt_ps_register(self.srv, ASSIGN, self.mirror.data_ptr(), nb)
+        # slot mirrors: var ids 2.. (refreshed every slot_sync_every applies and at exit)
+        self.slot_mirrors = []
+        if self.arena is not None:
+            for k, (nm, _) in enumerate(self.opt.slot_specs()):
+                m = torch.zeros(self.numel, dtype=torch.float32)
+                self.slot_mirrors.append((nm, m))
+                self.lib.dtfrt_ps_register(self.srv, 2 + k, m.data_ptr(), m.numel() * 4)
+        self.kv.set(f"ps/{self.index}/ready", "1")
+
+    def _refresh(self, var_id=GRAD, slots=False):
+        if self.arena is None:
+            return
+        tight = self.arena.flat.index_select(0, self.pidx)
+        self.lib.dtfrt_ps_lock(self.srv, GRAD)
+        self.mirror.copy_(tight)
+        self.lib.dtfrt_ps_unlock(self.srv, GRAD, 1)
+        if slots:
+            for k, (nm, m) in enumerate(self.slot_mirrors):
+                t = self.arena.slots[nm].index_select(0, self.pidx)
+                self.lib.dtfrt_ps_lock(self.srv, 2 + k)
+                m.copy_(t)
+                self.lib.dtfrt_ps_unlock(self.srv, 2 + k, 1)
+
+    def serve(self, poll_ms=100):
+        """Run until every trainer task has reported done (auto-stop PS)."""
+        self._build()
+        var_id, off, n, data = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_void_p()
+        while True:
+            tok = self.lib.dtfrt_ps_next_push(self.srv, poll_ms, ctypes.addressof(var_id), ctypes.addressof(off),
+                                              ctypes.addressof(n), ctypes.addressof(data))
+            if tok == 0:
+                if self.kv.wait_ge("done", self.num_trainers, timeout_s=0):
+                    break
+                continue
+            status = 0
+            try:
+                buf = np.frombuffer((ctypes.c_char * n.value).from_address(data.value), dtype=np.float32)
+                t = torch.from_numpy(buf.copy()).to(self.device)
+                if self.arena is not None:
+                    if var_id.value == ASSIGN:
+                        self.arena.flat.index_copy_(0, self.pidx, t)
+                        for nm, init in self.opt.slot_specs():
+                            self.arena.slots[nm].fill_(init)
+                    else:
+                        self.arena.grad.zero_()
+                        self.arena.grad.index_copy_(0, self.pidx, t)
+                        self.opt.apply_arena(self.arena, zero_grad=True)
+                        self.applies += 1
+                    self._refresh(slots=(var_id.value == ASSIGN or self.applies % self.slot_sync_every == 0))
+            except Exception as e:  # report to the pushing worker instead of dying silently
+                print(f"[ps{self.index}] apply failed: {e}", flush=True)
+                status = -7
+            self.lib.dtfrt_ps_push_done(self.srv, tok, status)
+        self._refresh(slots=True)
+        self.stop()
+
+    def stop(self):
+        if self.srv:
+            self.lib.dtfrt_ps_server_stop(self.srv)
+            self.srv = None
+        self.kv.close()
+
+
+def run_parameter_server(resolver=None, device=None):
+    """Entry point of a PS task (replaces ``server.join()`` / the auto-stop dequeue loop)."""
+    ps = ParameterServer(resolver, device)
+    ps.serve()
+    return 0
+
+
+# ---------------------------------------------------------------------------- worker side
+class ParameterServerStrategy(Strategy):
+    def __init__(self, cluster_resolver=None, variable_partitioner="round_robin", device=None, kv_timeout_s=900):
+        super().__init__()
+        self.r = cluster_resolver or TFConfigClusterResolver()
+        if self.r.standalone or self.r.cluster.num_tasks("ps") == 0:
+            raise ValueError("ParameterServerStrategy needs a TF_CONFIG cluster with ps tasks")
+        if self.r.is_ps:
+            raise ValueError("ps tasks run run_parameter_server(), not a strategy")
+        self.partitioner = variable_partitioner
+        self.num_ps = self.r.cluster.num_tasks("ps")
+        self.num_trainers = len(self.r.trainer_tasks())
+        self._device = context.parse_device(device) if device is not None else context.default_device()
+        kh, kp = kv_address(self.r)
+        self._kv_server = None
+        if self.r.is_chief:
+            self._kv_server = KVServer("0.0.0.0", kp)
+        self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
+        self._clients = None
+        self._layout = None
+        self._done = False
+
+    # ---- properties
+    @property
+    def device(self):
+        return self._device
+
+    @property
+    def is_chief(self):
+        return self.r.is_chief
+
+    @property
+    def worker_index(self):
+        return max(0, self.r.trainer_rank())
+
+    @property
+    def num_workers(self):
+        return self.num_trainers
+
+    @property
+    def num_replicas_in_sync(self):
+        return 1  # asynchronous: every worker applies its own gradients
+
+    def _connect(self):
+        if self._clients is None:
+            self._clients = [PSClient(*_host_port(self.r.cluster.task_address("ps", i))) for i in
+                             range(self.num_ps)]
+        return self._clients
+
+    # ---- setup: publish spec / initialise / wait
+    def setup_model(self, model, arena, optimizer=None):
+        self._arena = arena
+        opt = optimizer or model.optimizer
+        sizes = [v.numel() for v in arena.variables]
+        assign = partition(sizes, self.num_ps, self.partitioner)
+        spec = {"vars": [{"name": v.name, "shape": list(v.shape), "ps": p} for v, p in zip(arena.variables, assign)],
+                "optimizer": {"kind": opt.kind, "learning_rate": opt._lr_value(0), "name": opt.name,
+                              "hyper": opt.hyper},
+                "partitioner": self.partitioner}
+        dev = arena.flat.device
+        self._gidx, self._stage = [], []
+        for p in range(self.num_ps):
+            idx = [torch.arange(o, o + v.numel()) for v, o, a in zip(arena.variables, arena.offsets, assign) if a == p]
+            g = torch.cat(idx).to(dev) if idx else torch.zeros(0, dtype=torch.long, device=dev)
+            self._gidx.append(g)
+            host = torch.zeros(max(1, g.numel()), dtype=torch.float32)
+            if dev.type == "cuda":
+                host = host.pin_memory()
+            self._stage.append(host)
+        clients = self._connect()
+        if self.is_chief:
+            self.kv.set("ps/spec", json.dumps(spec))
+            for p in range(self.num_ps):
+                self.kv.get(f"ps/{p}/ready")
+            self._push_all(ASSIGN)
+            self.kv.set("ps/initialized", "1")
+        else:
+            self.kv.get("ps/initialized")  # Supervisor.wait_for_session: block until the chief initialised
+            got = self.kv.get_json("ps/spec")
+            if [v["name"] for v in got["vars"]] != [v["name"] for v in spec["vars"]]:
+                raise RuntimeError("worker model variables differ from the chief's spec")
+        self._pull_all()
+
+    def _push_all(self, kind):
+        clients = self._connect()
+        src = self._arena.flat if kind == ASSIGN else self._arena.grad
+        for p, c in enumerate(clients):
+            if self._gidx[p].numel() == 0:
+                continue
+            t = src.index_select(0, self._gidx[p])
+            self._stage[p][:t.numel()].copy_(t)
+            c.push(kind, self._stage[p][:t.numel()])
+
+    def _pull_all(self):
+        clients = self._connect()
+        for p, c in enumerate(clients):
+            n = self._gidx[p].numel()
+            if n == 0:
+                continue
+            c.pull(GRAD, self._stage[p][:n])
+            self._arena.flat.index_copy_(0, self._gidx[p], self._stage[p][:n].to(self._arena.flat.device))
+        self._arena.refresh_bf16()
+        from ..ops._util import bump_weights_epoch
+        bump_weights_epoch()
+
+    def pull_slots(self):
+        """Fetch the PS-side optimizer slots (for checkpoints): {slot_name: flat tensor in arena layout}."""
+        out = {}
+        clients = self._connect()
+        spec = self.kv.get_json("ps/spec")
+        from ..keras import optimizers as O
+        kind = spec["optimizer"]["kind"]
+        names = [n for n, _ in O._SLOTS[kind]]
+        for k, nm in enumerate(names):
+            flat = torch.zeros_like(self._arena.flat)
+            for p, c in enumerate(clients):
+                n = self._gidx[p].numel()
+                if n == 0:
+                    continue
+                buf = torch.zeros(n, dtype=torch.float32)
+                c.pull(2 + k, buf)
+                flat.index_copy_(0, self._gidx[p], buf.to(flat.device))
+            out[nm] = flat
+        return out
+
+    # ---- training-loop hooks
+    def apply_gradients(self, optimizer, arena):
+        """Async step: push this worker's gradients, the PS applies them, pull fresh values."""
+        self._push_all(GRAD)
+        arena.grad.zero_()
+        self._pull_all()
+        with torch.no_grad():
+            optimizer.iterations.add_(1)
+        self.kv.add("global_step", 1)
+
+    def global_step(self):
+        return self.kv.counter("global_step")
+
+    def pull(self):
+        self._pull_all()
+
+    def report_done(self):
+        """Signal the PS tasks that this trainer is finished (auto-stop)."""
+        if not self._done:
+            self._done = True
+            self.kv.add("done", 1)
+
+    def shutdown(self, timeout_s=600):
+        self.report_done()
+        if self.is_chief:
+            # keep the coordination service up until every trainer and the PS tasks are finished
+            self.kv.wait_ge("done", self.num_trainers, timeout_s)
+            time.sleep(0.5)
+        for c in self._clients or []:
+            c.close()
+        self.kv.close()
+        if self._kv_server is not None:
+            self._kv_server.stop()
+            self._kv_server = None
+
+
+class RemoteValue:
+    def __init__(self, fut):
+        self._fut = fut
+
+    def fetch(self):
+        return self._fut.result()
+
+    def get(self):
+        return self.fetch()
+
+
+class ClusterCoordinator:
+    """TF2 ClusterCoordinator surface. Between-graph design: each trainer process coordinates its own
+    closures (scheduled on a local worker thread); PS state is shared through the strategy."""
+
+    def __init__(self, strategy):
+        import concurrent.futures as cf
+        self.strategy = strategy
+        self._ex = cf.ThreadPoolExecutor(1)
+        self._pending = []
+
+    def schedule(self, fn, args=(), kwargs=None):
+        f = self._ex.submit(fn, *args, **(kwargs or {}))
+        self._pending.append(f)
+        return RemoteValue(f)
+
+    def join(self):
+        for f in self._pending:
+            f.result()
+        self._pending = []
+
+    def done(self):
+        return all(f.done() for f in self._pending)
+
+    def create_per_worker_dataset(self, fn):
+        return fn() if callable(fn) else fn
+
+    def fetch(self, value):
+        return value.fetch() if isinstance(value, RemoteValue) else value

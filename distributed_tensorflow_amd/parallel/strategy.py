@@ -104,6 +104,11 @@ class Strategy:
     def grad_scale(self):
         return 1.0
 
+    def apply_gradients(self, optimizer, arena):
+        """Apply the (already reduced) gradient arena: one fused optimizer launch."""
+        optimizer.set_grad_scale(self.grad_scale())
+        optimizer.apply_arena(arena, zero_grad=True)
+
     def local_batch_slice(self, n):
         """Which rows of a global batch of n rows this process consumes."""
         return slice(0, n)
