@@ -94,4 +94,6 @@ _ALIASES = {"accuracy": SparseCategoricalAccuracy, "sparse_categorical_accuracy"
 def get(identifier):
     if isinstance(identifier, Metric):
         return identifier
-    return _ALIASES[str(identifier).lower()]()
+    m = _ALIASES[str(identifier).lower()]()
+    m.name = str(identifier)  # Keras reports a metric under the string it was requested with
+    return m

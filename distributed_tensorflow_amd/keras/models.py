@@ -163,6 +163,9 @@ class Model(Layer):
 
     def _train_step_inproc(self, x, y, sw, devices):
         """In-process MirroredStrategy over several local devices."""
+        if self._arena is None and not self.built:
+            with torch.no_grad():  # build the variables before the arena is laid out
+                self(x[:1].to(devices[0]), training=False)
         arena = self._ensure_arena()
         R = len(devices)
         n = x.shape[0]

@@ -141,6 +141,36 @@ class GradientBucketer:
         self.reset()
 
 
+class ShmAllReduce:
+    """Host shared-memory all-reduce (csrc/runtime/shm_allreduce.cc) for CPU gradient arenas of
+    processes on one node: one reduce-scatter/all-gather through /dev/shm per step instead of gloo's
+    loopback TCP. Used by MultiWorkerMirroredStrategy on CPU when DTF_CPU_ALLREDUCE=shm (default)."""
+
+    def __init__(self, arena, rank, world, name):
+        from .. import _native
+        from .._runtime_sigs import err
+        self.lib = _native.runtime()
+        self.arena = arena
+        nbytes = min(arena.grad.numel() * 4, 64 << 20)
+        self.h = self.lib.dtfrt_shm_open(name.encode(), rank, world, nbytes)
+        if not self.h:
+            raise OSError(err(self.lib))
+        self.rank = rank
+
+    def install(self):
+        return self
+
+    def finalize(self):
+        g = self.arena.grad
+        if self.lib.dtfrt_shm_allreduce_f32(self.h, g.data_ptr(), g.numel()) != 0:
+            raise RuntimeError("shared-memory all-reduce timed out")
+
+    def close(self):
+        if self.h:
+            self.lib.dtfrt_shm_close(self.h, int(self.rank == 0))
+            self.h = None
+
+
 def broadcast_tensors(tensors, src=0, group=None):
     for t in tensors:
         dist.broadcast(t, src=src, group=group)

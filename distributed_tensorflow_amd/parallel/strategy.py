@@ -220,7 +220,17 @@ class MultiWorkerMirroredStrategy(Strategy):
         arena.refresh_bf16()
         from ..ops._util import bump_weights_epoch
         bump_weights_epoch()
-        b = collective.GradientBucketer(arena, bucket_mb=self.bucket_mb).install()
+        if arena.grad.device.type == "cpu" and os.environ.get("DTF_CPU_ALLREDUCE", "shm") == "shm":
+            # one node, CPU arenas: shared-memory reduce-scatter/all-gather instead of gloo TCP
+            name = f"ar{os.environ.get('MASTER_PORT', '0')}_{len(self._bucketers)}"
+            if dist.get_rank() == 0:
+                import secrets
+                name += "_" + secrets.token_hex(4)
+            obj = [name]
+            dist.broadcast_object_list(obj, src=0)
+            b = collective.ShmAllReduce(arena, self._rank, self._world, obj[0])
+        else:
+            b = collective.GradientBucketer(arena, bucket_mb=self.bucket_mb).install()
         self._bucketers[id(arena)] = b
 
     def backward(self, loss, arena):

@@ -1,0 +1,148 @@
+"""Distributed training on CPU: MultiWorkerMirroredStrategy over 2 processes (shared-memory and gloo
+all-reduce), the in-process MirroredStrategy(CPU:0, CPU:1) plumbing config of BASELINE.json, the
+gradient bucketer, and ParameterServerStrategy driven through Keras Model.fit."""
+import json
+import multiprocessing as mp
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _train_mlp(strategy, x, y, epochs=2, batch=64):
+    from distributed_tensorflow_amd.keras import initializers, losses, optimizers
+    from distributed_tensorflow_amd.models.mlp import MnistMLP
+    initializers.set_seed(0)
+    with strategy.scope():
+        m = MnistMLP(hidden=32)
+        m.compile(optimizers.SGD(0.1, momentum=0.9), losses.SparseCategoricalCrossentropy(from_logits=True),
+                  metrics=["accuracy"])
+    h = m.fit(x, y, batch_size=batch, epochs=epochs, shuffle=False, verbose=0)
+    return m, h
+
+
+def _mwms_worker(rank, world, port, mode, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), DTF_CPU_ALLREDUCE=mode, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    try:
+        from distributed_tensorflow_amd import parallel
+        from distributed_tensorflow_amd.models.mlp import synthetic_mnist
+        x, y = synthetic_mnist(512)
+        s = parallel.MultiWorkerMirroredStrategy()
+        m, h = _train_mlp(s, torch.as_tensor(x), torch.as_tensor(y))
+        q.put((rank, [w.detach().numpy().copy() for w in m.weights], h.history["loss"]))
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("mode", ["shm", "gloo"])
+def test_multi_worker_mirrored_matches_single_process(mode):
+    from distributed_tensorflow_amd import parallel
+    from distributed_tensorflow_amd.models.mlp import synthetic_mnist
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_mwms_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    [p.start() for p in ps]
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda t: t[0])
+    [p.join(60) for p in ps]
+    for r in res:
+        assert r[1] is not None, r[2]
+    # both replicas hold identical weights
+    for a, b in zip(res[0][1], res[1][1]):
+        np.testing.assert_allclose(a, b, rtol=0, atol=0)
+    # and equal single-process training on the same global batches
+    x, y = synthetic_mnist(512)
+    m, h = _train_mlp(parallel.OneDeviceStrategy("cpu"), torch.as_tensor(x), torch.as_tensor(y))
+    for a, w in zip(res[0][1], m.weights):
+        np.testing.assert_allclose(a, w.detach().numpy(), rtol=1e-4, atol=1e-5)
+    assert res[0][2][-1] < res[0][2][0]
+
+
+def test_mirrored_cpu0_cpu1_plumbing_config():
+    """BASELINE.json config 1: MNIST 2-layer MLP, MirroredStrategy on CPU:0,CPU:1."""
+    from distributed_tensorflow_amd import parallel
+    from distributed_tensorflow_amd.models.mlp import synthetic_mnist
+    x, y = synthetic_mnist(512)
+    X, Y = torch.as_tensor(x), torch.as_tensor(y)
+    s = parallel.MirroredStrategy(["CPU:0", "CPU:1"])
+    assert s.num_replicas_in_sync == 2
+    m2, h2 = _train_mlp(s, X, Y)
+    m1, h1 = _train_mlp(parallel.OneDeviceStrategy("cpu"), X, Y)
+    for a, b in zip(m2.weights, m1.weights):
+        np.testing.assert_allclose(a.detach().numpy(), b.detach().numpy(), rtol=1e-4, atol=1e-5)
+    assert h2.history["accuracy"][-1] > 0.5
+
+
+def test_gradient_buckets_cover_arena_in_reverse_order():
+    from distributed_tensorflow_amd import Variable
+    from distributed_tensorflow_amd.parallel.collective import GradientBucketer
+    from distributed_tensorflow_amd.variables import ParamArena
+    vs = [Variable(torch.randn(n), name=f"v{i}") for i, n in enumerate([1000, 3, 70000, 12, 500000, 7])]
+    a = ParamArena(vs)
+    b = GradientBucketer(a, bucket_mb=0.5)
+    cover = sorted(b.buckets)
+    assert cover[0][0] == 0 and cover[-1][1] == a.numel
+    for (l0, h0), (l1, h1) in zip(cover, cover[1:]):
+        assert h0 == l1
+    # bucket 0 holds the LAST variables (produced first by backward)
+    assert b.var_bucket[-1] == 0 and b.var_bucket[0] == len(b.buckets) - 1
+    assert sorted(b.var_bucket, reverse=True) == b.var_bucket
+
+
+PS_SCRIPT = r"""
+import os, sys, json, torch
+from distributed_tensorflow_amd.parallel import TFConfigClusterResolver, ParameterServerStrategy, run_parameter_server
+from distributed_tensorflow_amd.keras import losses, optimizers, initializers
+from distributed_tensorflow_amd.models.mlp import MnistMLP, synthetic_mnist
+r = TFConfigClusterResolver()
+if r.is_ps:
+    sys.exit(run_parameter_server(r, device="cpu"))
+s = ParameterServerStrategy(r, variable_partitioner="balanced", device="cpu")
+initializers.set_seed(0)
+x, y = synthetic_mnist(512, seed=1 + s.worker_index)
+with s.scope():
+    m = MnistMLP(hidden=32)
+    m.compile(optimizers.Adam(0.01), losses.SparseCategoricalCrossentropy(from_logits=True), metrics=["accuracy"])
+h = m.fit(torch.as_tensor(x), torch.as_tensor(y), batch_size=32, epochs=3, verbose=0)
+s.pull()
+acc = m.evaluate(torch.as_tensor(x), torch.as_tensor(y), verbose=0, return_dict=True)["accuracy"]
+print(json.dumps({"task": r.task_type, "acc": acc, "gs": s.global_step(), "loss": h.history["loss"]}), flush=True)
+s.shutdown()
+"""
+
+
+@pytest.mark.slow
+def test_parameter_server_strategy_keras_fit(tmp_path):
+    script = tmp_path / "ps_fit.py"
+    script.write_text(PS_SCRIPT)
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "distributed_tensorflow_amd.cli.launch", "--ps", "2", "--workers", "2",
+                        "--chief", "1", "--chief_job", "chief", "--timeout", "240", "--", sys.executable,
+                        str(script)], env=env, capture_output=True, text=True, timeout=300, cwd=tmp_path)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out
+    res = [json.loads(l.split("] ", 1)[1]) for l in out.splitlines() if '"acc"' in l]
+    assert len(res) == 3
+    for d in res:
+        assert d["acc"] > 0.8, out
+        assert d["loss"][-1] < d["loss"][0]
+    assert max(d["gs"] for d in res) >= 3 * 16  # async global_step counts every worker's steps
