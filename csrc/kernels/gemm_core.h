@@ -1,0 +1,495 @@
+// MFMA GEMM + implicit-GEMM convolution for gfx950 (MI355X / CDNA4).
+//
+// One kernel template covers every matmul-shaped op of the framework:
+//   dense Linear fwd / dgrad / wgrad, batched attention products, and
+//   NHWC Conv2D forward (im2col gather), data-gradient (dY gather) and
+//   weight-gradient (X gather on a K-outer operand) — the TF MatMul /
+//   Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter family that the
+//   reference drives through the TF runtime (call sites
+//   reference trainer/task.py:69,137 for the ops the linear model issues).
+//
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §5):
+//  * C[m][n] = sum_k A(m,k) * B(n,k). Both operands are staged through LDS as
+//    64-deep K tiles, double buffered, register staged (issue the next tile's
+//    global loads before the MFMA block, write LDS after it: T14) so any gather
+//    (conv padding, stride, dilation) and zero-fill is a per-lane address.
+//  * K-contiguous operands live in LDS as [rows][64] with a 16-B chunk XOR
+//    swizzle (c ^ ((row>>1)&7)) -> conflict-free ds_read_b128 fragment reads.
+//  * K-outer operands (weight-gradient and dgrad-of-Linear cases) live in LDS
+//    as [64][cols] with an 8-B granule swizzle and are read with the gfx950
+//    transpose read ds_read_b64_tr_b16 (T10) — no transpose pass in HBM.
+//  * v_mfma_f32_16x16x32_bf16, 4 waves (256 threads), 64-wide wave tiles.
+//    The MFMA is issued with (B,A) swapped so each lane owns 4 consecutive
+//    output columns -> 8-byte bf16 / 16-byte f32 stores.
+//  * XCD-aware, bijective block remap + grouped tile order for L2 reuse (T1).
+//  * Fused epilogue: alpha/beta, bias, ReLU/GELU, pre-activation side output,
+//    per-column sum/sum^2 (BatchNorm statistics) and split-K f32 atomics.
+#pragma once
+#include "common.h"
+#include <algorithm>
+#include <type_traits>
+
+namespace dtf {
+
+enum OpMode : int {
+  OP_KCONTIG = 0,  // X(r,k) = p[r*ld + k]
+  OP_KOUTER = 1,   // X(r,k) = p[k*ld + r]
+  OP_IM2COL = 2,   // conv fwd A: r = output pixel (n,p,q), k = (kh,kw,ci)
+  OP_DGRAD = 3,    // conv dgrad A: r = input pixel (n,h,w), k = (kh,kw,co) gathered from dY
+  OP_WGRADX = 4,   // conv wgrad B (k-outer): r = (kh,kw,ci), k = output pixel (n,p,q) gathered from X
+};
+
+struct ConvGeom {
+  int N, H, W, C;   // input NHWC
+  int Kout, R, S;   // filter KRSC
+  int P, Q;         // output spatial
+  int sh, sw, ph, pw, dh, dw;
+  FastDiv dPQ, dQ, dHW, dW, dC, dS, dK;
+};
+
+struct GemmArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  bf16_t* aux;          // optional pre-activation output (bf16, ldc)
+  const float* bias;    // optional [N]
+  const float* scales;  // optional [2] device scales (fp8: dequant factors of A and B; alpha *= s0*s1)
+  float* stats;         // optional [2*N]: column sum, sum of squares (f32 atomics)
+  long lda, ldb, ldc;
+  long sA, sB, sC;      // batch strides (elements)
+  int M, N, K;
+  int batch, splitk, kchunk;  // kchunk: K range per split (multiple of 64)
+  int tiles_m, tiles_n;
+  float alpha, beta;
+  int act;              // 0 none, 1 relu, 2 gelu(tanh)
+  int out_f32;          // C is float
+  int atomic_out;       // atomicAdd into float C (split-K / accumulate)
+  long slab;            // >0: split-K partials go to slab (blockIdx.z) of this many elements (plain stores)
+  ConvGeom g;
+};
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+// ---- K-contiguous operand: LDS tile [R][64] bf16, 128-B rows ---------------
+template <int R, int MODE>
+struct KContigLoader {
+  static constexpr int L = R / 32;  // 16-B loads per thread per K tile
+  const bf16_t* base[L];
+  int i0[L], i1[L], i2[L];  // per-row gather state
+  bool rv[L];
+  int chunk;
+  uint4 reg[L];
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot) {
+    const int t = threadIdx.x;
+    chunk = t & 7;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      int row = (t >> 3) + 32 * i;
+      int r = r0 + row;
+      rv[i] = r < Rtot;
+      if (!rv[i]) r = 0;
+      if constexpr (MODE == OP_KCONTIG) {
+        base[i] = p + (long)r * ld;
+      } else if constexpr (MODE == OP_IM2COL) {
+        uint32_t n, pq, pp, qq;
+        fdivmod((uint32_t)r, a.g.dPQ, n, pq);
+        fdivmod(pq, a.g.dQ, pp, qq);
+        base[i] = p + (long)n * a.g.H * a.g.W * a.g.C;
+        i0[i] = (int)pp * a.g.sh - a.g.ph;
+        i1[i] = (int)qq * a.g.sw - a.g.pw;
+      } else {  // OP_DGRAD: r indexes dX pixels, gather from dY [N][P][Q][Kout]
+        uint32_t n, hw, h, w;
+        fdivmod((uint32_t)r, a.g.dHW, n, hw);
+        fdivmod(hw, a.g.dW, h, w);
+        base[i] = p + (long)n * a.g.P * a.g.Q * a.g.Kout;
+        i0[i] = (int)h + a.g.ph;
+        i1[i] = (int)w + a.g.pw;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const GemmArgs& a, int k0, int Kend) {
+    const int k = k0 + chunk * 8;
+    const bool kv = k < Kend;
+    if constexpr (MODE == OP_KCONTIG) {
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        if (rv[i] && kv) reg[i] = *reinterpret_cast<const uint4*>(base[i] + k);
+        else reg[i] = make_uint4(0, 0, 0, 0);
+      }
+    } else if constexpr (MODE == OP_IM2COL) {
+      uint32_t rs, ci, kh, kw;
+      fdivmod((uint32_t)k, a.g.dC, rs, ci);
+      fdivmod(rs, a.g.dS, kh, kw);
+      const int dh = (int)kh * a.g.dh, dw = (int)kw * a.g.dw;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        int hi = i0[i] + dh, wi = i1[i] + dw;
+        bool v = rv[i] && kv && (unsigned)hi < (unsigned)a.g.H && (unsigned)wi < (unsigned)a.g.W;
+        if (v) reg[i] = *reinterpret_cast<const uint4*>(base[i] + ((long)hi * a.g.W + wi) * a.g.C + ci);
+        else reg[i] = make_uint4(0, 0, 0, 0);
+      }
+    } else {  // OP_DGRAD
+      uint32_t rs, co, kh, kw;
+      fdivmod((uint32_t)k, a.g.dK, rs, co);
+      fdivmod(rs, a.g.dS, kh, kw);
+      const int dh = (int)kh * a.g.dh, dw = (int)kw * a.g.dw;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        int th = i0[i] - dh, tw = i1[i] - dw;
+        bool v = rv[i] && kv && th >= 0 && tw >= 0;
+        int ho = th, wo = tw;
+        if (a.g.sh != 1) { v = v && (th % a.g.sh) == 0; ho = th / a.g.sh; }
+        if (a.g.sw != 1) { v = v && (tw % a.g.sw) == 0; wo = tw / a.g.sw; }
+        v = v && ho < a.g.P && wo < a.g.Q;
+        if (v) reg[i] = *reinterpret_cast<const uint4*>(base[i] + ((long)ho * a.g.Q + wo) * a.g.Kout + co);
+        else reg[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      int row = (t >> 3) + 32 * i;
+      int pc = chunk ^ ((row >> 1) & 7);
+      *reinterpret_cast<uint4*>(lds + row * 128 + pc * 16) = reg[i];
+    }
+  }
+};
+
+// fragment read from a [R][64] tile: rows rb..rb+15, k-substep kk
+__device__ __forceinline__ v8bf frag_kcontig(const char* lds, int rb, int kk, int lane) {
+  int row = rb + (lane & 15);
+  int c = (lane >> 4) + 4 * kk;
+  int pc = c ^ ((row >> 1) & 7);
+  return *reinterpret_cast<const v8bf*>(lds + row * 128 + pc * 16);
+}
+
+// ---- K-outer operand: LDS tile [64][R] bf16 -------------------------------
+template <int R>
+__device__ __forceinline__ int kouter_swz(int k) {
+  if constexpr (R >= 128) return (k & 3) | (((k >> 3) & 1) << 2);  // 8 values, granule bits 2..4
+  else return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);               // R == 64: 4 values
+}
+
+template <int R, int MODE>
+struct KOuterLoader {
+  static constexpr int CPR = R / 8;       // 16-B chunks per k-row
+  static constexpr int RPP = NT / CPR;    // k-rows per pass
+  static constexpr int L = BK / RPP;      // loads per thread
+  const bf16_t* p;
+  long ld;
+  int c, col;
+  bool cv;
+  int khoff, kwoff, ci;  // OP_WGRADX column decomposition
+  uint4 reg[L];
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld_, int r0, int Rtot) {
+    const int t = threadIdx.x;
+    p = ptr;
+    ld = ld_;
+    c = t % CPR;
+    col = r0 + c * 8;
+    cv = col < Rtot;
+    if constexpr (MODE == OP_WGRADX) {
+      uint32_t rs, cc, kh, kw;
+      fdivmod((uint32_t)(cv ? col : 0), a.g.dC, rs, cc);
+      fdivmod(rs, a.g.dS, kh, kw);
+      ci = (int)cc;
+      khoff = (int)kh * a.g.dh - a.g.ph;
+      kwoff = (int)kw * a.g.dw - a.g.pw;
+    }
+  }
+
+  __device__ __forceinline__ void load(const GemmArgs& a, int k0, int Kend) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      int kr = t / CPR + RPP * i;
+      int k = k0 + kr;
+      bool v = cv && k < Kend;
+      if constexpr (MODE == OP_KOUTER) {
+        if (v) reg[i] = *reinterpret_cast<const uint4*>(p + (long)k * ld + col);
+        else reg[i] = make_uint4(0, 0, 0, 0);
+      } else {  // OP_WGRADX: k is the output pixel
+        uint32_t n, pq, pp, qq;
+        fdivmod((uint32_t)(v ? k : 0), a.g.dPQ, n, pq);
+        fdivmod(pq, a.g.dQ, pp, qq);
+        int hi = (int)pp * a.g.sh + khoff, wi = (int)qq * a.g.sw + kwoff;
+        v = v && (unsigned)hi < (unsigned)a.g.H && (unsigned)wi < (unsigned)a.g.W;
+        if (v) reg[i] = *reinterpret_cast<const uint4*>(p + (((long)n * a.g.H + hi) * a.g.W + wi) * a.g.C + ci);
+        else reg[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      int kr = t / CPR + RPP * i;
+      int pc = c ^ (kouter_swz<R>(kr) << 1);
+      *reinterpret_cast<uint4*>(lds + kr * (R * 2) + pc * 16) = reg[i];
+    }
+  }
+};
+
+// fragment read from a [64][R] tile via ds_read_b64_tr_b16: cols cb..cb+15, k-substep kk
+template <int R>
+__device__ __forceinline__ v8bf frag_kouter(const char* lds, int cb, int kk, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  v4s r[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int k = 32 * kk + 8 * G + 4 * h + q;
+    int g = (cb >> 2) + p;
+    int pg = g ^ (kouter_swz<R>(k) << 2);
+    r[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, lds + k * (R * 2) + pg * 8));
+  }
+  // whole-vector casts: per-element short->__bf16 extraction miscompiles (ROCm 7.2)
+  v8s both = __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(v8bf, both);
+}
+
+template <int R, int MODE>
+using LoaderFor = typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE>,
+                                            KContigLoader<R, MODE>>::type;
+
+template <int R, int MODE>
+__device__ __forceinline__ v8bf frag(const char* lds, int rb, int kk, int lane) {
+  if constexpr (MODE == OP_KOUTER || MODE == OP_WGRADX) return frag_kouter<R>(lds, rb, kk, lane);
+  else return frag_kcontig(lds, rb, kk, lane);
+}
+
+// FP8 (OCP e4m3) fragment: lane holds 8 consecutive k bytes of row (rb + lane&15) for k-substep kk (0..3)
+// of a [R][128 fp8] tile (same byte geometry and swizzle as the bf16 [R][64] tile).
+__device__ __forceinline__ long frag_fp8(const char* lds, int rb, int kk, int lane) {
+  int row = rb + (lane & 15);
+  int G = lane >> 4;
+  int c = 2 * kk + (G >> 1);
+  int pc = c ^ ((row >> 1) & 7);
+  return *reinterpret_cast<const long*>(lds + row * 128 + pc * 16 + (G & 1) * 8);
+}
+
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0>
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // ---- block -> tile (XCD-aware bijective remap, then grouped order) ----
+  const int nwg = a.tiles_m * a.tiles_n;
+  int bid = blockIdx.x;
+  {
+    int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  }
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * a.tiles_n;
+  const int grp = bid / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(a.tiles_m - first_m, GROUP);
+  const int in_g = bid - grp * per_group;
+  const int tile_m = first_m + in_g % gsize;
+  const int tile_n = in_g / gsize;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  const int z = blockIdx.z;
+  const int bz = z / a.splitk, sk = z % a.splitk;
+  const int kbeg = sk * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
+  if (kbeg >= kend && a.atomic_out) return;  // (slab mode writes zeros for empty splits)
+
+  const bf16_t* Ap = a.A + (long)bz * a.sA;
+  const bf16_t* Bp = a.B + (long)bz * a.sB;
+
+  LoaderFor<BM, AM> la;
+  LoaderFor<BN, BMODE> lb;
+  la.init(a, Ap, a.lda, m0, a.M);
+  lb.init(a, Bp, a.ldb, n0, a.N);
+
+  v4f acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  char* sA0 = smem;
+  char* sB0 = smem + A_BYTES;
+  char* sA1 = smem + A_BYTES + B_BYTES;
+  char* sB1 = sA1 + A_BYTES;
+
+  if (nk > 0) {
+    la.load(a, kbeg, kend);
+    lb.load(a, kbeg, kend);
+    la.store(sA0);
+    lb.store(sB0);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.load(a, kbeg + (kt + 1) * BK, kend);
+      lb.load(a, kbeg + (kt + 1) * BK, kend);
+    }
+    const char* cA = (kt & 1) ? sA1 : sA0;
+    const char* cB = (kt & 1) ? sB1 : sB0;
+    if constexpr (FP8) {
+      // 128 fp8 of K per tile: four 16x16x32 fp8 MFMA k-substeps (same rate as bf16 per MFMA,
+      // half the staged bytes per FLOP)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        long fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag_fp8(cA, wm * WTM + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag_fp8(cB, wn * WTN + j * 16, kk, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+    } else
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8bf fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = frag<BM, AM>(cA, wm * WTM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = frag<BN, BMODE>(cB, wn * WTN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      la.store((kt & 1) ? sA0 : sA1);
+      lb.store((kt & 1) ? sB0 : sB1);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns row m = ..+(lane&15), cols n = ..+(lane>>4)*4 + r ----
+  const long cbase = a.slab > 0 ? (long)z * a.slab : (long)bz * a.sC;
+  const float alpha = a.scales ? a.alpha * a.scales[0] * a.scales[1] : a.alpha;
+  float csum[TN][4], csq[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) csum[j][r] = csq[j][r] = 0.f;
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WTM + i * 16 + (lane & 15);
+    const bool mv = m < a.M;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WTN + j * 16 + (lane >> 4) * 4;
+      if (!mv || n >= a.N) continue;  // N % 4 == 0 is required by the host
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
+      const long off = cbase + (long)m * a.ldc + n;
+      if (a.atomic_out) {
+        float* Cf = reinterpret_cast<float*>(a.C) + off;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(Cf + r, v[r]);
+        continue;
+      }
+      if (a.beta != 0.f) {
+        if (a.out_f32) {
+          float4 o = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(a.C) + off);
+          v[0] += a.beta * o.x; v[1] += a.beta * o.y; v[2] += a.beta * o.z; v[3] += a.beta * o.w;
+        } else {
+          uint2 o = *reinterpret_cast<const uint2*>(reinterpret_cast<bf16_t*>(a.C) + off);
+          v[0] += a.beta * __uint_as_float(o.x << 16); v[1] += a.beta * __uint_as_float(o.x & 0xffff0000u);
+          v[2] += a.beta * __uint_as_float(o.y << 16); v[3] += a.beta * __uint_as_float(o.y & 0xffff0000u);
+        }
+      }
+      if (a.bias) {
+        float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (a.aux) {
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(a.aux + off) = o;
+      }
+      if (a.act == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      } else if (a.act == 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+      }
+      if (a.out_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.C) + off) = o;
+        if (a.stats) {  // statistics of the stored (bf16-rounded) values
+          v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);
+          v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
+        }
+      }
+      if (a.stats) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { csum[j][r] += v[r]; csq[j][r] += v[r] * v[r]; }
+      }
+    }
+  }
+  if (a.stats) {
+    // Deterministic BN statistics: reduce the 16 rows of a lane group by shuffles, the WM wave rows of
+    // the tile through LDS, then write ONE partial row per M-tile: stats[tile_m][0,N) = sum,
+    // stats[tile_m][N,2N) = sum of squares (bn_finalize sums the tiles_m rows). No atomics.
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = csum[j][r], q = csq[j][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4 + r;
+        if ((lane & 15) == 0) {
+          red[wm * BN + nl] = s;
+          red[WM * BN + wm * BN + nl] = q;
+        }
+      }
+    }
+    __syncthreads();
+    float* prow = a.stats + (long)tile_m * 2 * a.N;
+    for (int nl = threadIdx.x; nl < BN; nl += NT) {
+      const int n = n0 + nl;
+      if (n >= a.N) continue;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) { s += red[w * BN + nl]; q += red[WM * BN + w * BN + nl]; }
+      prow[n] = s;
+      prow[a.N + n] = q;
+    }
+  }
+}
+
+}  // namespace dtf

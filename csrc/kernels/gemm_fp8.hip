@@ -1,0 +1,99 @@
+// FP8 (OCP e4m3, gfx950 native) GEMM + quantization for the GPT-2-medium fp8 config
+// (BASELINE.json: "GPT-2-medium fp8 weights (CDNA4 fp8 MFMA)").
+//
+//  * dtf_quant_fp8: x (bf16) -> e4m3 with a per-tensor scale; the SAME pass computes amax(|x|) into
+//    a device float (atomicMax on the bit pattern; values are non-negative) so the next step can use
+//    it ("delayed scaling": no extra reduction pass on the critical path).
+//  * dtf_gemm_fp8: C[M][N] = (sa*sb) * A_q[M][K] . B_q[N][K]^T (+bias, act, pre-activation aux), bf16 out,
+//    on v_mfma_f32_16x16x32_fp8_fp8 with the same LDS-staged, swizzled pipeline as the bf16 GEMM
+//    (gemm_core.h) — half the staged bytes per FLOP.
+#include "gemm_core.h"
+
+namespace {
+
+__device__ __forceinline__ float fp8_max() { return 448.f; }
+
+// 8 bf16 -> 8 e4m3 bytes; scale_inv = 1/scale
+__global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q, long n8,
+                                                        const float* __restrict__ scale, float* __restrict__ amax) {
+  __shared__ float red[16];
+  const float inv = 1.f / fmaxf(scale[0], 1e-30f);
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(x + i * 8, f);
+    uint32_t w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float a0 = fminf(fmaxf(f[4 * h + 0] * inv, -fp8_max()), fp8_max());
+      float a1 = fminf(fmaxf(f[4 * h + 1] * inv, -fp8_max()), fp8_max());
+      float a2 = fminf(fmaxf(f[4 * h + 2] * inv, -fp8_max()), fp8_max());
+      float a3 = fminf(fmaxf(f[4 * h + 3] * inv, -fp8_max()), fp8_max());
+      int r = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+      r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
+      w[h] = (uint32_t)r;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[j]));
+    *reinterpret_cast<uint2*>(q + i * 8) = make_uint2(w[0], w[1]);
+  }
+  if (amax) {
+    m = block_max(m, red);
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+  }
+}
+
+// new scale from the amax of the previous step: scale = amax / 448 * 2^-margin  (history length 1)
+__global__ void fp8_update_scale_kernel(const float* amax, float* scale, float margin) {
+  float a = amax[0];
+  scale[0] = a > 0.f ? a / 448.f * exp2f(margin) : 1.f;
+}
+
+}  // namespace
+
+using namespace dtf;
+
+DTF_API int dtf_quant_fp8(const void* x, void* q, long n, const float* scale, float* amax, int zero_amax,
+                          void* stream) {
+  if (n & 7) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  if (amax && zero_amax) (void)hipMemsetAsync(amax, 0, sizeof(float), st);
+  int grid = stream_grid(n / 8, 256);
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, (uint8_t*)q, n / 8, scale,
+                     amax);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_fp8_update_scale(const float* amax, float* scale, float margin, void* stream) {
+  hipLaunchKernelGGL(fp8_update_scale_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, amax, scale, margin);
+  return (int)hipGetLastError();
+}
+
+// A: [M][K] e4m3 (lda bytes), B: [N][K] e4m3 (ldb bytes); scales: device [sa, sb]; C bf16 [M][ldc]
+DTF_API int dtf_gemm_fp8(const void* A, const void* B, void* C, void* aux, const float* bias, const float* scales,
+                         int M, int N, int K, long lda, long ldb, long ldc, int act, int tile, void* stream) {
+  if ((N & 3) || (K & 15) || (lda & 1) || (ldb & 1) || M <= 0) return -1;
+  GemmArgs a{};
+  // the loaders move 16-B chunks: view fp8 rows as bf16_t pairs (K/2, ld/2)
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.aux = (bf16_t*)aux;
+  a.bias = bias; a.scales = scales;
+  a.M = M; a.N = N; a.K = K / 2;
+  a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
+  a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
+  a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = 0;
+  if (tile < 0) {
+    long b128 = (long)cdiv(M, 128) * cdiv(N, 128);
+    tile = b128 >= 256 ? 0 : 2;
+  }
+  a.tiles_m = cdiv(M, tile == 0 ? 128 : 128);
+  a.tiles_n = cdiv(N, tile == 0 ? 128 : 64);
+  dim3 grid(a.tiles_m * a.tiles_n, 1, 1);
+  if (tile == 0)
+    hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT), 0,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT), 0,
+                       (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}

@@ -56,6 +56,8 @@ _KERNEL_SIGS = {
     "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P],
     "dtf_gemm_fp8": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, P],
     "dtf_quant_fp8": [P, P, L, P, P, I, P],
+    "dtf_fp8_update_scale": [P, P, F, P],
+    "dtf_group_rows_once": [P, L, I, L, I, P, P],
 }
 
 

@@ -1,0 +1,190 @@
+"""BERT-base (post-LN encoder, MLM + NSP heads) and GPT-2 (pre-LN causal decoder, tied LM head).
+
+BASELINE.json configs: "BERT-base seq=512 MultiWorkerMirroredStrategy" and "GPT-2-medium fp8 weights
+MirroredStrategy". Dense layers run on the MFMA GEMM with fused bias/GELU epilogues; LayerNorm,
+softmax, embeddings and the vocab cross-entropy on their HIP kernels. ``fp8=True`` runs the
+projection GEMMs of the transformer blocks with OCP e4m3 operands (CDNA4 fp8 MFMA, per-tensor
+delayed scaling — ops.fp8).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..ops import attention as attn_ops
+from ..keras import layers as KL
+from ..keras.models import Model
+
+
+class _Proj(KL.Layer):
+    """Dense [units, in] with optional fp8 forward."""
+
+    def __init__(self, units, activation=None, fp8=False, init_std=0.02, **kw):
+        super().__init__(**kw)
+        self.units, self.activation, self.fp8, self.init_std = units, activation, fp8, init_std
+
+    def build(self, input_shape):
+        from ..keras.initializers import TruncatedNormal
+        self.kernel = self.add_weight("kernel", (self.units, input_shape[-1]), TruncatedNormal(0.0, self.init_std))
+        self.bias = self.add_weight("bias", (self.units,), "zeros")
+        self.built = True
+
+    def call(self, x, training=None):
+        if self.fp8 and x.is_cuda:
+            from ..ops.fp8 import dense_fp8
+            return dense_fp8(x, self.kernel, self.bias, self.activation, self)
+        return ops.dense(x, self.kernel, self.bias, act=self.activation)
+
+
+class MultiHeadSelfAttention(KL.Layer):
+    def __init__(self, hidden, heads, dropout=0.1, causal=False, fp8=False, **kw):
+        super().__init__(**kw)
+        self.heads, self.dropout, self.causal = heads, dropout, causal
+        self.qkv = _Proj(3 * hidden, fp8=fp8)
+        self.out = _Proj(hidden, fp8=fp8)
+
+    def call(self, x, mask=None, training=None):
+        q, k, v = attn_ops.split_qkv(self.qkv(x), self.heads)
+        o = attn_ops.attention(q, k, v, causal=self.causal, mask=mask, dropout=self.dropout,
+                                        training=training)
+        return self.out(attn_ops.merge_heads(o))
+
+
+class BertLayer(KL.Layer):
+    def __init__(self, hidden=768, heads=12, ffn=3072, dropout=0.1, **kw):
+        super().__init__(**kw)
+        self.att = MultiHeadSelfAttention(hidden, heads, dropout)
+        self.ln1 = KL.LayerNormalization(epsilon=1e-12)
+        self.ff1 = _Proj(ffn, activation="gelu")
+        self.ff2 = _Proj(hidden)
+        self.ln2 = KL.LayerNormalization(epsilon=1e-12)
+        self.dropout = dropout
+
+    def call(self, x, mask=None, training=None):
+        a = ops.dropout(self.att(x, mask, training=training), self.dropout, training=bool(training))
+        x = self.ln1(ops.add(x, a))
+        f = ops.dropout(self.ff2(self.ff1(x)), self.dropout, training=bool(training))
+        return self.ln2(ops.add(x, f))
+
+
+class BertModel(Model):
+    """BERT encoder with MLM (tied decoder) and NSP heads. Inputs: ids, type_ids, attention mask."""
+
+    def __init__(self, vocab=30522, hidden=768, layers=12, heads=12, ffn=3072, max_pos=512, type_vocab=2,
+                 dropout=0.1, name="bert", **kw):
+        super().__init__(name=name, **kw)
+        self.cfg = dict(vocab=vocab, hidden=hidden, layers=layers, heads=heads, ffn=ffn, max_pos=max_pos)
+        from ..keras.initializers import TruncatedNormal
+        # vocab padded to a multiple of 64 (MFMA tiles); padded logits carry a -1e9 bias -> zero probability
+        self.vocab, self.vocab_p = vocab, (vocab + 63) // 64 * 64
+        self.word = self.add_weight("embeddings/word", (self.vocab_p, hidden), TruncatedNormal(0.0, 0.02))
+        self.pos = self.add_weight("embeddings/position", (max_pos, hidden), TruncatedNormal(0.0, 0.02))
+        self.typ = self.add_weight("embeddings/type", (type_vocab, hidden), TruncatedNormal(0.0, 0.02))
+        self.emb_ln = KL.LayerNormalization(epsilon=1e-12)
+        self.blocks = [BertLayer(hidden, heads, ffn, dropout) for _ in range(layers)]
+        self.mlm_dense = _Proj(hidden, activation="gelu")
+        self.mlm_ln = KL.LayerNormalization(epsilon=1e-12)
+        self.mlm_bias = self.add_weight("mlm/bias", (self.vocab_p,), "zeros")
+        with torch.no_grad():
+            self.mlm_bias[vocab:] = -1e9
+        self.pool = _Proj(hidden)
+        self.nsp = _Proj(2)
+        self.dropout = dropout
+        self.built = True
+
+    def encode(self, ids, type_ids=None, attn_mask=None, training=None):
+        x = ops.embedding(ids, self.word, self.pos, type_ids, self.typ)
+        x = ops.dropout(self.emb_ln(x), self.dropout, training=bool(training))
+        mask = None
+        if attn_mask is not None:
+            mask = (1.0 - attn_mask.float()) * -10000.0
+        for b in self.blocks:
+            x = b(x, mask, training=training)
+        return x
+
+    def mlm_logits(self, h):
+        t = self.mlm_ln(self.mlm_dense(h))
+        return ops.dense(t, self.word, self.mlm_bias)
+
+    def call(self, inputs, training=None):
+        if isinstance(inputs, dict):
+            ids, tids, am = inputs["input_ids"], inputs.get("token_type_ids"), inputs.get("attention_mask")
+            mpos = inputs.get("masked_positions")
+        else:
+            ids, tids, am, mpos = inputs, None, None, None
+        h = self.encode(ids, tids, am, training=training)
+        if mpos is not None:  # gather the masked positions only (BERT pretraining)
+            B, S, Hd = h.shape
+            idx = (mpos + torch.arange(B, device=mpos.device)[:, None] * S).reshape(-1)
+            h = h.reshape(B * S, Hd).index_select(0, idx).reshape(B, -1, Hd)
+        return self.mlm_logits(h)
+
+    def nsp_logits(self, h):
+        return self.nsp(torch.tanh(self.pool(h[:, 0]).float()).to(h.dtype))
+
+
+class GPT2Block(KL.Layer):
+    def __init__(self, hidden, heads, dropout=0.1, fp8=False, **kw):
+        super().__init__(**kw)
+        self.ln1 = KL.LayerNormalization(epsilon=1e-5)
+        self.att = MultiHeadSelfAttention(hidden, heads, dropout, causal=True, fp8=fp8)
+        self.ln2 = KL.LayerNormalization(epsilon=1e-5)
+        self.fc = _Proj(4 * hidden, activation="gelu", fp8=fp8)
+        self.proj = _Proj(hidden, fp8=fp8)
+        self.dropout = dropout
+
+    def call(self, x, training=None):
+        x = ops.add(x, ops.dropout(self.att(self.ln1(x), training=training), self.dropout, training=bool(training)))
+        return ops.add(x, ops.dropout(self.proj(self.fc(self.ln2(x))), self.dropout, training=bool(training)))
+
+
+class GPT2(Model):
+    def __init__(self, vocab=50257, ctx=1024, hidden=1024, layers=24, heads=16, dropout=0.1, fp8=False,
+                 name="gpt2", **kw):
+        super().__init__(name=name, **kw)
+        self.cfg = dict(vocab=vocab, ctx=ctx, hidden=hidden, layers=layers, heads=heads, fp8=fp8)
+        from ..keras.initializers import TruncatedNormal
+        # vocab padded to a multiple of 64 for the MFMA tiles (padded logits are masked out of the loss)
+        self.vocab = vocab
+        self.vocab_p = (vocab + 63) // 64 * 64
+        self.wte = self.add_weight("wte", (self.vocab_p, hidden), TruncatedNormal(0.0, 0.02))
+        self.wpe = self.add_weight("wpe", (ctx, hidden), TruncatedNormal(0.0, 0.01))
+        self.blocks = [GPT2Block(hidden, heads, dropout, fp8) for _ in range(layers)]
+        self.ln_f = KL.LayerNormalization(epsilon=1e-5)
+        pad = torch.zeros(self.vocab_p)
+        pad[vocab:] = -1e9  # padded vocab entries never receive probability mass
+        self.pad_bias = self.add_weight("lm_pad_bias", (self.vocab_p,), "zeros", trainable=False)
+        with torch.no_grad():
+            self.pad_bias.copy_(pad.to(self.pad_bias.device))
+        self.dropout = dropout
+        self.built = True
+
+    def call(self, ids, training=None):
+        x = ops.dropout(ops.embedding(ids, self.wte, self.wpe), self.dropout, training=bool(training))
+        for b in self.blocks:
+            x = b(x, training=training)
+        return ops.dense(self.ln_f(x), self.wte, self.pad_bias)  # tied LM head, logits over vocab_p
+
+
+def bert_base(**kw):
+    return BertModel(**kw)
+
+
+def gpt2_medium(fp8=False, **kw):
+    return GPT2(hidden=1024, layers=24, heads=16, fp8=fp8, **kw)
+
+
+def gpt2_small(fp8=False, **kw):
+    return GPT2(hidden=768, layers=12, heads=12, fp8=fp8, **kw)
+
+
+def count_flops_per_token(cfg, seq):
+    """Approximate training FLOPs/token (6N + attention) for throughput reporting."""
+    h, L = cfg["hidden"], cfg["layers"]
+    n = 12 * L * h * h
+    return 6 * n + 12 * L * h * seq
+
+
+del math

@@ -1,0 +1,96 @@
+"""FP8 (OCP e4m3) projections for GPT-2-medium (csrc/kernels/gemm_fp8.hip).
+
+Forward: activations and weights are quantized to e4m3 with per-tensor scales and multiplied on the
+gfx950 fp8 MFMA (``v_mfma_f32_16x16x32_fp8_fp8``), f32 accumulate, dequant + bias + GELU fused in the
+epilogue. Activation scales use delayed scaling (the quantize pass of step t records amax(|x|), which
+sets the scale of step t+1: no extra reduction pass); weight scales are exact (recomputed once per
+optimizer step). Backward runs in bf16 against the bf16 weight copies (fp8 forward / bf16 backward
+recipe), so master weights, optimizer and gradients are unchanged.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._util import BF16, F32, bf16_shadow, call, ptr, stream, weights_epoch
+from .linalg import colsum, gemm
+
+E4M3_MAX = 448.0
+
+
+def quantize(x, scale, amax=None, zero_amax=True):
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    call("dtf_quant_fp8", ptr(x), ptr(q), x.numel(), ptr(scale), ptr(amax), int(zero_amax), stream())
+    return q
+
+
+class _Fp8State:
+    def __init__(self, dev):
+        self.buf = torch.zeros(4, dtype=F32, device=dev)  # [x_scale, w_scale, x_amax, w_amax]
+        self.x_ready = False
+        self.wq = None
+        self.w_key = None
+
+
+def _state(layer, dev):
+    st = getattr(layer, "_fp8", None)
+    if st is None:
+        st = _Fp8State(dev)
+        object.__setattr__(layer, "_fp8", st)
+    return st
+
+
+def _weight_fp8(st, w):
+    key = (weights_epoch(), w._version)
+    if st.wq is not None and st.w_key == key:
+        return st.wq
+    w16 = bf16_shadow(w)
+    amax = w16.abs().amax().float().clamp_min(1e-12)  # exact per-tensor weight scale
+    st.buf[1:2].copy_(amax / E4M3_MAX)
+    st.wq = quantize(w16, st.buf[1:2])
+    st.w_key = key
+    return st.wq
+
+
+class _DenseFP8(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act, st):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).contiguous()
+        if not st.x_ready:  # bootstrap the delayed activation scale once
+            st.buf[0:1].copy_(x2.abs().amax().float().clamp_min(1e-12) / E4M3_MAX)
+            st.x_ready = True
+        xq = quantize(x2, st.buf[0:1], st.buf[2:3])
+        wq = _weight_fp8(st, w)
+        M, K = x2.shape
+        N = w.shape[0]
+        y = torch.empty((M, N), dtype=BF16, device=x.device)
+        pre = torch.empty((M, N), dtype=BF16, device=x.device) if act else None
+        call("dtf_gemm_fp8", ptr(xq), ptr(wq), ptr(y), ptr(pre), ptr(b), ptr(st.buf), M, N, K, K, K, N, int(act), -1,
+             stream())
+        call("dtf_fp8_update_scale", ptr(st.buf[2:3]), ptr(st.buf[0:1]), 0.0, stream())  # next step's x scale
+        ctx.save_for_backward(x2, w, pre)
+        ctx.act = act
+        ctx.has_b = b is not None
+        ctx.shp = shp
+        return y.reshape(*shp[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, pre = ctx.saved_tensors
+        N = w.shape[0]
+        dz = dy.reshape(-1, N).to(BF16).contiguous()
+        if ctx.act:
+            g = torch.empty_like(dz)
+            call("dtf_act", ptr(pre), ptr(dz), ptr(g), g.numel(), ctx.act, 1, stream())
+            dz = g
+        dx = gemm(dz, bf16_shadow(w), b_kouter=True).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
+        dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32) if ctx.needs_input_grad[1] else None
+        db = colsum(dz) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None
+
+
+def dense_fp8(x, w, b, activation, layer):
+    from .linalg import act_code
+    a = act_code(activation)
+    st = _state(layer, x.device)
+    return _DenseFP8.apply(x.to(BF16), w, b, a, st)

@@ -259,3 +259,38 @@ def test_optimizers_match_reference(cuda, kind):
     opt = O.get(kind, learning_rate=0.01)
     out = O.fused_update_for_test(opt, p, [g.to(cuda) for g in gs])
     close(out.cpu(), ref, 1e-4)
+
+
+def test_fp8_quant_and_gemm(cuda):
+    from distributed_tensorflow_amd.ops import fp8
+    M, N, K = 512, 384, 1024
+    x = rnd(M, K, dev=cuda)
+    w = rnd(N, K, dev=cuda, scale=0.05)
+    sx = (x.float().abs().max() / 448).reshape(1)
+    sw = (w.float().abs().max() / 448).reshape(1)
+    amax = torch.zeros(1, device=cuda)
+    xq = fp8.quantize(x, sx, amax)
+    wq = fp8.quantize(w, sw)
+    assert abs(amax.item() - x.float().abs().max().item()) < 1e-6
+    # decode with torch's OCP e4m3 type and compare to the quantized reference
+    xd = xq.view(torch.float8_e4m3fn).float() * sx
+    assert (xd - x.float()).abs().max().item() <= 0.07 * x.float().abs().max().item()
+    scales = torch.cat([sx, sw])
+    y = torch.empty(M, N, dtype=BF, device=cuda)
+    from distributed_tensorflow_amd.ops._util import call, ptr, stream
+    call("dtf_gemm_fp8", ptr(xq), ptr(wq), ptr(y), None, None, ptr(scales), M, N, K, K, K, N, 0, -1, stream())
+    ref = (xq.view(torch.float8_e4m3fn).float() * sx) @ (wq.view(torch.float8_e4m3fn).float() * sw).t()
+    close(y, ref, 1e-2)
+
+
+def test_fp8_dense_layer_trains(cuda):
+    from distributed_tensorflow_amd.models.transformer import _Proj
+    torch.manual_seed(0)
+    layer = _Proj(256, activation="gelu", fp8=True)
+    x = rnd(128, 512, dev=cuda)
+    y = layer(x)
+    ref = torch.nn.functional.gelu(x.float() @ layer.kernel.detach().to(BF).float().t() + layer.bias.detach(),
+                                   approximate="tanh")
+    close(y, ref, 8e-2)
+    y.float().sum().backward()
+    assert layer.kernel.grad is not None and torch.isfinite(layer.kernel.grad).all()
