@@ -1,23 +1,84 @@
 #!/usr/bin/env python
 """Headline benchmark: ResNet-50 v1.5 bf16 training throughput (images/sec, whole job).
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is
-launched under ``torch.distributed.run`` with one rank per GPU (RCCL over xGMI).
-Per-GPU batch is fixed (weak scaling); the timed region holds exactly K full
-training steps — device-side input conversion, forward, loss, backward with the
-bucketed all-reduce, and the fused SGD-momentum update — bracketed by a barrier
-and ``torch.cuda.synchronize()``; the max over ranks is reported by rank 0 as
-one JSON line. Data: one synthetic ImageNet batch (random 224x224x3 f32 images,
-random labels) resident on each GPU; weights random-init.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched under
+``torch.distributed.run`` with one rank per GPU (RCCL over xGMI); launched directly with N>1 it
+re-launches itself that way as a child process. Per-GPU batch is fixed (weak scaling); the timed
+region holds exactly K full training steps — device-side input conversion, forward, loss, backward
+with the bucketed all-reduce, and the fused optimizer update — bracketed by a barrier and
+``torch.cuda.synchronize()``; the max over ranks is reported by rank 0 as one JSON line.
+Data: synthetic (random inputs + labels resident on each GPU); weights random-init.
+
+Other BASELINE.json configs: ``--model bert_base`` (seq 512, MultiWorkerMirroredStrategy, tokens/s)
+and ``--model gpt2_medium_fp8`` (ctx 1024, fp8 projections, MirroredStrategy, tokens/s).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+DEFAULT_BATCH = {"resnet50": 256, "resnet101": 256, "resnet152": 256, "bert_base": 32, "gpt2_medium_fp8": 8,
+                 "gpt2_medium": 8}
+
+
+def _relaunch(args):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def build(args, strategy, dev, rank):
+    import torch
+    from distributed_tensorflow_amd.data import synthetic_imagenet, synthetic_tokens
+    from distributed_tensorflow_amd.keras import losses, optimizers
+    m = args.model
+    with strategy.scope():
+        if m.startswith("resnet"):
+            from distributed_tensorflow_amd.models import ResNet
+            model = ResNet(int(m[6:]), num_classes=1000)
+            model.compile(optimizer=optimizers.SGD(args.lr, momentum=0.9),
+                          loss=losses.SparseCategoricalCrossentropy(from_logits=True))
+            data = iter(synthetic_imagenet(args.batch, dev, seed=1234 + rank))
+            return model, data, "images/sec", {"model": f"ResNet-{m[6:]} v1.5", "image_size": 224, "seq_len": None}
+        if m == "bert_base":
+            from distributed_tensorflow_amd.models.transformer import BertModel
+            model = BertModel()
+            model.compile(optimizer=optimizers.AdamW(1e-4, weight_decay=0.01, epsilon=1e-6),
+                          loss=losses.SparseCategoricalCrossentropy(from_logits=True))
+            S, P = 512, 76
+            g = torch.Generator().manual_seed(rank)
+            ids = torch.randint(0, 30522, (args.batch, S), generator=g).to(dev)
+            mpos = torch.stack([torch.randperm(S, generator=g)[:P] for _ in range(args.batch)]).to(dev)
+            lab = torch.randint(0, 30522, (args.batch, P), generator=g).to(dev)
+            x = {"input_ids": ids, "masked_positions": mpos, "token_type_ids": torch.zeros_like(ids),
+                 "attention_mask": torch.ones(args.batch, S, device=dev)}
+
+            def gen():
+                while True:
+                    yield x, lab
+            args.tokens_per_sample = S
+            return model, gen(), "tokens/sec", {"model": "BERT-base (MLM, 76 masked/seq)", "seq_len": S}
+        if m.startswith("gpt2_medium"):
+            from distributed_tensorflow_amd.models.transformer import gpt2_medium
+            model = gpt2_medium(fp8=m.endswith("fp8"))
+            model.compile(optimizer=optimizers.AdamW(3e-4, weight_decay=0.1),
+                          loss=losses.SparseCategoricalCrossentropy(from_logits=True))
+            S = 1024
+            args.tokens_per_sample = S
+            data = iter(synthetic_tokens(args.batch, S, 50257, dev, seed=rank))
+            return model, data, "tokens/sec", {"model": "GPT-2-medium" + (" fp8 (e4m3 fwd projections)" if
+                                                                           m.endswith("fp8") else ""), "seq_len": S}
+    raise ValueError(m)
 
 
 def main():
@@ -25,38 +86,29 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--bucket-mb", type=float, default=None)
-    ap.add_argument("--profile-steps", type=int, default=0)
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = DEFAULT_BATCH[args.model]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1 and "RANK" not in os.environ:
+        return _relaunch(args)  # before anything touches the GPU
 
     import torch
     import torch.distributed as dist
 
-    import distributed_tensorflow_amd as dtf
     from distributed_tensorflow_amd import parallel
-    from distributed_tensorflow_amd.data import synthetic_imagenet
-    from distributed_tensorflow_amd.keras import losses, optimizers
-    from distributed_tensorflow_amd.models import ResNet
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        if args.gpus > 1 and world == 1:
-            print(f"bench.py: --gpus {args.gpus} needs a torch.distributed.run launch with {args.gpus} ranks",
-                  file=sys.stderr)
-            return 2
-    strategy = parallel.MirroredStrategy(bucket_mb=args.bucket_mb)
+    if args.model == "bert_base":
+        strategy = parallel.MultiWorkerMirroredStrategy(bucket_mb=args.bucket_mb)
+    else:
+        strategy = parallel.MirroredStrategy(bucket_mb=args.bucket_mb)
     rank = strategy.worker_index
     dev = strategy.device
-    depth = {"resnet50": 50, "resnet101": 101, "resnet152": 152}[args.model]
-
-    with strategy.scope():
-        model = ResNet(depth, num_classes=1000)
-        model.compile(optimizer=optimizers.SGD(args.lr, momentum=0.9),
-                      loss=losses.SparseCategoricalCrossentropy(from_logits=True))
-    data = iter(synthetic_imagenet(args.batch, dev, seed=1234 + rank))
+    model, data, unit, cfg = build(args, strategy, dev, rank)
 
     def step():
         x, y = next(data)
@@ -83,29 +135,30 @@ def main():
     dt = float(t.item())
     ms = dt / args.steps * 1e3
     global_batch = args.batch * world
-    ips = global_batch * args.steps / dt
+    per_sample = getattr(args, "tokens_per_sample", 1)
+    value = global_batch * per_sample * args.steps / dt
     if rank == 0:
         with open(os.path.join(ROOT, "BASELINE.json")) as f:
             base = json.load(f)
         pub = base.get("published") or {}
-        ref = pub.get("resnet50_images_per_sec") if isinstance(pub, dict) else None
+        ref = pub.get(args.model) if isinstance(pub, dict) else None
+        metric = base["metric"] if args.model == "resnet50" else f"{unit} (whole node) {cfg['model']}"
         out = {
-            "metric": base["metric"],
-            "value": round(ips, 2),
-            "unit": "images/sec",
+            "metric": metric,
+            "value": round(value, 2),
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (ips / ref) if ref else None,
+            "vs_baseline": (value / ref) if ref else None,
             "dtype": "bf16",
-            "data": "synthetic (random 224x224x3 images + labels resident on GPU; random-init weights)",
-            "config": {"model": f"ResNet-{depth} v1.5", "global_batch": global_batch, "per_gpu_batch": args.batch,
-                       "image_size": 224, "seq_len": None, "parallelism": f"dp{world}",
-                       "strategy": "MirroredStrategy (1 process/GPU, RCCL)", "optimizer": "SGD momentum 0.9",
-                       "final_loss": round(loss, 4)},
+            "data": "synthetic (random inputs + labels resident on GPU; random-init weights)",
+            "config": dict(cfg, global_batch=global_batch, per_gpu_batch=args.batch, parallelism=f"dp{world}",
+                           strategy=type(strategy).__name__ + " (1 process/GPU, RCCL)",
+                           optimizer=type(model.optimizer).__name__, final_loss=round(loss, 4)),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
