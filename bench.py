@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: capture the whole train step in a hipGraph (compile(jit_compile=True))")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
@@ -109,10 +111,13 @@ def main():
     rank = strategy.worker_index
     dev = strategy.device
     model, data, unit, cfg = build(args, strategy, dev, rank)
+    model._jit = bool(args.graph)
+    train_fn = model.make_train_function(force=True)
+    cfg["hipgraph"] = type(train_fn).__name__ == "CapturedStep"
 
     def step():
         x, y = next(data)
-        return model.train_step((x, y))
+        return train_fn((x, y))
 
     for _ in range(args.warmup):
         logs = step()

@@ -95,7 +95,7 @@ def run_standalone():
         if i % FLAGS.checkpoint_period == 0:
             with torch.no_grad():
                 loss = float(loss_fn(Y[0], model(X[0])))
-            step = int(opt.iterations.item())
+            step = opt.host_iterations()
             writer.add_summary({"loss": loss, "training/hptuning/metric": loss}, step)
             print("Epoch: {}, loss: {}".format(i, loss))
     writer.close()

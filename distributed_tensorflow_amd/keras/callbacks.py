@@ -99,7 +99,7 @@ class StopAtStep(Callback):
         self.last_step = int(last_step)
 
     def on_train_batch_end(self, batch, logs=None):
-        if int(self.model.optimizer.iterations.item()) >= self.last_step:
+        if self.model.optimizer.host_iterations() >= self.last_step:
             self.model.stop_training = True
 
 
@@ -171,7 +171,7 @@ class ModelCheckpoint(Callback):
     def _save(self):
         if not getattr(self.model, "_is_chief", True):
             return
-        p = self._manager().save(checkpoint_number=int(self.model.optimizer.iterations.item()))
+        p = self._manager().save(checkpoint_number=self.model.optimizer.host_iterations())
         if self.verbose:
             print(f"saved checkpoint {p}")
         self._last = time.time()
@@ -241,7 +241,7 @@ class TensorBoard(Callback):
 
     def on_train_batch_end(self, batch, logs=None):
         if isinstance(self.update_freq, int) and (batch + 1) % self.update_freq == 0:
-            step = int(self.model.optimizer.iterations.item())
+            step = self.model.optimizer.host_iterations()
             for k, v in (logs or {}).items():
                 if isinstance(v, float):
                     self._writer().scalar(f"batch_{k}", v, step)

@@ -10,8 +10,13 @@ class Metric:
         self.reset_state()
 
     def reset_state(self):
-        self._total = None
-        self._count = None
+        # zero in place once allocated: a captured (hipGraph) step keeps accumulating into these
+        if getattr(self, "_total", None) is not None:
+            self._total.zero_()
+            self._count.zero_()
+        else:
+            self._total = None
+            self._count = None
 
     def _acc(self, total, count):
         if self._total is None:
@@ -26,7 +31,7 @@ class Metric:
         raise NotImplementedError
 
     def result(self):
-        if self._total is None:
+        if self._total is None or float(self._count) == 0.0:
             return 0.0
         return float(self._total / self._count.clamp_min(1e-12))
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 import time
 
 import numpy as np
@@ -104,6 +105,7 @@ class Model(Layer):
         self._strategy = S.get_strategy()
         self._is_chief = self._strategy.is_chief
         self._jit = bool(jit_compile)
+        self._train_fn = None
 
     @property
     def distribute_strategy(self):
@@ -151,6 +153,24 @@ class Model(Layer):
         strat.backward(loss, arena)
         strat.apply_gradients(self.optimizer, arena)
         return self._update_metrics(loss, y, y_pred)
+
+    def make_train_function(self, force=False):
+        """The per-batch step fit() drives. With ``compile(jit_compile=True)`` on one GPU rank it is a
+        hipGraph-captured step (graphs.CapturedStep): eager warmup, one capture, then one graph launch
+        per step. Multi-rank capture of the RCCL bucket all-reduces is opt-in (DTF_GRAPH_DIST=1)."""
+        if getattr(self, "_train_fn", None) is not None and not force:
+            return self._train_fn
+        strat = self.distribute_strategy
+        fn = self.train_step
+        dev = self._device()
+        multi = getattr(strat, "_world", 1) > 1 or bool(strat.inproc_replicas() if hasattr(
+            strat, "inproc_replicas") else None)
+        if getattr(self, "_jit", False) and dev.type == "cuda" and (
+                not multi or os.environ.get("DTF_GRAPH_DIST", "0") == "1"):
+            from ..graphs import CapturedStep
+            fn = CapturedStep(self.train_step, warmup=2, optimizers=[self.optimizer])
+        self._train_fn = fn
+        return fn
 
     def _update_metrics(self, loss, y, y_pred):
         with torch.no_grad():
@@ -292,6 +312,7 @@ class Model(Layer):
         if steps_per_epoch is not None:
             steps = steps_per_epoch
         ds_iter = None
+        train_fn = self.make_train_function()
         for epoch in range(start_epoch, epochs):
             for m in self.metrics:
                 m.reset_state()
@@ -305,7 +326,7 @@ class Model(Layer):
             for data in it:
                 cbl.on_train_batch_begin(step)
                 data = _to_device_tensor(data, dev)
-                logs = self.train_step(data)
+                logs = train_fn(data)
                 cbl.on_train_batch_end(step, logs)
                 step += 1
                 if self.stop_training or (steps is not None and step >= steps):

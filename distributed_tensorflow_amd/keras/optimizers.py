@@ -103,12 +103,14 @@ class Optimizer:
         self._hp = {}
         self._grad_scale = 1.0
         self._pinned = None
+        self._host_iter = None     # host mirror of `iterations` (no device sync per step)
+        self._graph = None         # set while captured in a hipGraph (see graphs.CapturedStep)
 
     # --------------------------------------------------------------- config
     def _lr_value(self, step=None):
         lr = self.learning_rate
         if isinstance(lr, LearningRateSchedule) or callable(lr):
-            return float(lr(int(self.iterations.item()) if step is None else step))
+            return float(lr(self.host_iterations() if step is None else step))
         return float(lr)
 
     def get_config(self):
@@ -195,9 +197,29 @@ class Optimizer:
         """Scale applied to every gradient inside the fused update (e.g. 1/num_replicas, 1/loss_scale)."""
         self._grad_scale = float(s)
 
+    def host_iterations(self):
+        if self._host_iter is None:
+            self._host_iter = int(self.iterations.item())
+        return self._host_iter
+
+    def reset_host_state(self):
+        """After iterations was restored (checkpoint), re-read it."""
+        self._host_iter = None
+
+    def _hp_values(self, lr):
+        return [lr, self._grad_scale / self.loss_scale, float(self.global_clipnorm or 0.0), 0.0]
+
     def _hp_tensor(self, a, lr):
         hp = self._hp.get(id(a))
-        vals = [lr, self._grad_scale / self.loss_scale, float(self.global_clipnorm or 0.0), 0.0]
+        vals = self._hp_values(lr)
+        if self._graph is not None:
+            # inside a capture: a fixed pinned buffer whose contents the capturer rewrites before
+            # every replay (graph_prestep); the captured memcpy node reads it at replay time
+            pinned = self._graph.get(id(a))
+            if pinned is None or hp is None:
+                raise RuntimeError("optimizer arena was not prepared for graph capture (graph_prepare())")
+            hp.copy_(pinned, non_blocking=True)
+            return hp
         if hp is None:
             hp = torch.tensor(vals, dtype=torch.float32, device=a.device)
             self._hp[id(a)] = hp
@@ -220,7 +242,7 @@ class Optimizer:
 
     def apply_arena(self, a, zero_grad=True):
         """Apply one update to a whole arena whose gradient buffer is already filled."""
-        t = int(self.iterations.item()) + 1
+        t = self.host_iterations() + 1
         lr = self._effective_lr(t)
         kw = self._kernel_kwargs()
         specs = self.slot_specs()
@@ -247,6 +269,27 @@ class Optimizer:
                 a.grad.zero_()
         with torch.no_grad():
             self.iterations.add_(1)
+        self._host_iter = t
+
+    def graph_prepare(self):
+        """Allocate (outside the capture: pinned allocation is not capturable) the fixed pinned
+        scalar buffer and device hp tensor of every arena, and switch `_hp_tensor` to graph mode."""
+        self._graph = {}
+        for a in self._arenas.values():
+            if a.device.type != "cuda":
+                continue
+            self._graph[id(a)] = torch.zeros(4, dtype=torch.float32).pin_memory()
+            if id(a) not in self._hp:
+                self._hp[id(a)] = torch.zeros(4, dtype=torch.float32, device=a.device)
+
+    def graph_prestep(self):
+        """Before a hipGraph replay of a captured step: advance the host step and publish the step's
+        scalars (bias-corrected lr, grad scale, clip) into the pinned buffers the graph copies from."""
+        t = self.host_iterations() + 1
+        lr = self._effective_lr(t)
+        for buf in (self._graph or {}).values():
+            buf.copy_(torch.tensor(self._hp_values(lr)))
+        self._host_iter = t
 
     def apply_gradients(self, grads_and_vars, zero_grad=True):
         gv = [(g, v) for g, v in grads_and_vars if g is not None]

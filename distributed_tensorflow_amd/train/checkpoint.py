@@ -448,6 +448,11 @@ class Checkpoint:
             r.close()
         from ..ops._util import bump_weights_epoch
         bump_weights_epoch()
+        for obj in self._objects.values():
+            if hasattr(obj, "reset_host_state"):
+                obj.reset_host_state()
+            for a in getattr(obj, "_arenas", {}).values():
+                a.refresh_bf16()
         return _RestoreStatus(matched, missing, unused)
 
     restore = read
