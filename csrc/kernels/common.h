@@ -121,3 +121,7 @@ static inline int stream_grid(long work_items, int block) {
 __global__ void __launch_bounds__(256) dtf_group_rows_kernel(float* __restrict__ rows, long stride, int nrows,
                                                              int sg, long W, float* __restrict__ out,
                                                              int accumulate);
+
+// Deterministic two-level reduction of `nrows` f32 rows (stride `stride`) into out (+= when accumulate);
+// the rows are used as scratch. Defined in gemm.hip.
+DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream);

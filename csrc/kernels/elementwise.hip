@@ -116,23 +116,43 @@ __global__ void dropout_kernel(const bf16_t* x, bf16_t* y, long n8, float keep, 
   }
 }
 
-// Column sum of a bf16 [M][N] matrix into f32 [N] (BiasAddGrad); N % 8 == 0
-__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, long M, int N,
-                                                     float* __restrict__ out) {
-  const int cols8 = N / 8;
-  const int TPR = cols8 < 256 ? cols8 : 256, RPB = 256 / TPR;
-  const int t = threadIdx.x;
-  if (t >= TPR * RPB) return;
-  for (int cc = t % TPR; cc < cols8; cc += TPR) {
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (long r = (long)blockIdx.x * RPB + t / TPR; r < M; r += (long)gridDim.x * RPB) {
+// Column partial sums of a bf16 [M][N] matrix (BiasAddGrad core), N % 8 == 0. Block (bx, by) owns columns
+// [256 bx, 256 bx + 256) (32 lanes x 8 columns, 512 contiguous bytes per row) and rows [by rpb, by rpb + rpb)
+// (8 row-threads); it writes its partial sums to part[by][N]. No atomics: dtf_sum_rows finishes the reduction
+// deterministically.
+__global__ void __launch_bounds__(256) colsum_part_kernel(const bf16_t* __restrict__ x, long M, int N, long rpb,
+                                                          float* __restrict__ part) {
+  __shared__ float red[8][257];
+  const int tc = threadIdx.x & 31, tr = threadIdx.x >> 5;
+  const long c0 = ((long)blockIdx.x * 32 + tc) * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < N) {
+    const long r0 = (long)blockIdx.y * rpb, r1 = min(M, r0 + rpb);
+    const bf16_t* p = x + c0;
+    long r = r0 + tr;
+    for (; r + 8 < r1; r += 16) {  // two independent rows in flight per thread
+      float f[8], g[8];
+      load8(p + r * N, f);
+      load8(p + (r + 8) * N, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j] + g[j];
+    }
+    if (r < r1) {
       float f[8];
-      load8(x + r * N + cc * 8, f);
+      load8(p + r * N, f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += f[j];
     }
+  }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(out + cc * 8 + j, s[j]);
+  for (int j = 0; j < 8; ++j) red[tr][tc * 8 + j] = s[j];
+  __syncthreads();
+  const long col = (long)blockIdx.x * 256 + threadIdx.x;
+  if (col < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][threadIdx.x];
+    part[(long)blockIdx.y * N + col] = t;
   }
 }
 
@@ -166,16 +186,61 @@ __global__ void embed_fwd_kernel(const bf16_t* __restrict__ t1, const long* __re
   }
 }
 
-// Embedding gradient: dtable[idx[t]] += dy[t] (f32 atomics; each wave-instruction covers contiguous row bytes)
-__global__ void embed_bwd_kernel(const bf16_t* __restrict__ dy, const long* __restrict__ idx, float* __restrict__ dt,
-                                 long T, int D, int pos_mod) {
-  long total = T * (long)D;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    long t = i / D;
-    int c = (int)(i % D);
-    long r = idx ? idx[t] : (t % pos_mod);
-    atomicAdd(dt + r * D + c, bf2f(dy[i]));
+// Embedding gradient over SORTED token ids (large vocabularies): each wave walks a slice of the sorted
+// positions; at every segment start (id differs from its predecessor) it sums the rows of the whole segment
+// (perm gives the source token) in registers and writes dtable[id] once. Deterministic, no atomics; rows of
+// untouched ids are left as they are (zeroed by the caller).
+__global__ void __launch_bounds__(256) embed_bwd_sorted_kernel(const bf16_t* __restrict__ dy,
+                                                               const long* __restrict__ sid,
+                                                               const long* __restrict__ perm,
+                                                               float* __restrict__ dt, long T, int D) {
+  const int lane = threadIdx.x & 63;
+  const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+  const int d8 = D / 8;
+  for (long i = wave; i < T; i += nw) {
+    const long id = sid[i];
+    if (i > 0 && sid[i - 1] == id) continue;
+    long e = i + 1;
+    while (e < T && sid[e] == id) ++e;
+    for (int c = lane; c < d8; c += 64) {
+      float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (long k = i; k < e; ++k) {
+        float f[8];
+        load8(dy + perm[k] * D + c * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+      float* o = dt + id * D + c * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += s[j];
+    }
   }
+}
+
+// Embedding gradient for SMALL tables (V <= 16, e.g. token types): LDS-resident [V][D] accumulators per block
+// (LDS atomics; lanes of one instruction hit distinct columns), block partials to part[block][V*D].
+__global__ void __launch_bounds__(256) embed_bwd_small_kernel(const bf16_t* __restrict__ dy,
+                                                              const long* __restrict__ idx, long T, int D, int V,
+                                                              long rpb, float* __restrict__ part) {
+  extern __shared__ float acc[];
+  const int VD = V * D;
+  for (int i = threadIdx.x; i < VD; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int d8 = D / 8;
+  const long r0 = (long)blockIdx.x * rpb, r1 = min(T, r0 + rpb);
+  for (long t = r0 + w; t < r1; t += 4) {
+    const long v = idx[t];
+    for (int c = lane; c < d8; c += 64) {
+      float f[8];
+      load8(dy + t * D + c * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(&acc[v * D + c * 8 + j], f[j]);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < VD; i += blockDim.x) part[(long)blockIdx.x * VD + i] = acc[i];
 }
 
 // Fused softmax cross-entropy over rows (logits f32 or bf16), int64 labels.
@@ -304,14 +369,23 @@ DTF_API int dtf_dropout(const void* x, void* y, long n, float keep, unsigned lon
   hipLaunchKernelGGL(dropout_kernel, GRID(n / 8), (const bf16_t*)x, (bf16_t*)y, n / 8, keep, (uint64_t)seed);
   return (int)hipGetLastError();
 }
-DTF_API int dtf_colsum(const void* x, long M, int N, float* out, int accumulate, void* stream) {
+// Column sums (BiasAddGrad): partial rows into ws, then a deterministic row reduction into out.
+DTF_API int dtf_colsum(const void* x, long M, int N, float* out, int accumulate, float* ws, long ws_elems,
+                       void* stream) {
   if (N & 7) return -1;
-  if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, (hipStream_t)stream);
-  int cols8 = N / 8, TPR = cols8 < 256 ? cols8 : 256, RPB = 256 / TPR;
-  long blocks = (M + RPB * 32L - 1) / (RPB * 32L);
-  if (blocks > 1024) blocks = 1024;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(colsum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, M, N, out);
+  hipStream_t st = (hipStream_t)stream;
+  const long gx = (N + 255) / 256;
+  long splits = std::max<long>(1, std::min<long>((M + 31) / 32, std::max<long>(1, 2048 / gx)));
+  splits = std::min<long>(splits, std::max<long>(1, ws_elems / N));
+  const long rpb = (M + splits - 1) / splits;
+  splits = (M + rpb - 1) / rpb;
+  if (M == 0) {
+    if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, st);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)gx, (unsigned)splits), dim3(256), 0, st, (const bf16_t*)x,
+                     M, N, rpb, ws);
+  dtf_sum_rows(ws, N, (int)splits, N, out, accumulate, stream);
   return (int)hipGetLastError();
 }
 DTF_API int dtf_embed_fwd(const void* t1, const long* i1, const void* t2, const long* i2, const void* t3,
@@ -321,8 +395,28 @@ DTF_API int dtf_embed_fwd(const void* t1, const long* i1, const void* t2, const 
                      (const bf16_t*)t3, i3, (bf16_t*)out, T, D, pos_mod < 1 ? 1 : pos_mod);
   return (int)hipGetLastError();
 }
-DTF_API int dtf_embed_bwd(const void* dy, const long* idx, float* dt, long T, int D, int pos_mod, void* stream) {
-  hipLaunchKernelGGL(embed_bwd_kernel, GRID(T * D), (const bf16_t*)dy, idx, dt, T, D, pos_mod < 1 ? 1 : pos_mod);
+// Large-table embedding gradient from sorted ids (see embed_bwd_sorted_kernel); dt must be pre-zeroed.
+DTF_API int dtf_embed_bwd_sorted(const void* dy, const long* sid, const long* perm, float* dt, long T, int D,
+                                 void* stream) {
+  if (D & 7) return -1;
+  long blocks = std::min<long>((T + 3) / 4, 4096);
+  hipLaunchKernelGGL(embed_bwd_sorted_kernel, dim3((unsigned)std::max<long>(blocks, 1)), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16_t*)dy, sid, perm, dt, T, D);
+  return (int)hipGetLastError();
+}
+// Small-table (V <= 16) embedding gradient: out[V][D] (+)= sum over tokens.
+DTF_API int dtf_embed_bwd_small(const void* dy, const long* idx, float* out, long T, int D, int V, int accumulate,
+                                float* ws, long ws_elems, void* stream) {
+  if ((D & 7) || V < 1 || V * D > 16384) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const long VD = (long)V * D;
+  long blocks = std::max<long>(1, std::min<long>((T + 63) / 64, 1024));
+  blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / VD));
+  const long rpb = (T + blocks - 1) / blocks;
+  blocks = (T + rpb - 1) / rpb;
+  hipLaunchKernelGGL(embed_bwd_small_kernel, dim3((unsigned)blocks), dim3(256), sizeof(float) * VD, st,
+                     (const bf16_t*)dy, idx, T, D, V, rpb, ws);
+  dtf_sum_rows(ws, VD, (int)blocks, VD, out, accumulate, stream);
   return (int)hipGetLastError();
 }
 DTF_API int dtf_softmax_ce(const void* logits, int in_f32, const long* labels, float* loss, void* dlogits,

@@ -253,7 +253,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
   }
 }
 
-// ---------------- LayerNorm: one wave per row, D % 8 == 0 ----------------
+// ---------------- LayerNorm: one wave per row, D % 8 == 0, D <= 512 * NC ----------------
+// The row lives in registers (NC 16-byte chunks per lane): one HBM read, one write.
+template <int NC>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -263,82 +265,110 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
   if (row >= M) return;
   const bf16_t* xr = x + row * D;
   const int d8 = D / 8;
-  float s = 0.f, q = 0.f;
-  for (int c = lane; c < d8; c += 64) {
-    float f[8];
-    load8(xr + c * 8, f);
+  float f[NC][8];
+  float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += f[j];
-  }
-  s = wave_sum(s);
-  const float mu = s / D;
-  for (int c = lane; c < d8; c += 64) {
-    float f[8];
-    load8(xr + c * 8, f);
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + 64 * k;
+    if (c < d8) {
+      load8(xr + c * 8, f[k]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { float t = f[j] - mu; q += t * t; }
+      for (int j = 0; j < 8; ++j) s += f[k][j];
+    }
   }
-  q = wave_sum(q);
-  const float rs = rsqrtf(q / D + eps);
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+    if (lane + 64 * k < d8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { float t = f[k][j] - mu; q += t * t; }
+    }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
   if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
-  for (int c = lane; c < d8; c += 64) {
-    float f[8];
-    load8(xr + c * 8, f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = (f[j] - mu) * rs * gamma[c * 8 + j] + beta[c * 8 + j];
-    store8(y + row * D + c * 8, f);
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + 64 * k;
+    if (c < d8) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (f[k][j] - mu) * rs * gamma[c * 8 + j] + beta[c * 8 + j];
+      store8(y + row * D + c * 8, o);
+    }
   }
 }
 
-// dx = rstd * (g*dy - mean(g*dy) - xhat*mean(g*dy*xhat)); dgamma/dbeta partials per block -> atomics
+// dx = rstd * (g*dy - mean(g*dy) - xhat*mean(g*dy*xhat)). Every lane owns the same columns in every row it
+// visits, so dgamma/dbeta accumulate in registers across rows; the 4 waves combine through LDS and each
+// block writes one partial row part[block][2D] (dgamma | dbeta) for a deterministic dtf_sum_rows.
+template <int NC>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, bf16_t* __restrict__ dx,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                     long M, int D, int rows_per_block) {
-  extern __shared__ float sred[];  // [2][D] block partials
+                                                     float* __restrict__ part, long M, int D) {
+  extern __shared__ float sred[];  // [4][2D]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) sred[i] = 0.f;
-  __syncthreads();
   const int d8 = D / 8;
-  const long r0 = (long)blockIdx.x * rows_per_block;
-  for (long row = r0 + w; row < min(M, r0 + rows_per_block); row += 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float a = 0.f, b = 0.f;
-    for (int c = lane; c < d8; c += 64) {
-      float f[8], g[8];
-      load8(x + row * D + c * 8, f);
-      load8(dy + row * D + c * 8, g);
+  float gm[NC][8], ag[NC][8], ab[NC][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float xh = (f[j] - mu) * rs;
-        float gd = g[j] * gamma[c * 8 + j];
-        a += gd;
-        b += gd * xh;
-        atomicAdd(&sred[c * 8 + j], g[j] * xh);
-        atomicAdd(&sred[D + c * 8 + j], g[j]);
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + 64 * k;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      gm[k][j] = c < d8 ? gamma[c * 8 + j] : 0.f;
+      ag[k][j] = 0.f;
+      ab[k][j] = 0.f;
+    }
+  }
+  for (long row = (long)blockIdx.x * 4 + w; row < M; row += (long)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NC][8], g[NC][8];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + 64 * k;
+      if (c < d8) {
+        load8(x + row * D + c * 8, xh[k]);
+        load8(dy + row * D + c * 8, g[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[k][j] = (xh[k][j] - mu) * rs;
+          const float gd = g[k][j] * gm[k][j];
+          a += gd;
+          b += gd * xh[k][j];
+          ag[k][j] += g[k][j] * xh[k][j];
+          ab[k][j] += g[k][j];
+        }
       }
     }
     a = wave_sum(a) / D;
     b = wave_sum(b) / D;
-    for (int c = lane; c < d8; c += 64) {
-      float f[8], g[8], o[8];
-      load8(x + row * D + c * 8, f);
-      load8(dy + row * D + c * 8, g);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + 64 * k;
+      if (c < d8) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (g[k][j] * gm[k][j] - a - xh[k][j] * b);
+        store8(dx + row * D + c * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + 64 * k;
+    if (c < d8) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float xh = (f[j] - mu) * rs;
-        o[j] = rs * (g[j] * gamma[c * 8 + j] - a - xh * b);
+        sred[w * 2 * D + c * 8 + j] = ag[k][j];
+        sred[w * 2 * D + D + c * 8 + j] = ab[k][j];
       }
-      store8(dx + row * D + c * 8, o);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < D; i += blockDim.x) {
-    atomicAdd(dgamma + i, sred[i]);
-    atomicAdd(dbeta + i, sred[D + i]);
-  }
+  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x)
+    part[(long)blockIdx.x * 2 * D + i] = sred[i] + sred[2 * D + i] + sred[4 * D + i] + sred[6 * D + i];
 }
 
 int red_grid(long M, int C) {
@@ -415,20 +445,32 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* x, const f
   return (int)hipGetLastError();
 }
 
+#define DTF_LN_DISPATCH(D, F) \
+  if ((D) <= 512) F(1); else if ((D) <= 1024) F(2); else if ((D) <= 1536) F(3); else F(4)
+
 DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
                               float* rstd, long M, int D, float eps, void* stream) {
-  if (D & 7) return -1;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, gamma,
-                     beta, (bf16_t*)y, mean, rstd, M, D, eps);
+  if ((D & 7) || D > 2048) return -1;
+#define LNF(NC) \
+  hipLaunchKernelGGL(ln_fwd_kernel<NC>, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream,             \
+                      (const bf16_t*)x, gamma, beta, (bf16_t*)y, mean, rstd, M, D, eps)
+  DTF_LN_DISPATCH(D, LNF);
+#undef LNF
   return (int)hipGetLastError();
 }
 
+// dgb = [dgamma | dbeta] (2D floats, overwritten); ws >= min(1024, M/16 + 1) * 2D floats.
 DTF_API int dtf_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
-                              void* dx, float* dgamma, float* dbeta, long M, int D, void* stream) {
-  if (D & 7) return -1;
-  int rpb = 64;
-  size_t sh = sizeof(float) * 2 * D;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(cdiv(M, rpb)), dim3(256), sh, (hipStream_t)stream, (const bf16_t*)dy,
-                     (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, dgamma, dbeta, M, D, rpb);
+                              void* dx, float* dgb, float* ws, long ws_elems, long M, int D, void* stream) {
+  if ((D & 7) || D > 2048) return -1;
+  long blocks = std::max<long>(1, std::min<long>(cdiv(M, 16), 1024));
+  blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / (2L * D)));
+  const size_t sh = sizeof(float) * 8 * D;
+#define LNB(NC) \
+  hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3((unsigned)blocks), dim3(256), sh, (hipStream_t)stream,       \
+                      (const bf16_t*)dy, (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, ws, M, D)
+  DTF_LN_DISPATCH(D, LNB);
+#undef LNB
+  dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, 0, stream);
   return (int)hipGetLastError();
 }

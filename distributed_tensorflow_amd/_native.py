@@ -32,7 +32,7 @@ _KERNEL_SIGS = {
     "dtf_bn_apply": [P, P, P, P, P, L, I, I, P],
     "dtf_bn_bwd": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, P],
     "dtf_layernorm_fwd": [P, P, P, P, P, P, L, I, F, P],
-    "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, I, P],
+    "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, P],
     "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "dtf_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
     "dtf_gap_fwd": [P, P, I, I, I, I, P],
@@ -46,9 +46,10 @@ _KERNEL_SIGS = {
     "dtf_add_bf16": [P, P, P, L, F, F, P],
     "dtf_act": [P, P, P, L, I, I, P],
     "dtf_dropout": [P, P, L, F, U, P],
-    "dtf_colsum": [P, L, I, P, I, P],
+    "dtf_colsum": [P, L, I, P, I, P, L, P],
     "dtf_embed_fwd": [P, P, P, P, P, P, P, L, I, I, P],
-    "dtf_embed_bwd": [P, P, P, L, I, I, P],
+    "dtf_embed_bwd_sorted": [P, P, P, P, L, I, P],
+    "dtf_embed_bwd_small": [P, P, P, L, I, I, I, P, L, P],
     "dtf_softmax_ce": [P, I, P, P, P, I, L, I, F, F, P],
     "dtf_softmax_fwd": [P, P, L, I, I, F, I, P, P],
     "dtf_softmax_bwd": [P, P, P, L, I, F, P],

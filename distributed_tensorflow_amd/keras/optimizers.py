@@ -290,6 +290,9 @@ class Optimizer:
         for buf in (self._graph or {}).values():
             buf.copy_(torch.tensor(self._hp_values(lr)))
         self._host_iter = t
+        if not self.iterations.is_cuda:  # host-resident counter: the capture ran its add_ only once
+            with torch.no_grad():
+                self.iterations.fill_(t)
 
     def apply_gradients(self, grads_and_vars, zero_grad=True):
         gv = [(g, v) for g, v in grads_and_vars if g is not None]

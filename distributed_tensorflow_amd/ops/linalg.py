@@ -119,7 +119,8 @@ def colsum(x2d, out=None, accumulate=False):
         return out.add_(r) if accumulate else out.copy_(r)
     if out is None:
         out = torch.empty(N, dtype=F32, device=x2d.device)
-    call("dtf_colsum", ptr(x2d), M, N, ptr(out), int(accumulate), stream())
+    ws = workspace(x2d.device)
+    call("dtf_colsum", ptr(x2d), M, N, ptr(out), int(accumulate), ptr(ws), ws.numel(), stream())
     return out
 
 

@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, call, on_gpu, ptr, stream
+from ._util import BF16, F32, call, on_gpu, ptr, stream, workspace
 from .conv import out_size
 
 
@@ -177,18 +177,26 @@ class _EmbedFn(torch.autograd.Function):
         dy = dy.to(BF16).contiguous()
         T = ids.numel()
         D = tshape[1]
+        ws = workspace(dy.device)
+        # word table: sort the ids once, then one deterministic segment-sum per distinct id (no atomics)
         dt = torch.zeros(tshape, dtype=F32, device=dy.device)
-        call("dtf_embed_bwd", ptr(dy), ptr(ids), ptr(dt), T, D, 1, stream())
+        sid, perm = torch.sort(ids.reshape(-1))
+        call("dtf_embed_bwd_sorted", ptr(dy), ptr(sid), ptr(perm), ptr(dt), T, D, stream())
         dp = dy_ = None
-        if pshape is not None:
+        if pshape is not None:  # positions: dp[s] = sum over the batch of dy[b, s]  (a column sum)
             dp = torch.zeros(pshape, dtype=F32, device=dy.device)
-            call("dtf_embed_bwd", ptr(dy), None, ptr(dp), T, D, int(seq_len), stream())
+            S = int(seq_len)
+            call("dtf_colsum", ptr(dy), T // S, S * D, ptr(dp), 0, ptr(ws), ws.numel(), stream())
         if yshape is not None:
             dy_ = torch.zeros(yshape, dtype=F32, device=dy.device)
-            if tid is not None:
-                call("dtf_embed_bwd", ptr(dy), ptr(tid), ptr(dy_), T, D, 1, stream())
-            else:
-                call("dtf_embed_bwd", ptr(dy), None, ptr(dy_), T, D, 1, stream())
+            if tid is not None and yshape[0] <= 16:
+                call("dtf_embed_bwd_small", ptr(dy), ptr(tid), ptr(dy_), T, D, yshape[0], 0, ptr(ws), ws.numel(),
+                     stream())
+            elif tid is not None:
+                sid2, perm2 = torch.sort(tid.reshape(-1))
+                call("dtf_embed_bwd_sorted", ptr(dy), ptr(sid2), ptr(perm2), ptr(dy_), T, D, stream())
+            else:  # no type ids: every token uses row 0
+                call("dtf_colsum", ptr(dy), T, D, ptr(dy_), 0, ptr(ws), ws.numel(), stream())
         return None, dt, dp, None, dy_, None
 
 

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, IntOut, call, on_gpu, ptr, stream
+from ._util import BF16, F32, IntOut, call, on_gpu, ptr, stream, workspace
 
 
 def batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training):
@@ -105,11 +105,11 @@ class _LNFn(torch.autograd.Function):
         M = x.numel() // D
         dy = dy.to(BF16).contiguous()
         dx = torch.empty_like(x)
-        dg = torch.zeros(D, dtype=F32, device=x.device)
-        db = torch.zeros(D, dtype=F32, device=x.device)
-        call("dtf_layernorm_bwd", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(dg), ptr(db), M, D,
-             stream())
-        return dx, dg, db, None
+        dgb = torch.empty(2 * D, dtype=F32, device=x.device)
+        ws = workspace(x.device)
+        call("dtf_layernorm_bwd", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(dgb), ptr(ws),
+             ws.numel(), M, D, stream())
+        return dx, dgb[:D], dgb[D:], None
 
 
 def layer_norm(x, gamma, beta, eps=1e-5):

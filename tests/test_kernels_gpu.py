@@ -209,6 +209,53 @@ def test_layernorm(cuda):
     close(b.grad, br.grad, 1e-2)
 
 
+@pytest.mark.parametrize("M,D", [(3001, 1024), (257, 1536), (64, 2048), (20000, 768), (5, 264)])
+def test_layernorm_shapes(cuda, M, D):
+    x = rnd(M, D, dev=cuda).requires_grad_(True)
+    g = (torch.rand(D, device=cuda) + 0.5).requires_grad_(True)
+    b = torch.randn(D, device=cuda).requires_grad_(True)
+    y = ops.layer_norm(x, g, b, 1e-5)
+    xr = x.detach().float().requires_grad_(True)
+    gr, br = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-5)
+    close(y, yr, 1e-2)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    y.backward(dy.to(BF))
+    close(x.grad, xr.grad, 2e-2)
+    close(g.grad, gr.grad, 1e-2)
+    close(b.grad, br.grad, 1e-2)
+
+
+@pytest.mark.parametrize("M,N", [(16384, 768), (7, 3072), (1000, 776), (33, 30528)])
+def test_colsum(cuda, M, N):
+    x = rnd(M, N, dev=cuda).to(BF)
+    out = ops.linalg.colsum(x)
+    close(out, x.float().sum(0), 1e-3)
+    out2 = torch.ones(N, device=cuda)
+    ops.linalg.colsum(x, out=out2, accumulate=True)
+    close(out2, x.float().sum(0) + 1, 1e-3)
+
+
+def test_embedding_types_random_grad(cuda):
+    V, S, B, D = 3000, 128, 8, 128
+    table = torch.randn(V, D, device=cuda).requires_grad_(True)
+    pos = torch.randn(256, D, device=cuda).requires_grad_(True)
+    typ = torch.randn(2, D, device=cuda).requires_grad_(True)
+    ids = torch.randint(0, 50, (B, S), device=cuda)  # heavy repetition
+    tids = torch.randint(0, 2, (B, S), device=cuda)
+    y = ops.embedding(ids, table, pos, tids, typ)
+    dy = torch.randn(B, S, D, device=cuda).to(BF)
+    y.backward(dy)
+    t_r, p_r, y_r = (t.detach().to(BF).float().requires_grad_(True) for t in (table, pos, typ))
+    yr = t_r[ids] + p_r[:S][None] + y_r[tids]
+    close(y, yr, 1e-2)
+    yr.backward(dy.float())
+    close(table.grad, t_r.grad, 1e-3)
+    close(pos.grad, p_r.grad, 1e-3)
+    close(typ.grad, y_r.grad, 1e-3)
+
+
 def test_softmax_masked(cuda):
     x = rnd(2, 4, 128, 128, dev=cuda).requires_grad_(True)
     y = ops.softmax(x, scale=0.125, causal=True)
