@@ -1,0 +1,588 @@
+// Fused multi-head attention for gfx950: FlashAttention-2-style forward (online softmax,
+// never materialising the [S, S] score matrix), and a two-kernel backward (dK/dV by key blocks, dQ by query
+// blocks: no atomics, deterministic). Head dim 64, bf16 in/out, f32 accumulation on
+// v_mfma_f32_16x16x32_bf16.
+//
+// Orientation trick: scores are computed TRANSPOSED (S^T = K Q^T, keys on MFMA rows, queries on the
+// 16-lane column index), so each lane owns one query column and its softmax statistics stay in the lane
+// that also owns that query's output accumulators (O^T = V^T P^T). The P fragment that feeds the second
+// MFMA is assembled from the lane's own score registers; the matching V^T fragment is read with
+// ds_read_b64_tr_b16 with its k-rows permuted to the same slot order (slot 4h+q <-> row 16h+4G+q).
+// Q, K, V, O and the gradients are addressed with (batch, seq, head) strides, so the kernels read the
+// packed QKV projection output [B, S, 3, H, 64] and write O as [B, S, H, 64] with no head transposes.
+// Dropout on P is regenerated from a counter hash of (b*H+h, q, k) in forward and backward.
+#include "common.h"
+
+namespace {
+
+constexpr int HD = 64;  // head dim
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct AttnArgs {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  bf16_t* o;
+  const bf16_t* dout;
+  bf16_t* dq;
+  bf16_t* dk;
+  bf16_t* dv;
+  float* lse;          // [B*H][Sq], log2 domain
+  float* dvec;         // [B*H][Sq], rowsum(dO * O)
+  const float* kmask;  // optional additive key mask [B][Sk] (natural-log units)
+  long qsb, qss, qsh;  // strides (elements) of q/k/v and dq/dk/dv: batch, sequence, head
+  long osb, oss, osh;  // strides of o / dout
+  int B, H, Sq, Sk;
+  float scale;
+  float keep;  // 1 - dropout rate
+  uint32_t seed;
+  int causal;
+};
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+// keep-decision for element (bh, q, k)
+__device__ __forceinline__ bool drop_keep(const AttnArgs& a, int bh, int q, int k) {
+  uint64_t idx = ((uint64_t)bh * (uint64_t)a.Sq + (uint64_t)q) * (uint64_t)a.Sk + (uint64_t)k;
+  uint32_t h = fmix32((uint32_t)idx ^ fmix32((uint32_t)(idx >> 32) + a.seed));
+  return (float)(h >> 8) * (1.f / 16777216.f) < a.keep;
+}
+
+// ---- [64 rows][64 cols] bf16 LDS tile, 128 B rows, 16-B chunk XOR swizzle ----
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+struct TileRegs {
+  uint4 r[2];
+};
+__device__ __forceinline__ void tile_load(TileRegs& t, const bf16_t* base, long rs, int row0, int nrows) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int idx = threadIdx.x + 256 * u, row = idx >> 3, c = idx & 7;
+    if (row0 + row < nrows)
+      t.r[u] = *reinterpret_cast<const uint4*>(base + (long)(row0 + row) * rs + c * 8);
+    else
+      t.r[u] = make_uint4(0, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void tile_store(const TileRegs& t, char* lds) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int idx = threadIdx.x + 256 * u, row = idx >> 3, c = idx & 7;
+    *reinterpret_cast<uint4*>(lds + swz(row, c)) = t.r[u];
+  }
+}
+// row fragment: lane (G, i) gets row rb + i, columns 32 kk + 8 G .. + 7
+__device__ __forceinline__ v8bf frag_row(const char* lds, int rb, int kk, int lane) {
+  return *reinterpret_cast<const v8bf*>(lds + swz(rb + (lane & 15), 4 * kk + (lane >> 4)));
+}
+// transposed fragment: lane (G, i) gets column cb + i at rows rb + 16 h + 4 G + q  (slot j = 4 h + q)
+__device__ __forceinline__ v8bf frag_tr(const char* lds, int rb, int cb, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  v4s r[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = rb + 16 * h + 4 * G + q, g = (cb >> 2) + p;
+    r[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, lds + swz(row, g >> 1) + (g & 1) * 8));
+  }
+  v8s both = __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(v8bf, both);
+}
+// global 16-B fragment of a row (zeros when out of range)
+__device__ __forceinline__ v8bf frag_global(const bf16_t* rowp, bool ok) {
+  uint4 u = ok ? *reinterpret_cast<const uint4*>(rowp) : make_uint4(0, 0, 0, 0);
+  return __builtin_bit_cast(v8bf, u);
+}
+// pack the lane's slot values: slots 0..3 from tile h=0 regs, 4..7 from tile h=1 regs
+__device__ __forceinline__ v8bf pack_slots(const v4f& t0, const v4f& t1) {
+  uint4 u;
+  u.x = pack2bf(t0[0], t0[1]);
+  u.y = pack2bf(t0[2], t0[3]);
+  u.z = pack2bf(t1[0], t1[1]);
+  u.w = pack2bf(t1[2], t1[3]);
+  return __builtin_bit_cast(v8bf, u);
+}
+__device__ __forceinline__ v4f mfma(v8bf a, v8bf b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void store4(bf16_t* p, const v4f& v, float s) {
+  uint2 u;
+  u.x = pack2bf(v[0] * s, v[1] * s);
+  u.y = pack2bf(v[2] * s, v[3] * s);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+
+// ------------------------------------------------------------------------------------------------ forward
+// block: 4 waves x (16 QT) queries; grid (cdiv(Sq, 64 QT), B*H)
+template <int QT>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sk[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sv[64 * 128];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qblk = gridDim.x - 1 - blockIdx.x;  // heavy (causal) blocks first
+  const int BM = 64 * QT;
+  const int q0 = qblk * BM + w * 16 * QT;
+  const bf16_t* Q = a.q + b * a.qsb + h * a.qsh;
+  const bf16_t* K = a.k + b * a.qsb + h * a.qsh;
+  const bf16_t* V = a.v + b * a.qsb + h * a.qsh;
+  const int off = a.Sk - a.Sq;
+  const float c = a.scale * LOG2E;
+  const bool drop = a.keep < 1.f;
+  const float inv_keep = 1.f / a.keep;
+
+  v8bf qf[QT][2];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int qi = q0 + 16 * qt + i;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) qf[qt][kk] = frag_global(Q + (long)qi * a.qss + 32 * kk + 8 * G, qi < a.Sq);
+  }
+  v4f o[4][QT];
+  float m[QT], l[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    m[qt] = -INFINITY;
+    l[qt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  int kend = a.Sk;
+  if (a.causal) kend = min(a.Sk, qblk * BM + BM + off);
+  const int ntiles = (kend + 63) / 64;
+  TileRegs tk, tv;
+  if (ntiles > 0) {
+    tile_load(tk, K, a.qss, 0, a.Sk);
+    tile_load(tv, V, a.qss, 0, a.Sk);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();
+    tile_store(tk, sk);
+    tile_store(tv, sv);
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      tile_load(tk, K, a.qss, (t + 1) * 64, a.Sk);
+      tile_load(tv, V, a.qss, (t + 1) * 64, a.Sk);
+    }
+    const int k0 = t * 64;
+    v4f s[4][QT];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const v8bf k0f = frag_row(sk, 16 * kt, 0, lane), k1f = frag_row(sk, 16 * kt, 1, lane);
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        v4f acc = {0.f, 0.f, 0.f, 0.f};
+        acc = mfma(k0f, qf[qt][0], acc);
+        s[kt][qt] = mfma(k1f, qf[qt][1], acc);
+      }
+    }
+    float km[4][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * kt + 4 * G + r;
+        km[kt][r] = key >= a.Sk ? -INFINITY : (a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f);
+      }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      const int qi = q0 + 16 * qt + i;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * kt + 4 * G + r;
+          float x = s[kt][qt][r] * c + km[kt][r];
+          if (a.causal && key > qi + off) x = -INFINITY;
+          s[kt][qt][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m[qt], mx);
+      const float ms = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = exp2f(m[qt] - ms);
+      m[qt] = mnew;
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = exp2f(s[kt][qt][r] - ms);
+          ls += p;
+          if (drop) p = drop_keep(a, bh, qi, k0 + 16 * kt + 4 * G + r) ? p * inv_keep : 0.f;
+          s[kt][qt][r] = p;
+        }
+      l[qt] = l[qt] * alpha + ls;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt][qt] *= alpha;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8bf pf[QT];
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) pf[qt] = pack_slots(s[2 * kk][qt], s[2 * kk + 1][qt]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const v8bf vf = frag_tr(sv, 32 * kk, 16 * dt, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) o[dt][qt] = mfma(vf, pf[qt], o[dt][qt]);
+      }
+    }
+  }
+  bf16_t* O = a.o + b * a.osb + h * a.osh;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    float L = l[qt] + __shfl_xor(l[qt], 16, 64);
+    L += __shfl_xor(L, 32, 64);
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    const int qi = q0 + 16 * qt + i;
+    if (qi < a.Sq) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4(O + (long)qi * a.oss + 16 * dt + 4 * G, o[dt][qt], inv);
+      if (G == 0) a.lse[(long)bh * a.Sq + qi] = L > 0.f ? m[qt] + log2f(L) : INFINITY;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ backward
+// D[q] = sum_d dO[q][d] * O[q][d]; one thread per (bh, q) row
+__global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
+  const long n = (long)a.B * a.H * a.Sq;
+  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(r % a.Sq);
+    const long bh = r / a.Sq;
+    const int b = (int)(bh / a.H), h = (int)(bh % a.H);
+    const long base = b * a.osb + h * a.osh + (long)q * a.oss;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < HD / 8; ++c) {
+      float x[8], y[8];
+      load8(a.o + base + c * 8, x);
+      load8(a.dout + base + c * 8, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+    }
+    a.dvec[r] = s;
+  }
+}
+
+// dK, dV: block = 4 waves x (16 KT) keys, loop over 64-query tiles; grid (cdiv(Sk, 64 KT), B*H)
+template <int KT>
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sq[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sdo[64 * 128];
+  __shared__ float slse[64], sdv[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int BN = 64 * KT;
+  const int kblk = blockIdx.x;
+  const int k0w = kblk * BN + w * 16 * KT;
+  const long hb = b * a.qsb + h * a.qsh, ob = b * a.osb + h * a.osh;
+  const bf16_t* Q = a.q + hb;
+  const bf16_t* K = a.k + hb;
+  const bf16_t* V = a.v + hb;
+  const bf16_t* dO = a.dout + ob;
+  const int off = a.Sk - a.Sq;
+  const float c = a.scale * LOG2E;
+  const bool drop = a.keep < 1.f;
+  const float inv_keep = 1.f / a.keep;
+
+  v8bf kf[KT][2], vf[KT][2];
+  float km[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const int key = k0w + 16 * kt + i;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      kf[kt][kk] = frag_global(K + (long)key * a.qss + 32 * kk + 8 * G, key < a.Sk);
+      vf[kt][kk] = frag_global(V + (long)key * a.qss + 32 * kk + 8 * G, key < a.Sk);
+    }
+    km[kt] = key >= a.Sk ? -INFINITY : (a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f);
+  }
+  v4f dk[4][KT], dv[4][KT];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      dk[dt][kt] = v4f{0.f, 0.f, 0.f, 0.f};
+      dv[dt][kt] = v4f{0.f, 0.f, 0.f, 0.f};
+    }
+  int qstart = 0;
+  if (a.causal) qstart = max(0, (kblk * BN - off) / 64 * 64);
+  const int ntiles = qstart >= a.Sq ? 0 : (a.Sq - qstart + 63) / 64;
+  TileRegs tq, td;
+  if (ntiles > 0) {
+    tile_load(tq, Q, a.qss, qstart, a.Sq);
+    tile_load(td, dO, a.oss, qstart, a.Sq);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    const int q0 = qstart + t * 64;
+    __syncthreads();
+    tile_store(tq, sq);
+    tile_store(td, sdo);
+    if (threadIdx.x < 64) {
+      const int qi = q0 + threadIdx.x;
+      slse[threadIdx.x] = qi < a.Sq ? a.lse[(long)bh * a.Sq + qi] : INFINITY;
+      sdv[threadIdx.x] = qi < a.Sq ? a.dvec[(long)bh * a.Sq + qi] : 0.f;
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      tile_load(tq, Q, a.qss, q0 + 64, a.Sq);
+      tile_load(td, dO, a.oss, q0 + 64, a.Sq);
+    }
+    v4f P[4][KT], dS[4][KT];
+#pragma unroll
+    for (int qs = 0; qs < 4; ++qs) {
+      const v8bf q0f = frag_row(sq, 16 * qs, 0, lane), q1f = frag_row(sq, 16 * qs, 1, lane);
+      const v8bf d0f = frag_row(sdo, 16 * qs, 0, lane), d1f = frag_row(sdo, 16 * qs, 1, lane);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+        s = mfma(q0f, kf[kt][0], s);
+        s = mfma(q1f, kf[kt][1], s);
+        dp = mfma(d0f, vf[kt][0], dp);
+        dp = mfma(d1f, vf[kt][1], dp);
+        const int key = k0w + 16 * kt + i;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = 16 * qs + 4 * G + r, qi = q0 + ql;
+          float x = s[r] * c + km[kt];
+          if (a.causal && key > qi + off) x = -INFINITY;
+          const float p = exp2f(x - slse[ql]);
+          float pd = p, dpv = dp[r];
+          if (drop) {
+            const bool z = drop_keep(a, bh, qi, key);
+            pd = z ? p * inv_keep : 0.f;
+            dpv = z ? dpv * inv_keep : 0.f;
+          }
+          P[qs][kt][r] = pd;
+          dS[qs][kt][r] = p * (dpv - sdv[ql]);
+        }
+      }
+    }
+#pragma unroll
+    for (int kq = 0; kq < 2; ++kq) {
+      v8bf pf[KT], sf[KT];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        pf[kt] = pack_slots(P[2 * kq][kt], P[2 * kq + 1][kt]);
+        sf[kt] = pack_slots(dS[2 * kq][kt], dS[2 * kq + 1][kt]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const v8bf dof = frag_tr(sdo, 32 * kq, 16 * dt, lane);
+        const v8bf qtf = frag_tr(sq, 32 * kq, 16 * dt, lane);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          dv[dt][kt] = mfma(dof, pf[kt], dv[dt][kt]);
+          dk[dt][kt] = mfma(qtf, sf[kt], dk[dt][kt]);
+        }
+      }
+    }
+  }
+  bf16_t* dK = a.dk + hb;
+  bf16_t* dV = a.dv + hb;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const int key = k0w + 16 * kt + i;
+    if (key < a.Sk) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        store4(dK + (long)key * a.qss + 16 * dt + 4 * G, dk[dt][kt], a.scale);
+        store4(dV + (long)key * a.qss + 16 * dt + 4 * G, dv[dt][kt], 1.f);
+      }
+    }
+  }
+}
+
+// dQ: block = 4 waves x (16 QT) queries, loop over 64-key tiles; grid (cdiv(Sq, 64 QT), B*H)
+template <int QT>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sk[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sv[64 * 128];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qblk = gridDim.x - 1 - blockIdx.x;
+  const int BM = 64 * QT;
+  const int q0 = qblk * BM + w * 16 * QT;
+  const long hb = b * a.qsb + h * a.qsh, ob = b * a.osb + h * a.osh;
+  const bf16_t* Q = a.q + hb;
+  const bf16_t* K = a.k + hb;
+  const bf16_t* V = a.v + hb;
+  const bf16_t* dO = a.dout + ob;
+  const int off = a.Sk - a.Sq;
+  const float c = a.scale * LOG2E;
+  const bool drop = a.keep < 1.f;
+  const float inv_keep = 1.f / a.keep;
+
+  v8bf qf[QT][2], df[QT][2];
+  float lse[QT], dd[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int qi = q0 + 16 * qt + i;
+    const bool ok = qi < a.Sq;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[qt][kk] = frag_global(Q + (long)qi * a.qss + 32 * kk + 8 * G, ok);
+      df[qt][kk] = frag_global(dO + (long)qi * a.oss + 32 * kk + 8 * G, ok);
+    }
+    lse[qt] = ok ? a.lse[(long)bh * a.Sq + qi] : INFINITY;
+    dd[qt] = ok ? a.dvec[(long)bh * a.Sq + qi] : 0.f;
+  }
+  v4f dq[4][QT];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) dq[dt][qt] = v4f{0.f, 0.f, 0.f, 0.f};
+  int kend = a.Sk;
+  if (a.causal) kend = min(a.Sk, qblk * BM + BM + off);
+  const int ntiles = (kend + 63) / 64;
+  TileRegs tk, tv;
+  if (ntiles > 0) {
+    tile_load(tk, K, a.qss, 0, a.Sk);
+    tile_load(tv, V, a.qss, 0, a.Sk);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();
+    tile_store(tk, sk);
+    tile_store(tv, sv);
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      tile_load(tk, K, a.qss, (t + 1) * 64, a.Sk);
+      tile_load(tv, V, a.qss, (t + 1) * 64, a.Sk);
+    }
+    const int k0 = t * 64;
+    v4f dS[4][QT];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const v8bf k0f = frag_row(sk, 16 * kt, 0, lane), k1f = frag_row(sk, 16 * kt, 1, lane);
+      const v8bf v0f = frag_row(sv, 16 * kt, 0, lane), v1f = frag_row(sv, 16 * kt, 1, lane);
+      float km[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * kt + 4 * G + r;
+        km[r] = key >= a.Sk ? -INFINITY : (a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f);
+      }
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+        s = mfma(k0f, qf[qt][0], s);
+        s = mfma(k1f, qf[qt][1], s);
+        dp = mfma(v0f, df[qt][0], dp);
+        dp = mfma(v1f, df[qt][1], dp);
+        const int qi = q0 + 16 * qt + i;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * kt + 4 * G + r;
+          float x = s[r] * c + km[r];
+          if (a.causal && key > qi + off) x = -INFINITY;
+          const float p = exp2f(x - lse[qt]);
+          float dpv = dp[r];
+          if (drop) dpv = drop_keep(a, bh, qi, key) ? dpv * inv_keep : 0.f;
+          dS[kt][qt][r] = p * (dpv - dd[qt]);
+        }
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8bf sf[QT];
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) sf[qt] = pack_slots(dS[2 * kk][qt], dS[2 * kk + 1][qt]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const v8bf ktf = frag_tr(sk, 32 * kk, 16 * dt, lane);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) dq[dt][qt] = mfma(ktf, sf[qt], dq[dt][qt]);
+      }
+    }
+  }
+  bf16_t* dQ = a.dq + hb;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int qi = q0 + 16 * qt + i;
+    if (qi < a.Sq) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store4(dQ + (long)qi * a.qss + 16 * dt + 4 * G, dq[dt][qt], a.scale);
+    }
+  }
+}
+
+AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const void* o, const void* dout,
+                   const long* ostr, int B, int H, int Sq, int Sk, float scale, float dropout,
+                   unsigned long long seed, int causal, const float* kmask) {
+  AttnArgs a{};
+  a.q = (const bf16_t*)q;
+  a.k = (const bf16_t*)k;
+  a.v = (const bf16_t*)v;
+  a.o = (bf16_t*)o;
+  a.dout = (const bf16_t*)dout;
+  a.qsb = qstr[0];
+  a.qss = qstr[1];
+  a.qsh = qstr[2];
+  a.osb = ostr[0];
+  a.oss = ostr[1];
+  a.osh = ostr[2];
+  a.B = B;
+  a.H = H;
+  a.Sq = Sq;
+  a.Sk = Sk;
+  a.scale = scale;
+  a.keep = 1.f - dropout;
+  a.seed = (uint32_t)(seed ^ (seed >> 32));
+  a.causal = causal;
+  a.kmask = kmask;
+  return a;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// q/k/v: bf16 with strides qstr = {batch, seq, head} (elements; head dim contiguous, 64), o/out strides ostr.
+// lse: f32 [B*H][Sq]. kmask: optional f32 [B][Sk] additive (0 keep, large negative drop). dropout on P.
+DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long* qstr, void* o, const long* ostr,
+                         float* lse, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
+                         float dropout, unsigned long long seed, int causal, void* stream) {
+  if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o)) return -1;
+  if ((qstr[0] | qstr[1] | qstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
+  if (dropout < 0.f || dropout >= 1.f) return -1;
+  AttnArgs a = make_args(q, k, v, qstr, o, nullptr, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
+  a.lse = lse;
+  dim3 grid((unsigned)((Sq + 127) / 128), (unsigned)(B * H));
+  hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// dq/dk/dv share the q/k/v strides; dvec: f32 [B*H][Sq] scratch.
+DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long* qstr, const void* o,
+                         const void* dout, const long* ostr, const float* lse, float* dvec, void* dq, void* dk,
+                         void* dv, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
+                         float dropout, unsigned long long seed, int causal, void* stream) {
+  if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
+      !aligned16(dq) || !aligned16(dk) || !aligned16(dv))
+    return -1;
+  if ((qstr[0] | qstr[1] | qstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
+  if (dropout < 0.f || dropout >= 1.f) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  AttnArgs a = make_args(q, k, v, qstr, o, dout, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
+  a.lse = const_cast<float*>(lse);
+  a.dvec = dvec;
+  a.dq = (bf16_t*)dq;
+  a.dk = (bf16_t*)dk;
+  a.dv = (bf16_t*)dv;
+  const long rows = (long)B * H * Sq;
+  hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)std::min<long>((rows + 255) / 256, 4096)), dim3(256), 0, st,
+                     a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3((unsigned)((Sk + 127) / 128), (unsigned)(B * H)), dim3(256), 0,
+                     st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, dim3((unsigned)((Sq + 127) / 128), (unsigned)(B * H)), dim3(256), 0,
+                     st, a);
+  return (int)hipGetLastError();
+}

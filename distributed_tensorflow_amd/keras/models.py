@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from .. import context
+from .. import profiler as prof
 from ..data import Dataset
 from ..parallel import strategy as S
 from . import callbacks as cbs
@@ -147,11 +148,14 @@ class Model(Layer):
         reps = strat.inproc_replicas() if hasattr(strat, "inproc_replicas") else None
         if reps:
             return self._train_step_inproc(x, y, sw, reps)
-        y_pred = self(x, training=True)
-        loss = self.compute_loss(x, y, y_pred, sw)
+        with prof.phase("forward"):
+            y_pred = self(x, training=True)
+            loss = self.compute_loss(x, y, y_pred, sw)
         arena = self._ensure_arena()
-        strat.backward(loss, arena)
-        strat.apply_gradients(self.optimizer, arena)
+        with prof.phase("backward"):  # includes the overlapped bucket all-reduces
+            strat.backward(loss, arena)
+        with prof.phase("optimizer"):
+            strat.apply_gradients(self.optimizer, arena)
         return self._update_metrics(loss, y, y_pred)
 
     def make_train_function(self, force=False):

@@ -46,10 +46,9 @@ class MultiHeadSelfAttention(KL.Layer):
         self.out = _Proj(hidden, fp8=fp8)
 
     def call(self, x, mask=None, training=None):
-        q, k, v = attn_ops.split_qkv(self.qkv(x), self.heads)
-        o = attn_ops.attention(q, k, v, causal=self.causal, mask=mask, dropout=self.dropout,
-                                        training=training)
-        return self.out(attn_ops.merge_heads(o))
+        o = attn_ops.attention_packed(self.qkv(x), self.heads, causal=self.causal, mask=mask,
+                                      dropout=self.dropout, training=training)
+        return self.out(o)
 
 
 class BertLayer(KL.Layer):

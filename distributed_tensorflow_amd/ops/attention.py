@@ -1,39 +1,124 @@
 """Scaled dot-product attention.
 
-GPU: scores = Q K^T on the batched MFMA GEMM, masked/causal softmax kernel, P V on the GEMM
-(K3 + K7 composition); every piece has a hand-written backward. CPU: f32 reference.
-Layout: q, k, v are [B, H, S, D] (bf16 on GPU).
+GPU: one fused HIP kernel per direction (csrc/kernels/attention.hip): online-softmax forward that never
+materialises the [S, S] scores, and a deterministic two-kernel backward (dK/dV by key blocks, dQ by
+query blocks), with causal and additive key masks and in-kernel dropout on the probabilities. The
+packed entry point reads Q/K/V straight out of the fused QKV projection [B, S, 3*H*64] and writes
+O as [B, S, H*64], so no head split/merge copies exist; its backward writes one packed dQKV.
+Head dims other than 64 use the composed path (MFMA batched GEMM + softmax kernel). CPU: f32 reference.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
 
-from ._util import BF16, on_gpu
+from ._util import BF16, F32, call, on_gpu, ptr, stream
 from .linalg import bmm
 from .nn import softmax
 
+_seed_counter = [0]
 
-def attention(q, k, v, causal=False, mask=None, scale=None, dropout=0.0, training=False):
-    """mask: optional additive f32 mask broadcastable as [B, 1, 1, Sk] (0 keep, -inf/-1e4 drop)."""
+
+def _next_seed():
+    _seed_counter[0] += 1
+    return (_seed_counter[0] * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+
+
+def _strides3(b, s, h):
+    arr = (ctypes.c_long * 3)(int(b), int(s), int(h))
+    return arr, ctypes.addressof(arr)
+
+
+class _FlashPackedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, kmask, heads, causal, scale, dropout, seed):
+        qkv = qkv.contiguous()
+        B, S, T = qkv.shape
+        D = T // (3 * heads)
+        HD = heads * D
+        o = torch.empty(B, S, HD, dtype=BF16, device=qkv.device)
+        lse = torch.empty(B * heads, S, dtype=F32, device=qkv.device)
+        qs, qsp = _strides3(S * T, T, D)
+        os_, osp = _strides3(S * HD, HD, D)
+        base = qkv.data_ptr()
+        call("dtf_attn_fwd", base, base + 2 * HD, base + 4 * HD, qsp, ptr(o), osp, ptr(lse), ptr(kmask), B, heads, S,
+             S, D, float(scale), float(dropout), seed, int(causal), stream())
+        ctx.save_for_backward(qkv, o, lse, kmask)
+        ctx.cfg = (heads, causal, scale, dropout, seed)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, kmask = ctx.saved_tensors
+        heads, causal, scale, dropout, seed = ctx.cfg
+        do = do.to(BF16).contiguous()
+        B, S, T = qkv.shape
+        D = T // (3 * heads)
+        HD = heads * D
+        dqkv = torch.empty_like(qkv)
+        dvec = torch.empty(B * heads, S, dtype=F32, device=qkv.device)
+        qs, qsp = _strides3(S * T, T, D)
+        os_, osp = _strides3(S * HD, HD, D)
+        base, gb = qkv.data_ptr(), dqkv.data_ptr()
+        call("dtf_attn_bwd", base, base + 2 * HD, base + 4 * HD, qsp, ptr(o), ptr(do), osp, ptr(lse), ptr(dvec),
+             gb, gb + 2 * HD, gb + 4 * HD, ptr(kmask), B, heads, S, S, D, float(scale), float(dropout), seed,
+             int(causal), stream())
+        return dqkv, None, None, None, None, None, None
+
+
+class _FlashFn(torch.autograd.Function):
+    """Separate q, k, v tensors in [B, H, S, D] layout."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, kmask, causal, scale, dropout, seed):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, H, Sq, D = q.shape
+        Sk = k.shape[2]
+        o = torch.empty_like(q)
+        lse = torch.empty(B * H, Sq, dtype=F32, device=q.device)
+        qs, qsp = _strides3(H * Sq * D, D, Sq * D)
+        call("dtf_attn_fwd", ptr(q), ptr(k), ptr(v), qsp, ptr(o), qsp, ptr(lse), ptr(kmask), B, H, Sq, Sk, D,
+             float(scale), float(dropout), seed, int(causal), stream())
+        ctx.save_for_backward(q, k, v, o, lse, kmask)
+        ctx.cfg = (causal, scale, dropout, seed)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, kmask = ctx.saved_tensors
+        causal, scale, dropout, seed = ctx.cfg
+        do = do.to(BF16).contiguous()
+        B, H, Sq, D = q.shape
+        Sk = k.shape[2]
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        dvec = torch.empty(B * H, Sq, dtype=F32, device=q.device)
+        qs, qsp = _strides3(H * Sq * D, D, Sq * D)
+        call("dtf_attn_bwd", ptr(q), ptr(k), ptr(v), qsp, ptr(o), ptr(do), qsp, ptr(lse), ptr(dvec), ptr(dq),
+             ptr(dk), ptr(dv), ptr(kmask), B, H, Sq, Sk, D, float(scale), float(dropout), seed, int(causal),
+             stream())
+        return dq, dk, dv, None, None, None, None, None
+
+
+def _kmask(mask, B, Sk):
+    if mask is None:
+        return None
+    return mask.reshape(B, Sk).float().contiguous()
+
+
+def attention(q, k, v, causal=False, mask=None, scale=None, dropout=0.0, training=False, seed=None):
+    """q, k, v: [B, H, S, D]. mask: optional additive f32 mask broadcastable as [B, 1, 1, Sk]."""
     B, H, Sq, D = q.shape
     Sk = k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    rate = float(dropout) if (dropout and training) else 0.0
     if on_gpu(q):
-        q3 = q.reshape(B * H, Sq, D)
-        k3 = k.reshape(B * H, Sk, D)
-        v3 = v.reshape(B * H, Sk, D)
-        s = bmm(q3, k3, transpose_b=True)  # [BH, Sq, Sk] bf16
-        am = None
-        if mask is not None:
-            am = mask.reshape(B, Sk).float().repeat_interleave(H, 0).contiguous()
-        p = softmax(s.reshape(B * H, Sq, Sk), scale=scale, causal=causal, add_mask=am)
-        if dropout and training:
-            from .nn import dropout as _drop
-            p = _drop(p, dropout)
-        o = bmm(p, v3)
-        return o.reshape(B, H, Sq, D)
+        if D == 64 and k.shape[2] == v.shape[2]:
+            seed = _next_seed() if seed is None else seed
+            return _FlashFn.apply(q.to(BF16), k.to(BF16), v.to(BF16), _kmask(mask, B, Sk), bool(causal),
+                                  float(scale), rate, seed)
+        return _composed(q, k, v, causal, mask, scale, rate)
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
     if causal:
         m = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).tril(Sk - Sq)
@@ -41,9 +126,57 @@ def attention(q, k, v, causal=False, mask=None, scale=None, dropout=0.0, trainin
     if mask is not None:
         s = s + mask.reshape(B, 1, 1, Sk).float()
     p = torch.softmax(s, -1)
-    if dropout and training:
-        p = torch.nn.functional.dropout(p, dropout)
+    if rate:
+        p = torch.nn.functional.dropout(p, rate)
     return torch.matmul(p, v.float()).to(q.dtype)
+
+
+def attention_packed(qkv, heads, causal=False, mask=None, scale=None, dropout=0.0, training=False, seed=None):
+    """Self-attention on the fused projection output qkv [B, S, 3*H*D] -> [B, S, H*D]."""
+    B, S, T = qkv.shape
+    D = T // (3 * heads)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    rate = float(dropout) if (dropout and training) else 0.0
+    if on_gpu(qkv) and D == 64 and qkv.dtype == BF16:
+        seed = _next_seed() if seed is None else seed
+        return _FlashPackedFn.apply(qkv, _kmask(mask, B, S), heads, bool(causal), float(scale), rate, seed)
+    q, k, v = split_qkv(qkv, heads)
+    return merge_heads(attention(q, k, v, causal, mask, scale, dropout, training))
+
+
+def _composed(q, k, v, causal, mask, scale, rate):
+    """K3 + K7 composition (batched MFMA GEMMs around the masked softmax kernel)."""
+    B, H, Sq, D = q.shape
+    Sk = k.shape[2]
+    q3 = q.reshape(B * H, Sq, D)
+    k3 = k.reshape(B * H, Sk, D)
+    v3 = v.reshape(B * H, Sk, D)
+    s = bmm(q3, k3, transpose_b=True)
+    am = None
+    if mask is not None:
+        am = mask.reshape(B, Sk).float().repeat_interleave(H, 0).contiguous()
+    p = softmax(s.reshape(B * H, Sq, Sk), scale=scale, causal=causal, add_mask=am)
+    if rate:
+        from .nn import dropout as _drop
+        p = _drop(p, rate)
+    return bmm(p, v3).reshape(B, H, Sq, D)
+
+
+def reference_attention(q, k, v, causal=False, mask=None, scale=None, keep_mask=None, keep=1.0):
+    """f32 reference with an explicit dropout keep-mask (tests)."""
+    B, H, Sq, D = q.shape
+    Sk = k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
+    if causal:
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).tril(Sk - Sq)
+        s = s.masked_fill(~m, float("-inf"))
+    if mask is not None:
+        s = s + mask.reshape(B, 1, 1, Sk).float()
+    p = torch.softmax(s, -1)
+    if keep_mask is not None:
+        p = p * keep_mask / keep
+    return torch.matmul(p, v.float())
 
 
 def split_heads(x, heads):
@@ -63,6 +196,3 @@ def split_qkv(qkv, heads):
     D = T // (3 * heads)
     x = qkv.reshape(B, S, 3, heads, D).permute(2, 0, 3, 1, 4).contiguous()
     return x[0], x[1], x[2]
-
-
-del BF16

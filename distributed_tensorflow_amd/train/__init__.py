@@ -4,3 +4,6 @@ from .checkpoint import (Saver, Checkpoint, CheckpointManager, latest_checkpoint
 from ..keras.optimizers import (GradientDescentOptimizer, AdadeltaOptimizer, AdagradOptimizer, AdamOptimizer,  # noqa
                                 FtrlOptimizer, RMSPropOptimizer, MomentumOptimizer)
 from ..parallel.cluster_resolver import ClusterSpec  # noqa
+from .supervisor import ManagedTraining  # noqa
+from .monitored import (MonitoredTrainingSession, SessionRunHook, StopAtStepHook, CheckpointSaverHook,  # noqa
+                        StepCounterHook, SummarySaverHook, LoggingTensorHook, NanTensorHook)

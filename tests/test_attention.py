@@ -1,0 +1,120 @@
+"""Fused attention kernel (csrc/kernels/attention.hip) vs an f32 PyTorch reference.
+
+Covers: non-causal / causal, ragged S (not a multiple of the 64-row tiles), additive key-padding masks,
+the packed-QKV entry point, and in-kernel dropout (the keep-mask is regenerated on the host from the
+same counter hash and fed to the reference).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from distributed_tensorflow_amd import ops
+import importlib
+
+A = importlib.import_module("distributed_tensorflow_amd.ops.attention")
+
+BF = torch.bfloat16
+
+
+def close(a, b, tol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item() + 1e-6
+    assert err <= tol * ref, f"max err {err} vs ref scale {ref} (tol {tol})"
+
+
+def _fmix32(h):
+    h = h ^ (h >> np.uint32(16))
+    h = h * np.uint32(0x85EBCA6B)
+    h = h ^ (h >> np.uint32(13))
+    h = h * np.uint32(0xC2B2AE35)
+    h = h ^ (h >> np.uint32(16))
+    return h
+
+
+def keep_mask(seed, B, H, Sq, Sk, keep):
+    s32 = np.uint32((seed ^ (seed >> 32)) & 0xFFFFFFFF)
+    bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
+    q = np.arange(Sq, dtype=np.uint64)[None, :, None]
+    k = np.arange(Sk, dtype=np.uint64)[None, None, :]
+    idx = (bh * np.uint64(Sq) + q) * np.uint64(Sk) + k
+    with np.errstate(over="ignore"):
+        lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        hi = (idx >> np.uint64(32)).astype(np.uint32)
+        h = _fmix32(lo ^ _fmix32(hi + s32))
+    u = (h >> np.uint32(8)).astype(np.float64) / 16777216.0
+    return torch.from_numpy((u < keep).reshape(B, H, Sq, Sk).astype(np.float32))
+
+
+def test_cpu_reference_paths():
+    q, k, v = (torch.randn(2, 3, 16, 8) for _ in range(3))
+    o = ops.attention(q, k, v, causal=True)
+    r = A.reference_attention(q, k, v, causal=True)
+    close(o, r, 1e-5)
+    qkv = torch.randn(2, 16, 3 * 3 * 8)
+    o2 = ops.attention_packed(qkv, 3)
+    qq, kk, vv = A.split_qkv(qkv, 3)
+    close(o2, A.merge_heads(A.reference_attention(qq, kk, vv)), 1e-5)
+    m = keep_mask(12345, 1, 2, 4, 5, 0.9)
+    assert m.shape == (1, 2, 4, 5)
+
+
+def _run(cuda, B, H, Sq, Sk, causal, masked, dropout=0.0, seed=7):
+    torch.manual_seed(0)
+    q = torch.randn(B, H, Sq, 64, device=cuda).to(BF).requires_grad_(True)
+    k = torch.randn(B, H, Sk, 64, device=cuda).to(BF).requires_grad_(True)
+    v = torch.randn(B, H, Sk, 64, device=cuda).to(BF).requires_grad_(True)
+    mask = None
+    if masked:
+        lens = torch.randint(Sk // 2, Sk + 1, (B,))
+        mask = torch.zeros(B, Sk, device=cuda)
+        for b in range(B):
+            mask[b, lens[b]:] = -10000.0
+    o = ops.attention(q, k, v, causal=causal, mask=mask, dropout=dropout, training=dropout > 0, seed=seed)
+    km = keep_mask(seed, B, H, Sq, Sk, 1 - dropout).to(cuda) if dropout else None
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    r = A.reference_attention(qr, kr, vr, causal=causal, mask=mask, keep_mask=km, keep=1 - dropout)
+    close(o, r, 2e-2)
+    do = torch.randn_like(r)
+    r.backward(do)
+    o.backward(do.to(BF))
+    close(q.grad, qr.grad, 3e-2)
+    close(k.grad, kr.grad, 3e-2)
+    close(v.grad, vr.grad, 3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,Sq,Sk,causal,masked", [
+    (2, 3, 128, 128, False, False),
+    (2, 2, 200, 200, False, True),
+    (1, 4, 256, 256, True, False),
+    (2, 2, 100, 164, True, False),
+    (3, 2, 64, 512, False, True),
+])
+def test_flash_attention(cuda, B, H, Sq, Sk, causal, masked):
+    _run(cuda, B, H, Sq, Sk, causal, masked)
+
+
+@pytest.mark.gpu
+def test_flash_attention_dropout(cuda):
+    _run(cuda, 2, 2, 128, 192, False, True, dropout=0.1, seed=99)
+    _run(cuda, 1, 2, 256, 256, True, False, dropout=0.2, seed=2**40 + 3)
+
+
+@pytest.mark.gpu
+def test_flash_attention_packed(cuda):
+    B, S, H = 2, 192, 4
+    qkv = (torch.randn(B, S, 3 * H * 64, device=cuda) * 0.5).to(BF).requires_grad_(True)
+    mask = torch.zeros(B, S, device=cuda)
+    mask[1, 150:] = -10000.0
+    o = ops.attention_packed(qkv, H, causal=False, mask=mask)
+    qr = qkv.detach().float().requires_grad_(True)
+    q, k, v = A.split_qkv(qr, H)
+    r = A.merge_heads(A.reference_attention(q, k, v, mask=mask))
+    close(o, r, 2e-2)
+    do = torch.randn_like(r)
+    r.backward(do)
+    o.backward(do.to(BF))
+    close(qkv.grad, qr.grad, 3e-2)
