@@ -30,7 +30,8 @@ struct AttnArgs {
   float* lse;          // [B*H][Sq], log2 domain
   float* dvec;         // [B*H][Sq], rowsum(dO * O)
   const float* kmask;  // optional additive key mask [B][Sk] (natural-log units)
-  long qsb, qss, qsh;  // strides (elements) of q/k/v and dq/dk/dv: batch, sequence, head
+  long qsb, qss, qsh;  // strides (elements) of q and dq: batch, sequence, head
+  long ksb, kss, ksh;  // strides of k/v and dk/dv
   long osb, oss, osh;  // strides of o / dout
   int B, H, Sq, Sk;
   float scale;
@@ -129,8 +130,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int BM = 64 * QT;
   const int q0 = qblk * BM + w * 16 * QT;
   const bf16_t* Q = a.q + b * a.qsb + h * a.qsh;
-  const bf16_t* K = a.k + b * a.qsb + h * a.qsh;
-  const bf16_t* V = a.v + b * a.qsb + h * a.qsh;
+  const bf16_t* K = a.k + b * a.ksb + h * a.ksh;
+  const bf16_t* V = a.v + b * a.ksb + h * a.ksh;
   const int off = a.Sk - a.Sq;
   const float c = a.scale * LOG2E;
   const bool drop = a.keep < 1.f;
@@ -157,8 +158,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int ntiles = (kend + 63) / 64;
   TileRegs tk, tv;
   if (ntiles > 0) {
-    tile_load(tk, K, a.qss, 0, a.Sk);
-    tile_load(tv, V, a.qss, 0, a.Sk);
+    tile_load(tk, K, a.kss, 0, a.Sk);
+    tile_load(tv, V, a.kss, 0, a.Sk);
   }
   for (int t = 0; t < ntiles; ++t) {
     __syncthreads();
@@ -166,8 +167,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     tile_store(tv, sv);
     __syncthreads();
     if (t + 1 < ntiles) {
-      tile_load(tk, K, a.qss, (t + 1) * 64, a.Sk);
-      tile_load(tv, V, a.qss, (t + 1) * 64, a.Sk);
+      tile_load(tk, K, a.kss, (t + 1) * 64, a.Sk);
+      tile_load(tv, V, a.kss, (t + 1) * 64, a.Sk);
     }
     const int k0 = t * 64;
     v4f s[4][QT];
@@ -284,10 +285,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   const int BN = 64 * KT;
   const int kblk = blockIdx.x;
   const int k0w = kblk * BN + w * 16 * KT;
-  const long hb = b * a.qsb + h * a.qsh, ob = b * a.osb + h * a.osh;
+  const long hb = b * a.qsb + h * a.qsh, kb = b * a.ksb + h * a.ksh, ob = b * a.osb + h * a.osh;
   const bf16_t* Q = a.q + hb;
-  const bf16_t* K = a.k + hb;
-  const bf16_t* V = a.v + hb;
+  const bf16_t* K = a.k + kb;
+  const bf16_t* V = a.v + kb;
   const bf16_t* dO = a.dout + ob;
   const int off = a.Sk - a.Sq;
   const float c = a.scale * LOG2E;
@@ -301,8 +302,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
     const int key = k0w + 16 * kt + i;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      kf[kt][kk] = frag_global(K + (long)key * a.qss + 32 * kk + 8 * G, key < a.Sk);
-      vf[kt][kk] = frag_global(V + (long)key * a.qss + 32 * kk + 8 * G, key < a.Sk);
+      kf[kt][kk] = frag_global(K + (long)key * a.kss + 32 * kk + 8 * G, key < a.Sk);
+      vf[kt][kk] = frag_global(V + (long)key * a.kss + 32 * kk + 8 * G, key < a.Sk);
     }
     km[kt] = key >= a.Sk ? -INFINITY : (a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f);
   }
@@ -387,16 +388,16 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
       }
     }
   }
-  bf16_t* dK = a.dk + hb;
-  bf16_t* dV = a.dv + hb;
+  bf16_t* dK = a.dk + kb;
+  bf16_t* dV = a.dv + kb;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     const int key = k0w + 16 * kt + i;
     if (key < a.Sk) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        store4(dK + (long)key * a.qss + 16 * dt + 4 * G, dk[dt][kt], a.scale);
-        store4(dV + (long)key * a.qss + 16 * dt + 4 * G, dv[dt][kt], 1.f);
+        store4(dK + (long)key * a.kss + 16 * dt + 4 * G, dk[dt][kt], a.scale);
+        store4(dV + (long)key * a.kss + 16 * dt + 4 * G, dv[dt][kt], 1.f);
       }
     }
   }
@@ -412,10 +413,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   const int qblk = gridDim.x - 1 - blockIdx.x;
   const int BM = 64 * QT;
   const int q0 = qblk * BM + w * 16 * QT;
-  const long hb = b * a.qsb + h * a.qsh, ob = b * a.osb + h * a.osh;
+  const long hb = b * a.qsb + h * a.qsh, kb = b * a.ksb + h * a.ksh, ob = b * a.osb + h * a.osh;
   const bf16_t* Q = a.q + hb;
-  const bf16_t* K = a.k + hb;
-  const bf16_t* V = a.v + hb;
+  const bf16_t* K = a.k + kb;
+  const bf16_t* V = a.v + kb;
   const bf16_t* dO = a.dout + ob;
   const int off = a.Sk - a.Sq;
   const float c = a.scale * LOG2E;
@@ -446,8 +447,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   const int ntiles = (kend + 63) / 64;
   TileRegs tk, tv;
   if (ntiles > 0) {
-    tile_load(tk, K, a.qss, 0, a.Sk);
-    tile_load(tv, V, a.qss, 0, a.Sk);
+    tile_load(tk, K, a.kss, 0, a.Sk);
+    tile_load(tv, V, a.kss, 0, a.Sk);
   }
   for (int t = 0; t < ntiles; ++t) {
     __syncthreads();
@@ -455,8 +456,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
     tile_store(tv, sv);
     __syncthreads();
     if (t + 1 < ntiles) {
-      tile_load(tk, K, a.qss, (t + 1) * 64, a.Sk);
-      tile_load(tv, V, a.qss, (t + 1) * 64, a.Sk);
+      tile_load(tk, K, a.kss, (t + 1) * 64, a.Sk);
+      tile_load(tv, V, a.kss, (t + 1) * 64, a.Sk);
     }
     const int k0 = t * 64;
     v4f dS[4][QT];
@@ -514,7 +515,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
-AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const void* o, const void* dout,
+AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, const void* o, const void* dout,
                    const long* ostr, int B, int H, int Sq, int Sk, float scale, float dropout,
                    unsigned long long seed, int causal, const float* kmask) {
   AttnArgs a{};
@@ -526,6 +527,9 @@ AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr
   a.qsb = qstr[0];
   a.qss = qstr[1];
   a.qsh = qstr[2];
+  a.ksb = kstr[0];
+  a.kss = kstr[1];
+  a.ksh = kstr[2];
   a.osb = ostr[0];
   a.oss = ostr[1];
   a.osh = ostr[2];
@@ -547,13 +551,14 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // q/k/v: bf16 with strides qstr = {batch, seq, head} (elements; head dim contiguous, 64), o/out strides ostr.
 // lse: f32 [B*H][Sq]. kmask: optional f32 [B][Sk] additive (0 keep, large negative drop). dropout on P.
-DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long* qstr, void* o, const long* ostr,
+DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, void* o,
+                         const long* ostr,
                          float* lse, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
                          float dropout, unsigned long long seed, int causal, void* stream) {
   if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o)) return -1;
-  if ((qstr[0] | qstr[1] | qstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
+  if ((qstr[0] | qstr[1] | qstr[2] | kstr[0] | kstr[1] | kstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
   if (dropout < 0.f || dropout >= 1.f) return -1;
-  AttnArgs a = make_args(q, k, v, qstr, o, nullptr, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
+  AttnArgs a = make_args(q, k, v, qstr, kstr, o, nullptr, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
   a.lse = lse;
   dim3 grid((unsigned)((Sq + 127) / 128), (unsigned)(B * H));
   hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, a);
@@ -561,17 +566,18 @@ DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long
 }
 
 // dq/dk/dv share the q/k/v strides; dvec: f32 [B*H][Sq] scratch.
-DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long* qstr, const void* o,
+DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long* qstr, const long* kstr,
+                         const void* o,
                          const void* dout, const long* ostr, const float* lse, float* dvec, void* dq, void* dk,
                          void* dv, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
                          float dropout, unsigned long long seed, int causal, void* stream) {
   if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
       !aligned16(dq) || !aligned16(dk) || !aligned16(dv))
     return -1;
-  if ((qstr[0] | qstr[1] | qstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
+  if ((qstr[0] | qstr[1] | qstr[2] | kstr[0] | kstr[1] | kstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
   if (dropout < 0.f || dropout >= 1.f) return -1;
   hipStream_t st = (hipStream_t)stream;
-  AttnArgs a = make_args(q, k, v, qstr, o, dout, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
+  AttnArgs a = make_args(q, k, v, qstr, kstr, o, dout, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
   a.lse = const_cast<float*>(lse);
   a.dvec = dvec;
   a.dq = (bf16_t*)dq;

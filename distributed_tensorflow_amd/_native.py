@@ -46,8 +46,8 @@ _KERNEL_SIGS = {
     "dtf_add_bf16": [P, P, P, L, F, F, P],
     "dtf_act": [P, P, P, L, I, I, P],
     "dtf_dropout": [P, P, L, F, U, P],
-    "dtf_attn_fwd": [P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
-    "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
+    "dtf_attn_fwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
+    "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
     "dtf_colsum": [P, L, I, P, I, P, L, P],
     "dtf_embed_fwd": [P, P, P, P, P, P, P, L, I, I, P],
     "dtf_embed_bwd_sorted": [P, P, P, P, L, I, P],
@@ -55,8 +55,6 @@ _KERNEL_SIGS = {
     "dtf_softmax_ce": [P, I, P, P, P, I, L, I, F, F, P],
     "dtf_softmax_fwd": [P, P, L, I, I, F, I, P, P],
     "dtf_softmax_bwd": [P, P, P, L, I, F, P],
-    "dtf_attn_fwd": [P, P, P, P, P, I, I, I, I, I, I, F, I, P],
-    "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P],
     "dtf_gemm_fp8": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, P],
     "dtf_quant_fp8": [P, P, L, P, P, I, P],
     "dtf_fp8_update_scale": [P, P, F, P],

@@ -13,7 +13,7 @@ import math
 import torch
 
 from .. import ops
-from ..ops import attention as attn_ops
+from ..ops import mha as attn_ops
 from ..keras import layers as KL
 from ..keras.models import Model
 

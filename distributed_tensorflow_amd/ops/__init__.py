@@ -6,4 +6,4 @@ from .norm import batch_norm, layer_norm  # noqa: F401
 from .nn import (max_pool2d, global_avg_pool, relu, gelu, dropout, add, embedding,  # noqa: F401
                  sparse_softmax_cross_entropy, softmax)
 from .optim import optim_apply  # noqa: F401
-from .attention import attention, attention_packed  # noqa: F401
+from .mha import attention, attention_packed  # noqa: F401

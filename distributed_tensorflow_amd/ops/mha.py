@@ -43,7 +43,7 @@ class _FlashPackedFn(torch.autograd.Function):
         qs, qsp = _strides3(S * T, T, D)
         os_, osp = _strides3(S * HD, HD, D)
         base = qkv.data_ptr()
-        call("dtf_attn_fwd", base, base + 2 * HD, base + 4 * HD, qsp, ptr(o), osp, ptr(lse), ptr(kmask), B, heads, S,
+        call("dtf_attn_fwd", base, base + 2 * HD, base + 4 * HD, qsp, qsp, ptr(o), osp, ptr(lse), ptr(kmask), B, heads, S,
              S, D, float(scale), float(dropout), seed, int(causal), stream())
         ctx.save_for_backward(qkv, o, lse, kmask)
         ctx.cfg = (heads, causal, scale, dropout, seed)
@@ -62,7 +62,7 @@ class _FlashPackedFn(torch.autograd.Function):
         qs, qsp = _strides3(S * T, T, D)
         os_, osp = _strides3(S * HD, HD, D)
         base, gb = qkv.data_ptr(), dqkv.data_ptr()
-        call("dtf_attn_bwd", base, base + 2 * HD, base + 4 * HD, qsp, ptr(o), ptr(do), osp, ptr(lse), ptr(dvec),
+        call("dtf_attn_bwd", base, base + 2 * HD, base + 4 * HD, qsp, qsp, ptr(o), ptr(do), osp, ptr(lse), ptr(dvec),
              gb, gb + 2 * HD, gb + 4 * HD, ptr(kmask), B, heads, S, S, D, float(scale), float(dropout), seed,
              int(causal), stream())
         return dqkv, None, None, None, None, None, None
@@ -79,7 +79,8 @@ class _FlashFn(torch.autograd.Function):
         o = torch.empty_like(q)
         lse = torch.empty(B * H, Sq, dtype=F32, device=q.device)
         qs, qsp = _strides3(H * Sq * D, D, Sq * D)
-        call("dtf_attn_fwd", ptr(q), ptr(k), ptr(v), qsp, ptr(o), qsp, ptr(lse), ptr(kmask), B, H, Sq, Sk, D,
+        ks, ksp = _strides3(H * Sk * D, D, Sk * D)
+        call("dtf_attn_fwd", ptr(q), ptr(k), ptr(v), qsp, ksp, ptr(o), qsp, ptr(lse), ptr(kmask), B, H, Sq, Sk, D,
              float(scale), float(dropout), seed, int(causal), stream())
         ctx.save_for_backward(q, k, v, o, lse, kmask)
         ctx.cfg = (causal, scale, dropout, seed)
@@ -95,7 +96,8 @@ class _FlashFn(torch.autograd.Function):
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         dvec = torch.empty(B * H, Sq, dtype=F32, device=q.device)
         qs, qsp = _strides3(H * Sq * D, D, Sq * D)
-        call("dtf_attn_bwd", ptr(q), ptr(k), ptr(v), qsp, ptr(o), ptr(do), qsp, ptr(lse), ptr(dvec), ptr(dq),
+        ks, ksp = _strides3(H * Sk * D, D, Sk * D)
+        call("dtf_attn_bwd", ptr(q), ptr(k), ptr(v), qsp, ksp, ptr(o), ptr(do), qsp, ptr(lse), ptr(dvec), ptr(dq),
              ptr(dk), ptr(dv), ptr(kmask), B, H, Sq, Sk, D, float(scale), float(dropout), seed, int(causal),
              stream())
         return dq, dk, dv, None, None, None, None, None

@@ -13,7 +13,7 @@ import torch
 from distributed_tensorflow_amd import ops
 import importlib
 
-A = importlib.import_module("distributed_tensorflow_amd.ops.attention")
+A = importlib.import_module("distributed_tensorflow_amd.ops.mha")
 
 BF = torch.bfloat16
 
