@@ -10,7 +10,13 @@
 // ds_read_b64_tr_b16 with its k-rows permuted to the same slot order (slot 4h+q <-> row 16h+4G+q).
 // Q, K, V, O and the gradients are addressed with (batch, seq, head) strides, so the kernels read the
 // packed QKV projection output [B, S, 3, H, 64] and write O as [B, S, H, 64] with no head transposes.
-// Dropout on P is regenerated from a counter hash of (b*H+h, q, k) in forward and backward.
+//
+// Dropout on P: one 64-bit counter hash per (b*H+h, q, k/4) block gives four 16-bit uniforms, one per key
+// of the block; an element is kept when its 16-bit value < thr = round(keep * 65536) and scaled by
+// 65536/thr (the exact inverse of the realised keep probability). The forward and dQ kernels own 4
+// consecutive keys of one query per lane (one hash per 4 elements); the dK/dV kernel owns 4 queries of
+// one key and gathers the bits across its lane quad. Masking work is skipped on tiles that are entirely
+// below the causal diagonal.
 #include "common.h"
 
 namespace {
@@ -35,8 +41,10 @@ struct AttnArgs {
   long osb, oss, osh;  // strides of o / dout
   int B, H, Sq, Sk;
   float scale;
-  float keep;  // 1 - dropout rate
+  uint32_t thr;     // keep threshold on 16-bit uniforms (65536 = no dropout)
+  float inv_keep;   // 65536 / thr
   uint32_t seed;
+  int nkq;          // (Sk + 3) / 4 hash blocks per query row
   int causal;
 };
 
@@ -48,12 +56,19 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
-// keep-decision for element (bh, q, k)
-__device__ __forceinline__ bool drop_keep(const AttnArgs& a, int bh, int q, int k) {
-  uint64_t idx = ((uint64_t)bh * (uint64_t)a.Sq + (uint64_t)q) * (uint64_t)a.Sk + (uint64_t)k;
-  uint32_t h = fmix32((uint32_t)idx ^ fmix32((uint32_t)(idx >> 32) + a.seed));
-  return (float)(h >> 8) * (1.f / 16777216.f) < a.keep;
+__device__ __forceinline__ uint32_t drop_salt(const AttnArgs& a, int bh) {
+  return fmix32(a.seed ^ ((uint32_t)bh * 0x9E3779B9u));
 }
+// 4 x 16-bit uniforms for keys 4 kq .. 4 kq + 3 of query q
+__device__ __forceinline__ uint2 drop_bits(const AttnArgs& a, uint32_t salt, int q, int kq) {
+  const uint32_t x = fmix32(((uint32_t)q * (uint32_t)a.nkq + (uint32_t)kq) ^ salt);
+  return make_uint2(x, fmix32(x + 0x9E3779B9u));
+}
+__device__ __forceinline__ bool keep_field(uint2 b, int j, uint32_t thr) {
+  const uint32_t w = j < 2 ? b.x : b.y;
+  return ((w >> (16 * (j & 1))) & 0xFFFFu) < thr;
+}
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // ---- [64 rows][64 cols] bf16 LDS tile, 128 B rows, 16-B chunk XOR swizzle ----
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -77,6 +92,11 @@ __device__ __forceinline__ void tile_store(const TileRegs& t, char* lds) {
     const int idx = threadIdx.x + 256 * u, row = idx >> 3, c = idx & 7;
     *reinterpret_cast<uint4*>(lds + swz(row, c)) = t.r[u];
   }
+}
+// additive key-mask value (log2 units) of key `key`: -inf past the end
+__device__ __forceinline__ float key_bias(const AttnArgs& a, int b, int key) {
+  if (key >= a.Sk) return -INFINITY;
+  return a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f;
 }
 // row fragment: lane (G, i) gets row rb + i, columns 32 kk + 8 G .. + 7
 __device__ __forceinline__ v8bf frag_row(const char* lds, int rb, int kk, int lane) {
@@ -124,6 +144,7 @@ template <int QT>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char sk[64 * 128];
   __shared__ __attribute__((aligned(16))) char sv[64 * 128];
+  __shared__ float smask[64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qblk = gridDim.x - 1 - blockIdx.x;  // heavy (causal) blocks first
@@ -134,8 +155,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const bf16_t* V = a.v + b * a.ksb + h * a.ksh;
   const int off = a.Sk - a.Sq;
   const float c = a.scale * LOG2E;
-  const bool drop = a.keep < 1.f;
-  const float inv_keep = 1.f / a.keep;
+  const bool drop = a.thr < 65536u;
+  const uint32_t salt = drop_salt(a, bh);
 
   v8bf qf[QT][2];
 #pragma unroll
@@ -157,20 +178,24 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   if (a.causal) kend = min(a.Sk, qblk * BM + BM + off);
   const int ntiles = (kend + 63) / 64;
   TileRegs tk, tv;
+  float mreg = 0.f;
   if (ntiles > 0) {
     tile_load(tk, K, a.kss, 0, a.Sk);
     tile_load(tv, V, a.kss, 0, a.Sk);
+    if (threadIdx.x < 64) mreg = key_bias(a, b, threadIdx.x);
   }
   for (int t = 0; t < ntiles; ++t) {
     __syncthreads();
     tile_store(tk, sk);
     tile_store(tv, sv);
+    if (threadIdx.x < 64) smask[threadIdx.x] = mreg;
     __syncthreads();
-    if (t + 1 < ntiles) {
-      tile_load(tk, K, a.kss, (t + 1) * 64, a.Sk);
-      tile_load(tv, V, a.kss, (t + 1) * 64, a.Sk);
-    }
     const int k0 = t * 64;
+    if (t + 1 < ntiles) {
+      tile_load(tk, K, a.kss, k0 + 64, a.Sk);
+      tile_load(tv, V, a.kss, k0 + 64, a.Sk);
+      if (threadIdx.x < 64) mreg = key_bias(a, b, k0 + 64 + threadIdx.x);
+    }
     v4f s[4][QT];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -186,10 +211,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * kt + 4 * G + r;
-        km[kt][r] = key >= a.Sk ? -INFINITY : (a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f);
-      }
+      for (int r = 0; r < 4; ++r) km[kt][r] = smask[16 * kt + 4 * G + r];
+    const bool diag = a.causal && (k0 + 63 > q0 + off);  // wave-uniform
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       const int qi = q0 + 16 * qt + i;
@@ -198,9 +221,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = k0 + 16 * kt + 4 * G + r;
-          float x = s[kt][qt][r] * c + km[kt][r];
-          if (a.causal && key > qi + off) x = -INFINITY;
+          float x = fmaf(s[kt][qt][r], c, km[kt][r]);
+          if (diag && k0 + 16 * kt + 4 * G + r > qi + off) x = -INFINITY;
           s[kt][qt][r] = x;
           mx = fmaxf(mx, x);
         }
@@ -208,18 +230,21 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m[qt], mx);
       const float ms = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = exp2f(m[qt] - ms);
+      const float alpha = ex2(m[qt] - ms);
       m[qt] = mnew;
       float ls = 0.f;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt) {
+        uint2 bits = make_uint2(0, 0);
+        if (drop) bits = drop_bits(a, salt, qi, (k0 >> 2) + 4 * kt + G);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = exp2f(s[kt][qt][r] - ms);
+          float p = ex2(s[kt][qt][r] - ms);
           ls += p;
-          if (drop) p = drop_keep(a, bh, qi, k0 + 16 * kt + 4 * G + r) ? p * inv_keep : 0.f;
+          if (drop) p = keep_field(bits, r, a.thr) ? p * a.inv_keep : 0.f;
           s[kt][qt][r] = p;
         }
+      }
       l[qt] = l[qt] * alpha + ls;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[dt][qt] *= alpha;
@@ -274,9 +299,10 @@ __global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
   }
 }
 
-// dK, dV: block = 4 waves x (16 KT) keys, loop over 64-query tiles; grid (cdiv(Sk, 64 KT), B*H)
+// dK, dV: block = 4 waves x (16 KT) keys, loop over 64-query tiles; grid (cdiv(Sk, 64 KT), B*H).
+// Query subtiles are processed in pairs (one 32-query MFMA k-step) so only 2 x KT score tiles are live.
 template <int KT>
-__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char sq[64 * 128];
   __shared__ __attribute__((aligned(16))) char sdo[64 * 128];
   __shared__ float slse[64], sdv[64];
@@ -292,8 +318,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   const bf16_t* dO = a.dout + ob;
   const int off = a.Sk - a.Sq;
   const float c = a.scale * LOG2E;
-  const bool drop = a.keep < 1.f;
-  const float inv_keep = 1.f / a.keep;
+  const bool drop = a.thr < 65536u;
+  const uint32_t salt = drop_salt(a, bh);
+  const int quad = lane & ~3, fld = i & 3;
 
   v8bf kf[KT][2], vf[KT][2];
   float km[KT];
@@ -305,7 +332,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
       kf[kt][kk] = frag_global(K + (long)key * a.kss + 32 * kk + 8 * G, key < a.Sk);
       vf[kt][kk] = frag_global(V + (long)key * a.kss + 32 * kk + 8 * G, key < a.Sk);
     }
-    km[kt] = key >= a.Sk ? -INFINITY : (a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f);
+    km[kt] = key_bias(a, b, key);
   }
   v4f dk[4][KT], dv[4][KT];
 #pragma unroll
@@ -319,9 +346,18 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
   if (a.causal) qstart = max(0, (kblk * BN - off) / 64 * 64);
   const int ntiles = qstart >= a.Sq ? 0 : (a.Sq - qstart + 63) / 64;
   TileRegs tq, td;
+  float lreg = 0.f, dreg = 0.f;
+  auto load_vec = [&](int q0) {
+    if (threadIdx.x < 64) {
+      const int qi = q0 + threadIdx.x;
+      lreg = qi < a.Sq ? a.lse[(long)bh * a.Sq + qi] : INFINITY;
+      dreg = qi < a.Sq ? a.dvec[(long)bh * a.Sq + qi] : 0.f;
+    }
+  };
   if (ntiles > 0) {
     tile_load(tq, Q, a.qss, qstart, a.Sq);
     tile_load(td, dO, a.oss, qstart, a.Sq);
+    load_vec(qstart);
   }
   for (int t = 0; t < ntiles; ++t) {
     const int q0 = qstart + t * 64;
@@ -329,52 +365,60 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnArgs a) {
     tile_store(tq, sq);
     tile_store(td, sdo);
     if (threadIdx.x < 64) {
-      const int qi = q0 + threadIdx.x;
-      slse[threadIdx.x] = qi < a.Sq ? a.lse[(long)bh * a.Sq + qi] : INFINITY;
-      sdv[threadIdx.x] = qi < a.Sq ? a.dvec[(long)bh * a.Sq + qi] : 0.f;
+      slse[threadIdx.x] = lreg;
+      sdv[threadIdx.x] = dreg;
     }
     __syncthreads();
     if (t + 1 < ntiles) {
       tile_load(tq, Q, a.qss, q0 + 64, a.Sq);
       tile_load(td, dO, a.oss, q0 + 64, a.Sq);
+      load_vec(q0 + 64);
     }
-    v4f P[4][KT], dS[4][KT];
-#pragma unroll
-    for (int qs = 0; qs < 4; ++qs) {
-      const v8bf q0f = frag_row(sq, 16 * qs, 0, lane), q1f = frag_row(sq, 16 * qs, 1, lane);
-      const v8bf d0f = frag_row(sdo, 16 * qs, 0, lane), d1f = frag_row(sdo, 16 * qs, 1, lane);
-#pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
-        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-        s = mfma(q0f, kf[kt][0], s);
-        s = mfma(q1f, kf[kt][1], s);
-        dp = mfma(d0f, vf[kt][0], dp);
-        dp = mfma(d1f, vf[kt][1], dp);
-        const int key = k0w + 16 * kt + i;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = 16 * qs + 4 * G + r, qi = q0 + ql;
-          float x = s[r] * c + km[kt];
-          if (a.causal && key > qi + off) x = -INFINITY;
-          const float p = exp2f(x - slse[ql]);
-          float pd = p, dpv = dp[r];
-          if (drop) {
-            const bool z = drop_keep(a, bh, qi, key);
-            pd = z ? p * inv_keep : 0.f;
-            dpv = z ? dpv * inv_keep : 0.f;
-          }
-          P[qs][kt][r] = pd;
-          dS[qs][kt][r] = p * (dpv - sdv[ql]);
-        }
-      }
-    }
+    const bool diag = a.causal && (k0w + 16 * KT - 1 > q0 + off);  // wave-uniform
 #pragma unroll
     for (int kq = 0; kq < 2; ++kq) {
+      v4f P[2][KT], dS[2][KT];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int qs = 2 * kq + hh;
+        const v8bf q0f = frag_row(sq, 16 * qs, 0, lane), q1f = frag_row(sq, 16 * qs, 1, lane);
+        const v8bf d0f = frag_row(sdo, 16 * qs, 0, lane), d1f = frag_row(sdo, 16 * qs, 1, lane);
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) {
+          v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+          s = mfma(q0f, kf[kt][0], s);
+          s = mfma(q1f, kf[kt][1], s);
+          dp = mfma(d0f, vf[kt][0], dp);
+          dp = mfma(d1f, vf[kt][1], dp);
+          const int key = k0w + 16 * kt + i;
+          uint2 mine = make_uint2(0, 0);
+          if (drop) mine = drop_bits(a, salt, q0 + 16 * qs + 4 * G + fld, key >> 2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = 16 * qs + 4 * G + r, qi = q0 + ql;
+            float x = fmaf(s[r], c, km[kt]);
+            if (diag && key > qi + off) x = -INFINITY;
+            const float p = ex2(x - slse[ql]);
+            float pd = p, dpv = dp[r];
+            if (drop) {
+              // bits of row r live in the quad lane whose field index is r
+              uint2 rb;
+              rb.x = (uint32_t)__shfl((int)mine.x, quad | r, 64);
+              rb.y = (uint32_t)__shfl((int)mine.y, quad | r, 64);
+              const bool z = keep_field(rb, fld, a.thr);
+              pd = z ? p * a.inv_keep : 0.f;
+              dpv = z ? dpv * a.inv_keep : 0.f;
+            }
+            P[hh][kt][r] = pd;
+            dS[hh][kt][r] = p * (dpv - sdv[ql]);
+          }
+        }
+      }
       v8bf pf[KT], sf[KT];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
-        pf[kt] = pack_slots(P[2 * kq][kt], P[2 * kq + 1][kt]);
-        sf[kt] = pack_slots(dS[2 * kq][kt], dS[2 * kq + 1][kt]);
+        pf[kt] = pack_slots(P[0][kt], P[1][kt]);
+        sf[kt] = pack_slots(dS[0][kt], dS[1][kt]);
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -408,6 +452,7 @@ template <int QT>
 __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char sk[64 * 128];
   __shared__ __attribute__((aligned(16))) char sv[64 * 128];
+  __shared__ float smask[64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qblk = gridDim.x - 1 - blockIdx.x;
@@ -420,8 +465,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   const bf16_t* dO = a.dout + ob;
   const int off = a.Sk - a.Sq;
   const float c = a.scale * LOG2E;
-  const bool drop = a.keep < 1.f;
-  const float inv_keep = 1.f / a.keep;
+  const bool drop = a.thr < 65536u;
+  const uint32_t salt = drop_salt(a, bh);
 
   v8bf qf[QT][2], df[QT][2];
   float lse[QT], dd[QT];
@@ -446,20 +491,25 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   if (a.causal) kend = min(a.Sk, qblk * BM + BM + off);
   const int ntiles = (kend + 63) / 64;
   TileRegs tk, tv;
+  float mreg = 0.f;
   if (ntiles > 0) {
     tile_load(tk, K, a.kss, 0, a.Sk);
     tile_load(tv, V, a.kss, 0, a.Sk);
+    if (threadIdx.x < 64) mreg = key_bias(a, b, threadIdx.x);
   }
   for (int t = 0; t < ntiles; ++t) {
     __syncthreads();
     tile_store(tk, sk);
     tile_store(tv, sv);
+    if (threadIdx.x < 64) smask[threadIdx.x] = mreg;
     __syncthreads();
-    if (t + 1 < ntiles) {
-      tile_load(tk, K, a.kss, (t + 1) * 64, a.Sk);
-      tile_load(tv, V, a.kss, (t + 1) * 64, a.Sk);
-    }
     const int k0 = t * 64;
+    if (t + 1 < ntiles) {
+      tile_load(tk, K, a.kss, k0 + 64, a.Sk);
+      tile_load(tv, V, a.kss, k0 + 64, a.Sk);
+      if (threadIdx.x < 64) mreg = key_bias(a, b, k0 + 64 + threadIdx.x);
+    }
+    const bool diag = a.causal && (k0 + 63 > q0 + off);
     v4f dS[4][QT];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -467,10 +517,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
       const v8bf v0f = frag_row(sv, 16 * kt, 0, lane), v1f = frag_row(sv, 16 * kt, 1, lane);
       float km[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * kt + 4 * G + r;
-        km[r] = key >= a.Sk ? -INFINITY : (a.kmask ? a.kmask[(long)b * a.Sk + key] * LOG2E : 0.f);
-      }
+      for (int r = 0; r < 4; ++r) km[r] = smask[16 * kt + 4 * G + r];
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) {
         v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
@@ -479,14 +526,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
         dp = mfma(v0f, df[qt][0], dp);
         dp = mfma(v1f, df[qt][1], dp);
         const int qi = q0 + 16 * qt + i;
+        uint2 bits = make_uint2(0, 0);
+        if (drop) bits = drop_bits(a, salt, qi, (k0 >> 2) + 4 * kt + G);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = k0 + 16 * kt + 4 * G + r;
-          float x = s[r] * c + km[r];
-          if (a.causal && key > qi + off) x = -INFINITY;
-          const float p = exp2f(x - lse[qt]);
+          float x = fmaf(s[r], c, km[r]);
+          if (diag && k0 + 16 * kt + 4 * G + r > qi + off) x = -INFINITY;
+          const float p = ex2(x - lse[qt]);
           float dpv = dp[r];
-          if (drop) dpv = drop_keep(a, bh, qi, key) ? dpv * inv_keep : 0.f;
+          if (drop) dpv = keep_field(bits, r, a.thr) ? dpv * a.inv_keep : 0.f;
           dS[kt][qt][r] = p * (dpv - dd[qt]);
         }
       }
@@ -515,8 +563,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
-AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, const void* o, const void* dout,
-                   const long* ostr, int B, int H, int Sq, int Sk, float scale, float dropout,
+AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, const void* o,
+                   const void* dout, const long* ostr, int B, int H, int Sq, int Sk, float scale, float dropout,
                    unsigned long long seed, int causal, const float* kmask) {
   AttnArgs a{};
   a.q = (const bf16_t*)q;
@@ -538,8 +586,12 @@ AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr
   a.Sq = Sq;
   a.Sk = Sk;
   a.scale = scale;
-  a.keep = 1.f - dropout;
+  long thr = lrintf((1.f - dropout) * 65536.f);
+  thr = thr < 1 ? 1 : (thr > 65536 ? 65536 : thr);
+  a.thr = (uint32_t)thr;
+  a.inv_keep = 65536.f / (float)thr;
   a.seed = (uint32_t)(seed ^ (seed >> 32));
+  a.nkq = (Sk + 3) / 4;
   a.causal = causal;
   a.kmask = kmask;
   return a;
@@ -549,12 +601,12 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
-// q/k/v: bf16 with strides qstr = {batch, seq, head} (elements; head dim contiguous, 64), o/out strides ostr.
-// lse: f32 [B*H][Sq]. kmask: optional f32 [B][Sk] additive (0 keep, large negative drop). dropout on P.
+// q/k/v: bf16 with strides {batch, seq, head} (elements; head dim 64 contiguous): qstr for q (and dq), kstr for
+// k/v (and dk/dv), ostr for o / dout. lse: f32 [B*H][Sq]. kmask: optional f32 [B][Sk] additive (0 keep, large
+// negative drop). dropout: probability of zeroing an attention weight (training).
 DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, void* o,
-                         const long* ostr,
-                         float* lse, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
-                         float dropout, unsigned long long seed, int causal, void* stream) {
+                         const long* ostr, float* lse, const float* kmask, int B, int H, int Sq, int Sk, int D,
+                         float scale, float dropout, unsigned long long seed, int causal, void* stream) {
   if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o)) return -1;
   if ((qstr[0] | qstr[1] | qstr[2] | kstr[0] | kstr[1] | kstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
   if (dropout < 0.f || dropout >= 1.f) return -1;
@@ -565,11 +617,10 @@ DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long
   return (int)hipGetLastError();
 }
 
-// dq/dk/dv share the q/k/v strides; dvec: f32 [B*H][Sq] scratch.
+// dvec: f32 [B*H][Sq] scratch.
 DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long* qstr, const long* kstr,
-                         const void* o,
-                         const void* dout, const long* ostr, const float* lse, float* dvec, void* dq, void* dk,
-                         void* dv, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
+                         const void* o, const void* dout, const long* ostr, const float* lse, float* dvec, void* dq,
+                         void* dk, void* dv, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
                          float dropout, unsigned long long seed, int causal, void* stream) {
   if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
       !aligned16(dq) || !aligned16(dk) || !aligned16(dv))

@@ -35,17 +35,22 @@ def _fmix32(h):
 
 
 def keep_mask(seed, B, H, Sq, Sk, keep):
+    """Host replica of the kernel's dropout hash: returns (keep-mask [B,H,Sq,Sk], realised keep prob)."""
+    thr = int(np.clip(np.rint(np.float32(keep) * np.float32(65536.0)), 1, 65536))
     s32 = np.uint32((seed ^ (seed >> 32)) & 0xFFFFFFFF)
-    bh = np.arange(B * H, dtype=np.uint64)[:, None, None]
-    q = np.arange(Sq, dtype=np.uint64)[None, :, None]
-    k = np.arange(Sk, dtype=np.uint64)[None, None, :]
-    idx = (bh * np.uint64(Sq) + q) * np.uint64(Sk) + k
+    nkq = (Sk + 3) // 4
     with np.errstate(over="ignore"):
-        lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
-        hi = (idx >> np.uint64(32)).astype(np.uint32)
-        h = _fmix32(lo ^ _fmix32(hi + s32))
-    u = (h >> np.uint32(8)).astype(np.float64) / 16777216.0
-    return torch.from_numpy((u < keep).reshape(B, H, Sq, Sk).astype(np.float32))
+        bh = np.arange(B * H, dtype=np.uint32)[:, None, None]
+        q = np.arange(Sq, dtype=np.uint32)[None, :, None]
+        k = np.arange(Sk, dtype=np.uint32)[None, None, :]
+        salt = _fmix32(s32 ^ (bh * np.uint32(0x9E3779B9)))
+        x = _fmix32((q * np.uint32(nkq) + (k >> np.uint32(2))) ^ salt)
+        y = _fmix32(x + np.uint32(0x9E3779B9))
+        j = k & np.uint32(3)
+        w = np.where(j < 2, x, y)
+        u = (w >> (np.uint32(16) * (j & np.uint32(1)))) & np.uint32(0xFFFF)
+    m = (u < thr).reshape(B, H, Sq, Sk).astype(np.float32)
+    return torch.from_numpy(m), thr / 65536.0
 
 
 def test_cpu_reference_paths():
@@ -57,8 +62,8 @@ def test_cpu_reference_paths():
     o2 = ops.attention_packed(qkv, 3)
     qq, kk, vv = A.split_qkv(qkv, 3)
     close(o2, A.merge_heads(A.reference_attention(qq, kk, vv)), 1e-5)
-    m = keep_mask(12345, 1, 2, 4, 5, 0.9)
-    assert m.shape == (1, 2, 4, 5)
+    m, keff = keep_mask(12345, 1, 2, 4, 5, 0.9)
+    assert m.shape == (1, 2, 4, 5) and abs(keff - 0.9) < 1e-4
 
 
 def _run(cuda, B, H, Sq, Sk, causal, masked, dropout=0.0, seed=7):
@@ -73,9 +78,10 @@ def _run(cuda, B, H, Sq, Sk, causal, masked, dropout=0.0, seed=7):
         for b in range(B):
             mask[b, lens[b]:] = -10000.0
     o = ops.attention(q, k, v, causal=causal, mask=mask, dropout=dropout, training=dropout > 0, seed=seed)
-    km = keep_mask(seed, B, H, Sq, Sk, 1 - dropout).to(cuda) if dropout else None
+    km, keff = keep_mask(seed, B, H, Sq, Sk, 1 - dropout) if dropout else (None, 1.0)
+    km = km.to(cuda) if km is not None else None
     qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
-    r = A.reference_attention(qr, kr, vr, causal=causal, mask=mask, keep_mask=km, keep=1 - dropout)
+    r = A.reference_attention(qr, kr, vr, causal=causal, mask=mask, keep_mask=km, keep=keff)
     close(o, r, 2e-2)
     do = torch.randn_like(r)
     r.backward(do)
