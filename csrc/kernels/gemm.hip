@@ -197,19 +197,84 @@ DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bi
 
 // NHWC conv data-gradient: dX[N,H,W,C] = dY[N,P,Q,K] (*) Wt where Wt is the filter
 // re-laid out as [C][R][S][K] (see dtf_filter_to_crsk).
+// Compact filter taps for one strided-dgrad phase: dst[c][j][jw][k] = src[c][rh + sh*j][rw + sw*jw][k]
+__global__ void tap_gather_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, int C, int R, int S,
+                                  int K, int rh, int rw, int sh, int sw, int nkh, int nkw) {
+  const long k8 = K / 8, total = (long)C * nkh * nkw * k8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long t = i;
+    const int kc = (int)(t % k8); t /= k8;
+    const int jw = (int)(t % nkw); t /= nkw;
+    const int j = (int)(t % nkh);
+    const int c = (int)(t / nkh);
+    const long so = (((long)c * R + rh + sh * j) * S + rw + sw * jw) * K + kc * 8;
+    *reinterpret_cast<uint4*>(dst + i * 8) = *reinterpret_cast<const uint4*>(src + so);
+  }
+}
+
+// NHWC conv data-gradient: dX[N][H][W][C] = sum over taps of dY gathered at the taps' output pixels x W.
+// Wcrsk: filter as [C][R][S][K]. Stride > 1 (dilation 1) is decomposed into sh*sw phases by output-pixel
+// parity: every phase is a stride-1 dgrad over its own pixel sub-grid using only the taps that reach it
+// (compact filter gathered into ws), stored through the epilogue's row remap. This removes the
+// (1 - 1/(sh*sw)) of MFMA work a direct strided gather would spend on structural zeros.
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
-                           float beta, int tile, void* stream) {
+                           float beta, int tile, void* ws, long ws_bf16, void* stream) {
   if ((C & 3) || (K & 7)) return -1;
-  GemmArgs a{};
-  a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
-  a.A = (const bf16_t*)dY; a.B = (const bf16_t*)Wcrsk; a.C = dX;
-  a.M = N * H * W; a.N = C; a.K = R * S * K;
-  a.lda = K; a.ldb = (long)R * S * K; a.ldc = C;
-  a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
-  a.alpha = 1.f; a.beta = beta; a.act = 0; a.out_f32 = out_f32;
-  bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
-  dispatch(a, pointwise ? OP_KCONTIG : OP_DGRAD, OP_KCONTIG, tile, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  const bool phased = (sh > 1 || sw > 1) && dh == 1 && dw == 1 && ws != nullptr &&
+                      ws_bf16 >= (long)C * R * S * K && !(C & 7);
+  if (!phased) {
+    GemmArgs a{};
+    a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
+    a.A = (const bf16_t*)dY; a.B = (const bf16_t*)Wcrsk; a.C = dX;
+    a.M = N * H * W; a.N = C; a.K = R * S * K;
+    a.lda = K; a.ldb = (long)R * S * K; a.ldc = C;
+    a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
+    a.alpha = 1.f; a.beta = beta; a.act = 0; a.out_f32 = out_f32;
+    bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+    dispatch(a, pointwise ? OP_KCONTIG : OP_DGRAD, OP_KCONTIG, tile, st);
+    return (int)hipGetLastError();
+  }
+  // phases without taps produce zeros: clear dX once unless accumulating
+  bool empty_phase = false;
+  for (int h0 = 0; h0 < sh; ++h0)
+    for (int w0 = 0; w0 < sw; ++w0) {
+      const int rh = (h0 + ph) % sh, rw = (w0 + pw) % sw;
+      if (rh >= R || rw >= S) empty_phase = true;
+    }
+  if (empty_phase && beta == 0.f)
+    (void)hipMemsetAsync(dX, 0, (size_t)N * H * W * C * (out_f32 ? 4 : 2), st);
+  bf16_t* wsb = (bf16_t*)ws;
+  long used = 0;
+  for (int h0 = 0; h0 < sh; ++h0) {
+    for (int w0 = 0; w0 < sw; ++w0) {
+      const int Hs = (H - h0 + sh - 1) / sh, Ws = (W - w0 + sw - 1) / sw;
+      const int rh = (h0 + ph) % sh, rw = (w0 + pw) % sw;
+      if (Hs <= 0 || Ws <= 0 || rh >= R || rw >= S) continue;
+      const int nkh = (R - rh + sh - 1) / sh, nkw = (S - rw + sw - 1) / sw;
+      const int ch = (h0 + ph - rh) / sh, cw = (w0 + pw - rw) / sw;
+      const long taps = (long)C * nkh * nkw * K;
+      bf16_t* Bp = wsb + used;
+      used += taps;
+      const long t8 = taps / 8;
+      hipLaunchKernelGGL(tap_gather_kernel, dim3((unsigned)std::min<long>((t8 + 255) / 256, 2048)), dim3(256), 0,
+                         st, (const bf16_t*)Wcrsk, Bp, C, R, S, K, rh, rw, sh, sw, nkh, nkw);
+      GemmArgs a{};
+      a.g = make_geom(N, Hs, Ws, C, K, nkh, nkw, P, Q, 1, 1, ch, cw, 1, 1);
+      a.A = (const bf16_t*)dY; a.B = Bp; a.C = dX;
+      a.M = N * Hs * Ws; a.N = C; a.K = nkh * nkw * K;
+      a.lda = K; a.ldb = (long)nkh * nkw * K; a.ldc = C;
+      a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
+      a.alpha = 1.f; a.beta = beta; a.act = 0; a.out_f32 = out_f32;
+      a.crm = 1;
+      a.dRm1 = make_fastdiv((uint32_t)(Hs * Ws)); a.dRm2 = make_fastdiv((uint32_t)Ws);
+      a.rmH = H; a.rmW = W; a.rmsh = sh; a.rmsw = sw; a.rmh0 = h0; a.rmw0 = w0;
+      // a 1x1 tap set reading dY pixel-for-pixel is a plain GEMM over dY rows
+      const bool pointwise = nkh == 1 && nkw == 1 && ch == 0 && cw == 0 && Hs == P && Ws == Q;
+      dispatch(a, pointwise ? OP_KCONTIG : OP_DGRAD, OP_KCONTIG, tile, st);
+    }
+  }
   return (int)hipGetLastError();
 }
 

@@ -66,7 +66,20 @@ struct GemmArgs {
   int atomic_out;       // atomicAdd into float C (split-K / accumulate)
   long slab;            // >0: split-K partials go to slab (blockIdx.z) of this many elements (plain stores)
   ConvGeom g;
+  // optional output-row remap (strided dgrad phases): row m = (n, hh, ww) over an rmHs x rmWs grid is stored
+  // at pixel (n, rmsh*hh + rmh0, rmsw*ww + rmw0) of an rmH x rmW image
+  int crm;
+  FastDiv dRm1, dRm2;
+  int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
 };
+
+__device__ __forceinline__ long out_row(const GemmArgs& a, int m) {
+  if (!a.crm) return m;
+  uint32_t n, hw, hh, ww;
+  fdivmod((uint32_t)m, a.dRm1, n, hw);
+  fdivmod(hw, a.dRm2, hh, ww);
+  return ((long)n * a.rmH + (long)(a.rmsh * (int)hh + a.rmh0)) * a.rmW + (a.rmsw * (int)ww + a.rmw0);
+}
 
 constexpr int BK = 64;
 constexpr int NT = 256;
@@ -400,6 +413,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * WTM + i * 16 + (lane & 15);
     const bool mv = m < a.M;
+    const long mrow = out_row(a, mv ? m : 0);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WTN + j * 16 + (lane >> 4) * 4;
@@ -407,7 +421,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
-      const long off = cbase + (long)m * a.ldc + n;
+      const long off = cbase + mrow * a.ldc + n;
       if (a.atomic_out) {
         float* Cf = reinterpret_cast<float*>(a.C) + off;
 #pragma unroll

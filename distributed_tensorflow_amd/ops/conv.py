@@ -56,8 +56,9 @@ def conv_dgrad_raw(dy, w_master, g):
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     wc = crsk_shadow(w_master, K, R * S, C)
     dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device)
+    ws = workspace(dy.device)  # strided convs: per-phase compact filters (bf16) live here
     call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0.0,
-         -1, stream())
+         -1, ptr(ws), 2 * ws.numel(), stream())
     return dx
 
 

@@ -91,6 +91,9 @@ CONV_CASES = [
     (2, 224, 224, 8, 64, 7, 7, 2, 3),
     (3, 7, 7, 512, 512, 3, 3, 1, 1),
     (1, 13, 11, 24, 40, 3, 5, 1, 2),
+    (1, 15, 13, 16, 32, 3, 3, 2, 1),   # odd sizes, strided dgrad phases
+    (2, 9, 9, 32, 64, 1, 1, 2, 0),     # strided 1x1: 3 of 4 phases have no taps
+    (1, 10, 11, 16, 16, 3, 3, 3, 1),   # stride 3
 ]
 
 
