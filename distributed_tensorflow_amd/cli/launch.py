@@ -52,42 +52,83 @@ def _pump(prefix, stream, out):
 
 
 def launch(cmd, num_ps=1, num_workers=1, num_chief=1, gpus=None, ps_gpus=False, chief_job="master", env=None,
-           timeout=None, log=sys.stdout):
+           timeout=None, log=sys.stdout, host_kv=False, max_restarts=0):
+    """Start every task and supervise them.
+
+    host_kv: the launcher itself hosts the coordination KV store (DTF_KV_ADDR), so it outlives any task.
+    max_restarts: a chief/worker task that exits abnormally is restarted (same TF_CONFIG and port, without
+    DTF_FAULT) up to this many times in total — the "kill -9 the chief, relaunch, restore from the
+    checkpoint" recovery path. Requires host_kv (the chief would otherwise take the
+    coordination service down with it)."""
+    import time
     cluster = make_cluster(num_ps, num_workers, num_chief, chief_job)
     tasks = [("ps", i) for i in range(num_ps)] + [(chief_job, i) for i in range(num_chief)] + \
             [("worker", i) for i in range(num_workers)]
     gpu_list = [g for g in (gpus.split(",") if gpus else []) if g != ""]
-    procs = []
+    kv_server = None
+    if host_kv or max_restarts:
+        from ..parallel.kv import KVServer
+        kv_server = KVServer("127.0.0.1", 0)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    envs = {}
     gi = 0
     for t, i in tasks:
         e = dict(os.environ, **(env or {}))
-        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
         e["TF_CONFIG"] = json.dumps({"cluster": cluster, "task": {"type": t, "index": i}})
         e["DTF_ROLE"] = f"{t}{i}"
+        if kv_server is not None:
+            e["DTF_KV_ADDR"] = f"127.0.0.1:{kv_server.port}"
         if gpu_list and (t != "ps" or ps_gpus):
             e["HIP_VISIBLE_DEVICES"] = gpu_list[gi % len(gpu_list)]
             gi += 1
         else:
             e["HIP_VISIBLE_DEVICES"] = ""
             e["CUDA_VISIBLE_DEVICES"] = ""
+        envs[(t, i)] = e
+
+    def spawn(t, i, e):
         p = subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
         th = threading.Thread(target=_pump, args=(f"{t}{i}", p.stdout, log), daemon=True)
         th.start()
-        procs.append((t, i, p, th))
+        return p, th
+
+    procs = {(t, i): spawn(t, i, envs[(t, i)]) for t, i in tasks}
+    restarts = 0
     rc = 0
+    deadline = None if timeout is None else time.time() + timeout
     try:
-        for t, i, p, th in procs:
-            r = p.wait(timeout=timeout)
-            th.join(timeout=5)
-            if r != 0 and rc == 0:
-                rc = r
-    except subprocess.TimeoutExpired:
-        rc = 124
+        running = set(procs)
+        while running:
+            for key in list(running):
+                p, th = procs[key]
+                r = p.poll()
+                if r is None:
+                    continue
+                th.join(timeout=5)
+                t, i = key
+                if r != 0 and t != "ps" and restarts < max_restarts:
+                    restarts += 1
+                    log.write(f"[launch] {t}{i} exited with {r}; restart {restarts}/{max_restarts}\n")
+                    log.flush()
+                    e = dict(envs[key])
+                    e.pop("DTF_FAULT", None)
+                    e["DTF_RESTART"] = str(restarts)
+                    procs[key] = spawn(t, i, e)
+                    continue
+                running.discard(key)
+                if r != 0 and rc == 0:
+                    rc = r
+            if deadline is not None and time.time() > deadline:
+                rc = 124
+                break
+            time.sleep(0.05)
     finally:
-        for t, i, p, th in procs:
+        for p, th in procs.values():
             if p.poll() is None:
                 p.kill()
+        if kv_server is not None:
+            kv_server.stop()
     return rc, cluster
 
 
@@ -100,12 +141,15 @@ def main(argv=None):
     ap.add_argument("--gpus", default=None)
     ap.add_argument("--ps_gpus", action="store_true")
     ap.add_argument("--timeout", type=float, default=None)
+    ap.add_argument("--host_kv", action="store_true", help="launcher hosts the coordination KV store")
+    ap.add_argument("--max_restarts", type=int, default=0, help="restart failed chief/worker tasks")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
     if not cmd:
         cmd = [sys.executable, "-m", "distributed_tensorflow_amd.cli.train"]
-    rc, _ = launch(cmd, a.ps, a.workers, a.chief, a.gpus, a.ps_gpus, a.chief_job, timeout=a.timeout)
+    rc, _ = launch(cmd, a.ps, a.workers, a.chief, a.gpus, a.ps_gpus, a.chief_job, timeout=a.timeout,
+                   host_kv=a.host_kv, max_restarts=a.max_restarts)
     return rc
 
 

@@ -110,6 +110,7 @@ def run_standalone():
 def run_distributed(resolver):
     from .. import context, summary
     from ..models.linear import LinearRegression
+    from ..parallel.fault import injector
     from ..parallel.parameter_server import ParameterServerStrategy
     from ..train.checkpoint import Saver
     from ..train.supervisor import ManagedTraining
@@ -143,10 +144,12 @@ def run_distributed(resolver):
         X = torch.as_tensor(train_X, device=dev).reshape(-1, 1, 1)
         Y = torch.as_tensor(train_Y, device=dev).reshape(-1, 1, 1)
         print("Run training with epoch number: {}".format(FLAGS.max_epochs))
+        faults = injector()
         for i in range(FLAGS.max_epochs):
             for j in range(X.shape[0]):
                 _step(model, loss_fn, X[j], Y[j])
                 strategy.apply_gradients(opt, arena)
+                faults.on_step(i * X.shape[0] + j + 1)
             if i % FLAGS.checkpoint_period == 0:
                 with torch.no_grad():
                     loss = float(loss_fn(Y[0], model(X[0])))

@@ -34,6 +34,7 @@ from .. import _native, context
 from .._runtime_sigs import err
 from ..variables import ParamArena, Variable
 from .cluster_resolver import TFConfigClusterResolver
+from .fault import Heartbeat, HeartbeatMonitor, retry
 from .kv import KVClient, KVServer
 from .strategy import Strategy
 
@@ -47,6 +48,11 @@ def _host_port(addr):
 
 
 def kv_address(resolver):
+    """Coordination-service address: DTF_KV_ADDR (hosted by a supervising launcher, so it survives task
+    restarts) or the first trainer task's port (hosted by the chief)."""
+    env = os.environ.get("DTF_KV_ADDR")
+    if env:
+        return _host_port(env)
     tasks = resolver.trainer_tasks()
     if not tasks:
         raise ValueError("cluster has no chief/worker task to host the coordination service")
@@ -119,6 +125,7 @@ class ParameterServer:
         self.device = context.parse_device(device) if device is not None else context.default_device()
         kh, kp = kv_address(self.r)
         self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
+        self._hb = Heartbeat(self.kv, f"ps{self.index}").start()
         self.slot_sync_every = slot_sync_every
         self.applies = 0
 
@@ -210,6 +217,7 @@ class ParameterServer:
         self.stop()
 
     def stop(self):
+        self._hb.stop()
         if self.srv:
             self.lib.dtfrt_ps_server_stop(self.srv)
             self.srv = None
@@ -238,9 +246,10 @@ class ParameterServerStrategy(Strategy):
         self._device = context.parse_device(device) if device is not None else context.default_device()
         kh, kp = kv_address(self.r)
         self._kv_server = None
-        if self.r.is_chief:
+        if self.r.is_chief and not os.environ.get("DTF_KV_ADDR"):
             self._kv_server = KVServer("0.0.0.0", kp)
         self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
+        self._hb = Heartbeat(self.kv, f"{self.r.task_type}{self.r.task_id}").start()
         self._clients = None
         self._layout = None
         self._done = False
@@ -370,7 +379,13 @@ class ParameterServerStrategy(Strategy):
             self._done = True
             self.kv.add("done", 1)
 
+    def dead_tasks(self, timeout=10.0):
+        """Cluster tasks (ps*, trainers) whose heartbeat is older than `timeout` seconds."""
+        names = [f"ps{i}" for i in range(self.num_ps)] + [f"{t}{i}" for t, i in self.r.trainer_tasks()]
+        return HeartbeatMonitor(self.kv, names).dead(timeout)
+
     def shutdown(self, timeout_s=600):
+        self._hb.stop()
         self.report_done()
         if self.is_chief:
             # keep the coordination service up until every trainer and the PS tasks are finished
@@ -405,8 +420,10 @@ class ClusterCoordinator:
         self._ex = cf.ThreadPoolExecutor(1)
         self._pending = []
 
-    def schedule(self, fn, args=(), kwargs=None):
-        f = self._ex.submit(fn, *args, **(kwargs or {}))
+    def schedule(self, fn, args=(), kwargs=None, retries=2):
+        """Run a closure asynchronously; transient transport failures (ConnectionError / TimeoutError)
+        reschedule it up to `retries` times before the error surfaces in fetch()/join()."""
+        f = self._ex.submit(retry, fn, *args, retries=retries, **(kwargs or {}))
         self._pending.append(f)
         return RemoteValue(f)
 

@@ -49,7 +49,9 @@ class ManagedTraining:
                 self.before_save()
             p = self.saver.save(None, os.path.join(self.logdir, self.base), global_step=self._step())
             self.saves += 1
-            return p
+        from ..parallel.fault import injector
+        injector().on_checkpoint(self.saves)  # DTF_FAULT=kill@ckpt=N (fault-tolerance tests)
+        return p
 
     def _timer(self):
         while not self._stop.wait(self.save_model_secs):
