@@ -94,6 +94,7 @@ def build_kernels(verbose=True, jobs=None):
 
 def build_runtime(verbose=True, jobs=None):
     srcs, hdrs = _sources("runtime", (".cc", ".cpp"))
+    srcs = [s for s in srcs if not os.path.basename(s).startswith("selftest")]  # sanitizer driver (tools/)
     if not srcs:
         return None
     cxx = os.environ.get("CXX", "g++")

@@ -305,3 +305,17 @@ def test_ps_transport_pull_push_roundtrip():
     assert torch.equal(buf, torch.arange(16, dtype=torch.float32) - 1)
     c.close()
     lib.dtfrt_ps_server_stop(srv)
+
+
+@pytest.mark.slow
+def test_runtime_under_sanitizers(tmp_path):
+    """ASan+UBSan and TSan builds of the C++ runtime run a concurrent self-test cleanly."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no host compiler")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["bash", os.path.join(root, "tools", "sanitize_runtime.sh"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "sanitizers clean" in r.stdout
