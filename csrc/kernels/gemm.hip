@@ -93,6 +93,8 @@ static int pick_tile(long M, long N, long batch_splits) {
   return 3;
 }
 
+int gemm256_try(GemmArgs& a, hipStream_t st);  // gemm256.hip
+
 static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st) {
   if (tile < 0) tile = pick_tile(a.M, a.N, (long)a.batch * a.splitk);
   if (amode == OP_KCONTIG && bmode == OP_KCONTIG) launch_modes<OP_KCONTIG, OP_KCONTIG>(a, tile, st);
@@ -171,6 +173,10 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
     }
   }
   if (stats && (a.batch > 1 || a.splitk > 1)) return -7;
+  // large K-contiguous problems: the 256x256 glds-pipelined kernel when it fills the chip
+  if (!a_kouter && !b_kouter && tile < 0 && !stats && a.splitk == 1 &&
+      (long)cdiv(M, 256) * cdiv(N, 256) * a.batch >= 240 && gemm256_try(a, (hipStream_t)stream) == 0)
+    return (int)hipGetLastError();
   dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
   if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();

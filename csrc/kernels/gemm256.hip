@@ -1,0 +1,243 @@
+// 256x256x64 bf16 GEMM for large K-contiguous problems (C = alpha * A B^T (+ beta C, bias, act)), gfx950.
+//
+// The register-staged 128x128 kernel (gemm_core.h) tops out near the ~0.9 PF ceiling of a one-barrier-per-
+// K-step structure; this kernel is the 1-block/CU pipelined form:
+//  * 8 waves (2 M x 4 N), each owning a 128x64 output tile = 8x4 MFMA 16x16 fragments (128 accumulators);
+//  * A and B tiles staged straight into LDS by global_load_lds (16 B/lane, no VGPR round trip), double-
+//    buffered, each K-tile split into four half-tiles A0 A1 B0 B1 (128 rows x 64 k, 16 KiB); the LDS image is
+//    lane-linear, so the bank-conflict XOR swizzle is applied to the per-lane SOURCE address and undone on
+//    the ds_read side (same involution);
+//  * every K-tile runs as 4 phases, one per output quadrant (A0B0, A0B1, A1B1, A1B0 — each phase reloads
+//    only the operand half that changed). Each phase issues the next half-tile of the prefetch stream
+//    (B0 B1 A1 of tile t+1, then A0 of tile t+2), so three half-tiles stay in flight across the raw
+//    s_barriers; the only waits are counted `s_waitcnt vmcnt(6)` before the barrier of the phase whose half
+//    just became due (never vmcnt(0) inside the loop).
+// Requirements (host-checked): K % 64 == 0, A/B rows 16-B aligned (lda, ldb % 8 == 0). M, N arbitrary
+// (rows past the edge are clamped on load and masked on store).
+#include "gemm_core.h"
+
+namespace dtf {
+namespace {
+
+constexpr int NT2 = 512;
+constexpr int HALF = 128 * 128;  // bytes of one half-tile image (128 rows x 64 bf16)
+constexpr int BUF = 4 * HALF;    // A0 | A1 | B0 | B1
+
+// LDS image row -> block-tile row (A: two 64-row slices per M-wave; B: two 32-col slices per N-wave)
+__device__ __forceinline__ int a_row(int r, int h) { return (r >> 6) * 128 + h * 64 + (r & 63); }
+__device__ __forceinline__ int b_row(int r, int h) { return (r >> 5) * 64 + h * 32 + (r & 31); }
+
+__device__ __forceinline__ void glds16(const bf16_t* g, char* lds) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+
+  // ---- block -> tile (XCD-aware bijective remap, grouped order) ----
+  const int nwg = a.tiles_m * a.tiles_n;
+  int bid = blockIdx.x;
+  {
+    int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+    bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  }
+  constexpr int GROUP = 4;
+  const int per_group = GROUP * a.tiles_n;
+  const int grp = bid / per_group;
+  const int first_m = grp * GROUP;
+  const int gsize = min(a.tiles_m - first_m, GROUP);
+  const int in_g = bid - grp * per_group;
+  const int tile_m = first_m + in_g % gsize;
+  const int tile_n = in_g / gsize;
+  const int m0 = tile_m * 256, n0 = tile_n * 256;
+  const int bz = blockIdx.z;
+  const bf16_t* Ap = a.A + (long)bz * a.sA;
+  const bf16_t* Bp = a.B + (long)bz * a.sB;
+
+  // ---- per-thread glds sources: half h (0,1 = A0,A1; 2,3 = B0,B1), instruction u ----
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = 8 * (u * 8 + w) + (lane >> 3);
+      const int lc = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at this physical slot
+      if (h < 2) {
+        const int g = min(m0 + a_row(r, h), a.M - 1);
+        src[h][u] = Ap + (long)g * a.lda + lc * 8;
+      } else {
+        const int g = min(n0 + b_row(r, h - 2), a.N - 1);
+        src[h][u] = Bp + (long)g * a.ldb + lc * 8;
+      }
+    }
+  auto issue = [&](int h, int t, int buf) {
+    const long ko = (long)t * BK;
+    char* d = smem + buf * BUF + h * HALF + w * 1024;
+    glds16(src[h][0] + ko, d);
+    glds16(src[h][1] + ko, d + 8 * 1024);
+  };
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  v8bf fa[4][2], fb[2][2];
+
+  auto read_a = [&](int buf, int h) {
+    const char* base = smem + buf * BUF + h * HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag_kcontig(base, wr * 64 + i * 16, kk, lane);
+  };
+  auto read_b = [&](int buf, int h) {
+    const char* base = smem + buf * BUF + (2 + h) * HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag_kcontig(base, wc * 32 + j * 16, kk, lane);
+  };
+  auto mma = [&](int ha, int hb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ha * 4 + i][hb * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = a.K / BK;
+  // prologue: A0 B0 B1 A1 of tile 0, A0 of tile 1
+  issue(0, 0, 0);
+  issue(2, 0, 0);
+  issue(3, 0, 0);
+  issue(1, 0, 0);
+  if (nk > 1) issue(0, 1, 1);
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1, nb = buf ^ 1;
+    const bool more = t + 1 < nk, more2 = t + 2 < nk;
+    // phase 1: quadrant (A0, B0); due: A0(t), B0(t)
+    if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if (more) issue(2, t + 1, nb);
+    mma(0, 0);
+    // phase 2: (A0, B1); due: B1(t)
+    if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    read_b(buf, 1);
+    if (more) issue(3, t + 1, nb);
+    mma(0, 1);
+    // phase 3: (A1, B1); due: A1(t)
+    if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    read_a(buf, 1);
+    if (more) issue(1, t + 1, nb);
+    mma(1, 1);
+    // phase 4: (A1, B0); nothing new due. A0 of this buffer was last read in phase 1 (two barriers ago)
+    read_b(buf, 0);
+    if (more2) issue(0, t + 2, buf);
+    mma(1, 0);
+  }
+
+  // ---- epilogue (no glds outstanding: the last tile drained with vmcnt(0)) ----
+  const float alpha = a.scales ? a.alpha * a.scales[0] * a.scales[1] : a.alpha;
+  const long cbase = (long)bz * a.sC;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= a.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + (lane >> 4) * 4;
+      if (n >= a.N) continue;  // N % 4 == 0 (host)
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
+      const long off = cbase + (long)m * a.ldc + n;
+      if (a.beta != 0.f) {
+        if (a.out_f32) {
+          float4 o = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(a.C) + off);
+          v[0] += a.beta * o.x; v[1] += a.beta * o.y; v[2] += a.beta * o.z; v[3] += a.beta * o.w;
+        } else {
+          uint2 o = *reinterpret_cast<const uint2*>(reinterpret_cast<bf16_t*>(a.C) + off);
+          v[0] += a.beta * __uint_as_float(o.x << 16); v[1] += a.beta * __uint_as_float(o.x & 0xffff0000u);
+          v[2] += a.beta * __uint_as_float(o.y << 16); v[3] += a.beta * __uint_as_float(o.y & 0xffff0000u);
+        }
+      }
+      if (a.bias) {
+        float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (a.aux) {
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(a.aux + off) = o;
+      }
+      if (a.act == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      } else if (a.act == 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+      }
+      if (a.out_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.C) + off) = o;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// Used by dtf_gemm for eligible problems; returns 0 if launched, 1 if not eligible.
+int gemm256_try(GemmArgs& a, hipStream_t st) {
+  if (a.K % BK || a.K < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.splitk != 1 || a.stats || a.atomic_out ||
+      a.slab || a.crm)
+    return 1;
+  if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return 1;
+  a.tiles_m = cdiv(a.M, 256);
+  a.tiles_n = cdiv(a.N, 256);
+  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch);
+  hipLaunchKernelGGL(gemm256_kernel, grid, dim3(NT2), 0, st, a);
+  return 0;
+}
+
+}  // namespace dtf
+
+// Direct entry for benchmarks/tests: C[M][N] = A[M][K] . B[N][K]^T (bf16 in, bf16 or f32 out)
+DTF_API int dtf_gemm256(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+                        int out_f32, void* stream) {
+  dtf::GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.batch = 1; a.splitk = 1; a.alpha = 1.f; a.beta = 0.f; a.out_f32 = out_f32;
+  if (N & 3) return -1;
+  if (dtf::gemm256_try(a, (hipStream_t)stream)) return -2;
+  return (int)hipGetLastError();
+}
