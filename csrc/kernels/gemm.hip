@@ -93,7 +93,7 @@ static int pick_tile(long M, long N, long batch_splits) {
   return 3;
 }
 
-int gemm256_try(GemmArgs& a, hipStream_t st);  // gemm256.hip
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st);  // gemm256.hip
 
 static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st) {
   if (tile < 0) tile = pick_tile(a.M, a.N, (long)a.batch * a.splitk);
@@ -164,7 +164,23 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
       a.C = ws;
       a.slab = (long)M * N;  // z = batch*splitk + split -> slab index
       a.beta = 0.f;
-      dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
+      bool big = false;
+      if (tile < 0 && M >= 256 && N >= 256) {  // 256x256 tiles: re-split for them (>= ~1 block per CU)
+        GemmArgs b = a;
+        const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * a.batch;
+        int s2 = (int)std::min<long>(std::max<long>(1, (256 + t256 - 1) / t256), std::max<long>(1, K / 1024));
+        if ((long)s2 * mn <= ws_elems) {
+          b.splitk = s2;
+          b.kchunk = ((K + s2 - 1) / s2 + BK - 1) / BK * BK;
+          if (gemm256_try(b, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG,
+                          (hipStream_t)stream) == 0) {
+            big = true;
+            splitk = s2;
+          }
+        }
+      }
+      if (!big)
+        dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
       // slabs are [batch][splitk][M*N]: reduce each batch separately
       for (int b = 0; b < a.batch; ++b)
         dtf_sum_rows(ws + (long)b * splitk * M * N, (long)M * N, splitk, (long)M * N, (float*)C + (long)b * M * N,
@@ -174,8 +190,8 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
   }
   if (stats && (a.batch > 1 || a.splitk > 1)) return -7;
   // large K-contiguous problems: the 256x256 glds-pipelined kernel when it fills the chip
-  if (!a_kouter && !b_kouter && tile < 0 && !stats && a.splitk == 1 &&
-      (long)cdiv(M, 256) * cdiv(N, 256) * a.batch >= 240 && gemm256_try(a, (hipStream_t)stream) == 0)
+  if (tile < 0 && !stats && a.splitk == 1 && (long)cdiv(M, 256) * cdiv(N, 256) * a.batch >= 240 &&
+      gemm256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream) == 0)
     return (int)hipGetLastError();
   dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
   if (stat_rows) *stat_rows = a.tiles_m;

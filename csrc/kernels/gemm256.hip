@@ -7,13 +7,17 @@
 //    buffered, each K-tile split into four half-tiles A0 A1 B0 B1 (128 rows x 64 k, 16 KiB); the LDS image is
 //    lane-linear, so the bank-conflict XOR swizzle is applied to the per-lane SOURCE address and undone on
 //    the ds_read side (same involution);
-//  * every K-tile runs as 4 phases, one per output quadrant (A0B0, A0B1, A1B1, A1B0 — each phase reloads
-//    only the operand half that changed). Each phase issues the next half-tile of the prefetch stream
-//    (B0 B1 A1 of tile t+1, then A0 of tile t+2), so three half-tiles stay in flight across the raw
-//    s_barriers; the only waits are counted `s_waitcnt vmcnt(6)` before the barrier of the phase whose half
-//    just became due (never vmcnt(0) inside the loop).
-// Requirements (host-checked): K % 64 == 0, A/B rows 16-B aligned (lda, ldb % 8 == 0). M, N arbitrary
-// (rows past the edge are clamped on load and masked on store).
+//  * every K-tile runs as 4 phases, one per output quadrant (A0B0, A0B1, A1B1, A1B0); each half is read
+//    from LDS once per tile. Each phase issues one half-tile of the prefetch stream, so 2-3 half-tiles stay
+//    in flight across the raw s_barriers; the only waits are counted `s_waitcnt vmcnt(N)` (never 0 inside
+//    the loop), and the two 4-wave groups run one phase apart so MFMA work of one group covers the LDS
+//    reads / barrier waits of the other on every SIMD (schedule and hazard distances: see the K-loop).
+// K-outer operands (stored [K][rows], e.g. dY^T and X^T of a weight gradient, or W of a data gradient) use
+// a [64 k][128 rows] half image (256-B k-rows, 16-B chunks XOR-swizzled by (k & 3) << 1) filled by the same
+// lane-linear glds and read with ds_read_b64_tr_b16. Split-K writes f32 slabs (blockIdx.z = batch*splitk +
+// split) reduced by dtf_sum_rows.
+// Requirements (host-checked): K % 64 == 0 per split, 16-B aligned rows (lda, ldb % 8 == 0), K-outer
+// operands need their row count % 8 == 0. M, N arbitrary (edge rows clamped on load, masked on store).
 #include "gemm_core.h"
 
 namespace dtf {
@@ -27,6 +31,22 @@ constexpr int BUF = 4 * HALF;    // A0 | A1 | B0 | B1
 __device__ __forceinline__ int a_row(int r, int h) { return (r >> 6) * 128 + h * 64 + (r & 63); }
 __device__ __forceinline__ int b_row(int r, int h) { return (r >> 5) * 64 + h * 32 + (r & 31); }
 
+// K-outer half image [64 k][128 cols]: physical 16-B chunk of logical chunk c in k-row k
+__device__ __forceinline__ int ko_swz(int k) { return (k & 3) << 1; }
+// transposed fragment of a K-outer half: lane (G, i) gets col rb + i, k = 32 kk + 8 G + 0..7
+__device__ __forceinline__ v8bf frag_ko(const char* lds, int rb, int kk, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  v4s r[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = 32 * kk + 8 * G + 4 * h + q, g = (rb >> 2) + p;
+    r[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(v4s, lds + k * 256 + (((g >> 1) ^ ko_swz(k)) << 4) + (g & 1) * 8));
+  }
+  v8s both = __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(v8bf, both);
+}
+
 __device__ __forceinline__ void glds16(const bf16_t* g, char* lds) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -38,6 +58,7 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
+template <int AM, int BMD>
 __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -59,28 +80,43 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   const int tile_m = first_m + in_g % gsize;
   const int tile_n = in_g / gsize;
   const int m0 = tile_m * 256, n0 = tile_n * 256;
-  const int bz = blockIdx.z;
+  const int z = blockIdx.z;
+  const int bz = z / a.splitk, sk = z % a.splitk;
+  const int kbeg = sk * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
   const bf16_t* Ap = a.A + (long)bz * a.sA;
   const bf16_t* Bp = a.B + (long)bz * a.sB;
 
-  // ---- per-thread glds sources: half h (0,1 = A0,A1; 2,3 = B0,B1), instruction u ----
+  // ---- per-thread glds sources: half h (0,1 = A0,A1; 2,3 = B0,B1), instruction u; advance per K-tile ----
   const bf16_t* src[4][2];
+  long kstep[4];
 #pragma unroll
-  for (int h = 0; h < 4; ++h)
+  for (int h = 0; h < 4; ++h) {
+    const bool isA = h < 2;
+    const bool ko = isA ? (AM == OP_KOUTER) : (BMD == OP_KOUTER);
+    const bf16_t* P = isA ? Ap : Bp;
+    const long ld = isA ? a.lda : a.ldb;
+    const int lim = isA ? a.M : a.N;
+    const int o0 = isA ? m0 : n0;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int r = 8 * (u * 8 + w) + (lane >> 3);
-      const int lc = (lane & 7) ^ ((r >> 1) & 7);  // logical chunk stored at this physical slot
-      if (h < 2) {
-        const int g = min(m0 + a_row(r, h), a.M - 1);
-        src[h][u] = Ap + (long)g * a.lda + lc * 8;
-      } else {
-        const int g = min(n0 + b_row(r, h - 2), a.N - 1);
-        src[h][u] = Bp + (long)g * a.ldb + lc * 8;
+      if (!ko) {  // [128 rows][64 k] image, 8 lanes per 128-B row
+        const int r = 8 * (u * 8 + w) + (lane >> 3);
+        const int lc = (lane & 7) ^ ((r >> 1) & 7);
+        const int g = min(o0 + (isA ? a_row(r, h) : b_row(r, h - 2)), lim - 1);
+        src[h][u] = P + (long)g * ld + kbeg + lc * 8;
+      } else {    // [64 k][128 cols] image, 16 lanes per 256-B k-row
+        const int k = 4 * (u * 8 + w) + (lane >> 4);
+        const int lc = (lane & 15) ^ ko_swz(k);
+        const int col = lc * 8;
+        const int g = min(o0 + (isA ? a_row(col, h) : b_row(col, h - 2)), lim - 8);
+        src[h][u] = P + (long)(kbeg + k) * ld + g;
       }
     }
+    kstep[h] = ko ? (long)BK * ld : (long)BK;
+  }
   auto issue = [&](int h, int t, int buf) {
-    const long ko = (long)t * BK;
+    const long ko = (long)t * kstep[h];
     char* d = smem + buf * BUF + h * HALF + w * 1024;
     glds16(src[h][0] + ko, d);
     glds16(src[h][1] + ko, d + 8 * 1024);
@@ -91,23 +127,27 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  v8bf fa[4][2], fb[2][2];
+  v8bf fa[4][2], fb0[2][2], fb1[2][2];
 
   auto read_a = [&](int buf, int h) {
     const char* base = smem + buf * BUF + h * HALF;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag_kcontig(base, wr * 64 + i * 16, kk, lane);
+      for (int kk = 0; kk < 2; ++kk)
+        fa[i][kk] = AM == OP_KOUTER ? frag_ko(base, wr * 64 + i * 16, kk, lane)
+                                    : frag_kcontig(base, wr * 64 + i * 16, kk, lane);
   };
-  auto read_b = [&](int buf, int h) {
+  auto read_b = [&](v8bf (&fb)[2][2], int buf, int h) {
     const char* base = smem + buf * BUF + (2 + h) * HALF;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag_kcontig(base, wc * 32 + j * 16, kk, lane);
+      for (int kk = 0; kk < 2; ++kk)
+        fb[j][kk] = BMD == OP_KOUTER ? frag_ko(base, wc * 32 + j * 16, kk, lane)
+                                     : frag_kcontig(base, wc * 32 + j * 16, kk, lane);
   };
-  auto mma = [&](int ha, int hb) {
+  auto mma = [&](const v8bf (&fb)[2][2], int ha, int hb) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -120,48 +160,63 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nk = a.K / BK;
-  // prologue: A0 B0 B1 A1 of tile 0, A0 of tile 1
-  issue(0, 0, 0);
-  issue(2, 0, 0);
-  issue(3, 0, 0);
-  issue(1, 0, 0);
+  // Schedule (phase index 4t+p, p = 0..3 for quadrants A0B0, A0B1, A1B1, A1B0). Each half of tile t is read
+  // from LDS once (B0 stays in registers for phase 3): A0,B0 at 4t, B1 at 4t+1, A1 at 4t+2. Prefetch issues:
+  // A0(t+1) at 4t-1, B0(t+1) at 4t, B1(t+1) at 4t+1, A1(t+1) at 4t+2 — each >= 2 phases after the previous
+  // content of its half was last read (WAR) and >= 3 before its first read (RAW). The two 4-wave groups run
+  // one phase apart (group 1 passes one extra barrier first), so group 1's MFMAs overlap group 0's LDS reads
+  // and barrier waits on every SIMD. With that stagger a barrier must also publish the NEXT phase's halves,
+  // so the wait before phase x covers the halves due at x and x+1: vmcnt(4|4|6|4).
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+  if (nk > 0) {
+    issue(0, 0, 0);
+    issue(2, 0, 0);
+    issue(3, 0, 0);
+    issue(1, 0, 0);
+  }
   if (nk > 1) issue(0, 1, 1);
-
+  if (wr == 1) {
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+  }
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1, nb = buf ^ 1;
     const bool more = t + 1 < nk, more2 = t + 2 < nk;
-    // phase 1: quadrant (A0, B0); due: A0(t), B0(t)
-    if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    // phase 0: (A0, B0)
+    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     read_a(buf, 0);
-    read_b(buf, 0);
+    read_b(fb0, buf, 0);
     if (more) issue(2, t + 1, nb);
-    mma(0, 0);
-    // phase 2: (A0, B1); due: B1(t)
-    if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    mma(fb0, 0, 0);
+    // phase 1: (A0, B1)
+    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
-    read_b(buf, 1);
+    read_b(fb1, buf, 1);
     if (more) issue(3, t + 1, nb);
-    mma(0, 1);
-    // phase 3: (A1, B1); due: A1(t)
+    mma(fb1, 0, 1);
+    // phase 2: (A1, B1)
     if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     read_a(buf, 1);
     if (more) issue(1, t + 1, nb);
-    mma(1, 1);
-    // phase 4: (A1, B0); nothing new due. A0 of this buffer was last read in phase 1 (two barriers ago)
-    read_b(buf, 0);
+    mma(fb1, 1, 1);
+    // phase 3: (A1, B0) from registers
+    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
     if (more2) issue(0, t + 2, buf);
-    mma(1, 0);
+    mma(fb0, 1, 0);
   }
+  if (wr == 0) barrier();
 
   // ---- epilogue (no glds outstanding: the last tile drained with vmcnt(0)) ----
   const float alpha = a.scales ? a.alpha * a.scales[0] * a.scales[1] : a.alpha;
-  const long cbase = (long)bz * a.sC;
+  const long cbase = a.slab > 0 ? (long)z * a.slab : (long)bz * a.sC;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);
@@ -216,28 +271,45 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
 }  // namespace
 
 // Used by dtf_gemm for eligible problems; returns 0 if launched, 1 if not eligible.
-int gemm256_try(GemmArgs& a, hipStream_t st) {
-  if (a.K % BK || a.K < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.splitk != 1 || a.stats || a.atomic_out ||
-      a.slab || a.crm)
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st) {
+  if (a.kchunk % BK || a.kchunk < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.stats || a.atomic_out || a.crm)
     return 1;
+  if ((a.splitk > 1 && a.K % a.kchunk && (a.K % a.kchunk) % BK) || a.K % BK) return 1;
   if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return 1;
+  if ((amode == OP_KOUTER && (a.M & 7)) || (bmode == OP_KOUTER && (a.N & 7))) return 1;
+  if ((amode != OP_KCONTIG && amode != OP_KOUTER) || (bmode != OP_KCONTIG && bmode != OP_KOUTER)) return 1;
   a.tiles_m = cdiv(a.M, 256);
   a.tiles_n = cdiv(a.N, 256);
-  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch);
-  hipLaunchKernelGGL(gemm256_kernel, grid, dim3(NT2), 0, st, a);
+  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
+  if (amode == OP_KCONTIG && bmode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
+  else if (amode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KOUTER>), grid, dim3(NT2), 0, st, a);
+  else if (bmode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
+  else hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KOUTER>), grid, dim3(NT2), 0, st, a);
   return 0;
 }
 
 }  // namespace dtf
 
-// Direct entry for benchmarks/tests: C[M][N] = A[M][K] . B[N][K]^T (bf16 in, bf16 or f32 out)
+// Direct entry for benchmarks/tests: C[M][N] = A(m,k) . B(n,k) (A [M][K] or [K][M] when a_kouter; B [N][K] or
+// [K][N] when b_kouter), bf16 in, bf16 or f32 out, optional split-K through f32 slabs in ws.
 DTF_API int dtf_gemm256(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
-                        int out_f32, void* stream) {
+                        int a_kouter, int b_kouter, int out_f32, int splitk, float* ws, long ws_elems,
+                        void* stream) {
   dtf::GemmArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
-  a.batch = 1; a.splitk = 1; a.alpha = 1.f; a.beta = 0.f; a.out_f32 = out_f32;
+  a.batch = 1; a.splitk = splitk < 1 ? 1 : splitk; a.alpha = 1.f; a.beta = 0.f; a.out_f32 = out_f32;
   if (N & 3) return -1;
-  if (dtf::gemm256_try(a, (hipStream_t)stream)) return -2;
+  a.kchunk = (K / a.splitk + dtf::BK - 1) / dtf::BK * dtf::BK;
+  hipStream_t st = (hipStream_t)stream;
+  if (a.splitk > 1) {
+    if (!out_f32 || ldc != N || !ws || ws_elems < (long)a.splitk * M * N) return -3;
+    a.C = ws;
+    a.slab = (long)M * N;
+  }
+  if (dtf::gemm256_try(a, a_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG, b_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG,
+                       st))
+    return -2;
+  if (a.splitk > 1) dtf_sum_rows(ws, (long)M * N, a.splitk, (long)M * N, (float*)C, 0, stream);
   return (int)hipGetLastError();
 }
