@@ -95,6 +95,17 @@ static int pick_tile(long M, long N, long batch_splits) {
 
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st);  // gemm256.hip
 
+// 256x256 (1 block/CU, ~1.12-1.24x faster per tile, more so at long K) vs 128x128 (2 blocks/CU): compare the
+// wave-quantisation efficiency of both tilings on 256 CUs.
+static bool prefer256(long M, long N, long K, long batch) {
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch, t128 = (long)cdiv(M, 128) * cdiv(N, 128) * batch;
+  if (t256 < 128) return false;
+  const double e256 = (double)t256 / (double)(((t256 + 255) / 256) * 256);
+  const double e128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
+  const double base = 1.12 + 0.12 * (double)std::min<long>(K, 4096) / 4096.0;
+  return base * e256 > e128;
+}
+
 static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st) {
   if (tile < 0) tile = pick_tile(a.M, a.N, (long)a.batch * a.splitk);
   if (amode == OP_KCONTIG && bmode == OP_KCONTIG) launch_modes<OP_KCONTIG, OP_KCONTIG>(a, tile, st);
@@ -168,8 +179,9 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
       if (tile < 0 && M >= 256 && N >= 256) {  // 256x256 tiles: re-split for them (>= ~1 block per CU)
         GemmArgs b = a;
         const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * a.batch;
-        int s2 = (int)std::min<long>(std::max<long>(1, (256 + t256 - 1) / t256), std::max<long>(1, K / 1024));
-        if ((long)s2 * mn <= ws_elems) {
+        // one round of 1-block/CU tiles: splits so that tiles x splits <= 256 CUs, >= 1024 of K per split
+        int s2 = (int)std::min<long>(std::max<long>(1, 256 / t256), std::max<long>(1, K / 1024));
+        if (t256 * s2 >= 200 && (long)s2 * mn <= ws_elems) {
           b.splitk = s2;
           b.kchunk = ((K + s2 - 1) / s2 + BK - 1) / BK * BK;
           if (gemm256_try(b, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG,
@@ -190,7 +202,7 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
   }
   if (stats && (a.batch > 1 || a.splitk > 1)) return -7;
   // large K-contiguous problems: the 256x256 glds-pipelined kernel when it fills the chip
-  if (tile < 0 && !stats && a.splitk == 1 && (long)cdiv(M, 256) * cdiv(N, 256) * a.batch >= 240 &&
+  if (tile < 0 && !stats && a.splitk == 1 && prefer256(M, N, K, a.batch) &&
       gemm256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream) == 0)
     return (int)hipGetLastError();
   dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
