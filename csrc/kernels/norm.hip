@@ -125,7 +125,7 @@ __global__ void bn_infer_coeff_kernel(const float* gamma, const float* beta, con
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
-                                                       long n8, int C, int relu) {
+                                                       long n8, int C, int relu, uint8_t* __restrict__ mbits) {
   const int c8 = C / 8;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % c8) * 8;
@@ -136,6 +136,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
     float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
     float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
     float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = f[j] * sc[j] + sh[j];
@@ -144,6 +145,31 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
       f[j] = v;
     }
     store8(y + i * 8, f);
+    if (mbits) {  // ReLU mask of the stored (bf16-rounded) values, 1 bit per element
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bits |= (uint32_t)(f2bf(f[j]) != 0 && f[j] > 0.f) << j;
+      mbits[i] = (uint8_t)bits;
+    }
+  }
+}
+
+// dz = dy masked by ReLU: either from the bf16 output (sign/zero test) or from the 1-bit mask
+__device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const uint8_t* mbits, long i8) {
+  if (mbits) {
+    const uint32_t b = mbits[i8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!((b >> j) & 1u)) d[j] = 0.f;
+  } else if (ymask) {
+    uint4 mv = *reinterpret_cast<const uint4*>(ymask + i8 * 8);
+    uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // bf16 > 0  <=>  sign bit clear and value bits non-zero
+      uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
+      if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
+      if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
+    }
   }
 }
 
@@ -151,6 +177,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
 // [0,C) sum dz, [C,2C) sum dz*xhat. No atomics; bn_bwd_finalize sums the rows.
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
                                                             const bf16_t* __restrict__ ymask,
+                                                            const uint8_t* __restrict__ mbits,
                                                             const bf16_t* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long M, int C,
@@ -170,17 +197,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
         float d[8], xv[8];
         load8(dy + r * C + cc * 8, d);
         load8(x + r * C + cc * 8, xv);
-        if (ymask) {
-          uint4 mv = *reinterpret_cast<const uint4*>(ymask + r * C + cc * 8);
-          uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            // bf16 > 0  <=>  sign bit clear and value bits non-zero
-            uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
-            if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
-            if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
-          }
-        }
+        relu_mask8(d, ymask, mbits, (r * C) / 8 + cc);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           s[j] += d[j];
@@ -221,6 +238,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ ymask,
+                                                           const uint8_t* __restrict__ mbits,
                                                            const bf16_t* __restrict__ x,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -232,15 +250,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
     float d[8], xv[8];
     load8(dy + i * 8, d);
     load8(x + i * 8, xv);
-    if (ymask) {
-      uint4 mv = *reinterpret_cast<const uint4*>(ymask + i * 8);
-      uint32_t w[4] = {mv.x, mv.y, mv.z, mv.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t lo = w[j] & 0xffffu, hi = w[j] >> 16;
-        if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
-        if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
-      }
+    if (ymask || mbits) {
+      relu_mask8(d, ymask, mbits, i);
       if (dz_out) store8(dz_out + i * 8, d);
     }
     float o[8];
@@ -414,17 +425,21 @@ DTF_API int dtf_bn_infer_coeff(const float* gamma, const float* beta, const floa
   return (int)hipGetLastError();
 }
 
+// mbits (optional, relu only): 1-bit ReLU mask, M*C/8 bytes, consumed by dtf_bn_bwd instead of re-reading y
 DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, const void* res, void* y, long M,
-                         int C, int relu, void* stream) {
+                         int C, int relu, void* mbits, void* stream) {
   if (C & 7) return -1;
   long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, n8, C, relu);
+                     (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, n8, C, relu,
+                     relu ? (uint8_t*)mbits : nullptr);
   return (int)hipGetLastError();
 }
 
 // work: (2*1024 + 3) * C floats (partials + coefficients)
-DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* x, const float* mean, const float* invstd,
+// ReLU mask from mbits (1 bit/element, preferred) or from the bf16 output ymask; neither = no ReLU
+DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
+                       const float* invstd,
                        const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma, float* dbeta,
                        int accumulate, float* work, void* stream) {
   if (C & 7) return -1;
@@ -433,14 +448,15 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* x, const f
   float* part = work + 3 * C;
   int G = red_grid(M, C);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
-                     (const bf16_t*)x, mean, invstd, M, C, part);
+                     (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part);
   long rs = 2L * C;
   int T = dtf_group_rows_once(part, rs, G, 2L * C, 32, &rs, stream);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);
   long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)ymask, (const bf16_t*)x, mean, invstd, coef, n8, C, (bf16_t*)dx,
+                     (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, coef, n8, C,
+                     (bf16_t*)dx,
                      (bf16_t*)dz_out);
   return (int)hipGetLastError();
 }

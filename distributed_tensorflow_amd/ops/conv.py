@@ -140,8 +140,11 @@ class _ConvBNFn(torch.autograd.Function):
         out = torch.empty_like(yc)
         if res is not None:
             res = res.contiguous()
-        call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), stream())
-        ctx.save_for_backward(x, w, gamma, yc, out if relu else None, mean, invstd)
+        mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if relu else None
+        call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
+             stream())
+        # backward needs the conv output and a 1-bit ReLU mask, not the bf16 BN output
+        ctx.save_for_backward(x, w, gamma, yc, mbits, mean, invstd)
         ctx.g = g
         ctx.relu = relu
         ctx.has_res = res is not None
@@ -150,7 +153,7 @@ class _ConvBNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        x, w, gamma, yc, out, mean, invstd = ctx.saved_tensors
+        x, w, gamma, yc, mbits, mean, invstd = ctx.saved_tensors
         g = ctx.g
         K = g[4]
         M = yc.numel() // K
@@ -160,7 +163,7 @@ class _ConvBNFn(torch.autograd.Function):
         dgamma = torch.empty(K, dtype=F32, device=yc.device)
         dbeta = torch.empty(K, dtype=F32, device=yc.device)
         work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
-        call("dtf_bn_bwd", ptr(dout), ptr(out), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K, ptr(dyc),
+        call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K, ptr(dyc),
              ptr(dres), ptr(dgamma), ptr(dbeta), 0, ptr(work), stream())
         if ctx.has_res and not ctx.relu:
             dres = dout

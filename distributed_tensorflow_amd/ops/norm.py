@@ -48,15 +48,17 @@ class _BNFn(torch.autograd.Function):
         out = torch.empty_like(x)
         if res is not None:
             res = res.to(BF16).contiguous()
-        call("dtf_bn_apply", ptr(x), ptr(scale), ptr(shift), ptr(res), ptr(out), M, C, int(relu), stream())
-        ctx.save_for_backward(x, gamma, out if relu else None, mean, invstd)
+        mbits = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if relu else None
+        call("dtf_bn_apply", ptr(x), ptr(scale), ptr(shift), ptr(res), ptr(out), M, C, int(relu), ptr(mbits),
+             stream())
+        ctx.save_for_backward(x, gamma, mbits, mean, invstd)
         ctx.relu = relu
         ctx.has_res = res is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, gamma, out, mean, invstd = ctx.saved_tensors
+        x, gamma, mbits, mean, invstd = ctx.saved_tensors
         C = x.shape[-1]
         M = x.numel() // C
         dout = dout.to(BF16).contiguous()
@@ -65,7 +67,8 @@ class _BNFn(torch.autograd.Function):
         dgamma = torch.empty(C, dtype=F32, device=x.device)
         dbeta = torch.empty(C, dtype=F32, device=x.device)
         work = torch.empty((2 * 1024 + 3) * C, dtype=F32, device=x.device)
-        call("dtf_bn_bwd", ptr(dout), ptr(out), ptr(x), ptr(mean), ptr(invstd), ptr(gamma), M, C, ptr(dx), ptr(dres),
+        call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(x), ptr(mean), ptr(invstd), ptr(gamma), M, C, ptr(dx),
+             ptr(dres),
              ptr(dgamma), ptr(dbeta), 0, ptr(work), stream())
         if ctx.has_res and not ctx.relu:
             dres = dout
