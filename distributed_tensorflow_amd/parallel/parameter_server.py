@@ -47,6 +47,17 @@ def _host_port(addr):
     return (h if h not in ("", "localhost") else "127.0.0.1"), int(p)
 
 
+def ps_transport(device):
+    """'collective' (torch.distributed P2P: RCCL between GPUs) or 'tcp' (native PS transport via host
+    memory). DTF_PS_TRANSPORT overrides; default: collective when the task computes on a GPU."""
+    t = os.environ.get("DTF_PS_TRANSPORT")
+    if t:
+        if t not in ("tcp", "collective"):
+            raise ValueError(f"DTF_PS_TRANSPORT={t!r}")
+        return t
+    return "collective" if device.type == "cuda" else "tcp"
+
+
 def kv_address(resolver):
     """Coordination-service address: DTF_KV_ADDR (hosted by a supervising launcher, so it survives task
     restarts) or the first trainer task's port (hosted by the chief)."""
@@ -117,15 +128,22 @@ class ParameterServer:
         self.num_trainers = len(self.r.trainer_tasks())
         host, port = _host_port(self.r.cluster.task_address("ps", self.index))
         self.lib = _native.runtime()
-        bound = ctypes.c_int()
-        self.srv = self.lib.dtfrt_ps_server_start(b"0.0.0.0", port, ctypes.addressof(bound))
-        if not self.srv:
-            raise OSError(err(self.lib))
-        self.port = bound.value
         self.device = context.parse_device(device) if device is not None else context.default_device()
+        self.transport = ps_transport(self.device)
+        self.srv = None
+        self.pg = None
+        if self.transport == "tcp":
+            bound = ctypes.c_int()
+            self.srv = self.lib.dtfrt_ps_server_start(b"0.0.0.0", port, ctypes.addressof(bound))
+            if not self.srv:
+                raise OSError(err(self.lib))
+            self.port = bound.value
         kh, kp = kv_address(self.r)
         self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
         self._hb = Heartbeat(self.kv, f"ps{self.index}").start()
+        if self.transport == "collective":
+            from .ps_collective import PSGroup
+            self.pg = PSGroup(self.kv, self.r, self.device, timeout_s=kv_timeout_s)
         self.slot_sync_every = slot_sync_every
         self.applies = 0
 
@@ -157,11 +175,14 @@ class ParameterServer:
             self.mirror = torch.zeros(self.numel, dtype=torch.float32)
             if torch.cuda.is_available() and self.device.type == "cuda":
                 self.mirror = self.mirror.pin_memory()
+        self.slot_mirrors = []
+        if self.srv is None:  # collective transport: values are served straight from the HBM arena
+            self.kv.set(f"ps/{self.index}/ready", "1")
+            return
         nb = self.mirror.numel() * 4
         self.lib.dtfrt_ps_register(self.srv, GRAD, self.mirror.data_ptr(), nb)
         self.lib.dtfrt_ps_register(self.srv, ASSIGN, self.mirror.data_ptr(), nb)
         # slot mirrors: var ids 2.. (refreshed every slot_sync_every applies and at exit)
-        self.slot_mirrors = []
         if self.arena is not None:
             for k, (nm, _) in enumerate(self.opt.slot_specs()):
                 m = torch.zeros(self.numel, dtype=torch.float32)
@@ -169,8 +190,32 @@ class ParameterServer:
                 self.lib.dtfrt_ps_register(self.srv, 2 + k, m.data_ptr(), m.numel() * 4)
         self.kv.set(f"ps/{self.index}/ready", "1")
 
-    def _refresh(self, var_id=GRAD, slots=False):
+    # ---- shard access used by the collective transport (ps_collective.PSServerLoop)
+    def apply_local(self, t, assign=False):
         if self.arena is None:
+            return
+        if assign:
+            self.arena.flat.index_copy_(0, self.pidx, t)
+            for nm, init in self.opt.slot_specs():
+                self.arena.slots[nm].fill_(init)
+        else:
+            self.arena.grad.zero_()
+            self.arena.grad.index_copy_(0, self.pidx, t)
+            self.opt.apply_arena(self.arena, zero_grad=True)
+            self.applies += 1
+
+    def params_local(self):
+        if self.arena is None:
+            return torch.zeros(0, dtype=torch.float32, device=self.device)
+        return self.arena.flat.index_select(0, self.pidx)
+
+    def slots_local(self):
+        if self.arena is None:
+            return []
+        return [self.arena.slots[nm].index_select(0, self.pidx) for nm, _ in self.opt.slot_specs()]
+
+    def _refresh(self, var_id=GRAD, slots=False):
+        if self.arena is None or self.srv is None:
             return
         tight = self.arena.flat.index_select(0, self.pidx)
         self.lib.dtfrt_ps_lock(self.srv, GRAD)
@@ -186,6 +231,11 @@ class ParameterServer:
     def serve(self, poll_ms=100):
         """Run until every trainer task has reported done (auto-stop PS)."""
         self._build()
+        if self.transport == "collective":
+            from .ps_collective import PSServerLoop
+            PSServerLoop(self, self.pg).run()  # returns once every trainer sent DONE
+            self.stop()
+            return
         var_id, off, n, data = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_void_p()
         while True:
             tok = self.lib.dtfrt_ps_next_push(self.srv, poll_ms, ctypes.addressof(var_id), ctypes.addressof(off),
@@ -221,6 +271,9 @@ class ParameterServer:
         if self.srv:
             self.lib.dtfrt_ps_server_stop(self.srv)
             self.srv = None
+        if self.pg is not None:
+            self.pg.close()
+            self.pg = None
         self.kv.close()
 
 
@@ -253,6 +306,11 @@ class ParameterServerStrategy(Strategy):
         self._clients = None
         self._layout = None
         self._done = False
+        self.transport = ps_transport(self._device)
+        self._pg = self._cg = None
+        if self.transport == "collective":
+            from .ps_collective import PSGroup
+            self._pg = PSGroup(self.kv, self.r, self._device, timeout_s=kv_timeout_s)
 
     # ---- properties
     @property
@@ -276,6 +334,11 @@ class ParameterServerStrategy(Strategy):
         return 1  # asynchronous: every worker applies its own gradients
 
     def _connect(self):
+        if self.transport == "collective":
+            if self._cg is None:
+                from .ps_collective import PSClientGroup
+                self._cg = PSClientGroup(self._pg, self.worker_index, [int(g.numel()) for g in self._gidx])
+            return self._cg
         if self._clients is None:
             self._clients = [PSClient(*_host_port(self.r.cluster.task_address("ps", i))) for i in
                              range(self.num_ps)]
@@ -315,7 +378,28 @@ class ParameterServerStrategy(Strategy):
                 raise RuntimeError("worker model variables differ from the chief's spec")
         self._pull_all()
 
+    def _collective_exchange(self, kind):
+        """One shard-parallel request to every PS; the replies (fresh parameter values) land in the arena."""
+        cg = self._connect()
+        cd = self._pg.comm_device
+        out = [torch.empty(max(1, int(g.numel())), dtype=torch.float32, device=cd)[:g.numel()] for g in self._gidx]
+        if kind is None:
+            cg.pull(out)
+        else:
+            src = self._arena.flat if kind == ASSIGN else self._arena.grad
+            payload = [src.index_select(0, g).to(cd) for g in self._gidx]
+            (cg.assign if kind == ASSIGN else cg.push)(payload, out)
+        for g, o in zip(self._gidx, out):
+            if g.numel():
+                self._arena.flat.index_copy_(0, g, o.to(self._arena.flat.device))
+        self._arena.refresh_bf16()
+        from ..ops._util import bump_weights_epoch
+        bump_weights_epoch()
+
     def _push_all(self, kind):
+        if self.transport == "collective":
+            self._collective_exchange(kind)
+            return
         clients = self._connect()
         src = self._arena.flat if kind == ASSIGN else self._arena.grad
         for p, c in enumerate(clients):
@@ -326,6 +410,9 @@ class ParameterServerStrategy(Strategy):
             c.push(kind, self._stage[p][:t.numel()])
 
     def _pull_all(self):
+        if self.transport == "collective":
+            self._collective_exchange(None)
+            return
         clients = self._connect()
         for p, c in enumerate(clients):
             n = self._gidx[p].numel()
@@ -345,6 +432,17 @@ class ParameterServerStrategy(Strategy):
         from ..keras import optimizers as O
         kind = spec["optimizer"]["kind"]
         names = [n for n, _ in O._SLOTS[kind]]
+        if self.transport == "collective":
+            cd = self._pg.comm_device
+            bufs = [[torch.zeros(int(g.numel()), dtype=torch.float32, device=cd) for _ in names] for g in self._gidx]
+            self._connect().pull_slots(bufs)
+            for k, nm in enumerate(names):
+                flat = torch.zeros_like(self._arena.flat)
+                for g, b in zip(self._gidx, bufs):
+                    if g.numel():
+                        flat.index_copy_(0, g, b[k].to(flat.device))
+                out[nm] = flat
+            return out
         for k, nm in enumerate(names):
             flat = torch.zeros_like(self._arena.flat)
             for p, c in enumerate(clients):
@@ -360,9 +458,10 @@ class ParameterServerStrategy(Strategy):
     # ---- training-loop hooks
     def apply_gradients(self, optimizer, arena):
         """Async step: push this worker's gradients, the PS applies them, pull fresh values."""
-        self._push_all(GRAD)
+        self._push_all(GRAD)  # the collective transport's push reply already carries the fresh values
         arena.grad.zero_()
-        self._pull_all()
+        if self.transport != "collective":
+            self._pull_all()
         with torch.no_grad():
             optimizer.iterations.add_(1)
         self.kv.add("global_step", 1)
@@ -377,6 +476,8 @@ class ParameterServerStrategy(Strategy):
         """Signal the PS tasks that this trainer is finished (auto-stop)."""
         if not self._done:
             self._done = True
+            if self.transport == "collective" and getattr(self, "_gidx", None) is not None:
+                self._connect().done()
             self.kv.add("done", 1)
 
     def dead_tasks(self, timeout=10.0):
@@ -393,6 +494,9 @@ class ParameterServerStrategy(Strategy):
             time.sleep(0.5)
         for c in self._clients or []:
             c.close()
+        if self._pg is not None:
+            self._pg.close()
+            self._pg = None
         self.kv.close()
         if self._kv_server is not None:
             self._kv_server.stop()

@@ -146,3 +146,28 @@ def test_parameter_server_strategy_keras_fit(tmp_path):
         assert d["acc"] > 0.8, out
         assert d["loss"][-1] < d["loss"][0]
     assert max(d["gs"] for d in res) >= 3 * 16  # async global_step counts every worker's steps
+
+
+@pytest.mark.slow
+def test_ps_runbook_collective_transport(tmp_path):
+    """The PS runbook over the torch.distributed point-to-point transport (gloo here; RCCL between GPUs):
+    2 PS + 1 worker + master, per-pair groups, shard-parallel push/pull, DONE-driven PS exit."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DTF_PS_TRANSPORT="collective")
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    cmd = [sys.executable, "-m", "distributed_tensorflow_amd.cli.launch", "--ps", "2", "--workers", "1", "--chief",
+           "1", "--timeout", "240", "--", sys.executable, "-m", "distributed_tensorflow_amd.cli.train", "--seed=0",
+           "--max_epochs=4", "--optimizer=adam", "--learning_rate=0.1"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert out.count("PS exits after all workers done") == 2
+    assert "Exported SavedModel" in out
+    from distributed_tensorflow_amd.train import checkpoint as C
+    ck = C.latest_checkpoint(str(tmp_path / "checkpoint"))
+    names = dict(C.list_variables(ck))
+    assert {"weight", "bias", "global_step"} <= set(names)
+    w = float(C.load_variable(ck, "weight"))
+    assert 1.0 < w < 3.0, w
