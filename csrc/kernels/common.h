@@ -59,6 +59,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Sum over the 16 lanes of each DPP row (lanes 16r..16r+15), result in every lane of the row: four
+// VALU adds with DPP operands (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror) instead of
+// ds_bpermute shuffles.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
 // Block-wide sum for blockDim.x multiple of 64 (<= 1024). `red` needs 16 floats.
 __device__ __forceinline__ float block_sum(float v, float* red) {
   v = wave_sum(v);

@@ -81,8 +81,13 @@ static void launch_modes(GemmArgs& a, int tile, hipStream_t st) {
 
 // Tile choice: prefer the largest tile that still yields >= ~2 waves of blocks on
 // 256 CUs (2 blocks/CU at ~64 KB LDS each); narrow N -> 256x64.
-static int pick_tile(long M, long N, long batch_splits) {
+static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
   auto blocks = [&](int bm, int bn) { return (long)cdiv(M, bm) * cdiv(N, bn) * batch_splits; };
+  // short K (one to eight k-tiles, e.g. the early 1x1 convolutions): latency/epilogue-bound, the smaller
+  // 128x64 tile keeps more blocks in flight per CU (measured 5-20 % faster than 128x128 there)
+  if (N > 64 && K <= 512 && blocks(128, 64) >= 1024) return 2;
+  // long K amortises the larger tile's epilogue: one round of 128x128 tiles beats two of 128x64
+  if (N > 64 && K >= 1024 && blocks(128, 128) >= 256) return 0;
   if (N <= 64) {
     if (blocks(256, 64) >= 512) return 1;
     if (blocks(128, 64) >= 256) return 2;
@@ -107,7 +112,7 @@ static bool prefer256(long M, long N, long K, long batch) {
 }
 
 static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st) {
-  if (tile < 0) tile = pick_tile(a.M, a.N, (long)a.batch * a.splitk);
+  if (tile < 0) tile = pick_tile(a.M, a.N, (long)a.batch * a.splitk, a.kchunk);
   if (amode == OP_KCONTIG && bmode == OP_KCONTIG) launch_modes<OP_KCONTIG, OP_KCONTIG>(a, tile, st);
   else if (amode == OP_KCONTIG && bmode == OP_KOUTER) launch_modes<OP_KCONTIG, OP_KOUTER>(a, tile, st);
   else if (amode == OP_KOUTER && bmode == OP_KOUTER) launch_modes<OP_KOUTER, OP_KOUTER>(a, tile, st);

@@ -482,9 +482,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     for (int j = 0; j < TN; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = csum[j][r], q = csq[j][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+        const float s = row16_sum(csum[j][r]), q = row16_sum(csq[j][r]);
         const int nl = wn * WTN + j * 16 + (lane >> 4) * 4 + r;
         if ((lane & 15) == 0) {
           red[wm * BN + nl] = s;
