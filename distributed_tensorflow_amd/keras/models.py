@@ -25,6 +25,7 @@ import torch
 
 from .. import context
 from .. import profiler as prof
+from ..ops._util import direct_grads
 from ..data import Dataset
 from ..parallel import strategy as S
 from . import callbacks as cbs
@@ -152,7 +153,7 @@ class Model(Layer):
             y_pred = self(x, training=True)
             loss = self.compute_loss(x, y, y_pred, sw)
         arena = self._ensure_arena()
-        with prof.phase("backward"):  # includes the overlapped bucket all-reduces
+        with prof.phase("backward"), direct_grads():  # includes the overlapped bucket all-reduces
             strat.backward(loss, arena)
         with prof.phase("optimizer"):
             strat.apply_gradients(self.optimizer, arena)

@@ -117,3 +117,33 @@ def crsk_shadow(param, K, RS, C):
     call("dtf_filter_to_crsk", ptr(w16), ptr(s), K, RS, C, stream())
     param._dtf_crsk_key = key
     return s
+
+
+# ---------------------------------------------------------------- direct gradient accumulation
+# Inside Model.train_step's backward the parameters' .grad are views of the flat arena gradient, zeroed by
+# the fused optimizer every step. Ops with hand-written backwards may then accumulate a parameter's gradient
+# straight into that view (GEMM beta=1 / accumulate flags) and return None to autograd, which saves one
+# AccumulateGrad add kernel + one temporary per parameter. Autograd still visits the parameter's
+# AccumulateGrad node (with an undefined gradient), so post-accumulate hooks (gradient bucketing) fire
+# unchanged. Outside `direct_grads()` (GradientTape, custom loops) every op returns its grads.
+_direct = [False]
+
+
+class direct_grads:
+    def __enter__(self):
+        self._prev = _direct[0]
+        _direct[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _direct[0] = self._prev
+
+
+def direct_grad(p):
+    """The arena gradient view to accumulate p's gradient into, or None (return the gradient instead)."""
+    if not _direct[0] or p is None or not getattr(p, "requires_grad", False):
+        return None
+    g = p.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != p.shape:
+        return None
+    return g if g.data_ptr() == getattr(p, "_dtf_grad_ptr", -1) else None

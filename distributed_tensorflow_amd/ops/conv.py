@@ -11,7 +11,8 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, IntOut, bf16_shadow, call, crsk_shadow, on_gpu, ptr, stream, workspace
+from ._util import (BF16, F32, IntOut, bf16_shadow, call, crsk_shadow, direct_grad, on_gpu, ptr,
+                    stream, workspace)
 
 
 def out_size(h, k, s, p, d=1):
@@ -62,12 +63,13 @@ def conv_dgrad_raw(dy, w_master, g):
     return dx
 
 
-def conv_wgrad_raw(x, dy, g):
+def conv_wgrad_raw(x, dy, g, out=None):
+    """dW [K,R,S,C] f32; with `out` (an arena gradient view) the result is accumulated into it."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
-    dw_ = torch.empty((K, R, S, C), dtype=F32, device=x.device)
+    dw_ = torch.empty((K, R, S, C), dtype=F32, device=x.device) if out is None else out
     ws = workspace(x.device)
-    call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw_), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0, -1,
-         ptr(ws), ws.numel(), stream())
+    call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw_), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+         int(out is not None), 0, -1, ptr(ws), ws.numel(), stream())
     return dw_
 
 
@@ -145,6 +147,7 @@ class _ConvBNFn(torch.autograd.Function):
              stream())
         # backward needs the conv output and a 1-bit ReLU mask, not the bf16 BN output
         ctx.save_for_backward(x, w, gamma, yc, mbits, mean, invstd)
+        ctx.bn_params = (gamma, beta)
         ctx.g = g
         ctx.relu = relu
         ctx.has_res = res is not None
@@ -160,18 +163,27 @@ class _ConvBNFn(torch.autograd.Function):
         dout = dout.to(BF16).contiguous()
         dyc = torch.empty_like(yc)
         dres = torch.empty_like(yc) if (ctx.has_res and ctx.relu) else None
-        dgamma = torch.empty(K, dtype=F32, device=yc.device)
-        dbeta = torch.empty(K, dtype=F32, device=yc.device)
+        gamma_p, beta_p = ctx.bn_params
+        tg, tb = direct_grad(gamma_p), direct_grad(beta_p)
+        direct_bn = tg is not None and tb is not None  # accumulate dgamma/dbeta into the arena grads
+        dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
+        dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
         work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
         call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K, ptr(dyc),
-             ptr(dres), ptr(dgamma), ptr(dbeta), 0, ptr(work), stream())
+             ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), stream())
         if ctx.has_res and not ctx.relu:
             dres = dout
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad_raw(dyc, w, g)
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad_raw(x, dyc, g)
+            tw = direct_grad(w)
+            dw = conv_wgrad_raw(x, dyc, g, out=tw)
+            if tw is not None:
+                dw = None  # (autograd still runs the parameter's AccumulateGrad node with an undefined
+                #            gradient, so its post-accumulate hooks — gradient bucketing — fire as usual)
+        if direct_bn:
+            dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
 
 

@@ -156,6 +156,7 @@ class ParamArena:
             self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
             for v, o in zip(self.variables, self.offsets):
                 v.grad = self.grad[o:o + v.numel()].view(v.shape)
+                v._dtf_grad_ptr = v.grad.data_ptr()  # ops may accumulate into it directly (ops._util)
         if with_bf16 is None:
             with_bf16 = self.device.type == "cuda"
         self.bf16 = None
@@ -204,3 +205,4 @@ class ParamArena:
                 v.data = self.flat[o:o + v.numel()].view(v.shape)
             if self.grad is not None:
                 v.grad = self.grad[o:o + v.numel()].view(v.shape)
+                v._dtf_grad_ptr = v.grad.data_ptr()

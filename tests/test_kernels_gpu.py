@@ -346,3 +346,34 @@ def test_fp8_dense_layer_trains(cuda):
     close(y, ref, 8e-2)
     y.float().sum().backward()
     assert layer.kernel.grad is not None and torch.isfinite(layer.kernel.grad).all()
+
+
+def test_conv_bn_direct_arena_grads(cuda):
+    """Inside direct_grads() ConvBN accumulates dW/dgamma/dbeta straight into the arena gradient views and
+    fires the post-accumulate hooks; the result equals the regular autograd path (twice: accumulation)."""
+    from distributed_tensorflow_amd.ops._util import direct_grads
+    from distributed_tensorflow_amd.variables import ParamArena, Variable
+    N, H, W, C, K = 2, 14, 14, 32, 64
+    x = rnd(N, H, W, C, dev=cuda)
+    results = []
+    for direct in (False, True):
+        torch.manual_seed(3)
+        w = Variable((torch.randn(K, 3, 3, C) / 20).to(cuda), name="w")
+        gm = Variable(torch.rand(K).to(cuda) + 0.5, name="g")
+        bt = Variable(torch.zeros(K).to(cuda), name="b")
+        arena = ParamArena([w, gm, bt], device=cuda)
+        fired = []
+        for v in (w, gm, bt):
+            v.register_post_accumulate_grad_hook(lambda p: fired.append(p.name))
+        rm, rv = torch.zeros(K, device=cuda), torch.ones(K, device=cuda)
+        for _ in range(2):
+            y = ops.conv_bn(x, w, gm, bt, rm, rv, pad=(1, 1), relu=True)
+            loss = y.float().square().mean()
+            if direct:
+                with direct_grads():
+                    loss.backward()
+            else:
+                loss.backward()
+        assert sorted(fired) == sorted(["w", "g", "b"] * 2)
+        results.append(arena.grad.clone())
+    close(results[1], results[0], 1e-5)
