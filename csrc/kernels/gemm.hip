@@ -162,7 +162,7 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
   a.M = M; a.N = N; a.K = K; a.batch = batch < 1 ? 1 : batch;
   a.alpha = alpha; a.beta = beta; a.act = act; a.out_f32 = out_f32;
-  if (splitk <= 0) splitk = out_f32 && beta == 0.f && !bias && !act && !aux && !stats
+  if (splitk <= 0) splitk = out_f32 && (beta == 0.f || beta == 1.f) && !bias && !act && !aux && !stats
                                 ? choose_splitk(M, N, K, 128, 128, a.batch) : 1;
   a.splitk = splitk;
   a.kchunk = ((K + splitk - 1) / splitk + BK - 1) / BK * BK;

@@ -475,9 +475,10 @@ DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* be
   return (int)hipGetLastError();
 }
 
-// dgb = [dgamma | dbeta] (2D floats, overwritten); ws >= min(1024, M/16 + 1) * 2D floats.
+// dgb = [dgamma | dbeta] (2D floats, overwritten or accumulated); ws >= min(1024, M/16 + 1) * 2D floats.
 DTF_API int dtf_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
-                              void* dx, float* dgb, float* ws, long ws_elems, long M, int D, void* stream) {
+                              void* dx, float* dgb, float* ws, long ws_elems, long M, int D, int accumulate,
+                              void* stream) {
   if ((D & 7) || D > 2048) return -1;
   long blocks = std::max<long>(1, std::min<long>(cdiv(M, 16), 1024));
   blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / (2L * D)));
@@ -487,6 +488,6 @@ DTF_API int dtf_layernorm_bwd(const void* dy, const void* x, const float* gamma,
                       (const bf16_t*)dy, (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, ws, M, D)
   DTF_LN_DISPATCH(D, LNB);
 #undef LNB
-  dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, 0, stream);
+  dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, accumulate, stream);
   return (int)hipGetLastError();
 }

@@ -32,7 +32,7 @@ _KERNEL_SIGS = {
     "dtf_bn_apply": [P, P, P, P, P, L, I, I, P, P],
     "dtf_bn_bwd": [P, P, P, P, P, P, P, L, I, P, P, P, P, I, P, P],
     "dtf_layernorm_fwd": [P, P, P, P, P, P, L, I, F, P],
-    "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, P],
+    "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],
     "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "dtf_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
     "dtf_gap_fwd": [P, P, I, I, I, I, P],

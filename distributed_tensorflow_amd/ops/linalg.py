@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, IntOut, bf16_shadow, call, on_gpu, ptr, stream, workspace
+from ._util import BF16, F32, IntOut, bf16_shadow, call, direct_grad, on_gpu, ptr, stream, workspace
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 _ACTS = {None: 0, "linear": 0, "relu": 1, "gelu": 2}
@@ -146,6 +146,7 @@ class _DenseFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w, pre)
         ctx.act = act
         ctx.has_b = b is not None
+        ctx.b_param = b
         ctx.shp = shp
         return y.reshape(*shp[:-1], w.shape[0])
 
@@ -166,10 +167,19 @@ class _DenseFn(torch.autograd.Function):
             # dx[t,i] = sum_o dz[t,o] W[o,i]  -> B stored [K=out][N=in] (k-outer)
             dx = gemm(dz, bf16_shadow(w), b_kouter=True).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
-            # dW[o,i] = sum_t dz[t,o] x[t,i]  -> both operands k-outer, f32 out
-            dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
+            # dW[o,i] = sum_t dz[t,o] x[t,i]  -> both operands k-outer, f32 out; inside Model.train_step
+            # accumulated straight into the arena gradient (beta = 1) instead of returned
+            tw = direct_grad(w)
+            if tw is not None and tw.dim() == 2:
+                gemm(dz, x2, a_kouter=True, b_kouter=True, out=tw, beta=1.0)
+            else:
+                dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = colsum(dz)
+            tb = direct_grad(ctx.b_param)
+            if tb is not None:
+                colsum(dz, out=tb, accumulate=True)
+            else:
+                db = colsum(dz)
         return dx, dw, db, None
 
 

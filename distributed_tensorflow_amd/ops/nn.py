@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, call, on_gpu, ptr, stream, workspace
+from ._util import BF16, F32, call, direct_grad, on_gpu, ptr, stream, workspace
 from .conv import out_size
 
 
@@ -166,6 +166,7 @@ class _EmbedFn(torch.autograd.Function):
         call("dtf_embed_fwd", ptr(t16), ptr(ids), ptr(p16), None, ptr(y16), ptr(tid), ptr(out), T, D, int(seq_len),
              stream())
         ctx.save_for_backward(ids, tid)
+        ctx.tables = (table, pos_table, type_table)
         ctx.shapes = (table.shape, None if pos_table is None else pos_table.shape,
                       None if type_table is None else type_table.shape, seq_len)
         return out.reshape(*ids.shape, D)
@@ -178,25 +179,34 @@ class _EmbedFn(torch.autograd.Function):
         T = ids.numel()
         D = tshape[1]
         ws = workspace(dy.device)
+        tables = ctx.tables
+        # inside Model.train_step the kernels accumulate straight into the arena gradients (no zero-filled
+        # temporaries, no AccumulateGrad adds); the returned gradient is then None
+        direct = [direct_grad(t) for t in tables]
         # word table: sort the ids once, then one deterministic segment-sum per distinct id (no atomics)
-        dt = torch.zeros(tshape, dtype=F32, device=dy.device)
+        dt = direct[0] if direct[0] is not None else torch.zeros(tshape, dtype=F32, device=dy.device)
         sid, perm = torch.sort(ids.reshape(-1))
         call("dtf_embed_bwd_sorted", ptr(dy), ptr(sid), ptr(perm), ptr(dt), T, D, stream())
         dp = dy_ = None
         if pshape is not None:  # positions: dp[s] = sum over the batch of dy[b, s]  (a column sum)
-            dp = torch.zeros(pshape, dtype=F32, device=dy.device)
+            dp = direct[1] if direct[1] is not None else torch.zeros(pshape, dtype=F32, device=dy.device)
             S = int(seq_len)
-            call("dtf_colsum", ptr(dy), T // S, S * D, ptr(dp), 0, ptr(ws), ws.numel(), stream())
+            call("dtf_colsum", ptr(dy), T // S, S * D, ptr(dp), int(direct[1] is not None), ptr(ws), ws.numel(),
+                 stream())
         if yshape is not None:
-            dy_ = torch.zeros(yshape, dtype=F32, device=dy.device)
+            acc = int(direct[2] is not None)
+            dy_ = direct[2] if acc else torch.zeros(yshape, dtype=F32, device=dy.device)
             if tid is not None and yshape[0] <= 16:
-                call("dtf_embed_bwd_small", ptr(dy), ptr(tid), ptr(dy_), T, D, yshape[0], 0, ptr(ws), ws.numel(),
+                call("dtf_embed_bwd_small", ptr(dy), ptr(tid), ptr(dy_), T, D, yshape[0], acc, ptr(ws), ws.numel(),
                      stream())
             elif tid is not None:
                 sid2, perm2 = torch.sort(tid.reshape(-1))
                 call("dtf_embed_bwd_sorted", ptr(dy), ptr(sid2), ptr(perm2), ptr(dy_), T, D, stream())
             else:  # no type ids: every token uses row 0
-                call("dtf_colsum", ptr(dy), T, D, ptr(dy_), 0, ptr(ws), ws.numel(), stream())
+                call("dtf_colsum", ptr(dy), T, D, ptr(dy_), acc, ptr(ws), ws.numel(), stream())
+        dt = None if direct[0] is not None else dt
+        dp = None if direct[1] is not None else dp
+        dy_ = None if direct[2] is not None else dy_
         return None, dt, dp, None, dy_, None
 
 

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, IntOut, call, on_gpu, ptr, stream, workspace
+from ._util import BF16, F32, IntOut, call, direct_grad, on_gpu, ptr, stream, workspace
 
 
 def batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training):
@@ -99,6 +99,7 @@ class _LNFn(torch.autograd.Function):
         call("dtf_layernorm_fwd", ptr(x), ptr(gamma), ptr(beta), ptr(y), ptr(mean), ptr(rstd), M, D, float(eps),
              stream())
         ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.ln_params = (gamma, beta)
         return y
 
     @staticmethod
@@ -108,10 +109,17 @@ class _LNFn(torch.autograd.Function):
         M = x.numel() // D
         dy = dy.to(BF16).contiguous()
         dx = torch.empty_like(x)
-        dgb = torch.empty(2 * D, dtype=F32, device=x.device)
         ws = workspace(x.device)
+        g_p, b_p = ctx.ln_params
+        tg, tb = direct_grad(g_p), direct_grad(b_p)
+        if tg is not None and tb is not None and tb.data_ptr() == tg.data_ptr() + 4 * D:
+            # gamma and beta are adjacent in the arena: accumulate [dgamma | dbeta] into their gradients
+            call("dtf_layernorm_bwd", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(tg), ptr(ws),
+                 ws.numel(), M, D, 1, stream())
+            return dx, None, None, None
+        dgb = torch.empty(2 * D, dtype=F32, device=x.device)
         call("dtf_layernorm_bwd", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(dgb), ptr(ws),
-             ws.numel(), M, D, stream())
+             ws.numel(), M, D, 0, stream())
         return dx, dgb[:D], dgb[D:], None
 
 

@@ -1,0 +1,109 @@
+#!/usr/bin/env python
+"""BASELINE.json config #4: ResNet-50 under ParameterServerStrategy (2 PS + 6 trainers on one 8-GPU node).
+
+    python tools/bench_ps.py --gpus 8 [--steps 20 --warmup 5 --batch 256]
+
+Without TF_CONFIG it launches the local cluster itself (cli.launch: one process per task, one GPU each,
+ps tasks included, launcher-hosted coordination store): P = max(1, gpus // 4) parameter servers holding
+the variable shards in their HBM, the rest trainers (the first is the chief). The data plane is the
+collective transport (RCCL point-to-point between GPUs; gloo + host staging when the PS runs on the CPU,
+`--ps_cpu`, which is also what a 1-GPU box needs). Training is asynchronous as in the reference: every
+trainer pushes its gradients to the PS shards after each step and continues with the returned values.
+Each trainer times its own `--steps` steps after `--warmup`; the chief sums the trainers' images/sec and
+prints one JSON line (metric: images/sec whole node, async PS).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--ps_cpu", action="store_true", help="PS shards in host memory (gloo transport)")
+    ap.add_argument("--timeout", type=float, default=1500)
+    return ap.parse_args()
+
+
+def launch(a):
+    from distributed_tensorflow_amd.cli.launch import launch as run_cluster
+    n_ps = 1 if a.ps_cpu else max(1, a.gpus // 4)
+    n_tr = a.gpus if a.ps_cpu else a.gpus - n_ps
+    if n_tr < 1:
+        raise SystemExit("need at least one trainer GPU (use --ps_cpu on a 1-GPU box)")
+    gpus = ",".join(str(i) for i in range(a.gpus))
+    env = {"DTF_PS_TRANSPORT": "collective", "DTF_BENCH_PS_CPU": "1" if a.ps_cpu else "0"}
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    if a.ps_cpu:
+        rc, _ = run_cluster(cmd, num_ps=n_ps, num_workers=n_tr - 1, num_chief=1, gpus=gpus, ps_gpus=False, env=env,
+                            timeout=a.timeout, host_kv=True)
+    else:  # PS tasks take the first GPUs
+        order = [str(i) for i in range(a.gpus)]
+        rc, _ = run_cluster(cmd, num_ps=n_ps, num_workers=n_tr - 1, num_chief=1, gpus=",".join(order), ps_gpus=True,
+                            env=env, timeout=a.timeout, host_kv=True)
+    return rc
+
+
+def task(a):
+    import torch
+    from distributed_tensorflow_amd.parallel import TFConfigClusterResolver
+    from distributed_tensorflow_amd.parallel.parameter_server import ParameterServerStrategy, run_parameter_server
+    r = TFConfigClusterResolver()
+    ps_cpu = os.environ.get("DTF_BENCH_PS_CPU") == "1"
+    if r.is_ps:
+        return run_parameter_server(r, device="cpu" if ps_cpu else "cuda:0")
+    from distributed_tensorflow_amd.data import synthetic_imagenet
+    from distributed_tensorflow_amd.keras import losses, optimizers
+    from distributed_tensorflow_amd.models import ResNet
+    dev = torch.device("cuda:0")
+    strat = ParameterServerStrategy(r, variable_partitioner="balanced", device=dev)
+    with strat.scope():
+        model = ResNet(a.depth, num_classes=1000)
+        model.compile(optimizer=optimizers.SGD(0.1, momentum=0.9),
+                      loss=losses.SparseCategoricalCrossentropy(from_logits=True))
+    data = iter(synthetic_imagenet(a.batch, dev, seed=1234 + strat.worker_index))
+    for _ in range(a.warmup):
+        logs = model.train_step(next(data))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        logs = model.train_step(next(data))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ips = a.batch * a.steps / dt
+    strat.kv.set(f"bench/{strat.worker_index}", json.dumps({"ips": ips, "ms": dt / a.steps * 1e3,
+                                                            "loss": float(logs["loss"])}))
+    if strat.is_chief:
+        res = [json.loads(strat.kv.get(f"bench/{i}").decode()) for i in range(strat.num_workers)]
+        total = sum(x["ips"] for x in res)
+        print(json.dumps({
+            "metric": f"images/sec (whole node) ResNet-{a.depth} bf16, ParameterServerStrategy (async)",
+            "value": round(total, 2), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(max(x["ms"] for x in res), 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": f"ResNet-{a.depth} v1.5", "per_trainer_batch": a.batch,
+                       "ps_tasks": r.cluster.num_tasks("ps"), "trainers": strat.num_workers,
+                       "ps_device": "cpu" if ps_cpu else "gpu", "transport": strat.transport,
+                       "per_trainer_images_per_sec": [round(x["ips"], 1) for x in res]}}), flush=True)
+    strat.shutdown()
+    return 0
+
+
+def main():
+    a = parse()
+    if not os.environ.get("TF_CONFIG"):
+        return launch(a)
+    return task(a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
