@@ -98,11 +98,11 @@ static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
   return 3;
 }
 
-int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st);  // gemm256.hip
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8 = 0);  // gemm256.hip
 
 // 256x256 (1 block/CU, ~1.12-1.24x faster per tile, more so at long K) vs 128x128 (2 blocks/CU): compare the
 // wave-quantisation efficiency of both tilings on 256 CUs.
-static bool prefer256(long M, long N, long K, long batch) {
+bool prefer256(long M, long N, long K, long batch) {
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch, t128 = (long)cdiv(M, 128) * cdiv(N, 128) * batch;
   if (t256 < 128) return false;
   const double e256 = (double)t256 / (double)(((t256 + 255) / 256) * 256);

@@ -58,7 +58,7 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int AM, int BMD>
+template <int AM, int BMD, int FP8 = 0>
 __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -127,36 +127,49 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  v8bf fa[4][2], fb0[2][2], fb1[2][2];
+  // bf16: 2 k-substeps of 32 per 64-wide K-tile (16-B fragments); fp8 (OCP e4m3, K-tile = 128 bytes): 4
+  // k-substeps of 32 (8-B fragments) on v_mfma_f32_16x16x32_fp8_fp8 — same LDS image, half the bytes per FLOP
+  using FragT = typename std::conditional<FP8 != 0, long, v8bf>::type;
+  constexpr int KS = FP8 ? 4 : 2;
+  FragT fa[4][KS], fb0[2][KS], fb1[2][KS];
 
   auto read_a = [&](int buf, int h) {
     const char* base = smem + buf * BUF + h * HALF;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        fa[i][kk] = AM == OP_KOUTER ? frag_ko(base, wr * 64 + i * 16, kk, lane)
-                                    : frag_kcontig(base, wr * 64 + i * 16, kk, lane);
+      for (int kk = 0; kk < KS; ++kk) {
+        if constexpr (FP8) fa[i][kk] = frag_fp8(base, wr * 64 + i * 16, kk, lane);
+        else if constexpr (AM == OP_KOUTER) fa[i][kk] = frag_ko(base, wr * 64 + i * 16, kk, lane);
+        else fa[i][kk] = frag_kcontig(base, wr * 64 + i * 16, kk, lane);
+      }
   };
-  auto read_b = [&](v8bf (&fb)[2][2], int buf, int h) {
+  auto read_b = [&](FragT (&fb)[2][KS], int buf, int h) {
     const char* base = smem + buf * BUF + (2 + h) * HALF;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        fb[j][kk] = BMD == OP_KOUTER ? frag_ko(base, wc * 32 + j * 16, kk, lane)
-                                     : frag_kcontig(base, wc * 32 + j * 16, kk, lane);
+      for (int kk = 0; kk < KS; ++kk) {
+        if constexpr (FP8) fb[j][kk] = frag_fp8(base, wc * 32 + j * 16, kk, lane);
+        else if constexpr (BMD == OP_KOUTER) fb[j][kk] = frag_ko(base, wc * 32 + j * 16, kk, lane);
+        else fb[j][kk] = frag_kcontig(base, wc * 32 + j * 16, kk, lane);
+      }
   };
-  auto mma = [&](const v8bf (&fb)[2][2], int ha, int hb) {
+  auto mma = [&](const FragT (&fb)[2][KS], int ha, int hb) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[ha * 4 + i][hb * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (FP8)
+            acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(
+                fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+          else
+            acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -271,7 +284,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
 }  // namespace
 
 // Used by dtf_gemm for eligible problems; returns 0 if launched, 1 if not eligible.
-int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st) {
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8) {
   if (a.kchunk % BK || a.kchunk < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.stats || a.atomic_out || a.crm)
     return 1;
   if ((a.splitk > 1 && a.K % a.kchunk && (a.K % a.kchunk) % BK) || a.K % BK) return 1;
@@ -281,7 +294,11 @@ int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st) {
   a.tiles_m = cdiv(a.M, 256);
   a.tiles_n = cdiv(a.N, 256);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
-  if (amode == OP_KCONTIG && bmode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
+  if (fp8) {
+    if (amode != OP_KCONTIG || bmode != OP_KCONTIG) return 1;
+    hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT2), 0, st, a);
+  } else if (amode == OP_KCONTIG && bmode == OP_KCONTIG)
+    hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
   else if (amode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KOUTER>), grid, dim3(NT2), 0, st, a);
   else if (bmode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
   else hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KOUTER>), grid, dim3(NT2), 0, st, a);
@@ -308,7 +325,7 @@ DTF_API int dtf_gemm256(const void* A, const void* B, void* C, int M, int N, int
     a.slab = (long)M * N;
   }
   if (dtf::gemm256_try(a, a_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG, b_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG,
-                       st))
+                       st, 0))
     return -2;
   if (a.splitk > 1) dtf_sum_rows(ws, (long)M * N, a.splitk, (long)M * N, (float*)C, 0, stream);
   return (int)hipGetLastError();

@@ -43,13 +43,64 @@ __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict
   }
 }
 
-// new scale from the amax of the previous step: scale = amax / 448 * 2^-margin  (history length 1)
-__global__ void fp8_update_scale_kernel(const float* amax, float* scale, float margin) {
+// new scale from the amax of the previous step: scale = amax / 448 * 2^-margin  (history length 1); the amax
+// accumulator is reset here, so the next quantize pass needs no memset
+__global__ void fp8_update_scale_kernel(float* amax, float* scale, float margin) {
   float a = amax[0];
   scale[0] = a > 0.f ? a / 448.f * exp2f(margin) : 1.f;
+  amax[0] = 0.f;
+}
+
+// exact per-tensor scale, pass 1: per-block max |x| partials (no atomics, no zeroing)
+__global__ void __launch_bounds__(256) absmax_part_kernel(const bf16_t* __restrict__ x, long n8,
+                                                          float* __restrict__ part) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(x + i * 8, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[j]));
+  }
+  m = block_max(m, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = m;
+}
+
+// pass 2: every block folds the partials into the scale (amax / 448), block 0 publishes it, then quantizes
+__global__ void __launch_bounds__(256) quant_fp8_exact_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q,
+                                                              long n8, const float* __restrict__ part, int nparts,
+                                                              float* __restrict__ scale_out) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) m = fmaxf(m, part[i]);
+  m = block_max(m, red);
+  const float scale = fmaxf(m, 1e-12f) / fp8_max();
+  if (blockIdx.x == 0 && threadIdx.x == 0) scale_out[0] = scale;
+  const float inv = 1.f / scale;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float f[8];
+    load8(x + i * 8, f);
+    uint32_t w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float a0 = fminf(fmaxf(f[4 * h + 0] * inv, -fp8_max()), fp8_max());
+      float a1 = fminf(fmaxf(f[4 * h + 1] * inv, -fp8_max()), fp8_max());
+      float a2 = fminf(fmaxf(f[4 * h + 2] * inv, -fp8_max()), fp8_max());
+      float a3 = fminf(fmaxf(f[4 * h + 3] * inv, -fp8_max()), fp8_max());
+      int r = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+      r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
+      w[h] = (uint32_t)r;
+    }
+    *reinterpret_cast<uint2*>(q + i * 8) = make_uint2(w[0], w[1]);
+  }
 }
 
 }  // namespace
+
+namespace dtf {
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8);  // gemm256.hip
+bool prefer256(long M, long N, long K, long batch);                           // gemm.hip
+}  // namespace dtf
 
 using namespace dtf;
 
@@ -65,7 +116,20 @@ DTF_API int dtf_quant_fp8(const void* x, void* q, long n, const float* scale, fl
   return (int)hipGetLastError();
 }
 
-DTF_API int dtf_fp8_update_scale(const float* amax, float* scale, float margin, void* stream) {
+// Exact per-tensor quantization (weights): scale_out = amax(|x|)/448 computed on the device, two launches,
+// ws >= 1024 floats of scratch for the per-block partials.
+DTF_API int dtf_quant_fp8_exact(const void* x, void* q, long n, float* scale_out, float* ws, void* stream) {
+  if (n & 7) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  int grid = stream_grid(n / 8, 256);
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(absmax_part_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, n / 8, ws);
+  hipLaunchKernelGGL(quant_fp8_exact_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, (uint8_t*)q, n / 8, ws,
+                     grid, scale_out);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_fp8_update_scale(float* amax, float* scale, float margin, void* stream) {
   hipLaunchKernelGGL(fp8_update_scale_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, amax, scale, margin);
   return (int)hipGetLastError();
 }
@@ -82,6 +146,9 @@ DTF_API int dtf_gemm_fp8(const void* A, const void* B, void* C, void* aux, const
   a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
   a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = 0;
+  // the 256x256 glds pipeline when its tiling fills the chip (fp8 halves its staged bytes per FLOP)
+  if (tile < 0 && prefer256(M, N, 2L * K, 1) && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, (hipStream_t)stream, 1) == 0)
+    return (int)hipGetLastError();
   if (tile < 0) {
     long b128 = (long)cdiv(M, 128) * cdiv(N, 128);
     tile = b128 >= 256 ? 0 : 2;

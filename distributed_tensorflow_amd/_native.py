@@ -47,6 +47,7 @@ _KERNEL_SIGS = {
     "dtf_act": [P, P, P, L, I, I, P],
     "dtf_dropout": [P, P, L, F, U, P],
     "dtf_gemm256": [P, P, P, I, I, I, L, L, L, I, I, I, I, P, L, P],
+    "dtf_quant_fp8_exact": [P, P, L, P, P, P],
     "dtf_attn_fwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
     "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
     "dtf_colsum": [P, L, I, P, I, P, L, P],

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, bf16_shadow, call, ptr, stream, weights_epoch
+from ._util import BF16, F32, bf16_shadow, call, direct_grad, ptr, stream, weights_epoch, workspace
 from .linalg import colsum, gemm
 
 E4M3_MAX = 448.0
@@ -44,9 +44,11 @@ def _weight_fp8(st, w):
     if st.wq is not None and st.w_key == key:
         return st.wq
     w16 = bf16_shadow(w)
-    amax = w16.abs().amax().float().clamp_min(1e-12)  # exact per-tensor weight scale
-    st.buf[1:2].copy_(amax / E4M3_MAX)
-    st.wq = quantize(w16, st.buf[1:2])
+    if st.wq is None:
+        st.wq = torch.empty(w16.shape, dtype=torch.uint8, device=w16.device)
+    # exact per-tensor weight scale (amax/448) computed and applied on the device: 2 launches, no host sync
+    ws = workspace(w16.device)
+    call("dtf_quant_fp8_exact", ptr(w16), ptr(st.wq), w16.numel(), ptr(st.buf[1:2]), ptr(ws), stream())
     st.w_key = key
     return st.wq
 
@@ -59,7 +61,7 @@ class _DenseFP8(torch.autograd.Function):
         if not st.x_ready:  # bootstrap the delayed activation scale once
             st.buf[0:1].copy_(x2.abs().amax().float().clamp_min(1e-12) / E4M3_MAX)
             st.x_ready = True
-        xq = quantize(x2, st.buf[0:1], st.buf[2:3])
+        xq = quantize(x2, st.buf[0:1], st.buf[2:3], zero_amax=False)  # reset by the scale update below
         wq = _weight_fp8(st, w)
         M, K = x2.shape
         N = w.shape[0]
@@ -69,6 +71,7 @@ class _DenseFP8(torch.autograd.Function):
              stream())
         call("dtf_fp8_update_scale", ptr(st.buf[2:3]), ptr(st.buf[0:1]), 0.0, stream())  # next step's x scale
         ctx.save_for_backward(x2, w, pre)
+        ctx.b_param = b
         ctx.act = act
         ctx.has_b = b is not None
         ctx.shp = shp
@@ -84,8 +87,19 @@ class _DenseFP8(torch.autograd.Function):
             call("dtf_act", ptr(pre), ptr(dz), ptr(g), g.numel(), ctx.act, 1, stream())
             dz = g
         dx = gemm(dz, bf16_shadow(w), b_kouter=True).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
-        dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32) if ctx.needs_input_grad[1] else None
-        db = colsum(dz) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dw = db = None
+        if ctx.needs_input_grad[1]:  # inside Model.train_step: accumulate into the arena gradient directly
+            tw = direct_grad(w)
+            if tw is not None:
+                gemm(dz, x2, a_kouter=True, b_kouter=True, out=tw, beta=1.0)
+            else:
+                dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            tb = direct_grad(ctx.b_param)
+            if tb is not None:
+                colsum(dz, out=tb, accumulate=True)
+            else:
+                db = colsum(dz)
         return dx, dw, db, None, None
 
 
