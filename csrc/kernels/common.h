@@ -22,15 +22,16 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
-// Round-to-nearest-even; NaN stays NaN (quiet bit forced).
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// gfx950 converts f32 -> bf16 in hardware (v_cvt_pk_bf16_f32, round-to-nearest-even, NaN kept quiet):
+// one VALU op per pair instead of the 4-5 op software rounding sequence.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
 // Load/store 8 bf16 (16 bytes) <-> 8 floats.

@@ -122,33 +122,71 @@ __global__ void bn_infer_coeff_kernel(const float* gamma, const float* beta, con
   shift[c] = bt - rmean[c] * gm * inv;
 }
 
+// Channels-last elementwise passes (apply / backward apply) use the reduction geometry: a thread owns one
+// fixed 8-channel chunk, so its per-channel coefficients sit in registers for the whole launch (no per-element
+// channel index division or coefficient reloads), and walks rows with a grid stride, EU rows per trip with all
+// loads issued before any use (memory-level parallelism for the HBM-bound pass).
+constexpr int EU = 4;
+
+__device__ __forceinline__ void load_coef8(const float* __restrict__ p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// y = [relu](x*scale + shift [+ res]); optional 1-bit ReLU mask of the stored (bf16) values
+__device__ __forceinline__ void bn_apply_row(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                             bf16_t* __restrict__ y, uint8_t* __restrict__ mbits, long i8,
+                                             const float* f, const float* r, const float* sc, const float* sh,
+                                             int relu) {
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = fmaf(f[j], sc[j], sh[j]);
+    if (res) v += r[j];
+    if (relu) v = fmaxf(v, 0.f);
+    o[j] = v;
+  }
+  store8(y + i8 * 8, o);
+  if (mbits) {
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bits |= (uint32_t)(f2bf(o[j]) != 0 && o[j] > 0.f) << j;
+    mbits[i8] = (uint8_t)bits;
+  }
+}
+
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
-                                                       long n8, int C, int relu, uint8_t* __restrict__ mbits) {
-  const int c8 = C / 8;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % c8) * 8;
-    float f[8], r[8];
-    load8(x + i * 8, f);
-    if (res) load8(res + i * 8, r);
-    float4 s0 = *reinterpret_cast<const float4*>(scale + c), s1 = *reinterpret_cast<const float4*>(scale + c + 4);
-    float4 h0 = *reinterpret_cast<const float4*>(shift + c), h1 = *reinterpret_cast<const float4*>(shift + c + 4);
-    float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    uint32_t bits = 0;
+                                                       long M, int C, int relu, uint8_t* __restrict__ mbits) {
+  const ColGeo g = colgeo(C);
+  const int t = threadIdx.x;
+  if (t >= g.TPR * g.RPB) return;
+  const int rsub = t / g.TPR;
+  const long rstep = (long)gridDim.x * g.RPB;
+  for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
+    float sc[8], sh[8];
+    load_coef8(scale + cc * 8, sc);
+    load_coef8(shift + cc * 8, sh);
+    long r = (long)blockIdx.x * g.RPB + rsub;
+    for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
+      float f[EU][8], rv[EU][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = f[j] * sc[j] + sh[j];
-      if (res) v += r[j];
-      if (relu) v = fmaxf(v, 0.f);
-      f[j] = v;
+      for (int u = 0; u < EU; ++u) {
+        const long i8 = (r + u * rstep) * g.cols8 + cc;
+        load8(x + i8 * 8, f[u]);
+        if (res) load8(res + i8 * 8, rv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u)
+        bn_apply_row(x, res, y, mbits, (r + u * rstep) * g.cols8 + cc, f[u], rv[u], sc, sh, relu);
     }
-    store8(y + i * 8, f);
-    if (mbits) {  // ReLU mask of the stored (bf16-rounded) values, 1 bit per element
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bits |= (uint32_t)(f2bf(f[j]) != 0 && f[j] > 0.f) << j;
-      mbits[i] = (uint8_t)bits;
+    for (; r < M; r += rstep) {
+      float f[8], rv[8];
+      const long i8 = r * g.cols8 + cc;
+      load8(x + i8 * 8, f);
+      if (res) load8(res + i8 * 8, rv);
+      bn_apply_row(x, res, y, mbits, i8, f, rv, sc, sh, relu);
     }
   }
 }
@@ -190,18 +228,38 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
     const int cc = cc0 + t % g.TPR;
     float s[8] = {0}, q[8] = {0};
     if (t < g.TPR * g.RPB && cc < g.cols8) {
-      float mu[8], is[8];
+      float mu[8];
+      load_coef8(mean + cc * 8, mu);
+      // sum dz*(x - mean) here; the invstd factor is applied once per channel in bn_bwd_finalize
+      const long rstep = (long)gridDim.x * g.RPB;
+      long r = (long)blockIdx.x * g.RPB + rsub;
+      for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
+        float d[EU][8], xv[EU][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { mu[j] = mean[cc * 8 + j]; is[j] = invstd[cc * 8 + j]; }
-      for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
+        for (int u = 0; u < EU; ++u) {
+          const long i8 = (r + u * rstep) * g.cols8 + cc;
+          load8(dy + i8 * 8, d[u]);
+          load8(x + i8 * 8, xv[u]);
+          relu_mask8(d[u], ymask, mbits, i8);
+        }
+#pragma unroll
+        for (int u = 0; u < EU; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            s[j] += d[u][j];
+            q[j] = fmaf(d[u][j], xv[u][j] - mu[j], q[j]);
+          }
+      }
+      for (; r < M; r += rstep) {
         float d[8], xv[8];
-        load8(dy + r * C + cc * 8, d);
-        load8(x + r * C + cc * 8, xv);
-        relu_mask8(d, ymask, mbits, (r * C) / 8 + cc);
+        const long i8 = r * g.cols8 + cc;
+        load8(dy + i8 * 8, d);
+        load8(x + i8 * 8, xv);
+        relu_mask8(d, ymask, mbits, i8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           s[j] += d[j];
-          q[j] += d[j] * (xv[j] - mu[j]) * is[j];
+          q[j] = fmaf(d[j], xv[j] - mu[j], q[j]);
         }
       }
     }
@@ -211,8 +269,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
 
 // Sum T partial rows; dgamma = sum dz*xhat, dbeta = sum dz; coefficients for the apply pass:
 //   dx = k1 * (dz - k2 - xhat * k3)   with k1 = gamma*invstd, k2 = sum_dz/M, k3 = sum_dzxhat/M
+// folded into dx = a*dz + b*x + c (a = k1, b = -k1*k3*invstd, c = k1*(mean*invstd*k3 - k2)).
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int T, long rs,
                                                               const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, long M, int C,
                                                               float* dgamma, float* dbeta, int accumulate,
                                                               float* __restrict__ coef) {
@@ -226,41 +286,68 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   red[1][grp][cl] = b;
   __syncthreads();
   if (grp != 0 || c >= C) return;
-  float sdz = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-  float sdx = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  const float sdz = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  const float is = invstd[c];
+  const float sdx = (red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl]) * is;
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + sdx;
   if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + sdz;
-  float gm = gamma ? gamma[c] : 1.f;
-  coef[c] = gm * invstd[c];
-  coef[C + c] = sdz / (float)M;
-  coef[2 * C + c] = sdx / (float)M;
+  const float gm = gamma ? gamma[c] : 1.f;
+  const float k1 = gm * is, k2 = sdz / (float)M, k3 = sdx / (float)M;
+  coef[c] = k1;
+  coef[C + c] = -k1 * k3 * is;
+  coef[2 * C + c] = k1 * (mean[c] * is * k3 - k2);
 }
 
+__device__ __forceinline__ void bn_bwd_apply_row(const float* d, const float* xv, const float* ka, const float* kb,
+                                                 const float* kc, bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out,
+                                                 long i8) {
+  if (dz_out) store8(dz_out + i8 * 8, d);
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = fmaf(ka[j], d[j], fmaf(kb[j], xv[j], kc[j]));
+  store8(dx + i8 * 8, o);
+}
+
+// dx = a*dz + b*x + c per channel (coefficients from bn_bwd_finalize); dz_out: the masked dz for the
+// residual branch (only when a ReLU mask is given)
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ ymask,
                                                            const uint8_t* __restrict__ mbits,
                                                            const bf16_t* __restrict__ x,
-                                                           const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd,
-                                                           const float* __restrict__ coef, long n8, int C,
+                                                           const float* __restrict__ coef, long M, int C,
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out) {
-  const int c8 = C / 8;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % c8) * 8;
-    float d[8], xv[8];
-    load8(dy + i * 8, d);
-    load8(x + i * 8, xv);
-    if (ymask || mbits) {
-      relu_mask8(d, ymask, mbits, i);
-      if (dz_out) store8(dz_out + i * 8, d);
-    }
-    float o[8];
+  const ColGeo g = colgeo(C);
+  const int t = threadIdx.x;
+  if (t >= g.TPR * g.RPB) return;
+  const int rsub = t / g.TPR;
+  const long rstep = (long)gridDim.x * g.RPB;
+  if (!ymask && !mbits) dz_out = nullptr;
+  for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
+    float ka[8], kb[8], kc[8];
+    load_coef8(coef + cc * 8, ka);
+    load_coef8(coef + C + cc * 8, kb);
+    load_coef8(coef + 2 * C + cc * 8, kc);
+    long r = (long)blockIdx.x * g.RPB + rsub;
+    for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
+      float d[EU][8], xv[EU][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float xh = (xv[j] - mean[c + j]) * invstd[c + j];
-      o[j] = coef[c + j] * (d[j] - coef[C + c + j] - xh * coef[2 * C + c + j]);
+      for (int u = 0; u < EU; ++u) {
+        const long i8 = (r + u * rstep) * g.cols8 + cc;
+        load8(dy + i8 * 8, d[u]);
+        load8(x + i8 * 8, xv[u]);
+        relu_mask8(d[u], ymask, mbits, i8);
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u) bn_bwd_apply_row(d[u], xv[u], ka, kb, kc, dx, dz_out, (r + u * rstep) * g.cols8 + cc);
     }
-    store8(dx + i * 8, o);
+    for (; r < M; r += rstep) {
+      float d[8], xv[8];
+      const long i8 = r * g.cols8 + cc;
+      load8(dy + i8 * 8, d);
+      load8(x + i8 * 8, xv);
+      relu_mask8(d, ymask, mbits, i8);
+      bn_bwd_apply_row(d, xv, ka, kb, kc, dx, dz_out, i8);
+    }
   }
 }
 
@@ -392,6 +479,15 @@ int red_grid(long M, int C) {
   return (int)blocks;
 }
 
+// elementwise channels-last passes: enough blocks to fill the chip, each with >= EU row trips when possible
+int ew_grid(long M, int C) {
+  ColGeo g = colgeo(C);
+  long blocks = (M + (long)g.RPB * EU - 1) / ((long)g.RPB * EU);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
 }  // namespace
 
 // Statistics of x: writes G partial rows into `part` (capacity >= 1024*2*C floats), returns G via *rows.
@@ -429,9 +525,8 @@ DTF_API int dtf_bn_infer_coeff(const float* gamma, const float* beta, const floa
 DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, const void* res, void* y, long M,
                          int C, int relu, void* mbits, void* stream) {
   if (C & 7) return -1;
-  long n8 = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, n8, C, relu,
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M, C)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, M, C, relu,
                      relu ? (uint8_t*)mbits : nullptr);
   return (int)hipGetLastError();
 }
@@ -451,12 +546,10 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
                      (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part);
   long rs = 2L * C;
   int T = dtf_group_rows_once(part, rs, G, 2L * C, 32, &rs, stream);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, invstd, M, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, mean, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);
-  long n8 = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, coef, n8, C,
-                     (bf16_t*)dx,
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M, C)), dim3(256), 0, st, (const bf16_t*)dy,
+                     (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
                      (bf16_t*)dz_out);
   return (int)hipGetLastError();
 }

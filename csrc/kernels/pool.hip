@@ -5,19 +5,21 @@
 namespace {
 
 // One thread = 8 channels of one output pixel.
+// Index decomposition is 32-bit with multiply-shift division (launchers require < 2^31 work items).
+struct PoolDivs {
+  FastDiv c8, a, b;  // chunks per pixel, then the two spatial extents (Q,P for fwd; W,H for bwd)
+};
+
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C,
                                                           int P, int Q, int R, int S, int sh, int sw, int ph,
-                                                          int pw) {
-  const int c8 = C / 8;
-  const long total = (long)N * P * Q * c8;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int cc = (int)(i % c8);
-    long pix = i / c8;
-    int q = (int)(pix % Q);
-    long t = pix / Q;
-    int p = (int)(t % P);
-    int n = (int)(t / P);
+                                                          int pw, PoolDivs dv) {
+  const uint32_t total = (uint32_t)N * P * Q * (C / 8);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    uint32_t pix, cc, t, q, n, p;
+    fdivmod(i, dv.c8, pix, cc);
+    fdivmod(pix, dv.a, t, q);
+    fdivmod(t, dv.b, n, p);
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -29,18 +31,18 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restri
         int wi = q * sw - pw + s;
         if ((unsigned)wi >= (unsigned)W) continue;
         float f[8];
-        load8(x + (((long)n * H + hi) * W + wi) * C + cc * 8, f);
+        load8(x + ((long)(n * H + hi) * W + wi) * C + cc * 8, f);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (f[j] > best[j]) { best[j] = f[j]; bi[j] = (uint8_t)(r * S + s); }
       }
     }
-    store8(y + i * 8, best);
+    store8(y + (long)i * 8, best);
     if (arg) {
       uint2 a;
       a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
       a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
-      *reinterpret_cast<uint2*>(arg + i * 8) = a;
+      *reinterpret_cast<uint2*>(arg + (long)i * 8) = a;
     }
   }
 }
@@ -49,28 +51,25 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restri
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
                                                           int N, int H, int W, int C, int P, int Q, int R, int S,
-                                                          int sh, int sw, int ph, int pw) {
-  const int c8 = C / 8;
-  const long total = (long)N * H * W * c8;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int cc = (int)(i % c8);
-    long pix = i / c8;
-    int w = (int)(pix % W);
-    long t = pix / W;
-    int h = (int)(t % H);
-    int n = (int)(t / H);
+                                                          int sh, int sw, int ph, int pw, PoolDivs dv) {
+  const uint32_t total = (uint32_t)N * H * W * (C / 8);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    uint32_t pix, cc, t, w, n, h;
+    fdivmod(i, dv.c8, pix, cc);
+    fdivmod(pix, dv.a, t, w);
+    fdivmod(t, dv.b, n, h);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int r = 0; r < R; ++r) {
-      int th = h + ph - r;
+      int th = (int)h + ph - r;
       if (th < 0 || th % sh) continue;
       int p = th / sh;
       if (p >= P) continue;
       for (int s = 0; s < S; ++s) {
-        int tw = w + pw - s;
+        int tw = (int)w + pw - s;
         if (tw < 0 || tw % sw) continue;
         int q = tw / sw;
         if (q >= Q) continue;
-        long o = (((long)n * P + p) * Q + q) * C + cc * 8;
+        long o = ((long)(n * P + p) * Q + q) * C + cc * 8;
         uint2 a = *reinterpret_cast<const uint2*>(arg + o);
         uint8_t bi[8] = {(uint8_t)a.x, (uint8_t)(a.x >> 8), (uint8_t)(a.x >> 16), (uint8_t)(a.x >> 24),
                          (uint8_t)a.y, (uint8_t)(a.y >> 8), (uint8_t)(a.y >> 16), (uint8_t)(a.y >> 24)};
@@ -82,7 +81,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restri
           if (bi[j] == me) acc[j] += g[j];
       }
     }
-    store8(dx + i * 8, acc);
+    store8(dx + (long)i * 8, acc);
   }
 }
 
@@ -140,8 +139,10 @@ DTF_API int dtf_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H, 
                             int S, int sh, int sw, int ph, int pw, void* stream) {
   if (C & 7) return -1;
   long total = (long)N * P * Q * (C / 8);
+  if (total >= (1L << 31) || R * S > 256) return -1;
+  PoolDivs dv{make_fastdiv(C / 8), make_fastdiv(Q), make_fastdiv(P)};
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)x, (bf16_t*)y, (uint8_t*)argmax, N, H, W, C, P, Q, R, S, sh, sw, ph, pw);
+                     (const bf16_t*)x, (bf16_t*)y, (uint8_t*)argmax, N, H, W, C, P, Q, R, S, sh, sw, ph, pw, dv);
   return (int)hipGetLastError();
 }
 
@@ -149,9 +150,11 @@ DTF_API int dtf_maxpool_bwd(const void* dy, const void* argmax, void* dx, int N,
                             int R, int S, int sh, int sw, int ph, int pw, void* stream) {
   if (C & 7) return -1;
   long total = (long)N * H * W * (C / 8);
+  if (total >= (1L << 31) || R * S > 256) return -1;
+  PoolDivs dv{make_fastdiv(C / 8), make_fastdiv(W), make_fastdiv(H)};
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)dy, (const uint8_t*)argmax, (bf16_t*)dx, N, H, W, C, P, Q, R, S, sh, sw, ph,
-                     pw);
+                     pw, dv);
   return (int)hipGetLastError();
 }
 

@@ -303,14 +303,15 @@ class ConvBN(Layer):
         self.moving_variance = self.add_weight("bn/moving_variance", (self.filters,), "ones", trainable=False)
         self.built = True
 
-    def call(self, x, residual=None, training=None):
+    def call(self, x, residual=None, training=None, link=None, role=None):
+        """link/role: residual-gradient join of a block (ops.conv.ResidualGradLink)."""
         if self.padding == "same":
             pad = ((self.kernel_size[0] - 1) // 2, (self.kernel_size[1] - 1) // 2)
         else:
             pad = (0, 0)
         return ops.conv_bn(x, self.kernel, self.gamma, self.beta, self.moving_mean, self.moving_variance,
                            stride=self.strides, pad=pad, relu=self.relu, residual=residual, momentum=self.momentum,
-                           eps=self.epsilon, training=bool(training))
+                           eps=self.epsilon, training=bool(training), link=link, role=role)
 
 
 class MaxPooling2D(Layer):

@@ -13,10 +13,17 @@ gradient and never influence the output).
 """
 from __future__ import annotations
 
+import os
+
+import torch
+
 from .. import ops
 from ..keras import layers as KL
 from ..keras.models import Model
 
+from ..ops.conv import ResidualGradLink
+
+RES_LINK = os.environ.get("DTF_RES_LINK", "1") != "0"
 STAGES = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3), 26: (2, 2, 2, 2)}
 
 
@@ -30,10 +37,16 @@ class Bottleneck(KL.Layer):
         self.proj = KL.ConvBN(width * 4, 1, stride, relu=False, **m) if project else None
 
     def call(self, x, training=None):
-        sc = self.proj(x, training=training) if self.proj is not None else x
-        y = self.c1(x, training=training)
+        # The projection runs after c1 so that its backward runs before c1's: the shortcut gradient is then
+        # parked in `link` and c1's dgrad epilogue adds into it (no separate add of the two gradients of x).
+        link = ResidualGradLink() if (training and RES_LINK and torch.is_grad_enabled()) else None
+        y = self.c1(x, training=training, link=link, role="acc")
+        if self.proj is not None:
+            sc = self.proj(x, training=training, link=link, role="proj")
+            y = self.c2(y, training=training)
+            return self.c3(y, residual=sc, training=training)
         y = self.c2(y, training=training)
-        return self.c3(y, residual=sc, training=training)
+        return self.c3(y, residual=x, training=training, link=link, role="res")
 
 
 class ResNet(Model):

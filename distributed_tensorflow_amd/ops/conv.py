@@ -53,13 +53,15 @@ def conv_fwd_raw(x, w16, g, stats=False, bias=None, act=0):
     return y
 
 
-def conv_dgrad_raw(dy, w_master, g):
+def conv_dgrad_raw(dy, w_master, g, acc=None):
+    """dX (bf16); with `acc` (a bf16 [N,H,W,C] gradient already holding another contribution) the epilogue
+    adds into it (beta = 1) and returns it."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     wc = crsk_shadow(w_master, K, R * S, C)
-    dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device)
+    dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device) if acc is None else acc
     ws = workspace(dy.device)  # strided convs: per-phase compact filters (bf16) live here
-    call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0.0,
-         -1, ptr(ws), 2 * ws.numel(), stream())
+    call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0,
+         0.0 if acc is None else 1.0, -1, ptr(ws), 2 * ws.numel(), stream())
     return dx
 
 
@@ -119,11 +121,44 @@ def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0), dil=(1, 1), act=0):
     return torch.relu(y) if act == 1 else y
 
 
+class ResidualGradLink:
+    """Joins the two gradient contributions of a residual block's input without an extra add pass.
+
+    The block input x feeds the first conv (role "acc") and the shortcut: either directly as the residual of
+    the last conv (role "res") or through a projection conv (role "proj"). The shortcut's backward parks its
+    gradient of x here instead of returning it, and the first conv's dgrad epilogue adds into that buffer
+    (beta = 1) and returns the sum — autograd sees one gradient for x and runs no add kernel. If the first
+    conv's backward happens to run before the projection's (autograd schedules by creation order; the block
+    creates the projection after the first conv so that it runs first), the link closes and both return their
+    gradients normally, so the result is the same either way.
+    """
+    __slots__ = ("buf", "closed")
+
+    def __init__(self):
+        self.buf = None
+        self.closed = False
+
+    def park(self, g):
+        """Shortcut side: returns what to hand autograd (None when parked)."""
+        if self.closed or g is None:
+            return g
+        self.buf = g
+        return None
+
+    def take(self):
+        """First-conv side: the parked gradient to accumulate into (or None; then the link closes)."""
+        buf, self.buf = self.buf, None
+        if buf is None:
+            self.closed = True
+        return buf
+
+
 class _ConvBNFn(torch.autograd.Function):
     """y = [relu]( BN_train(conv(x, w)) [+ residual] ) with batch statistics from the conv epilogue."""
 
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, res, rmean, rvar, stride, pad, dil, relu, momentum, eps, training):
+    def forward(ctx, x, w, gamma, beta, res, rmean, rvar, stride, pad, dil, relu, momentum, eps, training,
+                link=None, role=None):
         x = x.contiguous()
         g = _geom(x, w, stride, pad, dil)
         N, H, W, C, K, R, S, P, Q = g[:9]
@@ -152,6 +187,7 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = res is not None
         ctx.training = training
+        ctx.link, ctx.role = link, role
         return out
 
     @staticmethod
@@ -173,9 +209,15 @@ class _ConvBNFn(torch.autograd.Function):
              ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), stream())
         if ctx.has_res and not ctx.relu:
             dres = dout
+        link, role = ctx.link, ctx.role
+        if link is not None and role == "res":
+            dres = link.park(dres)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = conv_dgrad_raw(dyc, w, g)
+            acc = link.take() if (link is not None and role == "acc") else None
+            dx = conv_dgrad_raw(dyc, w, g, acc=acc)
+            if link is not None and role == "proj":
+                dx = link.park(dx)
         if ctx.needs_input_grad[1]:
             tw = direct_grad(w)
             dw = conv_wgrad_raw(x, dyc, g, out=tw)
@@ -184,16 +226,16 @@ class _ConvBNFn(torch.autograd.Function):
                 #            gradient, so its post-accumulate hooks — gradient bucketing — fire as usual)
         if direct_bn:
             dgamma = dbeta = None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 def conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1), relu=True, residual=None,
-            momentum=0.9, eps=1e-5, training=True):
-    """Fused Conv2D -> FusedBatchNorm -> (+residual) -> ReLU, NHWC."""
+            momentum=0.9, eps=1e-5, training=True, link=None, role=None):
+    """Fused Conv2D -> FusedBatchNorm -> (+residual) -> ReLU, NHWC. `link`/`role`: see ResidualGradLink."""
     stride, pad, dil = tuple(stride), tuple(pad), tuple(dil)
     if on_gpu(x):
         return _ConvBNFn.apply(x.to(BF16), w, gamma, beta, residual, rmean, rvar, stride, pad, dil, bool(relu),
-                               float(momentum), float(eps), bool(training))
+                               float(momentum), float(eps), bool(training), link, role)
     y = _ref_conv(x, w, None, stride, pad, dil)
     from .norm import batch_norm_ref
     y = batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training)
