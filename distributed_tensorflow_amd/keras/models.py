@@ -81,6 +81,17 @@ def _unpack(data):
     return data, None, None
 
 
+def _head(x, n=1):
+    """The first n samples of a (possibly nested) input batch: enough to build lazily created weights."""
+    if isinstance(x, torch.Tensor):
+        return x[:n]
+    if isinstance(x, dict):
+        return {k: _head(v, n) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_head(v, n) for v in x)
+    return x
+
+
 class Model(Layer):
     def __init__(self, inputs=None, outputs=None, name=None, **kw):
         super().__init__(name=name, **kw)
@@ -132,6 +143,11 @@ class Model(Layer):
             self.distribute_strategy.setup_model(self, self._arena)
         return self._arena
 
+    def _fully_built(self):
+        def rec(layer):
+            return layer.built and all(rec(c) for c in layer._layers)
+        return rec(self)
+
     def compute_loss(self, x=None, y=None, y_pred=None, sample_weight=None):
         loss = self.compiled_loss(y, y_pred, sample_weight) if self.compiled_loss is not None else y_pred.sum()
         reg = getattr(self, "losses", None)
@@ -149,6 +165,13 @@ class Model(Layer):
         reps = strat.inproc_replicas() if hasattr(strat, "inproc_replicas") else None
         if reps:
             return self._train_step_inproc(x, y, sw, reps)
+        if self._arena is None:
+            # lay out the arena (and let the strategy broadcast rank 0's initial state) BEFORE the first
+            # forward: otherwise every replica's first gradients come from its own, unsynchronised weights
+            if not self._fully_built():
+                with torch.no_grad():
+                    self(_head(x), training=False)
+            self._ensure_arena()
         with prof.phase("forward"):
             y_pred = self(x, training=True)
             loss = self.compute_loss(x, y, y_pred, sw)

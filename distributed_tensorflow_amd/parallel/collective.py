@@ -28,6 +28,12 @@ _DEFAULT_BUCKET_MB = float(os.environ.get("DTF_BUCKET_MB", "32"))
 
 
 def backend_for(device_type: str) -> str:
+    """RCCL ("nccl" on ROCm) for GPU replicas, gloo for CPU. ``DTF_COLLECTIVE_BACKEND=gloo`` forces gloo for
+    GPU tensors too: it lets several ranks share ONE GPU (RCCL refuses duplicate devices), which is how the
+    multi-process GPU data path is rehearsed on a 1-GPU box (tests/test_dp_gpu.py)."""
+    forced = os.environ.get("DTF_COLLECTIVE_BACKEND")
+    if forced:
+        return forced
     return "nccl" if device_type == "cuda" else "gloo"
 
 

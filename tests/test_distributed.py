@@ -23,10 +23,10 @@ def _port():
     return p
 
 
-def _train_mlp(strategy, x, y, epochs=2, batch=64):
+def _train_mlp(strategy, x, y, epochs=2, batch=64, seed=0):
     from distributed_tensorflow_amd.keras import initializers, losses, optimizers
     from distributed_tensorflow_amd.models.mlp import MnistMLP
-    initializers.set_seed(0)
+    initializers.set_seed(seed)
     with strategy.scope():
         m = MnistMLP(hidden=32)
         m.compile(optimizers.SGD(0.1, momentum=0.9), losses.SparseCategoricalCrossentropy(from_logits=True),
@@ -43,7 +43,8 @@ def _mwms_worker(rank, world, port, mode, q):
         from distributed_tensorflow_amd.models.mlp import synthetic_mnist
         x, y = synthetic_mnist(512)
         s = parallel.MultiWorkerMirroredStrategy()
-        m, h = _train_mlp(s, torch.as_tensor(x), torch.as_tensor(y))
+        # every rank starts from its own random init: rank 0's must be broadcast before the first step
+        m, h = _train_mlp(s, torch.as_tensor(x), torch.as_tensor(y), seed=rank)
         q.put((rank, [w.detach().numpy().copy() for w in m.weights], h.history["loss"]))
         import torch.distributed as dist
         dist.barrier()

@@ -1,0 +1,126 @@
+"""Multi-process data parallelism on the GPU path, rehearsed on ONE MI355X.
+
+Two ranks share cuda:0 and reduce over gloo (``DTF_COLLECTIVE_BACKEND=gloo``; RCCL refuses two ranks on
+one device). Everything else is the production path the 8-GPU bench takes: MultiWorkerMirroredStrategy
+under torchrun-style env, initial-state broadcast, the HIP kernels with direct arena-gradient
+accumulation, the bucketed all-reduce issued from post-accumulate hooks while backward runs (tiny
+buckets here, so there are many of them), 1/N folded into the fused optimizer.
+
+* GPT-2 (LayerNorm only, no batch statistics): 2 ranks x half batch must equal one process on the whole
+  batch, and both replicas must hold identical weights.
+* ResNet (BatchNorm statistics are per replica, as in tf.distribute): replicas must stay identical.
+"""
+import multiprocessing as mp
+import os
+import socket
+import traceback
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gpt2(seed):
+    from distributed_tensorflow_amd.keras import initializers, losses, optimizers
+    from distributed_tensorflow_amd.models.transformer import GPT2
+    initializers.set_seed(seed)
+    m = GPT2(vocab=320, ctx=128, hidden=128, layers=2, heads=2, dropout=0.0)
+    # SGD, not Adam: Adam's per-element normalisation turns rounding noise in near-zero gradients into
+    # full-size steps, which would hide a wrong reduction scale instead of exposing it
+    m.compile(optimizer=optimizers.SGD(0.1, momentum=0.9),
+              loss=losses.SparseCategoricalCrossentropy(from_logits=True))
+    return m
+
+
+def _resnet(seed):
+    from distributed_tensorflow_amd.keras import initializers, losses, optimizers
+    from distributed_tensorflow_amd.models import ResNet
+    initializers.set_seed(seed)
+    m = ResNet(50, num_classes=16, width=16)
+    m.compile(optimizer=optimizers.SGD(0.05, momentum=0.9),
+              loss=losses.SparseCategoricalCrossentropy(from_logits=True))
+    return m
+
+
+def _batches(kind, dev, steps=3):
+    g = torch.Generator().manual_seed(5)
+    out = []
+    for _ in range(steps):
+        if kind == "gpt2":
+            ids = torch.randint(0, 320, (8, 128), generator=g)
+            out.append((ids.to(dev), torch.roll(ids, -1, 1).to(dev)))
+        else:
+            out.append((torch.randn(8, 3, 64, 64, generator=g).to(dev), torch.randint(0, 16, (8,), generator=g).to(dev)))
+    return out
+
+
+def _worker(rank, world, port, kind, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), DTF_COLLECTIVE_BACKEND="gloo")
+    try:
+        import torch.distributed as dist
+        from distributed_tensorflow_amd import parallel
+        s = parallel.MultiWorkerMirroredStrategy(bucket_mb=0.25)
+        assert s.device == torch.device("cuda", 0) and s.num_replicas_in_sync == world
+        with s.scope():
+            m = _gpt2(100 + rank) if kind == "gpt2" else _resnet(100 + rank)  # rank 0's init wins (broadcast)
+        losses = []
+        per = 8 // world
+        for x, y in _batches(kind, s.device):
+            sl = slice(rank * per, (rank + 1) * per)
+            losses.append(float(m.train_step((x[sl], y[sl]))["loss"]))
+        torch.cuda.synchronize()
+        b = s._bucketers[id(m._arena)]
+        # numpy, not torch CPU tensors: those travel as shared-memory fds that vanish when the worker exits
+        q.put((rank, [w.detach().float().cpu().numpy() for w in m.trainable_variables], losses, len(b.buckets)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put((rank, None, traceback.format_exc(), 0))
+
+
+def _run_ranks(kind, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    [p.start() for p in ps]
+    try:
+        res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda t: t[0])
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    for r in res:
+        assert r[1] is not None, r[2]
+    return res
+
+
+def test_two_rank_gpt2_equals_single_process(cuda):
+    res = _run_ranks("gpt2")
+    assert res[0][3] > 3, "expected several gradient buckets"
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a == b).all(), "replicas diverged"
+    m = _gpt2(100)
+    for x, y in _batches("gpt2", cuda):
+        m.train_step((x, y))
+    torch.cuda.synchronize()
+    for a, w in zip(res[0][1], m.trainable_variables):
+        torch.testing.assert_close(torch.from_numpy(a), w.detach().float().cpu(), rtol=2e-3, atol=2e-4)
+
+
+def test_two_rank_resnet_replicas_stay_identical(cuda):
+    res = _run_ranks("resnet")
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a == b).all(), "replicas diverged"
+    assert all(x == x for x in res[0][2])
