@@ -89,6 +89,8 @@ static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
   // long K amortises the larger tile's epilogue: one round of 128x128 tiles beats two of 128x64
   if (N > 64 && K >= 1024 && blocks(128, 128) >= 256) return 0;
   if (N <= 64) {
+    // narrow N: 128x64 beats 256x64 at every ResNet-50 shape measured (tools/conv_roofline.py --tiles)
+    if (blocks(128, 64) >= 512) return 2;
     if (blocks(256, 64) >= 512) return 1;
     if (blocks(128, 64) >= 256) return 2;
     return 3;
@@ -119,7 +121,10 @@ static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st
   else if (amode == OP_KOUTER && bmode == OP_KCONTIG) launch_modes<OP_KOUTER, OP_KCONTIG>(a, tile, st);
   else if (amode == OP_IM2COL && bmode == OP_KCONTIG) launch_modes<OP_IM2COL, OP_KCONTIG>(a, tile, st);
   else if (amode == OP_DGRAD && bmode == OP_KCONTIG) launch_modes<OP_DGRAD, OP_KCONTIG>(a, tile, st);
+  else if (amode == OP_IM2COL_T && bmode == OP_KCONTIG) launch_modes<OP_IM2COL_T, OP_KCONTIG>(a, tile, st);
+  else if (amode == OP_DGRAD_T && bmode == OP_KCONTIG) launch_modes<OP_DGRAD_T, OP_KCONTIG>(a, tile, st);
   else if (amode == OP_KOUTER && bmode == OP_WGRADX) launch_modes<OP_KOUTER, OP_WGRADX>(a, tile, st);
+  else if (amode == OP_KOUTER_R && bmode == OP_WGRADX_R) launch_modes<OP_KOUTER_R, OP_WGRADX_R>(a, tile, st);
 }
 
 static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw,
@@ -130,6 +135,30 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int P
   g.dPQ = make_fastdiv(P * Q); g.dQ = make_fastdiv(Q); g.dHW = make_fastdiv(H * W);
   g.dW = make_fastdiv(W); g.dC = make_fastdiv(C); g.dS = make_fastdiv(S); g.dK = make_fastdiv(K);
   return g;
+}
+
+static uint64_t rowrep(int R, int S) {
+  uint64_t r = 0;
+  for (int kh = 0; kh < R && kh * S < 64; ++kh) r |= 1ull << (kh * S);
+  return r;
+}
+
+// Tap-uniform gather eligibility (OP_IM2COL_T / OP_DGRAD_T): 64-channel K-tiles never straddle a tap, the tap
+// mask fits 32 bits, the gathered tensor's byte offsets fit 31 bits. Opt out with DTF_CONV_TAPS=0.
+static bool tap_uniform(int chans, int taps, long gathered_elems) {
+  static const bool on = [] {
+    const char* e = getenv("DTF_CONV_TAPS");
+    return !(e && e[0] == '0');
+  }();
+  return on && chans % 64 == 0 && taps <= 32 && gathered_elems * 2 < (1l << 31);
+}
+
+static bool rowmap_ok() {
+  static const bool on = [] {
+    const char* e = getenv("DTF_WGRAD_ROWMAP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 static int choose_splitk(long M, long N, long K, int tile_m, int tile_n, long batch) {
@@ -223,13 +252,15 @@ DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bi
   if ((C & 7) || (K & 3)) return -1;
   GemmArgs a{};
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
+  a.g_rowrep = rowrep(a.g.R, a.g.S);
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)Wt; a.C = Y; a.bias = bias; a.stats = stats;
   a.M = N * P * Q; a.N = K; a.K = R * S * C;
   a.lda = C; a.ldb = (long)R * S * C; a.ldc = K;
   a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
-  dispatch(a, pointwise ? OP_KCONTIG : OP_IM2COL, OP_KCONTIG, tile, (hipStream_t)stream);
+  const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
+  dispatch(a, am, OP_KCONTIG, tile, (hipStream_t)stream);
   if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();
 }
@@ -266,13 +297,16 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
   if (!phased) {
     GemmArgs a{};
     a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
+    a.g_rowrep = rowrep(a.g.R, a.g.S);
     a.A = (const bf16_t*)dY; a.B = (const bf16_t*)Wcrsk; a.C = dX;
     a.M = N * H * W; a.N = C; a.K = R * S * K;
     a.lda = K; a.ldb = (long)R * S * K; a.ldc = C;
     a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
     a.alpha = 1.f; a.beta = beta; a.act = 0; a.out_f32 = out_f32;
     bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
-    dispatch(a, pointwise ? OP_KCONTIG : OP_DGRAD, OP_KCONTIG, tile, st);
+    const int am = pointwise ? OP_KCONTIG
+                   : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
+    dispatch(a, am, OP_KCONTIG, tile, st);
     return (int)hipGetLastError();
   }
   // phases without taps produce zeros: clear dX once unless accumulating
@@ -301,6 +335,7 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
                          st, (const bf16_t*)Wcrsk, Bp, C, R, S, K, rh, rw, sh, sw, nkh, nkw);
       GemmArgs a{};
       a.g = make_geom(N, Hs, Ws, C, K, nkh, nkw, P, Q, 1, 1, ch, cw, 1, 1);
+      a.g_rowrep = rowrep(a.g.R, a.g.S);
       a.A = (const bf16_t*)dY; a.B = Bp; a.C = dX;
       a.M = N * Hs * Ws; a.N = C; a.K = nkh * nkw * K;
       a.lda = K; a.ldb = (long)nkh * nkw * K; a.ldc = C;
@@ -311,7 +346,9 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
       a.rmH = H; a.rmW = W; a.rmsh = sh; a.rmsw = sw; a.rmh0 = h0; a.rmw0 = w0;
       // a 1x1 tap set reading dY pixel-for-pixel is a plain GEMM over dY rows
       const bool pointwise = nkh == 1 && nkw == 1 && ch == 0 && cw == 0 && Hs == P && Ws == Q;
-      dispatch(a, pointwise ? OP_KCONTIG : OP_DGRAD, OP_KCONTIG, tile, st);
+      const int am = pointwise ? OP_KCONTIG
+                     : tap_uniform(K, nkh * nkw, (long)N * P * Q * K) ? OP_DGRAD_T : OP_DGRAD;
+      dispatch(a, am, OP_KCONTIG, tile, st);
     }
   }
   return (int)hipGetLastError();
@@ -326,6 +363,7 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   hipStream_t st = (hipStream_t)stream;
   GemmArgs a{};
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
+  a.g_rowrep = rowrep(a.g.R, a.g.S);
   a.A = (const bf16_t*)dY; a.B = (const bf16_t*)X;
   a.M = K; a.N = R * S * C; a.K = N * P * Q;
   a.lda = K; a.ldb = C; a.ldc = (long)R * S * C;
@@ -339,15 +377,22 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   a.splitk = splitk;
   a.kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  if (tile < 0) {  // measured on ResNet-50's filters (tools/conv_roofline.py --only wgrad --tiles)
+    if (a.M <= 64) tile = 3;                       // Kout = 64: no half-empty 128-row tiles
+    else if (R * S > 1 && a.M >= 256) tile = 2;    // spatial filters, wide Kout: 128x64
+  }
+  // spatial filters: row-mapped pixel-gather loaders (one pixel decode per thread per K-tile)
+  const bool rowmap = !pointwise && rowmap_ok() && (long)N * H * W * C * 2 < (1l << 31) &&
+                      (long)N * P * Q * K * 2 < (1l << 31);
   if (splitk == 1) {
     a.C = dW;
     a.beta = accumulate ? 1.f : 0.f;
-    dispatch(a, OP_KOUTER, pointwise ? OP_KOUTER : OP_WGRADX, tile, st);
+    dispatch(a, rowmap ? OP_KOUTER_R : OP_KOUTER, rowmap ? OP_WGRADX_R : pointwise ? OP_KOUTER : OP_WGRADX, tile, st);
     return (int)hipGetLastError();
   }
   a.C = ws;
   a.slab = mn;
-  dispatch(a, OP_KOUTER, pointwise ? OP_KOUTER : OP_WGRADX, tile, st);
+  dispatch(a, rowmap ? OP_KOUTER_R : OP_KOUTER, rowmap ? OP_WGRADX_R : pointwise ? OP_KOUTER : OP_WGRADX, tile, st);
   dtf_sum_rows(ws, mn, splitk, mn, dW, accumulate, st);
   return (int)hipGetLastError();
 }

@@ -37,6 +37,19 @@ enum OpMode : int {
   OP_IM2COL = 2,   // conv fwd A: r = output pixel (n,p,q), k = (kh,kw,ci)
   OP_DGRAD = 3,    // conv dgrad A: r = input pixel (n,h,w), k = (kh,kw,co) gathered from dY
   OP_WGRADX = 4,   // conv wgrad B (k-outer): r = (kh,kw,ci), k = output pixel (n,p,q) gathered from X
+  // Tap-uniform forms of IM2COL / DGRAD (C resp. Kout % 64 == 0, R*S <= 32, stride-1 DGRAD): every 64-wide
+  // K-tile is ONE filter tap x 64 channels, so the per-K-tile gather is a wave-uniform tap offset added to
+  // a per-row base offset, with a per-row bit mask of the taps that fall inside the image; loads go through
+  // a buffer descriptor, masked rows get an out-of-range offset and read zeros (no per-row index math, no
+  // selects on the 16-B data).
+  OP_IM2COL_T = 5,
+  OP_DGRAD_T = 6,
+  // Row-mapped K-outer forms for the conv weight gradient (operands < 2 GiB): each thread owns ONE k-row
+  // (pixel) of the 64-deep tile and R/32 of its 16-B chunks, so the pixel decode / row address is computed
+  // once per thread per K-tile (not once per chunk row), loads go through a buffer descriptor with
+  // immediate chunk offsets, and out-of-image taps or rows past K read zeros via the range check.
+  OP_KOUTER_R = 7,   // A = dY [pixels][Kout]
+  OP_WGRADX_R = 8,   // B = X gathered at (pixel, tap)
 };
 
 struct ConvGeom {
@@ -68,6 +81,7 @@ struct GemmArgs {
   ConvGeom g;
   // optional output-row remap (strided dgrad phases): row m = (n, hh, ww) over an rmHs x rmWs grid is stored
   // at pixel (n, rmsh*hh + rmh0, rmsw*ww + rmw0) of an rmH x rmW image
+  uint64_t g_rowrep;    // tap-uniform gathers: sum over kh < R of 2^(kh*S)
   int crm;
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
@@ -90,6 +104,16 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.f + tanhf(u));
 }
 
+// Bit mask over the taps (kh * S + kw) of an R x S filter with kh in [h0, h1] and kw in [w0, w1] (empty when
+// a range is empty), without a loop over taps: the kw range is one S-bit row pattern, replicated into the
+// kept kh rows by a multiply with rowrep = sum_kh 2^(kh*S) (precomputed on the host) masked to [h0, h1].
+__device__ __forceinline__ uint32_t tap_mask(int R, int S, int h0, int h1, int w0, int w1, uint64_t rowrep) {
+  if (h0 > h1 || w0 > w1) return 0u;
+  const uint64_t wm = (1ull << (w1 + 1)) - (1ull << w0);
+  const uint64_t rows = ((rowrep >> (h0 * S)) << (h0 * S)) & ((1ull << ((h1 + 1) * S)) - 1);
+  return (uint32_t)(wm * rows);
+}
+
 // ---- K-contiguous operand: LDS tile [R][64] bf16, 128-B rows ---------------
 template <int R, int MODE>
 struct KContigLoader {
@@ -99,10 +123,64 @@ struct KContigLoader {
   bool rv[L];
   int chunk;
   uint4 reg[L];
+  // tap-uniform modes: byte offset of the row's tap-(0,0) pixel and its in-image tap mask
+  int roff[L];
+  uint32_t tmask[L];
+  __amdgpu_buffer_rsrc_t rsrc;
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot) {
     const int t = threadIdx.x;
     chunk = t & 7;
+    if constexpr (MODE == OP_IM2COL_T || MODE == OP_DGRAD_T) {
+      const ConvGeom& g = a.g;
+      // the host guarantees the gathered tensor is < 2 GiB, so byte offsets fit 31 bits
+      const uint32_t bytes = MODE == OP_IM2COL_T ? (uint32_t)((long)g.N * g.H * g.W * g.C * 2)
+                                                 : (uint32_t)((long)g.N * g.P * g.Q * g.Kout * 2);
+      rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const int r = r0 + (t >> 3) + 32 * i;
+        uint32_t m = 0;
+        int off = 0;
+        if (r < Rtot) {
+          uint32_t n, rem, y, x;
+          if constexpr (MODE == OP_IM2COL_T) {
+            fdivmod((uint32_t)r, g.dPQ, n, rem);
+            fdivmod(rem, g.dQ, y, x);
+            const int hb = (int)y * g.sh - g.ph, wb = (int)x * g.sw - g.pw;
+            off = (((int)n * g.H + hb) * g.W + wb) * g.C * 2;
+            if (g.dh == 1 && g.dw == 1) {  // taps in range: kh in [-hb, H-1-hb], kw in [-wb, W-1-wb]
+              m = tap_mask(g.R, g.S, max(0, -hb), min(g.R - 1, g.H - 1 - hb), max(0, -wb), min(g.S - 1, g.W - 1 - wb),
+                           a.g_rowrep);
+            } else {
+              for (int kh = 0; kh < g.R; ++kh)
+                for (int kw = 0; kw < g.S; ++kw) {
+                  const int hi = hb + kh * g.dh, wi = wb + kw * g.dw;
+                  if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W) m |= 1u << (kh * g.S + kw);
+                }
+            }
+          } else {  // stride-1 dgrad: dX pixel (n, h, w) gathers dY(n, h + ph - kh*dh, w + pw - kw*dw)
+            fdivmod((uint32_t)r, g.dHW, n, rem);
+            fdivmod(rem, g.dW, y, x);
+            const int hb = (int)y + g.ph, wb = (int)x + g.pw;
+            off = (((int)n * g.P + hb) * g.Q + wb) * g.Kout * 2;
+            if (g.dh == 1 && g.dw == 1) {  // taps in range: kh in [hb-P+1, hb], kw in [wb-Q+1, wb]
+              m = tap_mask(g.R, g.S, max(0, hb - g.P + 1), min(g.R - 1, hb), max(0, wb - g.Q + 1), min(g.S - 1, wb),
+                           a.g_rowrep);
+            } else {
+              for (int kh = 0; kh < g.R; ++kh)
+                for (int kw = 0; kw < g.S; ++kw) {
+                  const int ho = hb - kh * g.dh, wo = wb - kw * g.dw;
+                  if ((unsigned)ho < (unsigned)g.P && (unsigned)wo < (unsigned)g.Q) m |= 1u << (kh * g.S + kw);
+                }
+            }
+          }
+        }
+        roff[i] = off;
+        tmask[i] = m;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       int row = (t >> 3) + 32 * i;
@@ -130,6 +208,23 @@ struct KContigLoader {
   }
 
   __device__ __forceinline__ void load(const GemmArgs& a, int k0, int Kend) {
+    if constexpr (MODE == OP_IM2COL_T || MODE == OP_DGRAD_T) {
+      // k0 is wave-uniform: the tap decomposition runs on the scalar unit
+      const ConvGeom& g = a.g;
+      uint32_t tap, c0, kh, kw;
+      fdivmod((uint32_t)k0, MODE == OP_IM2COL_T ? g.dC : g.dK, tap, c0);
+      fdivmod(tap, g.dS, kh, kw);
+      const int toff = MODE == OP_IM2COL_T
+                           ? (((int)kh * g.dh * g.W + (int)kw * g.dw) * g.C + (int)c0) * 2
+                           : ((int)c0 - ((int)kh * g.dh * g.Q + (int)kw * g.dw) * g.Kout) * 2;
+      const int lo = toff + chunk * 16;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const uint32_t off = ((tmask[i] >> tap) & 1u) ? (uint32_t)(roff[i] + lo) : 0x80000000u;
+        reg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+      }
+      return;
+    }
     const int k = k0 + chunk * 8;
     const bool kv = k < Kend;
     if constexpr (MODE == OP_KCONTIG) {
@@ -257,6 +352,90 @@ struct KOuterLoader {
   }
 };
 
+template <int R, int MODE>
+struct PixelRowLoader {
+  static constexpr int CPT = R / 32;  // 16-B chunks per thread (4 threads per 64-deep k-row)
+  int kr;
+  int coff[CPT];                      // byte offset of the chunk's column within a pixel row (+ tap shift)
+  int hoff[CPT], woff[CPT];           // OP_WGRADX_R: tap displacement kh*dh - ph, kw*dw - pw
+  bool cv[CPT];
+  bool one_tap;                       // every column of the tile belongs to one filter tap
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint4 reg[CPT];
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld, int r0, int Rtot) {
+    const int t = threadIdx.x;
+    const ConvGeom& g = a.g;
+    kr = t >> 2;
+    const uint32_t bytes = MODE == OP_WGRADX_R ? (uint32_t)((long)g.N * g.H * g.W * g.C * 2)
+                                               : (uint32_t)((long)g.N * g.P * g.Q * g.Kout * 2);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ptr, (short)0, (int)bytes, 0x00020000);
+    one_tap = MODE == OP_WGRADX_R && (g.C % R == 0);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int col = r0 + ((t & 3) + 4 * i) * 8;
+      cv[i] = col < Rtot;
+      if constexpr (MODE == OP_WGRADX_R) {
+        uint32_t rs, ci, kh, kw;
+        fdivmod((uint32_t)(cv[i] ? col : 0), g.dC, rs, ci);
+        fdivmod(rs, g.dS, kh, kw);
+        hoff[i] = (int)kh * g.dh - g.ph;
+        woff[i] = (int)kw * g.dw - g.pw;
+        coff[i] = ((hoff[i] * g.W + woff[i]) * g.C + (int)ci) * 2;
+      } else {
+        coff[i] = col * 2;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const GemmArgs& a, int k0, int Kend) {
+    const ConvGeom& g = a.g;
+    const int k = k0 + kr;
+    const bool kv = k < Kend;
+    if constexpr (MODE == OP_WGRADX_R) {
+      uint32_t n, pq, pp, qq;
+      fdivmod((uint32_t)(kv ? k : 0), g.dPQ, n, pq);
+      fdivmod(pq, g.dQ, pp, qq);
+      const int hb = (int)pp * g.sh, wb = (int)qq * g.sw;
+      const int pix = (((int)n * g.H + hb) * g.W + wb) * g.C * 2;
+      if (one_tap) {
+        const int hi = hb + hoff[0], wi = wb + woff[0];
+        const bool v = kv && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          const uint32_t off = (v && cv[i]) ? (uint32_t)(pix + coff[i]) : 0x80000000u;
+          reg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          const int hi = hb + hoff[i], wi = wb + woff[i];
+          const bool v = kv && cv[i] && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+          const uint32_t off = v ? (uint32_t)(pix + coff[i]) : 0x80000000u;
+          reg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+        }
+      }
+    } else {  // dY rows: k = pixel, row stride ld = Kout
+      const int rowb = k * g.Kout * 2;
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const uint32_t off = (kv && cv[i]) ? (uint32_t)(rowb + coff[i]) : 0x80000000u;
+        reg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = (t & 3) + 4 * i;
+      const int pc = c ^ (kouter_swz<R>(kr) << 1);
+      *reinterpret_cast<uint4*>(lds + kr * (R * 2) + pc * 16) = reg[i];
+    }
+  }
+};
+
 // fragment read from a [64][R] tile via ds_read_b64_tr_b16: cols cb..cb+15, k-substep kk
 template <int R>
 __device__ __forceinline__ v8bf frag_kouter(const char* lds, int cb, int kk, int lane) {
@@ -275,12 +454,18 @@ __device__ __forceinline__ v8bf frag_kouter(const char* lds, int cb, int kk, int
 }
 
 template <int R, int MODE>
-using LoaderFor = typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE>,
-                                            KContigLoader<R, MODE>>::type;
+using LoaderFor = typename std::conditional<
+    (MODE == OP_KOUTER_R || MODE == OP_WGRADX_R), PixelRowLoader<R, MODE>,
+    typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE>,
+                              KContigLoader<R, MODE>>::type>::type;
+
+constexpr bool kouter_mode(int m) {
+  return m == OP_KOUTER || m == OP_WGRADX || m == OP_KOUTER_R || m == OP_WGRADX_R;
+}
 
 template <int R, int MODE>
 __device__ __forceinline__ v8bf frag(const char* lds, int rb, int kk, int lane) {
-  if constexpr (MODE == OP_KOUTER || MODE == OP_WGRADX) return frag_kouter<R>(lds, rb, kk, lane);
+  if constexpr (kouter_mode(MODE)) return frag_kouter<R>(lds, rb, kk, lane);
   else return frag_kcontig(lds, rb, kk, lane);
 }
 

@@ -94,6 +94,9 @@ CONV_CASES = [
     (1, 15, 13, 16, 32, 3, 3, 2, 1),   # odd sizes, strided dgrad phases
     (2, 9, 9, 32, 64, 1, 1, 2, 0),     # strided 1x1: 3 of 4 phases have no taps
     (1, 10, 11, 16, 16, 3, 3, 3, 1),   # stride 3
+    (1, 12, 12, 32, 64, 3, 3, 1, 1),   # tap-uniform dgrad gather only (Kout % 64 == 0, C % 64 != 0)
+    (2, 12, 10, 64, 32, 3, 3, 1, 1),   # tap-uniform fwd gather only
+    (1, 17, 17, 128, 64, 3, 3, 2, 0),  # tap-uniform, unpadded stride-2 (phases with partial tap sets)
 ]
 
 
