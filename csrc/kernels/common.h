@@ -137,3 +137,32 @@ __global__ void __launch_bounds__(256) dtf_group_rows_kernel(float* __restrict__
 // Deterministic two-level reduction of `nrows` f32 rows (stride `stride`) into out (+= when accumulate);
 // the rows are used as scratch. Defined in gemm.hip.
 DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream);
+
+// ---------------------------------------------------------------------------------------------------------
+// In-launch "last arriver" hand-off (cdna_hip_programming.md §6 Guideline 16): every block of a group writes
+// its partial result with plain stores, then one lane publishes with an agent-scope release + ticket add; the
+// block that draws the last ticket acquires and combines the partials IN A FIXED ORDER (deterministic), then
+// resets the ticket so the next stream-ordered launch finds it at zero. Replaces a second reduction launch.
+__device__ __forceinline__ bool last_arriver(int* ticket, int expected, int* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == expected - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *lds_flag = last;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+// Zero-initialised ticket counters for last_arriver launches on the current device: `n` consecutive slots from
+// a ring (each launch leaves its slots at zero again). nullptr if they cannot be provided (caller falls back
+// to two launches). Must first be called outside stream capture (it allocates once per device).
+DTF_API int* dtf_tickets(int n);

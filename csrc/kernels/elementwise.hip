@@ -78,6 +78,39 @@ __global__ void filter_krsc_to_crsk_kernel(const bf16_t* __restrict__ w, bf16_t*
   }
 }
 
+// Batched KRSC -> CRSK for many filters in ONE launch (every conv filter of a model after each optimizer
+// step): table[f] = {src, dst, K, RS, C, first_tile}; block = one 64(k) x 64(c) tile of one tap rs, transposed
+// through LDS so both the reads (along c) and the writes (along k) are contiguous.
+__global__ void __launch_bounds__(256) filters_to_crsk_kernel(const long* __restrict__ table, int nf) {
+  __shared__ bf16_t tile[64][66];
+  const int b = blockIdx.x;
+  int f = 0;
+  while (f + 1 < nf && table[(f + 1) * 6 + 5] <= b) ++f;
+  const long* d = table + f * 6;
+  const bf16_t* __restrict__ w = reinterpret_cast<const bf16_t*>(d[0]);
+  bf16_t* __restrict__ o = reinterpret_cast<bf16_t*>(d[1]);
+  const int K = (int)d[2], RS = (int)d[3], C = (int)d[4];
+  const int kt_n = (K + 63) / 64, ct_n = (C + 63) / 64;
+  int t = b - (int)d[5];
+  const int ct = t % ct_n; t /= ct_n;
+  const int kt = t % kt_n;
+  const int rs = t / kt_n;
+  const int k0 = kt * 64, c0 = ct * 64;
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int e = threadIdx.x + 256 * i, kl = e >> 6, cl = e & 63;
+    const int k = k0 + kl, c = c0 + cl;
+    tile[kl][cl] = (k < K && c < C) ? w[((long)k * RS + rs) * C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = 0; i < 16; ++i) {
+    const int e = threadIdx.x + 256 * i, cl = e >> 6, kl = e & 63;
+    const int k = k0 + kl, c = c0 + cl;
+    if (k < K && c < C) o[((long)c * RS + rs) * K + k] = tile[kl][cl];
+  }
+}
+
 __global__ void add_bf16_kernel(const bf16_t* a, const bf16_t* b, bf16_t* y, long n8, float alpha, float beta) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     float fa[8], fb[8];
@@ -351,6 +384,11 @@ DTF_API int dtf_nchw_to_nhwc_pad(const float* x, void* y, int N, int C, int HW, 
 }
 DTF_API int dtf_filter_to_crsk(const void* w, void* o, int K, int RS, int C, void* stream) {
   hipLaunchKernelGGL(filter_krsc_to_crsk_kernel, GRID((long)K * RS * C), (const bf16_t*)w, (bf16_t*)o, K, RS, C);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_filters_to_crsk(const long* table, int nfilters, int total_tiles, void* stream) {
+  if (nfilters <= 0 || total_tiles <= 0) return 0;
+  hipLaunchKernelGGL(filters_to_crsk_kernel, dim3(total_tiles), dim3(256), 0, (hipStream_t)stream, table, nfilters);
   return (int)hipGetLastError();
 }
 DTF_API int dtf_add_bf16(const void* a, const void* b, void* y, long n, float alpha, float beta, void* stream) {

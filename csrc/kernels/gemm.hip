@@ -35,6 +35,32 @@ DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int
   return groups;
 }
 
+#include <mutex>
+
+DTF_API int* dtf_tickets(int n) {
+  constexpr int RING = 1 << 16;
+  static std::mutex mu;
+  static int* base[64] = {};
+  static int next[64] = {};
+  if (n <= 0 || n > RING / 4) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!base[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(nullptr, &cs);
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
+    int* p = nullptr;
+    if (hipMalloc(&p, sizeof(int) * RING) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, sizeof(int) * RING) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+    base[dev] = p;
+  }
+  if (next[dev] + n > RING) next[dev] = 0;
+  int* r = base[dev] + next[dev];
+  next[dev] += n;
+  return r;
+}
+
 // Two-level deterministic reduction of `nrows` rows into out (or into row 0 if out == nullptr).
 // Returns nothing; stream-ordered.
 DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream) {

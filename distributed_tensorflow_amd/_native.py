@@ -43,6 +43,7 @@ _KERNEL_SIGS = {
     "dtf_cast_bf16_f32": [P, P, L, P],
     "dtf_nchw_to_nhwc_pad": [P, P, I, I, I, I, P],
     "dtf_filter_to_crsk": [P, P, I, I, I, P],
+    "dtf_filters_to_crsk": [P, I, I, P],
     "dtf_add_bf16": [P, P, P, L, F, F, P],
     "dtf_act": [P, P, P, L, I, I, P],
     "dtf_dropout": [P, P, L, F, U, P],

@@ -104,18 +104,57 @@ def weights_epoch():
     return _WeightsEpoch.value
 
 
+_CRSK = []        # weakrefs of the filters that own a CRSK copy
+_CRSK_TABLES = {}  # (device, filter set) -> device descriptor table for the batched transform
+
+
+def _crsk_key(p):
+    return (weights_epoch(), p._version)
+
+
 def crsk_shadow(param, K, RS, C):
-    """bf16 [C][R][S][K] copy of a KRSC filter for the dgrad implicit GEMM."""
-    key = (weights_epoch(), param._version)
+    """bf16 [C][R][S][K] copy of a KRSC filter for the dgrad implicit GEMM.
+
+    The copies go stale together (every optimizer step updates every filter), so a miss refreshes ALL stale
+    registered filters of the device in one batched launch (dtf_filters_to_crsk: LDS-tiled transposes) rather
+    than one launch per conv in the backward pass."""
+    import weakref
     s = getattr(param, "_dtf_crsk", None)
-    if s is not None and getattr(param, "_dtf_crsk_key", None) == key:
+    if s is not None and getattr(param, "_dtf_crsk_key", None) == _crsk_key(param):
         return s
-    w16 = bf16_shadow(param)
     if s is None:
         s = torch.empty((C, RS, K), dtype=BF16, device=param.device)
         param._dtf_crsk = s
-    call("dtf_filter_to_crsk", ptr(w16), ptr(s), K, RS, C, stream())
-    param._dtf_crsk_key = key
+        param._dtf_crsk_geom = (K, RS, C)
+        _CRSK.append(weakref.ref(param))
+    live = []
+    for r in list(_CRSK):
+        p = r()
+        if p is None:
+            _CRSK.remove(r)
+            continue
+        if p.device == param.device and getattr(p, "_dtf_crsk_key", None) != _crsk_key(p):
+            live.append(p)
+    if not any(p is param for p in live):
+        live.append(param)
+    if len(live) == 1:
+        call("dtf_filter_to_crsk", ptr(bf16_shadow(param)), ptr(s), K, RS, C, stream())
+    else:
+        rows, tiles = [], 0
+        for p in live:
+            k, rs, c = p._dtf_crsk_geom
+            rows.append((ptr(bf16_shadow(p)), ptr(p._dtf_crsk), k, rs, c, tiles))
+            tiles += rs * ((k + 63) // 64) * ((c + 63) // 64)
+        tkey = (param.device.index, tuple(rows))
+        table = _CRSK_TABLES.get(tkey)
+        if table is None:
+            if len(_CRSK_TABLES) > 64:
+                _CRSK_TABLES.clear()
+            table = torch.tensor(rows, dtype=torch.int64).to(param.device)
+            _CRSK_TABLES[tkey] = table
+        call("dtf_filters_to_crsk", ptr(table), len(rows), tiles, stream())
+    for p in live:
+        p._dtf_crsk_key = _crsk_key(p)
     return s
 
 

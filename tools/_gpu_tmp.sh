@@ -1,7 +1,9 @@
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "conv" > gpurun_out/t_conv.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/t_conv.log; exit 1; }
-tail -n 2 gpurun_out/t_conv.log
-timeout -k 10 400 python tools/conv_roofline.py --only wgrad --tiles > gpurun_out/rf_wg1.log 2>&1
-DTF_WGRAD_ROWMAP=0 timeout -k 10 300 python tools/conv_roofline.py --only wgrad > gpurun_out/rf_wg0.log 2>&1
-tail -n 1 gpurun_out/rf_wg0.log gpurun_out/rf_wg1.log
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/ -m gpu > gpurun_out/t_all.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/t_all.log; exit 1; }
+tail -n 2 gpurun_out/t_all.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || { echo BENCHFAIL; tail -20 gpurun_out/bench.log; exit 1; }
+tail -n 1 gpurun_out/bench.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 3 --warmup 2 > $R/gpurun_out/prof.log 2>&1 || { echo PROFFAIL; tail -5 $R/gpurun_out/prof.log; exit 1; }
+head -25 $R/gpurun_out/prof/run_kernel_stats.csv | cut -c1-150
