@@ -87,20 +87,26 @@ namespace dtf {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int AM, int BMODE>
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int NBUF = 2>
 static void launch_t(GemmArgs& a, hipStream_t st) {
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE>), grid, dim3(NT), 0, st, a);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE, 0, NBUF>), grid, dim3(NT), 0, st, a);
 }
 
 template <int AM, int BMODE>
 static void launch_modes(GemmArgs& a, int tile, hipStream_t st) {
   switch (tile) {
-    case 0: launch_t<128, 128, 2, 2, AM, BMODE>(a, st); break;
+    // 128-row tiles use ONE LDS buffer: the register-staged prefetch already overlaps the next tile's loads
+    // with the MFMAs, and half the LDS per block doubles the blocks (and bytes in flight) per CU — faster
+    // on every ResNet-50 conv measured (tools/conv_roofline.py --tiles; tiles 5/6 = the double-buffered forms)
+    case 0: launch_t<128, 128, 2, 2, AM, BMODE, 1>(a, st); break;
     case 1: launch_t<256, 64, 4, 1, AM, BMODE>(a, st); break;
-    case 2: launch_t<128, 64, 2, 2, AM, BMODE>(a, st); break;
+    case 2: launch_t<128, 64, 2, 2, AM, BMODE, 1>(a, st); break;
+    case 4: launch_t<64, 256, 1, 4, AM, BMODE>(a, st); break;
+    case 5: launch_t<128, 64, 2, 2, AM, BMODE, 2>(a, st); break;
+    case 6: launch_t<128, 128, 2, 2, AM, BMODE, 2>(a, st); break;
     default: launch_t<64, 64, 2, 2, AM, BMODE>(a, st); break;
   }
 }
@@ -109,19 +115,15 @@ static void launch_modes(GemmArgs& a, int tile, hipStream_t st) {
 // 256 CUs (2 blocks/CU at ~64 KB LDS each); narrow N -> 256x64.
 static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
   auto blocks = [&](int bm, int bn) { return (long)cdiv(M, bm) * cdiv(N, bn) * batch_splits; };
-  // short K (one to eight k-tiles, e.g. the early 1x1 convolutions): latency/epilogue-bound, the smaller
-  // 128x64 tile keeps more blocks in flight per CU (measured 5-20 % faster than 128x128 there)
-  if (N > 64 && K <= 512 && blocks(128, 64) >= 1024) return 2;
-  // long K amortises the larger tile's epilogue: one round of 128x128 tiles beats two of 128x64
-  if (N > 64 && K >= 1024 && blocks(128, 128) >= 256) return 0;
   if (N <= 64) {
-    // narrow N: 128x64 beats 256x64 at every ResNet-50 shape measured (tools/conv_roofline.py --tiles)
     if (blocks(128, 64) >= 512) return 2;
     if (blocks(256, 64) >= 512) return 1;
     if (blocks(128, 64) >= 256) return 2;
     return 3;
   }
-  if (blocks(128, 128) >= 512) return 0;
+  // short K (the memory-bound 1x1 convolutions): 128x64 keeps the most blocks in flight per CU
+  if (K <= 256 && blocks(128, 64) >= 1024) return 2;
+  if (blocks(128, 128) >= 256) return 0;
   if (blocks(128, 64) >= 256) return 2;
   return 3;
 }
@@ -404,8 +406,8 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   a.kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   if (tile < 0) {  // measured on ResNet-50's filters (tools/conv_roofline.py --only wgrad --tiles)
-    if (a.M <= 64) tile = 3;                       // Kout = 64: no half-empty 128-row tiles
-    else if (R * S > 1 && a.M >= 256) tile = 2;    // spatial filters, wide Kout: 128x64
+    if (a.M <= 64) tile = pointwise && a.N >= 256 ? 4 : 3;  // Kout = 64: no half-empty 128-row tiles
+    else if (R * S > 1) tile = 0;                  // spatial filters: 128x128
   }
   // spatial filters: row-mapped pixel-gather loaders (one pixel decode per thread per K-tile)
   const bool rowmap = !pointwise && rowmap_ok() && (long)N * H * W * C * 2 < (1l << 31) &&

@@ -479,12 +479,15 @@ __device__ __forceinline__ long frag_fp8(const char* lds, int rb, int kk, int la
   return *reinterpret_cast<const long*>(lds + row * 128 + pc * 16 + (G & 1) * 8);
 }
 
-template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0>
+// NBUF = 2: double-buffered LDS K-tiles (one barrier per K-tile). NBUF = 1: one LDS buffer (a second barrier
+// before each restage) — half the LDS per block, so short-K, memory-bound GEMMs (1x1 convolutions with
+// K <= 256) keep twice as many blocks, and bytes, in flight per CU.
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int NBUF = 2>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * (A_BYTES + B_BYTES)];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -529,8 +532,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const int nk = (kend - kbeg + BK - 1) / BK;
   char* sA0 = smem;
   char* sB0 = smem + A_BYTES;
-  char* sA1 = smem + A_BYTES + B_BYTES;
-  char* sB1 = sA1 + A_BYTES;
+  char* sA1 = NBUF == 2 ? smem + A_BYTES + B_BYTES : sA0;
+  char* sB1 = NBUF == 2 ? sA1 + A_BYTES : sB0;
 
   if (nk > 0) {
     la.load(a, kbeg, kend);
@@ -579,6 +582,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
     if (more) {
+      if constexpr (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
       la.store((kt & 1) ? sA0 : sA1);
       lb.store((kt & 1) ? sB0 : sB1);
     }
@@ -594,6 +598,69 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) csum[j][r] = csq[j][r] = 0.f;
 
+  // bf16 outputs without beta/atomics: the tile goes through LDS so that the global stores are whole
+  // 16-B chunks of contiguous row segments (a lane's MFMA fragment covers 4 columns x 1 row, i.e. 8-B
+  // pieces of 16 different rows per store instruction). The main loop ended on a barrier: LDS is free.
+  constexpr int CS = BN + 8;  // LDS row stride (elements): 16-B pad keeps the fragment writes conflict-free
+  constexpr bool can_stage = BM * CS * 2 <= NBUF * (A_BYTES + B_BYTES);  // the C tile fits the LDS buffers
+  const bool staged = can_stage && !a.atomic_out && !a.out_f32 && a.beta == 0.f && !(a.N & 7) &&
+                      !(a.ldc & 7) && !(reinterpret_cast<uintptr_t>(a.C) & 15);
+  if (staged) {
+    bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WTM + i * 16 + (lane & 15);
+      const int m = m0 + ml;
+      const bool mv = m < a.M;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4;
+        const int n = n0 + nl;
+        const bool nv = n < a.N;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
+        if (a.bias && nv) {
+          float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        if (a.aux && mv && nv) {
+          uint2 o;
+          o.x = pack2bf(v[0], v[1]);
+          o.y = pack2bf(v[2], v[3]);
+          *reinterpret_cast<uint2*>(a.aux + cbase + out_row(a, m) * a.ldc + n) = o;
+        }
+        if (a.act == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        } else if (a.act == 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+        }
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(ct + ml * CS + nl) = o;
+        if (a.stats && mv && nv) {  // statistics of the stored (bf16-rounded) values
+          v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);
+          v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { csum[j][r] += v[r]; csq[j][r] += v[r] * v[r]; }
+        }
+      }
+    }
+    __syncthreads();
+    constexpr int C8 = BN / 8;
+#pragma unroll 4
+    for (int c = threadIdx.x; c < BM * C8; c += NT) {
+      const int ml = c / C8, c8 = c - ml * C8;
+      const int m = m0 + ml, n = n0 + c8 * 8;
+      if (m >= a.M || n >= a.N) continue;
+      const uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8 * 8);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C) + cbase + out_row(a, m) * a.ldc + n) = val;
+    }
+    if (a.stats) __syncthreads();  // the statistics reduction below reuses the LDS
+  } else
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * WTM + i * 16 + (lane & 15);

@@ -4,6 +4,9 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -n 2 gpurun_out/t_all.log
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || { echo BENCHFAIL; tail -20 gpurun_out/bench.log; exit 1; }
 tail -n 1 gpurun_out/bench.log
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 3 --warmup 2 > $R/gpurun_out/prof.log 2>&1 || { echo PROFFAIL; tail -5 $R/gpurun_out/prof.log; exit 1; }
-head -25 $R/gpurun_out/prof/run_kernel_stats.csv | cut -c1-150
+timeout -k 10 300 python bench.py --model bert_base --steps 10 --warmup 3 > gpurun_out/bench_bert.log 2>&1 || { echo BERTFAIL; tail -20 gpurun_out/bench_bert.log; exit 1; }
+tail -n 1 gpurun_out/bench_bert.log
+timeout -k 10 300 python bench.py --model gpt2_medium_fp8 --steps 10 --warmup 3 > gpurun_out/bench_gpt2.log 2>&1 || { echo GPTFAIL; tail -20 gpurun_out/bench_gpt2.log; exit 1; }
+tail -n 1 gpurun_out/bench_gpt2.log
+timeout -k 10 300 python tools/conv_roofline.py > gpurun_out/rf_all.log 2>&1
+tail -n 4 gpurun_out/rf_all.log

@@ -104,7 +104,7 @@ def main():
                     f"({'mem' if byts / 5e12 > fl / 1.3e15 else 'mfma'}) x{t / floor:4.1f}")
             best = t
             if args.tiles:
-                for tile in range(0, 4):
+                for tile in range(0, 7):
                     try:
                         tt = timeit(mk(tile))
                     except Exception:  # noqa: BLE001 - tile not instantiated for this mode
