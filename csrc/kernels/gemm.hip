@@ -315,11 +315,26 @@ __global__ void tap_gather_kernel(const bf16_t* __restrict__ src, bf16_t* __rest
 // parity: every phase is a stride-1 dgrad over its own pixel sub-grid using only the taps that reach it
 // (compact filter gathered into ws), stored through the epilogue's row remap. This removes the
 // (1 - 1/(sh*sw)) of MFMA work a direct strided gather would spend on structural zeros.
+//
+// Optional fused BatchNorm-backward statistics of dX (bnx != nullptr; dX is the gradient of a BN(+ReLU) output
+// whose BN input is bnx [N,H,W,C] with 1-bit ReLU mask bnmask and batch mean bnmean): partial rows
+// [rows][2C] of sum(dz), sum(dz*(x-mean)) go to bnpart (capacity ceil(N*H*W/64) + sh*sw rows: a strided dgrad
+// writes one set per phase launch); *bnrows = rows.
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
-                           float beta, int tile, void* ws, long ws_bf16, void* stream) {
+                           float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
+                           const float* bnmean, float* bnpart, int* bnrows, void* stream) {
   if ((C & 3) || (K & 7)) return -1;
+  if (bnx && (out_f32 || (C & 7) || !bnpart || !bnmean || !bnrows)) return -9;
   hipStream_t st = (hipStream_t)stream;
+  int prow = 0;  // BN partial rows written so far (strided dgrad: one set per phase)
+  auto bn_args = [&](GemmArgs& a) {
+    if (!bnx) return;
+    a.stats = bnpart + (long)prow * 2 * C;
+    a.bnx = (const bf16_t*)bnx;
+    a.bnmask = (const uint8_t*)bnmask;
+    a.bnmean = bnmean;
+  };
   const bool phased = (sh > 1 || sw > 1) && dh == 1 && dw == 1 && ws != nullptr &&
                       ws_bf16 >= (long)C * R * S * K && !(C & 7);
   if (!phased) {
@@ -331,10 +346,12 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
     a.lda = K; a.ldb = (long)R * S * K; a.ldc = C;
     a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
     a.alpha = 1.f; a.beta = beta; a.act = 0; a.out_f32 = out_f32;
+    bn_args(a);
     bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
     dispatch(a, am, OP_KCONTIG, tile, st);
+    if (bnrows) *bnrows = bnx ? a.tiles_m : 0;
     return (int)hipGetLastError();
   }
   // phases without taps produce zeros: clear dX once unless accumulating
@@ -372,13 +389,16 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
       a.crm = 1;
       a.dRm1 = make_fastdiv((uint32_t)(Hs * Ws)); a.dRm2 = make_fastdiv((uint32_t)Ws);
       a.rmH = H; a.rmW = W; a.rmsh = sh; a.rmsw = sw; a.rmh0 = h0; a.rmw0 = w0;
+      bn_args(a);
       // a 1x1 tap set reading dY pixel-for-pixel is a plain GEMM over dY rows
       const bool pointwise = nkh == 1 && nkw == 1 && ch == 0 && cw == 0 && Hs == P && Ws == Q;
       const int am = pointwise ? OP_KCONTIG
                      : tap_uniform(K, nkh * nkw, (long)N * P * Q * K) ? OP_DGRAD_T : OP_DGRAD;
       dispatch(a, am, OP_KCONTIG, tile, st);
+      prow += a.tiles_m;
     }
   }
+  if (bnrows) *bnrows = bnx ? prow : 0;
   return (int)hipGetLastError();
 }
 

@@ -82,6 +82,12 @@ struct GemmArgs {
   // optional output-row remap (strided dgrad phases): row m = (n, hh, ww) over an rmHs x rmWs grid is stored
   // at pixel (n, rmsh*hh + rmh0, rmsw*ww + rmw0) of an rmH x rmW image
   uint64_t g_rowrep;    // tap-uniform gathers: sum over kh < R of 2^(kh*S)
+  // BatchNorm-backward statistics instead of forward ones (stats != nullptr and bnx != nullptr): the output is
+  // the gradient dy of a BN(+ReLU) output; partial rows get sum(dz) and sum(dz * (x - mean)) with
+  // dz = dy * relu_mask, x = the BN input [pixels][N] saved by the forward (ldc == N), mask 1 bit/element.
+  const bf16_t* bnx;
+  const uint8_t* bnmask;
+  const float* bnmean;
   int crm;
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
@@ -97,6 +103,30 @@ __device__ __forceinline__ long out_row(const GemmArgs& a, int m) {
 
 constexpr int BK = 64;
 constexpr int NT = 256;
+
+// Per-column statistics of 4 stored output values (columns n..n+3 of output pixel row mrow): forward BN
+// (sum, sum of squares) or, with a.bnx, backward BN (sum dz, sum dz*(x - mean)).
+__device__ __forceinline__ void stat_acc(const GemmArgs& a, long mrow, int n, const float (&v)[4], float (&cs)[4],
+                                         float (&cq)[4]) {
+  if (a.bnx) {
+    const long e = mrow * a.ldc + n;
+    const uint2 xr = *reinterpret_cast<const uint2*>(a.bnx + e);
+    const float x[4] = {__uint_as_float(xr.x << 16), __uint_as_float(xr.x & 0xffff0000u),
+                        __uint_as_float(xr.y << 16), __uint_as_float(xr.y & 0xffff0000u)};
+    const uint32_t bits = a.bnmask ? ((uint32_t)a.bnmask[e >> 3] >> (e & 4)) : 0xFu;  // e % 8 is 0 or 4
+    const float4 mu = *reinterpret_cast<const float4*>(a.bnmean + n);
+    const float m4[4] = {mu.x, mu.y, mu.z, mu.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float dz = ((bits >> r) & 1u) ? v[r] : 0.f;
+      cs[r] += dz;
+      cq[r] = fmaf(dz, x[r] - m4[r], cq[r]);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { cs[r] += v[r]; cq[r] = fmaf(v[r], v[r], cq[r]); }
+  }
+}
 
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -603,8 +633,14 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   // pieces of 16 different rows per store instruction). The main loop ended on a barrier: LDS is free.
   constexpr int CS = BN + 8;  // LDS row stride (elements): 16-B pad keeps the fragment writes conflict-free
   constexpr bool can_stage = BM * CS * 2 <= NBUF * (A_BYTES + B_BYTES);  // the C tile fits the LDS buffers
-  const bool staged = can_stage && !a.atomic_out && !a.out_f32 && a.beta == 0.f && !(a.N & 7) &&
-                      !(a.ldc & 7) && !(reinterpret_cast<uintptr_t>(a.C) & 15);
+  // beta != 0 (accumulate into C) is staged too when there is no bias/activation/aux: the bf16 product goes
+  // through LDS and the old C is added in the coalesced store pass (one extra bf16 rounding of the product).
+  const bool staged = can_stage && !a.atomic_out && !a.out_f32 && !(a.N & 7) && !(a.ldc & 7) &&
+                      !(reinterpret_cast<uintptr_t>(a.C) & 15) &&
+                      (a.beta == 0.f || (!a.bias && !a.act && !a.aux && (!a.stats || a.bnx)));
+  // BN-backward statistics are taken in the store pass from whole 16-B chunks (coalesced reads of the BN
+  // input and one mask byte per 8 channels) instead of per fragment
+  const bool bn_bwd = a.stats != nullptr && a.bnx != nullptr;
   if (staged) {
     bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
 #pragma unroll
@@ -641,25 +677,86 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
         o.x = pack2bf(v[0], v[1]);
         o.y = pack2bf(v[2], v[3]);
         *reinterpret_cast<uint2*>(ct + ml * CS + nl) = o;
-        if (a.stats && mv && nv) {  // statistics of the stored (bf16-rounded) values
+        if (a.stats && !bn_bwd && a.beta == 0.f && mv && nv) {  // statistics of the stored (bf16) values
           v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);
           v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) { csum[j][r] += v[r]; csq[j][r] += v[r] * v[r]; }
+          stat_acc(a, out_row(a, m), n, v, csum[j], csq[j]);
         }
       }
     }
     __syncthreads();
     constexpr int C8 = BN / 8;
+    static_assert(NT % C8 == 0, "a thread's channel chunk must stay fixed across the store pass");
+    const int c8t = threadIdx.x % C8;  // this thread's 8-channel chunk (constant over the pass)
+    float bs[8], bq[8], bmu[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bs[r] = bq[r] = bmu[r] = 0.f;
+    if (bn_bwd && n0 + c8t * 8 < a.N) {
+      const float4 m0v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8);
+      const float4 m1v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8 + 4);
+      bmu[0] = m0v.x; bmu[1] = m0v.y; bmu[2] = m0v.z; bmu[3] = m0v.w;
+      bmu[4] = m1v.x; bmu[5] = m1v.y; bmu[6] = m1v.z; bmu[7] = m1v.w;
+    }
 #pragma unroll 4
     for (int c = threadIdx.x; c < BM * C8; c += NT) {
-      const int ml = c / C8, c8 = c - ml * C8;
-      const int m = m0 + ml, n = n0 + c8 * 8;
+      const int ml = c / C8;
+      const int m = m0 + ml, n = n0 + c8t * 8;
       if (m >= a.M || n >= a.N) continue;
-      const uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8 * 8);
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(a.C) + cbase + out_row(a, m) * a.ldc + n) = val;
+      uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8t * 8);
+      const long e = out_row(a, m) * a.ldc + n;
+      bf16_t* cp = reinterpret_cast<bf16_t*>(a.C) + cbase + e;
+      if (a.beta != 0.f) {
+        const uint4 old = *reinterpret_cast<const uint4*>(cp);
+        float f[8], g[8];
+        const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, ow[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f[2 * q] = __uint_as_float(vw[q] << 16); f[2 * q + 1] = __uint_as_float(vw[q] & 0xffff0000u);
+          g[2 * q] = __uint_as_float(ow[q] << 16); g[2 * q + 1] = __uint_as_float(ow[q] & 0xffff0000u);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) f[r] = fmaf(a.beta, g[r], f[r]);
+        val.x = pack2bf(f[0], f[1]); val.y = pack2bf(f[2], f[3]);
+        val.z = pack2bf(f[4], f[5]); val.w = pack2bf(f[6], f[7]);
+      }
+      *reinterpret_cast<uint4*>(cp) = val;
+      if (bn_bwd) {
+        const uint4 xr = *reinterpret_cast<const uint4*>(a.bnx + e);
+        const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3] : 0xFFu;  // e % 8 == 0
+        const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int r = 2 * q + h;
+            const float dv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
+            const float xv = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
+            const float dz = ((bits >> r) & 1u) ? dv : 0.f;
+            bs[r] += dz;
+            bq[r] = fmaf(dz, xv - bmu[r], bq[r]);
+          }
+        }
+      }
     }
-    if (a.stats) __syncthreads();  // the statistics reduction below reuses the LDS
+    if (bn_bwd) {
+      // reduce the NT/C8 threads that share a channel chunk (fixed order: deterministic), one partial row
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) { red[threadIdx.x * 16 + r] = bs[r]; red[threadIdx.x * 16 + 8 + r] = bq[r]; }
+      __syncthreads();
+      float* prow = a.stats + (long)tile_m * 2 * a.N;
+      for (int nl = threadIdx.x; nl < BN; nl += NT) {
+        const int n = n0 + nl;
+        if (n >= a.N) continue;
+        float sv = 0.f, qv = 0.f;
+        for (int t = nl >> 3; t < NT; t += C8) { sv += red[t * 16 + (nl & 7)]; qv += red[t * 16 + 8 + (nl & 7)]; }
+        prow[n] = sv;
+        prow[a.N + n] = qv;
+      }
+    } else if (a.stats) {
+      __syncthreads();  // the statistics reduction below reuses the LDS
+    }
   } else
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -719,13 +816,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
           v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
         }
       }
-      if (a.stats) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { csum[j][r] += v[r]; csq[j][r] += v[r] * v[r]; }
-      }
+      if (a.stats) stat_acc(a, mrow, n, v, csum[j], csq[j]);
     }
   }
-  if (a.stats) {
+  if (a.stats && !(staged && bn_bwd)) {
     // Deterministic BN statistics: reduce the 16 rows of a lane group by shuffles, the WM wave rows of
     // the tile through LDS, then write ONE partial row per M-tile: stats[tile_m][0,N) = sum,
     // stats[tile_m][N,2N) = sum of squares (bn_finalize sums the tiles_m rows). No atomics.

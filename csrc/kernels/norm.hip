@@ -636,6 +636,10 @@ DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, 
   return (int)hipGetLastError();
 }
 
+static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
+                       const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
+                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st);
+
 // work: (2*1024 + 3) * C floats (partials + coefficients)
 // ReLU mask from mbits (1 bit/element, preferred) or from the bf16 output ymask; neither = no ReLU
 DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
@@ -649,6 +653,25 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
   int G = red_grid(M, C);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
                      (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part);
+  return bn_bwd_tail(dy, ymask, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, G,
+                     coef, st);
+}
+
+// Backward with the reduction already done by the GEMM that produced dy (dtf_conv_dgrad's fused BN-backward
+// statistics): `part` holds T partial rows [T][2C] (used as scratch); coef: 3*C floats.
+DTF_API int dtf_bn_bwd_partials(const void* dy, const void* mbits, const void* x, const float* mean,
+                                const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out,
+                                float* dgamma, float* dbeta, int accumulate, float* part, int T, float* coef,
+                                void* stream) {
+  if ((C & 7) || T < 1) return -1;
+  return bn_bwd_tail(dy, nullptr, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, T,
+                     coef, (hipStream_t)stream);
+}
+
+static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
+                       const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
+                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st) {
+  void* stream = (void*)st;
   long rs = 2L * C;
   int sg = 0;
   const int G2 = bn_groups(G, &sg);

@@ -53,15 +53,27 @@ def conv_fwd_raw(x, w16, g, stats=False, bias=None, act=0):
     return y
 
 
-def conv_dgrad_raw(dy, w_master, g, acc=None):
+def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None):
     """dX (bf16); with `acc` (a bf16 [N,H,W,C] gradient already holding another contribution) the epilogue
-    adds into it (beta = 1) and returns it."""
+    adds into it (beta = 1) and returns it. With `bn` (the _BNSource of the BatchNorm whose output this conv
+    consumed) the epilogue also produces that BatchNorm's backward reduction of the final dX values and
+    stores it on `bn` (see _BNSource)."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     wc = crsk_shadow(w_master, K, R * S, C)
     dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device) if acc is None else acc
     ws = workspace(dy.device)  # strided convs: per-phase compact filters (bf16) live here
+    part = rows = None
+    if bn is not None:
+        # one partial row per M-tile (>= 64 rows) of every launch: a strided dgrad runs sh*sw phase launches,
+        # each of which may end in a partial tile
+        part = torch.empty(((N * H * W + 63) // 64 + sh * sw) * 2 * C, dtype=F32, device=dy.device)
+        rows = IntOut()
     call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0,
-         0.0 if acc is None else 1.0, -1, ptr(ws), 2 * ws.numel(), stream())
+         0.0 if acc is None else 1.0, -1, ptr(ws), 2 * ws.numel(),
+         ptr(bn.yc) if bn is not None else None, ptr(bn.mbits) if bn is not None else None,
+         ptr(bn.mean) if bn is not None else None, ptr(part), rows.addr if rows else None, stream())
+    if bn is not None:
+        bn.provide(dx, part, rows.value)
     return dx
 
 
@@ -153,12 +165,48 @@ class ResidualGradLink:
         return buf
 
 
+class _BNSource:
+    """What the consumer of a training-mode ConvBN output needs to fuse that BatchNorm's backward reduction
+    into its own data-gradient GEMM: the BN input (conv output) yc, the 1-bit ReLU mask and the batch mean.
+
+    Attached to the ConvBN output tensor. A consuming ConvBN whose dgrad produces the COMPLETE gradient of
+    that output (its only consumer, or the residual-link "acc" conv that also adds the shortcut's parked
+    gradient) lets the GEMM epilogue write sum(dz), sum(dz*(x-mean)) partial rows; the producing ConvBN's
+    backward then skips its reduction pass (bn_bwd_reduce), provided the gradient it receives is exactly the
+    tensor that dgrad wrote (same storage: autograd added nothing else to it)."""
+    __slots__ = ("yc", "mbits", "mean", "consumers", "part", "rows", "dptr", "__weakref__")
+
+    def __init__(self, yc, mbits, mean):
+        self.yc, self.mbits, self.mean = yc, mbits, mean
+        self.consumers = 0
+        self.part = self.rows = self.dptr = None
+
+    def provide(self, dx, part, rows):
+        self.part, self.rows, self.dptr = part, rows, dx.data_ptr()
+
+    def take(self, dout):
+        """The partial rows for this gradient, or None (then the regular reduction runs)."""
+        part, rows, dptr = self.part, self.rows, self.dptr
+        self.part = self.rows = self.dptr = None
+        if part is None or rows < 1 or dout.data_ptr() != dptr or not dout.is_contiguous():
+            return None
+        return part, rows
+
+
+_FUSE_BN_BWD = __import__("os").environ.get("DTF_FUSE_BN_BWD", "1") != "0"
+
+
 class _ConvBNFn(torch.autograd.Function):
     """y = [relu]( BN_train(conv(x, w)) [+ residual] ) with batch statistics from the conv epilogue."""
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, res, rmean, rvar, stride, pad, dil, relu, momentum, eps, training,
                 link=None, role=None):
+        in_src = getattr(x, "_dtf_bnsrc", None)
+        if in_src is not None:
+            in_src.consumers += 1
+        if res is not None and getattr(res, "_dtf_bnsrc", None) is not None:
+            res._dtf_bnsrc.consumers += 1
         x = x.contiguous()
         g = _geom(x, w, stride, pad, dil)
         N, H, W, C, K, R, S, P, Q = g[:9]
@@ -188,6 +236,12 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.has_res = res is not None
         ctx.training = training
         ctx.link, ctx.role = link, role
+        ctx.in_src = in_src if (ctx.needs_input_grad[0] and _FUSE_BN_BWD) else None
+        ctx.src = None
+        if training and _FUSE_BN_BWD and any(ctx.needs_input_grad):
+            src = _BNSource(yc, mbits, mean)
+            out._dtf_bnsrc = src
+            ctx.src = src
         return out
 
     @staticmethod
@@ -204,9 +258,17 @@ class _ConvBNFn(torch.autograd.Function):
         direct_bn = tg is not None and tb is not None  # accumulate dgamma/dbeta into the arena grads
         dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
         dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
-        work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
-        call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K, ptr(dyc),
-             ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), stream())
+        fused = ctx.src.take(dout) if ctx.src is not None else None
+        if fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
+            coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+            call("dtf_bn_bwd_partials", ptr(dout), ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
+                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(fused[0]), fused[1], ptr(coef),
+                 stream())
+        else:
+            work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
+            call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
+                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), stream())
+        ctx.src = None
         if ctx.has_res and not ctx.relu:
             dres = dout
         link, role = ctx.link, ctx.role
@@ -215,7 +277,11 @@ class _ConvBNFn(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             acc = link.take() if (link is not None and role == "acc") else None
-            dx = conv_dgrad_raw(dyc, w, g, acc=acc)
+            src = ctx.in_src
+            complete = src is not None and role != "proj" and (
+                src.consumers == 1 or (role == "acc" and acc is not None and src.consumers == 2))
+            dx = conv_dgrad_raw(dyc, w, g, acc=acc, bn=src if complete else None)
+            ctx.in_src = None
             if link is not None and role == "proj":
                 dx = link.park(dx)
         if ctx.needs_input_grad[1]:

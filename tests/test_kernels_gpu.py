@@ -380,3 +380,38 @@ def test_conv_bn_direct_arena_grads(cuda):
         assert sorted(fired) == sorted(["w", "g", "b"] * 2)
         results.append(arena.grad.clone())
     close(results[1], results[0], 1e-5)
+
+
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 3, 3, 1, 1), (2, 16, 16, 64, 128, 3, 3, 2, 1),
+                                  (2, 12, 12, 256, 64, 1, 1, 1, 0), (4, 8, 8, 16, 32, 3, 3, 1, 1)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta):
+    """dtf_conv_dgrad's BN-backward epilogue: partial rows of sum(dz), sum(dz*(x-mean)) with dz = dX*mask."""
+    from distributed_tensorflow_amd.ops import conv as C
+    from distributed_tensorflow_amd.ops._util import IntOut, call, crsk_shadow, ptr, stream, workspace
+    N, H, W, Cin, K, R, S, st, pd = case
+    dy = rnd(N, (H + 2 * pd - R) // st + 1, (W + 2 * pd - S) // st + 1, K, dev=cuda)
+    w = torch.randn(K, R, S, Cin, device=cuda) / math.sqrt(R * S * Cin)
+    x = rnd(N, H, W, Cin, dev=cuda)
+    g = C._geom(x, w, (st, st), (pd, pd), (1, 1))
+    M = N * H * W
+    yc = rnd(N, H, W, Cin, dev=cuda)
+    mask = torch.rand(M * Cin, device=cuda) > 0.4
+    bits = (mask.view(-1, 8).to(torch.uint8) << torch.arange(8, device=cuda, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    mean = torch.randn(Cin, device=cuda) * 0.1
+    acc0 = rnd(N, H, W, Cin, dev=cuda)
+    dx = acc0.clone()
+    part = torch.empty(((M + 63) // 64 + st * st) * 2 * Cin, dtype=torch.float32, device=cuda)
+    rows = IntOut()
+    ws = workspace(cuda)
+    wc = crsk_shadow(w, K, R * S, Cin)
+    call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, Cin, K, R, S, g[7], g[8], st, st, pd, pd, 1, 1, 0,
+         beta, -1, ptr(ws), 2 * ws.numel(), ptr(yc), ptr(bits), ptr(mean), ptr(part), rows.addr, stream())
+    T = rows.value
+    assert T >= 1
+    p = part[:T * 2 * Cin].view(T, 2 * Cin).sum(0)
+    dz = dx.float().reshape(M, Cin) * mask.view(M, Cin).float()
+    s_ref = dz.sum(0)
+    q_ref = (dz * (yc.float().reshape(M, Cin) - mean)).sum(0)
+    close(p[:Cin], s_ref, 1e-3)
+    close(p[Cin:], q_ref, 1e-3)

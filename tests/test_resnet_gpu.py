@@ -84,3 +84,36 @@ def test_residual_grad_link_matches_reference(cuda, monkeypatch):
         worst_link = max(worst_link, (b - r).abs().max().item() / s)
     assert worst_plain < 0.03, worst_plain
     assert worst_link < 0.03, (worst_link, worst_plain)  # both at the bf16 rounding level (~1 ulp)
+
+
+@pytest.mark.gpu
+def test_fused_bn_backward_reduction_matches_separate_pass(cuda, monkeypatch):
+    """The BatchNorm backward reduction computed in the consumer conv's dgrad epilogue (ops.conv._BNSource)
+    equals the separate bn_bwd_reduce pass: same sums, different f32 summation order."""
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 16, 16, 64, generator=g).to(cuda).to(torch.bfloat16)
+    seen = []
+    real_call = OC.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return real_call(name, *args)
+
+    monkeypatch.setattr(OC, "call", spy)
+    runs = {}
+    for fuse in (False, True):
+        monkeypatch.setattr(OC, "_FUSE_BN_BWD", fuse)
+        seen.clear()
+        runs[fuse] = _run(_blocks(), x)
+        n_fused = seen.count("dtf_bn_bwd_partials")
+        if fuse:
+            # bn1 and bn2 of both blocks (via the c2/c3 dgrads) and block 0's output BN (via block 1's
+            # residual-link c1 dgrad)
+            assert n_fused == 5, seen
+        else:
+            assert n_fused == 0
+    worst = 0.0
+    for a, b in zip(runs[False], runs[True]):
+        s = a.abs().max().item() + 1e-6
+        worst = max(worst, (a - b).abs().max().item() / s)
+    assert worst < 0.02, worst
