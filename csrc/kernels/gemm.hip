@@ -87,12 +87,12 @@ namespace dtf {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int AM, int BMODE, int NBUF = 2>
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int PIPE = 2>
 static void launch_t(GemmArgs& a, hipStream_t st) {
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE, 0, NBUF>), grid, dim3(NT), 0, st, a);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE, 0, PIPE>), grid, dim3(NT), 0, st, a);
 }
 
 template <int AM, int BMODE>
@@ -107,6 +107,16 @@ static void launch_modes(GemmArgs& a, int tile, hipStream_t st) {
     case 4: launch_t<64, 256, 1, 4, AM, BMODE>(a, st); break;
     case 5: launch_t<128, 64, 2, 2, AM, BMODE, 2>(a, st); break;
     case 6: launch_t<128, 128, 2, 2, AM, BMODE, 2>(a, st); break;
+    case 7: case 8: case 9: case 10:  // LDS-DMA staging (K-contiguous operands only; callers check)
+      if constexpr (glds_mode(AM) && glds_mode(BMODE)) {
+        if (tile == 7) launch_t<128, 128, 2, 2, AM, BMODE, 3>(a, st);
+        else if (tile == 8) launch_t<128, 64, 2, 2, AM, BMODE, 3>(a, st);
+        else if (tile == 9) launch_t<128, 128, 2, 2, AM, BMODE, 4>(a, st);
+        else launch_t<128, 64, 2, 2, AM, BMODE, 4>(a, st);
+      } else {
+        launch_t<128, 128, 2, 2, AM, BMODE, 1>(a, st);
+      }
+      break;
     default: launch_t<64, 64, 2, 2, AM, BMODE>(a, st); break;
   }
 }
@@ -139,6 +149,24 @@ bool prefer256(long M, long N, long K, long batch) {
   const double e128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
   const double base = 1.12 + 0.12 * (double)std::min<long>(K, 4096) / 4096.0;
   return base * e256 > e128;
+}
+
+// LDS-DMA staged tiles for K-contiguous operands (both operand images filled by buffer_load ... lds):
+// 128x64 synchronous (occupancy hides the DMA) almost everywhere, 128x128 double-buffered when there are
+// few tiles and a long K (ResNet-50 stage 4). Measured per layer: tools/conv_roofline.py --tiles.
+static bool glds_on() {
+  static const bool on = [] {
+    const char* e = getenv("DTF_GLDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static int pick_glds_tile(const GemmArgs& a, int amode, int bmode) {
+  if (!glds_on() || !glds_mode(amode) || !glds_mode(bmode) || a.atomic_out) return -1;
+  if (amode == OP_KCONTIG && (long)a.M * a.lda * 2 >= (1l << 31)) return -1;
+  if (bmode == OP_KCONTIG && (long)a.N * a.ldb * 2 >= (1l << 31)) return -1;
+  const long blocks = (long)cdiv(a.M, 128) * cdiv(a.N, 64) * a.batch * a.splitk;
+  return (blocks <= 1600 && a.kchunk >= 1024) ? 9 : 8;
 }
 
 static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st) {
@@ -288,6 +316,7 @@ DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bi
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
+  if (tile < 0) tile = pick_glds_tile(a, am, OP_KCONTIG);
   dispatch(a, am, OP_KCONTIG, tile, (hipStream_t)stream);
   if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();
@@ -350,7 +379,7 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
     bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
-    dispatch(a, am, OP_KCONTIG, tile, st);
+    dispatch(a, am, OP_KCONTIG, tile < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : tile, st);
     if (bnrows) *bnrows = bnx ? a.tiles_m : 0;
     return (int)hipGetLastError();
   }
@@ -394,7 +423,7 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
       const bool pointwise = nkh == 1 && nkw == 1 && ch == 0 && cw == 0 && Hs == P && Ws == Q;
       const int am = pointwise ? OP_KCONTIG
                      : tap_uniform(K, nkh * nkw, (long)N * P * Q * K) ? OP_DGRAD_T : OP_DGRAD;
-      dispatch(a, am, OP_KCONTIG, tile, st);
+      dispatch(a, am, OP_KCONTIG, tile < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : tile, st);
       prow += a.tiles_m;
     }
   }

@@ -403,7 +403,7 @@ struct PixelRowLoader {
     one_tap = MODE == OP_WGRADX_R && (g.C % R == 0);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int col = r0 + ((t & 3) + 4 * i) * 8;
+      const int col = r0 + chunk(t, i) * 8;
       cv[i] = col < Rtot;
       if constexpr (MODE == OP_WGRADX_R) {
         uint32_t rs, ci, kh, kw;
@@ -459,11 +459,15 @@ struct PixelRowLoader {
     const int t = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = (t & 3) + 4 * i;
-      const int pc = c ^ (kouter_swz<R>(kr) << 1);
+      const int pc = chunk(t, i) ^ (kouter_swz<R>(kr) << 1);
       *reinterpret_cast<uint4*>(lds + kr * (R * 2) + pc * 16) = reg[i];
     }
   }
+
+  // Logical 16-B chunk written by thread t in store instruction i. Odd k-rows take their chunks in the
+  // other half-order (^4): a ds_write_b128 8-lane group spans two k-rows (4 lanes each), and this puts the
+  // two rows' 64-B pieces on different banks (the rows are 256 B apart, i.e. the same bank set).
+  __device__ __forceinline__ int chunk(int t, int i) const { return ((t & 3) + 4 * i) ^ ((kr & 1) << 2); }
 };
 
 // fragment read from a [64][R] tile via ds_read_b64_tr_b16: cols cb..cb+15, k-substep kk
@@ -483,11 +487,97 @@ __device__ __forceinline__ v8bf frag_kouter(const char* lds, int cb, int kk, int
   return __builtin_bit_cast(v8bf, both);
 }
 
+// K-contiguous operand staged straight into LDS (buffer_load_dwordx4 ... lds): no VGPR round trip, no
+// ds_write. A wave instruction fills 1 KiB = 8 rows x 128 B of the [R][64] image lane-linearly, so each lane
+// fetches the LOGICAL chunk that belongs at its physical slot (the XOR swizzle is undone on the source side).
+// Rows past the operand, k past Kend and (tap-uniform gathers) out-of-image taps get an out-of-range offset
+// and the range check writes zeros.
+template <int R, int MODE>
+struct GldsLoader {
+  static_assert(MODE == OP_KCONTIG || MODE == OP_IM2COL_T || MODE == OP_DGRAD_T, "K-contiguous modes only");
+  static constexpr int L = R / 32;  // wave instructions per thread per K-tile
+  __amdgpu_buffer_rsrc_t rsrc;
+  int roff[L];        // byte offset of the row (KCONTIG) / of the row's tap-(0,0) pixel (gathers)
+  uint32_t tmask[L];  // KCONTIG: ~0 for valid rows; gathers: in-image tap mask
+  int coff[L];        // byte offset of this lane's logical chunk in the 64-wide K-tile
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot) {
+    const int t = threadIdx.x;
+    const ConvGeom& g = a.g;
+    uint32_t bytes;
+    if constexpr (MODE == OP_KCONTIG) bytes = (uint32_t)((long)Rtot * ld * 2);  // host: < 2 GiB
+    else if constexpr (MODE == OP_IM2COL_T) bytes = (uint32_t)((long)g.N * g.H * g.W * g.C * 2);
+    else bytes = (uint32_t)((long)g.N * g.P * g.Q * g.Kout * 2);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int row = 32 * i + (t >> 3);
+      coff[i] = ((t & 7) ^ ((row >> 1) & 7)) * 16;
+      const int r = r0 + row;
+      uint32_t m = 0;
+      int off = 0;
+      if (r < Rtot) {
+        if constexpr (MODE == OP_KCONTIG) {
+          m = ~0u;
+          off = (int)((long)r * ld * 2);
+        } else {
+          uint32_t n, rem, y, x;
+          if constexpr (MODE == OP_IM2COL_T) {
+            fdivmod((uint32_t)r, g.dPQ, n, rem);
+            fdivmod(rem, g.dQ, y, x);
+            const int hb = (int)y * g.sh - g.ph, wb = (int)x * g.sw - g.pw;
+            off = (((int)n * g.H + hb) * g.W + wb) * g.C * 2;
+            m = tap_mask(g.R, g.S, max(0, -hb), min(g.R - 1, g.H - 1 - hb), max(0, -wb), min(g.S - 1, g.W - 1 - wb),
+                         a.g_rowrep);
+          } else {
+            fdivmod((uint32_t)r, g.dHW, n, rem);
+            fdivmod(rem, g.dW, y, x);
+            const int hb = (int)y + g.ph, wb = (int)x + g.pw;
+            off = (((int)n * g.P + hb) * g.Q + wb) * g.Kout * 2;
+            m = tap_mask(g.R, g.S, max(0, hb - g.P + 1), min(g.R - 1, hb), max(0, wb - g.Q + 1), min(g.S - 1, wb),
+                         a.g_rowrep);
+          }
+        }
+      }
+      roff[i] = off;
+      tmask[i] = m;
+    }
+  }
+
+  __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int Kend, char* lds) {
+    const int wave = threadIdx.x >> 6;
+    int toff;
+    uint32_t tap = 0;
+    if constexpr (MODE == OP_KCONTIG) {
+      toff = k0 * 2;
+    } else {
+      const ConvGeom& g = a.g;
+      uint32_t c0, kh, kw;
+      fdivmod((uint32_t)k0, MODE == OP_IM2COL_T ? g.dC : g.dK, tap, c0);
+      fdivmod(tap, g.dS, kh, kw);
+      toff = MODE == OP_IM2COL_T ? (((int)kh * g.dh * g.W + (int)kw * g.dw) * g.C + (int)c0) * 2
+                                 : ((int)c0 - ((int)kh * g.dh * g.Q + (int)kw * g.dw) * g.Kout) * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      bool ok;
+      if constexpr (MODE == OP_KCONTIG) ok = tmask[i] != 0u && k0 + (coff[i] >> 1) < Kend;
+      else ok = (tmask[i] >> tap) & 1u;
+      const uint32_t off = ok ? (uint32_t)(roff[i] + toff + coff[i]) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 +
+                                                                                              wave * 1024),
+                                               16, off, 0, 0, 0);
+    }
+  }
+};
+
 template <int R, int MODE>
 using LoaderFor = typename std::conditional<
     (MODE == OP_KOUTER_R || MODE == OP_WGRADX_R), PixelRowLoader<R, MODE>,
     typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE>,
                               KContigLoader<R, MODE>>::type>::type;
+
+constexpr bool glds_mode(int m) { return m == OP_KCONTIG || m == OP_IM2COL_T || m == OP_DGRAD_T; }
 
 constexpr bool kouter_mode(int m) {
   return m == OP_KOUTER || m == OP_WGRADX || m == OP_KOUTER_R || m == OP_WGRADX_R;
@@ -509,11 +599,16 @@ __device__ __forceinline__ long frag_fp8(const char* lds, int rb, int kk, int la
   return *reinterpret_cast<const long*>(lds + row * 128 + pc * 16 + (G & 1) * 8);
 }
 
-// NBUF = 2: double-buffered LDS K-tiles (one barrier per K-tile). NBUF = 1: one LDS buffer (a second barrier
-// before each restage) — half the LDS per block, so short-K, memory-bound GEMMs (1x1 convolutions with
-// K <= 256) keep twice as many blocks, and bytes, in flight per CU.
-template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int NBUF = 2>
+// Staging pipeline (PIPE):
+//  1: register-staged, ONE LDS buffer (a second barrier before each restage) — half the LDS per block, so
+//     twice the blocks (and bytes in flight) per CU; the default for 128-row tiles.
+//  2: register-staged, double-buffered LDS (one barrier per K-tile).
+//  3: LDS-DMA (GldsLoader), one buffer, synchronous per K-tile: no staging VGPRs, occupancy hides latency.
+//  4: LDS-DMA, double-buffered: the next K-tile's DMA runs under this tile's MFMAs.
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int PIPE = 2>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
+  constexpr int NBUF = (PIPE == 2 || PIPE == 4) ? 2 : 1;
+  constexpr bool GLDS = PIPE >= 3;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -548,8 +643,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const bf16_t* Ap = a.A + (long)bz * a.sA;
   const bf16_t* Bp = a.B + (long)bz * a.sB;
 
-  LoaderFor<BM, AM> la;
-  LoaderFor<BN, BMODE> lb;
+  typename std::conditional<GLDS, GldsLoader<BM, AM>, LoaderFor<BM, AM>>::type la;
+  typename std::conditional<GLDS, GldsLoader<BN, BMODE>, LoaderFor<BN, BMODE>>::type lb;
   la.init(a, Ap, a.lda, m0, a.M);
   lb.init(a, Bp, a.ldb, n0, a.N);
 
@@ -565,22 +660,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   char* sA1 = NBUF == 2 ? smem + A_BYTES + B_BYTES : sA0;
   char* sB1 = NBUF == 2 ? sA1 + A_BYTES : sB0;
 
-  if (nk > 0) {
-    la.load(a, kbeg, kend);
-    lb.load(a, kbeg, kend);
-    la.store(sA0);
-    lb.store(sB0);
-  }
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      la.load(a, kbeg + (kt + 1) * BK, kend);
-      lb.load(a, kbeg + (kt + 1) * BK, kend);
-    }
-    const char* cA = (kt & 1) ? sA1 : sA0;
-    const char* cB = (kt & 1) ? sB1 : sB0;
+  auto compute = [&](const char* cA, const char* cB) {
     if constexpr (FP8) {
       // 128 fp8 of K per tile: four 16x16x32 fp8 MFMA k-substeps (same rate as bf16 per MFMA,
       // half the staged bytes per FLOP)
@@ -611,12 +691,58 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      if constexpr (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
-      la.store((kt & 1) ? sA0 : sA1);
-      lb.store((kt & 1) ? sB0 : sB1);
+  };
+
+  if constexpr (GLDS) {
+    // (the loaders issue only LDS-DMA loads: no ordinary global load is waited for inside the loop)
+    if constexpr (NBUF == 2) {
+      if (nk > 0) {
+        la.issue(a, kbeg, kend, sA0);
+        lb.issue(a, kbeg, kend, sB0);
+      }
+      for (int kt = 0; kt < nk; ++kt) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // tile kt landed for every wave; every wave is done reading tile kt-1's buffer
+        if (kt + 1 < nk) {
+          la.issue(a, kbeg + (kt + 1) * BK, kend, (kt & 1) ? sA0 : sA1);
+          lb.issue(a, kbeg + (kt + 1) * BK, kend, (kt & 1) ? sB0 : sB1);
+        }
+        compute((kt & 1) ? sA1 : sA0, (kt & 1) ? sB1 : sB0);
+      }
+    } else {
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt) __syncthreads();  // every wave is done reading the single buffer
+        la.issue(a, kbeg + kt * BK, kend, sA0);
+        lb.issue(a, kbeg + kt * BK, kend, sB0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        compute(sA0, sB0);
+      }
+    }
+    __syncthreads();  // the epilogue may reuse the LDS
+  } else {
+    if (nk > 0) {
+      la.load(a, kbeg, kend);
+      lb.load(a, kbeg, kend);
+      la.store(sA0);
+      lb.store(sB0);
     }
     __syncthreads();
+
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        la.load(a, kbeg + (kt + 1) * BK, kend);
+        lb.load(a, kbeg + (kt + 1) * BK, kend);
+      }
+      compute((kt & 1) ? sA1 : sA0, (kt & 1) ? sB1 : sB0);
+      if (more) {
+        if constexpr (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
+        la.store((kt & 1) ? sA0 : sA1);
+        lb.store((kt & 1) ? sB0 : sB1);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: lane owns row m = ..+(lane&15), cols n = ..+(lane>>4)*4 + r ----

@@ -415,3 +415,41 @@ def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta):
     q_ref = (dz * (yc.float().reshape(M, Cin) - mean)).sum(0)
     close(p[:Cin], s_ref, 1e-3)
     close(p[Cin:], q_ref, 1e-3)
+
+
+@pytest.mark.parametrize("tile", [0, 2, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 9, 128, 64, 1, 1, 1, 0),
+                                  (2, 15, 15, 64, 64, 3, 3, 2, 1)])
+def test_conv_staging_pipelines_agree(cuda, case, tile):
+    """Every staging pipeline (register-staged single/double LDS buffer, LDS-DMA single/double buffer) and
+    tile shape computes bitwise the same conv forward and data gradient (same per-element K order)."""
+    from distributed_tensorflow_amd.ops import conv as C
+    from distributed_tensorflow_amd.ops._util import call, crsk_shadow, ptr, stream, workspace
+    N, H, W, Cin, K, R, S, st, pd = case
+    x = rnd(N, H, W, Cin, dev=cuda)
+    w = torch.randn(K, R, S, Cin, device=cuda) / math.sqrt(R * S * Cin)
+    g = C._geom(x, w, (st, st), (pd, pd), (1, 1))
+    P, Q = g[7], g[8]
+    w16 = w.to(BF)
+
+    def fwd(t):
+        y = torch.empty(N, P, Q, K, dtype=BF, device=cuda)
+        call("dtf_conv_fwd", ptr(x), ptr(w16), ptr(y), None, None, None, N, H, W, Cin, K, R, S, P, Q, st, st, pd, pd,
+             1, 1, 0, 0, t, stream())
+        return y
+
+    dy = rnd(N, P, Q, K, dev=cuda)
+    wc = crsk_shadow(w, K, R * S, Cin)
+    ws = workspace(cuda)
+
+    def dgrad(t):
+        dx = torch.empty_like(x)
+        call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, Cin, K, R, S, P, Q, st, st, pd, pd, 1, 1, 0, 0.0, t,
+             ptr(ws), 2 * ws.numel(), None, None, None, None, None, stream())
+        return dx
+
+    assert torch.equal(fwd(tile), fwd(-1))
+    assert torch.equal(dgrad(tile), dgrad(-1))
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w16.float().permute(0, 3, 1, 2), stride=st,
+                                    padding=pd)
+    close(fwd(tile).permute(0, 3, 1, 2), yr, 1e-2)

@@ -20,6 +20,7 @@ from distributed_tensorflow_amd.ops._util import IntOut, call, ptr, stream, work
 
 BF = torch.bfloat16
 NB = 256
+TILES = None
 
 
 def layers():
@@ -59,7 +60,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", action="store_true", help="also time every forced tile shape")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--tile-list", default=None, help="comma-separated tiles for --tiles")
     args = ap.parse_args()
+    global TILES
+    TILES = [int(t) for t in args.tile_list.split(",")] if args.tile_list else None
     dev = torch.device("cuda")
     torch.manual_seed(0)
     tot = {"fwd": [0.0, 0.0, 0.0], "dgrad": [0.0, 0.0, 0.0], "wgrad": [0.0, 0.0, 0.0]}
@@ -88,7 +92,7 @@ def main():
 
         def dgrad(tile):
             return lambda: call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), NB, H, H, Cin, K, R, R, P, Q, s, s, p, p,
-                                1, 1, 0, 0.0, tile, ptr(ws), 2 * ws.numel(), stream())
+                                1, 1, 0, 0.0, tile, ptr(ws), 2 * ws.numel(), None, None, None, None, None, stream())
 
         def wgrad(tile):
             return lambda: call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dwacc), NB, H, H, Cin, K, R, R, P, Q, s, s, p,
@@ -104,7 +108,7 @@ def main():
                     f"({'mem' if byts / 5e12 > fl / 1.3e15 else 'mfma'}) x{t / floor:4.1f}")
             best = t
             if args.tiles:
-                for tile in range(0, 7):
+                for tile in (TILES or range(0, 11)):
                     try:
                         tt = timeit(mk(tile))
                     except Exception:  # noqa: BLE001 - tile not instantiated for this mode
