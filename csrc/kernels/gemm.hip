@@ -161,6 +161,20 @@ static bool glds_on() {
   }();
   return on;
 }
+static bool wgrad_glds_on() {
+  static const bool on = [] {
+    const char* e = getenv("DTF_GLDS_WGRAD");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static bool dense_glds_on() {
+  static const bool on = [] {
+    const char* e = getenv("DTF_GLDS_DENSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 static int pick_glds_tile(const GemmArgs& a, int amode, int bmode) {
   if (!glds_on() || !glds_mode(amode) || !glds_mode(bmode) || a.atomic_out) return -1;
   if (amode == OP_KCONTIG && (long)a.M * a.lda * 2 >= (1l << 31)) return -1;
@@ -295,7 +309,9 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
   if (tile < 0 && !stats && a.splitk == 1 && prefer256(M, N, K, a.batch) &&
       gemm256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream) == 0)
     return (int)hipGetLastError();
-  dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
+  const int am = a_kouter ? OP_KOUTER : OP_KCONTIG, bm = b_kouter ? OP_KOUTER : OP_KCONTIG;
+  if (tile < 0 && dense_glds_on() && a.batch == 1) tile = pick_glds_tile(a, am, bm);
+  dispatch(a, am, bm, tile, (hipStream_t)stream);
   if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();
 }
@@ -454,13 +470,17 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   a.splitk = splitk;
   a.kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  const bool small = (long)N * H * W * C * 2 < (1l << 31) && (long)N * P * Q * K * 2 < (1l << 31);
+  // spatial filters: LDS-DMA staged 128x128 (measured best for every ResNet-50 3x3 filter); 1x1 filters keep
+  // the register-staged kernels (tools/conv_roofline.py --only wgrad --tiles)
+  const bool use_glds = small && wgrad_glds_on() && (tile >= 7 || (tile < 0 && R * S > 1));
+  // row-mapped / LDS-DMA loaders: one pixel decode per lane per K-tile row (spatial filters), buffer loads
+  const bool rowmap = small && (use_glds || (!pointwise && rowmap_ok()));
+  if (tile < 0 && use_glds) tile = 7;
   if (tile < 0) {  // measured on ResNet-50's filters (tools/conv_roofline.py --only wgrad --tiles)
     if (a.M <= 64) tile = pointwise && a.N >= 256 ? 4 : 3;  // Kout = 64: no half-empty 128-row tiles
     else if (R * S > 1) tile = 0;                  // spatial filters: 128x128
   }
-  // spatial filters: row-mapped pixel-gather loaders (one pixel decode per thread per K-tile)
-  const bool rowmap = !pointwise && rowmap_ok() && (long)N * H * W * C * 2 < (1l << 31) &&
-                      (long)N * P * Q * K * 2 < (1l << 31);
   if (splitk == 1) {
     a.C = dW;
     a.beta = accumulate ? 1.f : 0.f;

@@ -571,13 +571,90 @@ struct GldsLoader {
   }
 };
 
+// K-outer operand ([64 k][R cols] image, read with ds_read_b64_tr_b16) staged by LDS-DMA: a wave instruction
+// fills 1 KiB = 1024/(2R) consecutive k-rows lane-linearly; each lane fetches the logical 16-B column chunk that
+// the XOR swizzle puts at its physical slot. OP_KOUTER_R: plain rows (dY of a weight gradient: row stride
+// = Kout); OP_WGRADX_R: the row is an output pixel whose input pixel is decoded per K-tile, the column a
+// (tap, channel) pair fixed per lane; out-of-image taps / rows past K read zeros via the range check.
+template <int R, int MODE>
+struct GldsKOuter {
+  static_assert(MODE == OP_KOUTER_R || MODE == OP_WGRADX_R, "conv weight-gradient operands only");
+  static constexpr int L = R / 32;
+  static constexpr int ROWB = R * 2;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int kr[L];        // k-row of the tile this lane fills in instruction i
+  int coff[L];      // byte offset of the lane's column chunk (+ tap shift for OP_WGRADX_R)
+  int hoff[L], woff[L];
+  bool cv[L];
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld, int r0, int Rtot) {
+    const int t = threadIdx.x;
+    const ConvGeom& g = a.g;
+    const uint32_t bytes = MODE == OP_WGRADX_R ? (uint32_t)((long)g.N * g.H * g.W * g.C * 2)
+                                               : (uint32_t)((long)g.N * g.P * g.Q * g.Kout * 2);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ptr, (short)0, (int)bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int P = i * 4096 + t * 16;
+      kr[i] = P / ROWB;
+      const int c = ((P % ROWB) >> 4) ^ (kouter_swz<R>(kr[i]) << 1);
+      const int col = r0 + c * 8;
+      cv[i] = col < Rtot;
+      if constexpr (MODE == OP_WGRADX_R) {
+        uint32_t rs, ci, kh, kw;
+        fdivmod((uint32_t)(cv[i] ? col : 0), g.dC, rs, ci);
+        fdivmod(rs, g.dS, kh, kw);
+        hoff[i] = (int)kh * g.dh - g.ph;
+        woff[i] = (int)kw * g.dw - g.pw;
+        coff[i] = ((hoff[i] * g.W + woff[i]) * g.C + (int)ci) * 2;
+      } else {
+        coff[i] = col * 2;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int Kend, char* lds) {
+    const ConvGeom& g = a.g;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int k = k0 + kr[i];
+      bool ok = cv[i] && k < Kend;
+      int off;
+      if constexpr (MODE == OP_WGRADX_R) {
+        if (g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0) {
+          off = k * g.C * 2 + coff[i];  // pointwise: output pixel == input pixel
+        } else {
+          uint32_t n, pq, pp, qq;
+          fdivmod((uint32_t)(ok ? k : 0), g.dPQ, n, pq);
+          fdivmod(pq, g.dQ, pp, qq);
+          const int hb = (int)pp * g.sh, wb = (int)qq * g.sw;
+          const int hi = hb + hoff[i], wi = wb + woff[i];
+          ok = ok && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+          off = (((int)n * g.H + hb) * g.W + wb) * g.C * 2 + coff[i];
+        }
+      } else {
+        off = k * g.Kout * 2 + coff[i];
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 + wave * 1024), 16,
+          ok ? (uint32_t)off : 0x80000000u, 0, 0, 0);
+    }
+  }
+};
+
 template <int R, int MODE>
 using LoaderFor = typename std::conditional<
     (MODE == OP_KOUTER_R || MODE == OP_WGRADX_R), PixelRowLoader<R, MODE>,
     typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE>,
                               KContigLoader<R, MODE>>::type>::type;
 
-constexpr bool glds_mode(int m) { return m == OP_KCONTIG || m == OP_IM2COL_T || m == OP_DGRAD_T; }
+constexpr bool glds_kcontig(int m) { return m == OP_KCONTIG || m == OP_IM2COL_T || m == OP_DGRAD_T; }
+constexpr bool glds_kouter(int m) { return m == OP_KOUTER_R || m == OP_WGRADX_R; }
+constexpr bool glds_mode(int m) { return glds_kcontig(m) || glds_kouter(m); }
+
+template <int R, int MODE>
+using GldsFor = typename std::conditional<glds_kouter(MODE), GldsKOuter<R, MODE>, GldsLoader<R, MODE>>::type;
 
 constexpr bool kouter_mode(int m) {
   return m == OP_KOUTER || m == OP_WGRADX || m == OP_KOUTER_R || m == OP_WGRADX_R;
@@ -643,8 +720,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const bf16_t* Ap = a.A + (long)bz * a.sA;
   const bf16_t* Bp = a.B + (long)bz * a.sB;
 
-  typename std::conditional<GLDS, GldsLoader<BM, AM>, LoaderFor<BM, AM>>::type la;
-  typename std::conditional<GLDS, GldsLoader<BN, BMODE>, LoaderFor<BN, BMODE>>::type lb;
+  typename std::conditional<GLDS, GldsFor<BM, AM>, LoaderFor<BM, AM>>::type la;
+  typename std::conditional<GLDS, GldsFor<BN, BMODE>, LoaderFor<BN, BMODE>>::type lb;
   la.init(a, Ap, a.lda, m0, a.M);
   lb.init(a, Bp, a.ldb, n0, a.N);
 

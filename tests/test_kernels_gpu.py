@@ -453,3 +453,32 @@ def test_conv_staging_pipelines_agree(cuda, case, tile):
     yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w16.float().permute(0, 3, 1, 2), stride=st,
                                     padding=pd)
     close(fwd(tile).permute(0, 3, 1, 2), yr, 1e-2)
+
+
+@pytest.mark.parametrize("tile", [7, 8, 9, 10])
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 9, 128, 64, 1, 1, 1, 0),
+                                  (2, 15, 15, 64, 64, 3, 3, 2, 1), (2, 12, 12, 64, 256, 1, 1, 2, 0)])
+def test_conv_wgrad_lds_dma_matches(cuda, case, tile, monkeypatch):
+    """Weight gradient with LDS-DMA staged K-outer operands (DTF_GLDS_WGRAD path, forced tiles) equals the
+    register-staged kernel bitwise (same K order) and the f32 reference."""
+    from distributed_tensorflow_amd.ops import conv as C
+    from distributed_tensorflow_amd.ops._util import call, ptr, stream, workspace
+    N, H, W, Cin, K, R, S, st, pd = case
+    x = rnd(N, H, W, Cin, dev=cuda)
+    g = C._geom(x, torch.empty(K, R, S, Cin), (st, st), (pd, pd), (1, 1))
+    P, Q = g[7], g[8]
+    dy = rnd(N, P, Q, K, dev=cuda)
+    ws = workspace(cuda)
+
+    def wgrad(t):
+        dw = torch.zeros(K, R, S, Cin, device=cuda)
+        call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw), N, H, W, Cin, K, R, S, P, Q, st, st, pd, pd, 1, 1, 0, 1, t,
+             ptr(ws), ws.numel(), stream())
+        return dw
+    got = wgrad(tile)
+    base = wgrad(0)
+    assert torch.equal(got, base)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = torch.zeros(K, Cin, R, S, device=cuda, requires_grad=True)
+    torch.nn.functional.conv2d(xr, wr, stride=st, padding=pd).backward(dy.float().permute(0, 3, 1, 2))
+    close(got.permute(0, 3, 1, 2), wr.grad, 1e-2)
