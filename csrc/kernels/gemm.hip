@@ -68,8 +68,18 @@ DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* ou
   const int gx = (int)((W + 255) / 256);
   long s = stride;
   int n = nrows;
+  if (gx < 64 && n > 32) {
+    // narrow rows (LayerNorm/bias partials: W of a few thousand): ONE grouping pass to <= 32 leader rows,
+    // then the final pass — two launches instead of a cascade of small ones
+    const int sg = (n + 31) / 32;
+    const int groups = (n + sg - 1) / sg;
+    hipLaunchKernelGGL(dtf_group_rows_kernel, dim3(gx, groups), dim3(256), 0, st, rows, s, n, sg, W,
+                       (float*)nullptr, 0);
+    s *= sg;
+    n = groups;
+  }
   // stage 1: enough groups to fill the chip, each summing sg rows into its leader row
-  while (n > 8 && gx < 2048) {
+  while (n > 8 && gx < 2048 && gx >= 64) {
     int groups = (int)std::min<long>(n, std::max<long>(1, 1024 / gx));
     int sg = std::max(8, (n + groups - 1) / groups);
     groups = (n + sg - 1) / sg;
@@ -169,9 +179,11 @@ static bool wgrad_glds_on() {
   return on;
 }
 static bool dense_glds_on() {
+  // opt-in: on BERT-base / GPT-2-medium the transformer GEMMs measured 1-3 % slower end to end with the
+  // LDS-DMA tiles than with the register-staged / 256x256 kernels (they mostly go to gemm256 anyway)
   static const bool on = [] {
     const char* e = getenv("DTF_GLDS_DENSE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -179,6 +191,8 @@ static int pick_glds_tile(const GemmArgs& a, int amode, int bmode) {
   if (!glds_on() || !glds_mode(amode) || !glds_mode(bmode) || a.atomic_out) return -1;
   if (amode == OP_KCONTIG && (long)a.M * a.lda * 2 >= (1l << 31)) return -1;
   if (bmode == OP_KCONTIG && (long)a.N * a.ldb * 2 >= (1l << 31)) return -1;
+  if (amode == OP_KOUTER && ((long)a.K * a.lda * 2 >= (1l << 31) || (a.M & 7))) return -1;
+  if (bmode == OP_KOUTER && ((long)a.K * a.ldb * 2 >= (1l << 31) || (a.N & 7))) return -1;
   const long blocks = (long)cdiv(a.M, 128) * cdiv(a.N, 64) * a.batch * a.splitk;
   return (blocks <= 1600 && a.kchunk >= 1024) ? 9 : 8;
 }
@@ -295,8 +309,12 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
           }
         }
       }
-      if (!big)
-        dispatch(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, tile, (hipStream_t)stream);
+      if (!big) {
+        const int am = a_kouter ? OP_KOUTER : OP_KCONTIG, bm = b_kouter ? OP_KOUTER : OP_KCONTIG;
+        int t = tile;
+        if (t < 0 && dense_glds_on() && a.batch == 1) t = pick_glds_tile(a, am, bm);
+        dispatch(a, am, bm, t, (hipStream_t)stream);
+      }
       // slabs are [batch][splitk][M*N]: reduce each batch separately
       for (int b = 0; b < a.batch; ++b)
         dtf_sum_rows(ws + (long)b * splitk * M * N, (long)M * N, splitk, (long)M * N, (float*)C + (long)b * M * N,

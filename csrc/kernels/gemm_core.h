@@ -578,10 +578,11 @@ struct GldsLoader {
 // (tap, channel) pair fixed per lane; out-of-image taps / rows past K read zeros via the range check.
 template <int R, int MODE>
 struct GldsKOuter {
-  static_assert(MODE == OP_KOUTER_R || MODE == OP_WGRADX_R, "conv weight-gradient operands only");
+  static_assert(MODE == OP_KOUTER_R || MODE == OP_WGRADX_R || MODE == OP_KOUTER, "K-outer operands only");
   static constexpr int L = R / 32;
   static constexpr int ROWB = R * 2;
   __amdgpu_buffer_rsrc_t rsrc;
+  int ldb;          // row stride in bytes (OP_KOUTER: dense operand stored [K][rows])
   int kr[L];        // k-row of the tile this lane fills in instruction i
   int coff[L];      // byte offset of the lane's column chunk (+ tap shift for OP_WGRADX_R)
   int hoff[L], woff[L];
@@ -591,7 +592,9 @@ struct GldsKOuter {
     const int t = threadIdx.x;
     const ConvGeom& g = a.g;
     const uint32_t bytes = MODE == OP_WGRADX_R ? (uint32_t)((long)g.N * g.H * g.W * g.C * 2)
-                                               : (uint32_t)((long)g.N * g.P * g.Q * g.Kout * 2);
+                           : MODE == OP_KOUTER_R ? (uint32_t)((long)g.N * g.P * g.Q * g.Kout * 2)
+                                                 : (uint32_t)((long)a.K * ld * 2);  // host: < 2 GiB
+    ldb = MODE == OP_KOUTER_R ? g.Kout * 2 : (int)(ld * 2);
     rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)ptr, (short)0, (int)bytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < L; ++i) {
@@ -634,7 +637,7 @@ struct GldsKOuter {
           off = (((int)n * g.H + hb) * g.W + wb) * g.C * 2 + coff[i];
         }
       } else {
-        off = k * g.Kout * 2 + coff[i];
+        off = k * ldb + coff[i];
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 + wave * 1024), 16,
@@ -650,7 +653,7 @@ using LoaderFor = typename std::conditional<
                               KContigLoader<R, MODE>>::type>::type;
 
 constexpr bool glds_kcontig(int m) { return m == OP_KCONTIG || m == OP_IM2COL_T || m == OP_DGRAD_T; }
-constexpr bool glds_kouter(int m) { return m == OP_KOUTER_R || m == OP_WGRADX_R; }
+constexpr bool glds_kouter(int m) { return m == OP_KOUTER_R || m == OP_WGRADX_R || m == OP_KOUTER; }
 constexpr bool glds_mode(int m) { return glds_kcontig(m) || glds_kouter(m); }
 
 template <int R, int MODE>
