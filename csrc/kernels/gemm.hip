@@ -386,12 +386,15 @@ __global__ void tap_gather_kernel(const bf16_t* __restrict__ src, bf16_t* __rest
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
-                           const float* bnmean, float* bnpart, int* bnrows, void* stream) {
+                           const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
+                           void* stream) {
   if ((C & 3) || (K & 7)) return -1;
   if (bnx && (out_f32 || (C & 7) || !bnpart || !bnmean || !bnrows)) return -9;
+  if (betamask && (out_f32 || beta == 0.f || (C & 7) || sh > 1 || sw > 1)) return -10;
   hipStream_t st = (hipStream_t)stream;
   int prow = 0;  // BN partial rows written so far (strided dgrad: one set per phase)
   auto bn_args = [&](GemmArgs& a) {
+    a.betamask = (const uint8_t*)betamask;
     if (!bnx) return;
     a.stats = bnpart + (long)prow * 2 * C;
     a.bnx = (const bf16_t*)bnx;

@@ -88,6 +88,7 @@ struct GemmArgs {
   const bf16_t* bnx;
   const uint8_t* bnmask;
   const float* bnmean;
+  const uint8_t* betamask;  // optional 1-bit mask on the beta*C term (staged bf16 epilogue only)
   int crm;
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
@@ -920,8 +921,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
           f[2 * q] = __uint_as_float(vw[q] << 16); f[2 * q + 1] = __uint_as_float(vw[q] & 0xffff0000u);
           g[2 * q] = __uint_as_float(ow[q] << 16); g[2 * q + 1] = __uint_as_float(ow[q] & 0xffff0000u);
         }
+        // betamask: the old C is a BN(+ReLU) output gradient whose ReLU mask was not applied yet (the
+        // residual shortcut's gradient, taken lazily instead of materialised by the BN backward)
+        const uint32_t bm = a.betamask ? (uint32_t)a.betamask[(e + cbase) >> 3] : 0xFFu;  // e % 8 == 0
 #pragma unroll
-        for (int r = 0; r < 8; ++r) f[r] = fmaf(a.beta, g[r], f[r]);
+        for (int r = 0; r < 8; ++r) f[r] = ((bm >> r) & 1u) ? fmaf(a.beta, g[r], f[r]) : f[r];
         val.x = pack2bf(f[0], f[1]); val.y = pack2bf(f[2], f[3]);
         val.z = pack2bf(f[4], f[5]); val.w = pack2bf(f[6], f[7]);
       }
@@ -989,6 +993,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
           v[0] += a.beta * o.x; v[1] += a.beta * o.y; v[2] += a.beta * o.z; v[3] += a.beta * o.w;
         } else {
           uint2 o = *reinterpret_cast<const uint2*>(reinterpret_cast<bf16_t*>(a.C) + off);
+          if (a.betamask) {  // zero the old values whose ReLU bit is clear (see the staged path)
+            const uint32_t bm = ((uint32_t)a.betamask[off >> 3] >> (off & 4)) & 0xFu;  // off % 4 == 0
+            o.x &= ((bm & 1u) ? 0x0000ffffu : 0u) | ((bm & 2u) ? 0xffff0000u : 0u);
+            o.y &= ((bm & 4u) ? 0x0000ffffu : 0u) | ((bm & 8u) ? 0xffff0000u : 0u);
+          }
           v[0] += a.beta * __uint_as_float(o.x << 16); v[1] += a.beta * __uint_as_float(o.x & 0xffff0000u);
           v[2] += a.beta * __uint_as_float(o.y << 16); v[3] += a.beta * __uint_as_float(o.y & 0xffff0000u);
         }

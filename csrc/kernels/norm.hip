@@ -163,17 +163,21 @@ __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restri
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int r0 = blockIdx.y * sg, r1 = min(T, r0 + sg);
-  float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+  // 4 independent accumulator pairs: 8 partial-row loads in flight per thread (the pass is L2-latency bound)
+  float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     int r = r0 + grp;
-    for (; r + 4 < r1; r += 8) {
-      a0 += part[(long)r * rs + c]; b0 += part[(long)r * rs + C + c];
-      a1 += part[(long)(r + 4) * rs + c]; b1 += part[(long)(r + 4) * rs + C + c];
+    for (; r + 12 < r1; r += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a4[u] += part[(long)(r + 4 * u) * rs + c];
+        b4[u] += part[(long)(r + 4 * u) * rs + C + c];
+      }
     }
-    for (; r < r1; r += 4) { a0 += part[(long)r * rs + c]; b0 += part[(long)r * rs + C + c]; }
+    for (; r < r1; r += 4) { a4[0] += part[(long)r * rs + c]; b4[0] += part[(long)r * rs + C + c]; }
   }
-  red[0][grp][cl] = a0 + a1;
-  red[1][grp][cl] = b0 + b1;
+  red[0][grp][cl] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  red[1][grp][cl] = (b4[0] + b4[1]) + (b4[2] + b4[3]);
   __syncthreads();
   if (grp == 0 && c < C) {
     part[(long)r0 * rs + c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);

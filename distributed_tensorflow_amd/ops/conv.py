@@ -53,11 +53,12 @@ def conv_fwd_raw(x, w16, g, stats=False, bias=None, act=0):
     return y
 
 
-def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None):
+def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None):
     """dX (bf16); with `acc` (a bf16 [N,H,W,C] gradient already holding another contribution) the epilogue
-    adds into it (beta = 1) and returns it. With `bn` (the _BNSource of the BatchNorm whose output this conv
-    consumed) the epilogue also produces that BatchNorm's backward reduction of the final dX values and
-    stores it on `bn` (see _BNSource)."""
+    adds into it (beta = 1) and returns it; `acc_mask` (1 bit per element) first zeroes the acc values whose
+    bit is clear (a residual gradient whose ReLU mask was deferred). With `bn` (the _BNSource of the
+    BatchNorm whose output this conv consumed) the epilogue also produces that BatchNorm's backward
+    reduction of the final dX values and stores it on `bn` (see _BNSource)."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     wc = crsk_shadow(w_master, K, R * S, C)
     dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device) if acc is None else acc
@@ -71,7 +72,8 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None):
     call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0,
          0.0 if acc is None else 1.0, -1, ptr(ws), 2 * ws.numel(),
          ptr(bn.yc) if bn is not None else None, ptr(bn.mbits) if bn is not None else None,
-         ptr(bn.mean) if bn is not None else None, ptr(part), rows.addr if rows else None, stream())
+         ptr(bn.mean) if bn is not None else None, ptr(part), rows.addr if rows else None,
+         ptr(acc_mask) if acc is not None else None, stream())
     if bn is not None:
         bn.provide(dx, part, rows.value)
     return dx
@@ -143,26 +145,34 @@ class ResidualGradLink:
     conv's backward happens to run before the projection's (autograd schedules by creation order; the block
     creates the projection after the first conv so that it runs first), the link closes and both return their
     gradients normally, so the result is the same either way.
+
+    An identity shortcut may park LAZILY: the last conv's BatchNorm(+ReLU) backward then parks its incoming
+    gradient together with the ReLU mask instead of writing the masked residual gradient, and the first conv's
+    epilogue applies the mask while adding (one activation-sized write saved per identity block; the parked
+    tensor is overwritten in place, it has no other reader).
     """
-    __slots__ = ("buf", "closed")
+    __slots__ = ("buf", "mask", "closed")
 
     def __init__(self):
         self.buf = None
+        self.mask = None
         self.closed = False
 
-    def park(self, g):
+    def park(self, g, mask=None):
         """Shortcut side: returns what to hand autograd (None when parked)."""
         if self.closed or g is None:
             return g
-        self.buf = g
+        self.buf, self.mask = g, mask
         return None
 
     def take(self):
-        """First-conv side: the parked gradient to accumulate into (or None; then the link closes)."""
-        buf, self.buf = self.buf, None
+        """First-conv side: (parked gradient to accumulate into, its deferred ReLU mask or None), or
+        (None, None); then the link closes."""
+        buf, mask = self.buf, self.mask
+        self.buf = self.mask = None
         if buf is None:
             self.closed = True
-        return buf
+        return buf, mask
 
 
 class _BNSource:
@@ -194,6 +204,7 @@ class _BNSource:
 
 
 _FUSE_BN_BWD = __import__("os").environ.get("DTF_FUSE_BN_BWD", "1") != "0"
+_LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -252,7 +263,11 @@ class _ConvBNFn(torch.autograd.Function):
         M = yc.numel() // K
         dout = dout.to(BF16).contiguous()
         dyc = torch.empty_like(yc)
-        dres = torch.empty_like(yc) if (ctx.has_res and ctx.relu) else None
+        link, role = ctx.link, ctx.role
+        # identity shortcut with ReLU: park dout + the ReLU mask instead of writing the masked residual gradient
+        lazy_res = (ctx.has_res and ctx.relu and link is not None and role == "res" and not link.closed
+                    and _LAZY_RES and mbits is not None)
+        dres = torch.empty_like(yc) if (ctx.has_res and ctx.relu and not lazy_res) else None
         gamma_p, beta_p = ctx.bn_params
         tg, tb = direct_grad(gamma_p), direct_grad(beta_p)
         direct_bn = tg is not None and tb is not None  # accumulate dgamma/dbeta into the arena grads
@@ -271,16 +286,17 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.src = None
         if ctx.has_res and not ctx.relu:
             dres = dout
-        link, role = ctx.link, ctx.role
-        if link is not None and role == "res":
+        if lazy_res:
+            dres = link.park(dout, mask=mbits)  # (None: parked; dout is overwritten by the first conv's dgrad)
+        elif link is not None and role == "res":
             dres = link.park(dres)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            acc = link.take() if (link is not None and role == "acc") else None
+            acc, acc_mask = link.take() if (link is not None and role == "acc") else (None, None)
             src = ctx.in_src
             complete = src is not None and role != "proj" and (
                 src.consumers == 1 or (role == "acc" and acc is not None and src.consumers == 2))
-            dx = conv_dgrad_raw(dyc, w, g, acc=acc, bn=src if complete else None)
+            dx = conv_dgrad_raw(dyc, w, g, acc=acc, bn=src if complete else None, acc_mask=acc_mask)
             ctx.in_src = None
             if link is not None and role == "proj":
                 dx = link.park(dx)

@@ -406,7 +406,7 @@ def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta):
     ws = workspace(cuda)
     wc = crsk_shadow(w, K, R * S, Cin)
     call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, Cin, K, R, S, g[7], g[8], st, st, pd, pd, 1, 1, 0,
-         beta, -1, ptr(ws), 2 * ws.numel(), ptr(yc), ptr(bits), ptr(mean), ptr(part), rows.addr, stream())
+         beta, -1, ptr(ws), 2 * ws.numel(), ptr(yc), ptr(bits), ptr(mean), ptr(part), rows.addr, None, stream())
     T = rows.value
     assert T >= 1
     p = part[:T * 2 * Cin].view(T, 2 * Cin).sum(0)
@@ -445,7 +445,7 @@ def test_conv_staging_pipelines_agree(cuda, case, tile):
     def dgrad(t):
         dx = torch.empty_like(x)
         call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, Cin, K, R, S, P, Q, st, st, pd, pd, 1, 1, 0, 0.0, t,
-             ptr(ws), 2 * ws.numel(), None, None, None, None, None, stream())
+             ptr(ws), 2 * ws.numel(), None, None, None, None, None, None, stream())
         return dx
 
     assert torch.equal(fwd(tile), fwd(-1))

@@ -117,3 +117,17 @@ def test_fused_bn_backward_reduction_matches_separate_pass(cuda, monkeypatch):
         s = a.abs().max().item() + 1e-6
         worst = max(worst, (a - b).abs().max().item() / s)
     assert worst < 0.02, worst
+
+
+@pytest.mark.gpu
+def test_lazy_residual_gradient_is_bitwise_identical(cuda, monkeypatch):
+    """Deferring the ReLU mask of the identity-shortcut gradient into the first conv's dgrad epilogue
+    (ResidualGradLink lazy parking) changes no bit of any gradient."""
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(8, 16, 16, 64, generator=g).to(cuda).to(torch.bfloat16)
+    runs = {}
+    for lazy in (False, True):
+        monkeypatch.setattr(OC, "_LAZY_RES", lazy)
+        runs[lazy] = _run(_blocks(), x)
+    for a, b in zip(runs[False], runs[True]):
+        assert torch.equal(a, b)

@@ -39,7 +39,7 @@ for _ in range(iters):
              p, p, 1, 1, 0, 0, tile, stream())
     elif kind == "dgrad":
         call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), NB, H, H, Cin, K, Rk, Rk, P, Q, s, s, p, p, 1, 1, 0, 0.0, tile,
-             ptr(ws), 2 * ws.numel(), None, None, None, None, None, stream())
+             ptr(ws), 2 * ws.numel(), None, None, None, None, None, None, stream())
     else:
         call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dwacc), NB, H, H, Cin, K, Rk, Rk, P, Q, s, s, p, p, 1, 1, 1, 0, tile,
              ptr(ws), ws.numel(), stream())

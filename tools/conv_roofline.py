@@ -92,7 +92,8 @@ def main():
 
         def dgrad(tile):
             return lambda: call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), NB, H, H, Cin, K, R, R, P, Q, s, s, p, p,
-                                1, 1, 0, 0.0, tile, ptr(ws), 2 * ws.numel(), None, None, None, None, None, stream())
+                                1, 1, 0, 0.0, tile, ptr(ws), 2 * ws.numel(), None, None, None, None, None, None,
+                                stream())
 
         def wgrad(tile):
             return lambda: call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dwacc), NB, H, H, Cin, K, R, R, P, Q, s, s, p,
