@@ -449,6 +449,240 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
   }
 }
 
+// ---------------- BatchNorm + ReLU + MaxPool (the ResNet stem) ----------------
+// Forward: one pass over the conv output yc produces the pooled BN+ReLU output and a 1-byte argmax per
+// (pixel, channel) — the BN output is never written. Argmax byte = window tap (r*S+s) | 0x80 when the pooled
+// value is > 0: a tap's value IS the pooled value of every window it wins, so bit 7 doubles as the BN's
+// ReLU mask in the backward. Backward: the pooled gradient is gathered back per input pixel on the fly (no
+// materialised maxpool gradient) by two passes: reduce (sum dz, sum dz*(x-mean)) and apply (dx of the BN).
+struct PoolGeo {
+  int N, H, W, C, P, Q, R, S, sh, sw, ph, pw;
+  FastDiv c8, dQ, dP, dW, dHW;  // forward: C/8, Q, P; backward: W, H*W
+};
+
+__global__ void __launch_bounds__(256) bn_relu_maxpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                                  const float* __restrict__ scale,
+                                                                  const float* __restrict__ shift,
+                                                                  bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                                  PoolGeo pg) {
+  const uint32_t total = (uint32_t)pg.N * pg.P * pg.Q * (pg.C / 8);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    uint32_t pix, cc, t, q, n, p;
+    fdivmod(i, pg.c8, pix, cc);
+    fdivmod(pix, pg.dQ, t, q);
+    fdivmod(t, pg.dP, n, p);
+    float sc[8], sh[8], best[8];
+    uint32_t bi[8];
+    load_coef8(scale + cc * 8, sc);
+    load_coef8(shift + cc * 8, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int r = 0; r < pg.R; ++r) {
+      const int hi = (int)p * pg.sh - pg.ph + r;
+      if ((unsigned)hi >= (unsigned)pg.H) continue;
+      for (int s = 0; s < pg.S; ++s) {
+        const int wi = (int)q * pg.sw - pg.pw + s;
+        if ((unsigned)wi >= (unsigned)pg.W) continue;
+        float f[8];
+        load8(x + (((long)n * pg.H + hi) * pg.W + wi) * pg.C + cc * 8, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // the value the unfused BN apply would have stored (bf16), compared as the unfused pool does
+          const float v = bf2f(f2bf(fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f)));
+          if (v > best[j]) { best[j] = v; bi[j] = (uint32_t)(r * pg.S + s); }
+        }
+      }
+    }
+    store8(y + (long)i * 8, best);
+    uint32_t b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = bi[j] | (best[j] > 0.f ? 0x80u : 0u);
+    uint2 a;
+    a.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    a.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+    *reinterpret_cast<uint2*>(arg + (long)i * 8) = a;
+  }
+}
+
+// dz of input pixel (n, h, w), channels [8cc, 8cc+8): the pooled gradients of the windows this pixel won with a
+// positive value, summed in tap order and rounded to bf16 (what the unfused pool backward stored). Any geometry.
+__device__ __forceinline__ void pool_grad8(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                           uint32_t n, int h, int w, int cc, const PoolGeo& pg, float* dz) {
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int rr = 0; rr < pg.R; ++rr) {
+    const int th = h + pg.ph - rr;
+    if (th < 0 || th % pg.sh) continue;
+    const int p = th / pg.sh;
+    if (p >= pg.P) continue;
+    for (int ss = 0; ss < pg.S; ++ss) {
+      const int tw = w + pg.pw - ss;
+      if (tw < 0 || tw % pg.sw) continue;
+      const int q = tw / pg.sw;
+      if (q >= pg.Q) continue;
+      const long o = (((long)n * pg.P + p) * pg.Q + q) * pg.C + cc * 8;
+      const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
+      float g[8];
+      load8(dy + o, g);
+      const uint32_t me = (uint32_t)(rr * pg.S + ss) | 0x80u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t bj = ((j < 4 ? a.x : a.y) >> (8 * (j & 3))) & 0xffu;
+        if (bj == me) acc[j] += g[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dz[j] = bf2f(f2bf(acc[j]));
+}
+
+// 3x3 / stride 2 / pad 1 windows over an input of exactly 2P x 2Q: the 2x2 input block (rows 2i, 2i+1; cols 2j,
+// 2j+1) is covered by the 4 windows (i|i+1, j|j+1) only, so one thread gathers all four windows once (4 regular
+// loads, no per-tap branching) and hands out dz for the block's pixels [(2i,2j), (2i,2j+1), (2i+1,2j),
+// (2i+1,2j+1)], each summed in the same tap order as pool_grad8 (bitwise the same result).
+struct Win8 {
+  uint2 a;
+  float g[8];
+};
+__device__ __forceinline__ void load_win(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg, long o,
+                                         bool valid, Win8& w) {
+  if (valid) {
+    w.a = *reinterpret_cast<const uint2*>(arg + o);
+    load8(dy + o, w.g);
+  } else {
+    w.a = make_uint2(0u, 0u);  // no bit 7: never selected
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w.g[j] = 0.f;
+  }
+}
+__device__ __forceinline__ void win_add(const Win8& w, uint32_t tap, float* acc) {
+  const uint32_t me = tap | 0x80u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t bj = ((j < 4 ? w.a.x : w.a.y) >> (8 * (j & 3))) & 0xffu;
+    if (bj == me) acc[j] += w.g[j];
+  }
+}
+__device__ __forceinline__ void pool_grad8_2x2(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                               uint32_t n, int i, int j, int cc, const PoolGeo& pg,
+                                               float (&dz)[4][8]) {
+  const bool vi = i + 1 < pg.P, vj = j + 1 < pg.Q;
+  const long o00 = (((long)n * pg.P + i) * pg.Q + j) * pg.C + cc * 8;
+  const long rowq = (long)pg.Q * pg.C;
+  Win8 w00, w01, w10, w11;
+  load_win(dy, arg, o00, true, w00);
+  load_win(dy, arg, o00 + pg.C, vj, w01);
+  load_win(dy, arg, o00 + rowq, vi, w10);
+  load_win(dy, arg, o00 + rowq + pg.C, vi && vj, w11);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) dz[k][c] = 0.f;
+  win_add(w00, 4, dz[0]);                                                       // (2i, 2j): tap (1,1)
+  win_add(w01, 3, dz[1]); win_add(w00, 5, dz[1]);                               // (2i, 2j+1)
+  win_add(w10, 1, dz[2]); win_add(w00, 7, dz[2]);                               // (2i+1, 2j)
+  win_add(w11, 0, dz[3]); win_add(w10, 2, dz[3]); win_add(w01, 6, dz[3]); win_add(w00, 8, dz[3]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) dz[k][c] = bf2f(f2bf(dz[k][c]));
+}
+
+// Reduce pass. B2: rows are 2x2 input blocks (pool_grad8_2x2 geometry; dHW divides by P*Q, dW by Q);
+// otherwise rows are input pixels (pool_grad8; dHW = H*W, dW = W).
+template <bool B2>
+__global__ void __launch_bounds__(256) maxpool_bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
+                                                                    const uint8_t* __restrict__ arg,
+                                                                    const bf16_t* __restrict__ x,
+                                                                    const float* __restrict__ mean, PoolGeo pg,
+                                                                    float* __restrict__ part) {
+  __shared__ float red[4096];
+  const int C = pg.C;
+  const long M = B2 ? (long)pg.N * pg.P * pg.Q : (long)pg.N * pg.H * pg.W;
+  ColGeo g = colgeo(C);
+  const int t = threadIdx.x;
+  const int rsub = t / g.TPR;
+  for (int cc0 = 0; cc0 < g.cols8; cc0 += g.TPR) {
+    const int cc = cc0 + t % g.TPR;
+    float s[8] = {0}, q[8] = {0};
+    if (t < g.TPR * g.RPB && cc < g.cols8) {
+      float mu[8];
+      load_coef8(mean + cc * 8, mu);
+      for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
+        uint32_t n, hw, h, w;
+        fdivmod((uint32_t)r, pg.dHW, n, hw);
+        fdivmod(hw, pg.dW, h, w);
+        if constexpr (B2) {
+          float d[4][8], xv[4][8];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            load8(x + ((((long)n * pg.H + 2 * h + (k >> 1)) * pg.W + 2 * w + (k & 1)) * g.cols8 + cc) * 8, xv[k]);
+          pool_grad8_2x2(dy, arg, n, (int)h, (int)w, cc, pg, d);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              s[j] += d[k][j];
+              q[j] = fmaf(d[k][j], xv[k][j] - mu[j], q[j]);
+            }
+        } else {
+          float d[8], xv[8];
+          load8(x + (r * g.cols8 + cc) * 8, xv);
+          pool_grad8(dy, arg, n, (int)h, (int)w, cc, pg, d);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            s[j] += d[j];
+            q[j] = fmaf(d[j], xv[j] - mu[j], q[j]);
+          }
+        }
+      }
+    }
+    block_col_partials(s, q, cc0, g.TPR, g.RPB, C, part + (long)blockIdx.x * 2 * C, red);
+  }
+}
+
+template <bool B2>
+__global__ void __launch_bounds__(256) maxpool_bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
+                                                                   const uint8_t* __restrict__ arg,
+                                                                   const bf16_t* __restrict__ x,
+                                                                   const float* __restrict__ coef, PoolGeo pg,
+                                                                   bf16_t* __restrict__ dx) {
+  const int C = pg.C;
+  const long M = B2 ? (long)pg.N * pg.P * pg.Q : (long)pg.N * pg.H * pg.W;
+  const ColGeo g = colgeo(C);
+  const int t = threadIdx.x;
+  if (t >= g.TPR * g.RPB) return;
+  const int rsub = t / g.TPR;
+  for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
+    float ka[8], kb[8], kc[8];
+    load_coef8(coef + cc * 8, ka);
+    load_coef8(coef + C + cc * 8, kb);
+    load_coef8(coef + 2 * C + cc * 8, kc);
+    for (long r = (long)blockIdx.x * g.RPB + rsub; r < M; r += (long)gridDim.x * g.RPB) {
+      uint32_t n, hw, h, w;
+      fdivmod((uint32_t)r, pg.dHW, n, hw);
+      fdivmod(hw, pg.dW, h, w);
+      if constexpr (B2) {
+        float d[4][8], xv[4][8];
+        long i8[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          i8[k] = (((long)n * pg.H + 2 * h + (k >> 1)) * pg.W + 2 * w + (k & 1)) * g.cols8 + cc;
+          load8(x + i8[k] * 8, xv[k]);
+        }
+        pool_grad8_2x2(dy, arg, n, (int)h, (int)w, cc, pg, d);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bn_bwd_apply_row(d[k], xv[k], ka, kb, kc, dx, nullptr, i8[k]);
+      } else {
+        float d[8], xv[8];
+        const long i8 = r * g.cols8 + cc;
+        load8(x + i8 * 8, xv);
+        pool_grad8(dy, arg, n, (int)h, (int)w, cc, pg, d);
+        bn_bwd_apply_row(d, xv, ka, kb, kc, dx, nullptr, i8);
+      }
+    }
+  }
+}
+
 // ---------------- LayerNorm: one wave per row, D % 8 == 0, D <= 512 * NC ----------------
 // The row lives in registers (NC 16-byte chunks per lane): one HBM read, one write.
 template <int NC>
@@ -672,10 +906,11 @@ DTF_API int dtf_bn_bwd_partials(const void* dy, const void* mbits, const void* x
                      coef, (hipStream_t)stream);
 }
 
-static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
-                       const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
-                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st) {
-  void* stream = (void*)st;
+// Sum the G partial rows [G][2C] of a BN backward reduction and finalize: dgamma/dbeta and the apply
+// coefficients `coef` (3*C floats). One launch (last-arriver hand-off) when tickets are available.
+static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const float* invstd, const float* gamma,
+                                   long M, int C, float* dgamma, float* dbeta, int accumulate, float* coef,
+                                   hipStream_t st) {
   long rs = 2L * C;
   int sg = 0;
   const int G2 = bn_groups(G, &sg);
@@ -684,14 +919,78 @@ static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, con
     hipLaunchKernelGGL((bn_reduce_finalize_kernel<true>), dim3(cdiv(C, 64), G2), dim3(256), 0, st, part, G, rs, sg,
                        C, M, gamma, mean, const_cast<float*>(invstd), nullptr, 0.f, 0.f, dgamma, dbeta, coef, nullptr,
                        accumulate, tk);
-  } else {
-  int T = dtf_group_rows_once(part, rs, G, 2L * C, 32, &rs, stream);
+    return;
+  }
+  int T = dtf_group_rows_once(part, rs, G, 2L * C, 32, &rs, (void*)st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, mean, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);
-  }
+}
+
+static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
+                       const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
+                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st) {
+  bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M, C)), dim3(256), 0, st, (const bf16_t*)dy,
                      (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
                      (bf16_t*)dz_out);
+  return (int)hipGetLastError();
+}
+
+static bool pool_geo(int N, int H, int W, int C, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
+                     PoolGeo* pg) {
+  if ((C & 7) || R * S > 127 || sh < 1 || sw < 1) return false;
+  if ((long)N * H * W * C >= (1L << 31) || (long)N * P * Q * C >= (1L << 31)) return false;
+  *pg = PoolGeo{N, H, W, C, P, Q, R, S, sh, sw, ph, pw, make_fastdiv(C / 8), make_fastdiv(Q), make_fastdiv(P),
+                make_fastdiv(W), make_fastdiv((uint32_t)(H * W))};
+  return true;
+}
+
+// Fused BatchNorm(scale/shift) + ReLU + MaxPool forward over the conv output x [N,H,W,C] -> y [N,P,Q,C] and
+// the argmax/mask bytes arg [N,P,Q,C] (see bn_relu_maxpool_fwd_kernel).
+DTF_API int dtf_bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, void* y, void* arg, int N,
+                                    int H, int W, int C, int P, int Q, int R, int S, int sh, int sw, int ph, int pw,
+                                    void* stream) {
+  PoolGeo pg;
+  if (!pool_geo(N, H, W, C, P, Q, R, S, sh, sw, ph, pw, &pg)) return -1;
+  const long total = (long)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, scale, shift, (bf16_t*)y, (uint8_t*)arg, pg);
+  return (int)hipGetLastError();
+}
+
+// Backward of dtf_bn_relu_maxpool_fwd: dy = gradient of the pooled output; writes dx (gradient of the conv
+// output x), dgamma/dbeta (+= when accumulate). work: (2*1024 + 3) * C floats.
+DTF_API int dtf_maxpool_bn_bwd(const void* dy, const void* arg, const void* x, const float* mean, const float* invstd,
+                               const float* gamma, int N, int H, int W, int C, int P, int Q, int R, int S, int sh,
+                               int sw, int ph, int pw, void* dx, float* dgamma, float* dbeta, int accumulate,
+                               float* work, void* stream) {
+  PoolGeo pg;
+  if (!pool_geo(N, H, W, C, P, Q, R, S, sh, sw, ph, pw, &pg)) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const long M = (long)N * H * W;
+  float* coef = work;
+  float* part = work + 3 * C;
+  // the stem's 3x3/2 pad-1 pool over an even-sized map: 2x2-block gathers (pool_grad8_2x2)
+  const bool b2 = R == 3 && S == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 && H == 2 * P && W == 2 * Q;
+  if (b2) {
+    pg.dHW = make_fastdiv((uint32_t)(P * Q));
+    pg.dW = make_fastdiv((uint32_t)Q);
+  }
+  const long rows = b2 ? (long)N * P * Q : M;
+  const int G = red_grid(rows, C);
+  if (b2)
+    hipLaunchKernelGGL((maxpool_bn_bwd_reduce_kernel<true>), dim3(G), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const uint8_t*)arg, (const bf16_t*)x, mean, pg, part);
+  else
+    hipLaunchKernelGGL((maxpool_bn_bwd_reduce_kernel<false>), dim3(G), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const uint8_t*)arg, (const bf16_t*)x, mean, pg, part);
+  bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
+  if (b2)
+    hipLaunchKernelGGL((maxpool_bn_bwd_apply_kernel<true>), dim3(ew_grid(rows, C)), dim3(256), 0, st,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, coef, pg, (bf16_t*)dx);
+  else
+    hipLaunchKernelGGL((maxpool_bn_bwd_apply_kernel<false>), dim3(ew_grid(M, C)), dim3(256), 0, st,
+                       (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, coef, pg, (bf16_t*)dx);
   return (int)hipGetLastError();
 }
 

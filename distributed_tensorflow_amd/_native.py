@@ -36,6 +36,8 @@ _KERNEL_SIGS = {
     "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],
     "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "dtf_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
+    "dtf_bn_relu_maxpool_fwd": [P, P, P, P, P] + [I] * 12 + [P],
+    "dtf_maxpool_bn_bwd": [P, P, P, P, P, P] + [I] * 12 + [P, P, P, I, P, P],
     "dtf_gap_fwd": [P, P, I, I, I, I, P],
     "dtf_gap_bwd": [P, I, P, I, I, I, P],
     "dtf_optim_apply": [I, P, P, P, P, P, L, F, F, F, F, F, F, F, I, I, P, P, P],

@@ -303,12 +303,20 @@ class ConvBN(Layer):
         self.moving_variance = self.add_weight("bn/moving_variance", (self.filters,), "ones", trainable=False)
         self.built = True
 
-    def call(self, x, residual=None, training=None, link=None, role=None):
-        """link/role: residual-gradient join of a block (ops.conv.ResidualGradLink)."""
+    def call(self, x, residual=None, training=None, link=None, role=None, pool=None):
+        """link/role: residual-gradient join of a block (ops.conv.ResidualGradLink). pool: a MaxPooling2D
+        applied to the (ReLU) output, fused with the BatchNorm (ops.conv_bn_maxpool)."""
         if self.padding == "same":
             pad = ((self.kernel_size[0] - 1) // 2, (self.kernel_size[1] - 1) // 2)
         else:
             pad = (0, 0)
+        if pool is not None:
+            if not (self.relu and residual is None and link is None):
+                return pool(self.call(x, residual, training, link, role))
+            return ops.conv_bn_maxpool(x, self.kernel, self.gamma, self.beta, self.moving_mean,
+                                       self.moving_variance, stride=self.strides, pad=pad, momentum=self.momentum,
+                                       eps=self.epsilon, training=bool(training), pool_size=pool.pool_size,
+                                       pool_strides=pool.strides, pool_pad=pool.pads())
         return ops.conv_bn(x, self.kernel, self.gamma, self.beta, self.moving_mean, self.moving_variance,
                            stride=self.strides, pad=pad, relu=self.relu, residual=residual, momentum=self.momentum,
                            eps=self.epsilon, training=bool(training), link=link, role=role)
@@ -321,11 +329,13 @@ class MaxPooling2D(Layer):
         self.strides = _pair(strides if strides is not None else pool_size)
         self.padding = padding
 
-    def call(self, x, training=None):
-        pad = (0, 0)
+    def pads(self):
         if self.padding == "same":
-            pad = ((self.pool_size[0] - 1) // 2, (self.pool_size[1] - 1) // 2)
-        return ops.max_pool2d(x, self.pool_size, self.strides, pad)
+            return ((self.pool_size[0] - 1) // 2, (self.pool_size[1] - 1) // 2)
+        return (0, 0)
+
+    def call(self, x, training=None):
+        return ops.max_pool2d(x, self.pool_size, self.strides, self.pads())
 
 
 class GlobalAveragePooling2D(Layer):

@@ -24,6 +24,7 @@ from ..keras.models import Model
 from ..ops.conv import ResidualGradLink
 
 RES_LINK = os.environ.get("DTF_RES_LINK", "1") != "0"
+FUSE_STEM = os.environ.get("DTF_FUSE_STEM", "1") != "0"  # stem BN + ReLU + MaxPool as one pass
 STAGES = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3), 26: (2, 2, 2, 2)}
 
 
@@ -71,8 +72,11 @@ class ResNet(Model):
             x = ops.image_to_nhwc_bf16(images.float() if not images.is_floating_point() else images, self.in_pad)
         else:
             x = images
-        x = self.stem(x, training=training)
-        x = self.pool(x)
+        if FUSE_STEM:  # BN + ReLU + MaxPool in one pass (ops.conv_bn_maxpool)
+            x = self.stem(x, training=training, pool=self.pool)
+        else:
+            x = self.stem(x, training=training)
+            x = self.pool(x)
         for b in self.blocks:
             x = b(x, training=training)
         x = self.gap(x)

@@ -326,6 +326,86 @@ def conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1
     return torch.relu(y) if relu else y
 
 
+class _ConvBNPoolFn(torch.autograd.Function):
+    """y = MaxPool( relu( BN_train(conv(x, w)) ) ) — the ResNet stem as one autograd node.
+
+    The BN+ReLU output is never materialised: one pass over the conv output produces the pooled output and an
+    argmax byte per pooled element whose bit 7 is the ReLU mask (norm.hip bn_relu_maxpool_fwd_kernel). The
+    backward gathers the pooled gradient per conv-output pixel on the fly in the BN backward's reduce and
+    apply passes, instead of writing the pool gradient and re-reading it twice."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, rmean, rvar, stride, pad, dil, momentum, eps, training, pk, ps, pp):
+        x = x.contiguous()
+        g = _geom(x, w, stride, pad, dil)
+        N, H, W, C, K, R, S, P, Q = g[:9]
+        M = N * P * Q
+        dev = x.device
+        work = torch.empty(4 * K, dtype=F32, device=dev)  # scale shift mean invstd
+        scale, shift, mean, invstd = work[:K], work[K:2 * K], work[2 * K:3 * K], work[3 * K:]
+        if training:
+            yc, part, rows = conv_fwd_raw(x, bf16_shadow(w), g, stats=True)
+            call("dtf_bn_finalize", ptr(part), rows, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, K,
+                 float(momentum), float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
+        else:
+            yc = conv_fwd_raw(x, bf16_shadow(w), g)
+            call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
+                 ptr(shift), stream())
+        P2, Q2 = out_size(P, pk[0], ps[0], pp[0]), out_size(Q, pk[1], ps[1], pp[1])
+        y = torch.empty((N, P2, Q2, K), dtype=BF16, device=dev)
+        arg = torch.empty((N, P2, Q2, K), dtype=torch.uint8, device=dev)
+        call("dtf_bn_relu_maxpool_fwd", ptr(yc), ptr(scale), ptr(shift), ptr(y), ptr(arg), N, P, Q, K, P2, Q2,
+             pk[0], pk[1], ps[0], ps[1], pp[0], pp[1], stream())
+        ctx.save_for_backward(x, w, gamma, yc, arg, mean, invstd)
+        ctx.bn_params = (gamma, beta)
+        ctx.g = g
+        ctx.pool = (P2, Q2, pk, ps, pp)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, gamma, yc, arg, mean, invstd = ctx.saved_tensors
+        g = ctx.g
+        N, H, W, C, K, R, S, P, Q = g[:9]
+        P2, Q2, pk, ps, pp = ctx.pool
+        dy = dy.to(BF16).contiguous()
+        dyc = torch.empty_like(yc)
+        gamma_p, beta_p = ctx.bn_params
+        tg, tb = direct_grad(gamma_p), direct_grad(beta_p)
+        direct_bn = tg is not None and tb is not None
+        dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
+        dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
+        work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
+        call("dtf_maxpool_bn_bwd", ptr(dy), ptr(arg), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), N, P, Q, K, P2,
+             Q2, pk[0], pk[1], ps[0], ps[1], pp[0], pp[1], ptr(dyc), ptr(dgamma), ptr(dbeta), int(direct_bn),
+             ptr(work), stream())
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad_raw(dyc, w, g)
+        if ctx.needs_input_grad[1]:
+            tw = direct_grad(w)
+            dw = conv_wgrad_raw(x, dyc, g, out=tw)
+            if tw is not None:
+                dw = None
+        if direct_bn:
+            dgamma = dbeta = None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
+
+
+def conv_bn_maxpool(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1), momentum=0.9, eps=1e-5,
+                    training=True, pool_size=(3, 3), pool_strides=(2, 2), pool_pad=(1, 1)):
+    """MaxPool(ReLU(FusedBatchNorm(Conv2D(x)))), NHWC — the ResNet stem fused (see _ConvBNPoolFn)."""
+    stride, pad, dil = tuple(stride), tuple(pad), tuple(dil)
+    pk, ps, pp = tuple(pool_size), tuple(pool_strides), tuple(pool_pad)
+    if on_gpu(x) and w.shape[0] % 8 == 0 and pk[0] * pk[1] <= 127:
+        return _ConvBNPoolFn.apply(x.to(BF16), w, gamma, beta, rmean, rvar, stride, pad, dil, float(momentum),
+                                   float(eps), bool(training), pk, ps, pp)
+    from .nn import max_pool2d
+    y = conv_bn(x, w, gamma, beta, rmean, rvar, stride, pad, dil, relu=True, momentum=momentum, eps=eps,
+                training=training)
+    return max_pool2d(y, pk, ps, pp)
+
+
 def image_to_nhwc_bf16(x_nchw, cpad=8):
     """Device-side input pipeline step: f32 NCHW images -> bf16 NHWC, channels padded to `cpad`."""
     N, C, H, W = x_nchw.shape

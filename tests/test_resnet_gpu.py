@@ -131,3 +131,67 @@ def test_lazy_residual_gradient_is_bitwise_identical(cuda, monkeypatch):
         runs[lazy] = _run(_blocks(), x)
     for a, b in zip(runs[False], runs[True]):
         assert torch.equal(a, b)
+
+
+def _stem_run(x, fused, monkeypatch):
+    from distributed_tensorflow_amd.keras import initializers
+    from distributed_tensorflow_amd.keras import layers as KL
+    initializers.set_seed(11)
+    stem = KL.ConvBN(64, 7, 2, relu=True)
+    pool = KL.MaxPooling2D(3, 2, padding="same")
+    xx = x.clone().requires_grad_(False)
+    y = stem(xx, training=True, pool=pool) if fused else pool(stem(xx, training=True))
+    loss = (y.float() * torch.linspace(-1, 1, y.shape[-1], device=y.device)).square().mean()
+    grads = torch.autograd.grad(loss, stem.trainable_weights)
+    return [y.float().cpu()] + [g.float().cpu() for g in grads] + [stem.moving_mean.cpu(),
+                                                                    stem.moving_variance.cpu()]
+
+
+@pytest.mark.gpu
+def test_fused_stem_bn_relu_maxpool_is_bitwise_identical(cuda, monkeypatch):
+    """The ResNet stem's BN + ReLU + MaxPool in one pass (ops.conv_bn_maxpool: no materialised BN output,
+    argmax byte doubling as the ReLU mask, pool gradient gathered inside the BN backward) produces the same
+    bits as ConvBN followed by MaxPooling2D for the output and running statistics; the gradients differ only by
+    the f32 summation order of the BN backward reduction (2x2-block gathers walk the pixels in another order)."""
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(4, 64, 64, 8, generator=g)
+    x[..., 3:] = 0  # the padded colour channels of the real stem input
+    x = x.to(cuda).to(torch.bfloat16)
+    a = _stem_run(x, False, monkeypatch)
+    b = _stem_run(x, True, monkeypatch)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[-2], b[-2]) and torch.equal(a[-1], b[-1])
+    for u, v in zip(a[1:-2], b[1:-2]):
+        assert (u - v).abs().max().item() <= 2e-3 * u.abs().max().item()
+
+
+@pytest.mark.gpu
+def test_fused_stem_matches_f32_reference(cuda):
+    """Fused stem vs an f32 PyTorch reference (conv -> batch-stat BN -> ReLU -> maxpool) on the same bf16
+    inputs, rounding the conv output, the pooled activation and the gradients to bf16 where the GPU stores them
+    (against a pure-f32 pool, bf16 near-ties route ~2% of the window gradients to another tap and the filter
+    gradient, a sum of random-sign terms, moves by ~sqrt(2%) ~ 14%): forward and filter gradient agree to bf16
+    tolerance."""
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(2, 32, 32, 8, generator=g).to(torch.bfloat16)
+    w = (torch.randn(64, 7, 7, 8, generator=g) * 0.05)
+    gamma = torch.rand(64, generator=g) + 0.5
+    beta = torch.randn(64, generator=g) * 0.1
+    dyv = torch.randn(2, 8, 8, 64, generator=g)
+
+    def ref():
+        ww = w.clone().requires_grad_(True)
+        rnd = _RoundBF16.apply
+        y = rnd(OC._ref_conv(x.float(), ww.to(torch.bfloat16).float(), None, (2, 2), (3, 3), (1, 1)))
+        y = batch_norm_ref(y, gamma, beta, None, None, 0.9, 1e-5, True)
+        y = rnd(torch.relu(y)).permute(0, 3, 1, 2)
+        y = torch.nn.functional.max_pool2d(y, 3, 2, 1).permute(0, 2, 3, 1)
+        (gw,) = torch.autograd.grad((y * dyv).sum(), [ww])
+        return y.detach(), gw
+
+    yr, gwr = ref()
+    wd = w.to(cuda).requires_grad_(True)
+    rm, rv = torch.zeros(64, device=cuda), torch.ones(64, device=cuda)
+    y = ops.conv_bn_maxpool(x.to(cuda), wd, gamma.to(cuda), beta.to(cuda), rm, rv, stride=(2, 2), pad=(3, 3))
+    (gw,) = torch.autograd.grad((y.float() * dyv.to(cuda)).sum(), [wd])
+    assert (y.float().cpu() - yr).abs().max().item() < 0.05 * yr.abs().max().item()
+    assert (gw.cpu() - gwr).abs().max().item() < 0.03 * gwr.abs().max().item()
