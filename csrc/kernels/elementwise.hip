@@ -64,6 +64,30 @@ __global__ void nchw_to_nhwc_pad_kernel(const float* __restrict__ x, bf16_t* __r
   }
 }
 
+// f32 NCHW images (C <= 4, even H, W) -> bf16 2x2 space-to-depth image [N, H/2+3, W/2+3, 16] with channel index
+// (dh*2 + dw)*4 + c and 2 zero rows/cols of padding before, 1 after: the ResNet stem's 7x7/2 pad-3 conv is then a
+// 4x4/1 unpadded conv over it (K = 256 instead of 7*7*8 = 392, ops.conv.stem_s2d_filter). One thread = one
+// s2d pixel (two 16-B stores).
+__global__ void nchw_to_s2d_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int H, int W) {
+  const int Hs = H / 2 + 3, Ws = W / 2 + 3;
+  const long total = (long)N * Hs * Ws;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int v = (int)(i % Ws);
+    const long t = i / Ws;
+    const int u = (int)(t % Hs);
+    const long n = t / Hs;
+    float f[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int dh = k >> 3, dw = (k >> 2) & 1, c = k & 3;
+      const int h = 2 * (u - 2) + dh, w = 2 * (v - 2) + dw;
+      f[k] = (c < C && h >= 0 && h < H && w >= 0 && w < W) ? x[((n * C + c) * H + h) * W + w] : 0.f;
+    }
+    store8(y + i * 16, f);
+    store8(y + i * 16 + 8, f + 8);
+  }
+}
+
 // Filter KRSC (f32 master or bf16) -> bf16 CRSK (the dgrad operand layout).
 __global__ void filter_krsc_to_crsk_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ o, int K, int RS,
                                            int C) {
@@ -380,6 +404,11 @@ DTF_API int dtf_cast_bf16_f32(const void* x, float* y, long n, void* stream) {
 DTF_API int dtf_nchw_to_nhwc_pad(const float* x, void* y, int N, int C, int HW, int Cp, void* stream) {
   if (Cp & 7) return -1;
   hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel, GRID((long)N * HW), x, (bf16_t*)y, N, C, HW, Cp);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_nchw_to_s2d(const float* x, void* y, int N, int C, int H, int W, void* stream) {
+  if (C > 4 || (H & 1) || (W & 1)) return -1;
+  hipLaunchKernelGGL(nchw_to_s2d_kernel, GRID((long)N * (H / 2 + 3) * (W / 2 + 3)), x, (bf16_t*)y, N, C, H, W);
   return (int)hipGetLastError();
 }
 DTF_API int dtf_filter_to_crsk(const void* w, void* o, int K, int RS, int C, void* stream) {

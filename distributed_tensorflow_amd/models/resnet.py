@@ -25,6 +25,7 @@ from ..ops.conv import ResidualGradLink
 
 RES_LINK = os.environ.get("DTF_RES_LINK", "1") != "0"
 FUSE_STEM = os.environ.get("DTF_FUSE_STEM", "1") != "0"  # stem BN + ReLU + MaxPool as one pass
+S2D_STEM = os.environ.get("DTF_S2D_STEM", "1") != "0"  # stem conv over the 2x2 space-to-depth image
 STAGES = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3), 26: (2, 2, 2, 2)}
 
 
@@ -68,15 +69,27 @@ class ResNet(Model):
         self.fc = KL.Dense(num_classes, kernel_initializer="glorot_uniform")
 
     def call(self, images, training=None):
-        if images.dim() == 4 and images.shape[1] in (1, 3) and images.shape[-1] not in (1, 3, self.in_pad):
-            x = ops.image_to_nhwc_bf16(images.float() if not images.is_floating_point() else images, self.in_pad)
+        nchw = images.dim() == 4 and images.shape[1] in (1, 3) and images.shape[-1] not in (1, 3, self.in_pad)
+        if nchw and FUSE_STEM and S2D_STEM and images.is_cuda and images.shape[2] % 2 == 0 \
+                and images.shape[3] % 2 == 0:
+            # 7x7/2 stem as a 4x4/1 conv over the 2x2 space-to-depth image, BN + ReLU + MaxPool fused
+            N, _, H, W = images.shape
+            if not self.stem.built:  # the 7x7 filter keeps its [64, 7, 7, in_pad] shape (checkpoints)
+                self.stem.build((N, H, W, self.in_pad))
+                self.stem.built = True
+            xs = ops.image_to_s2d_bf16(images if images.is_floating_point() else images.float())
+            x = self.stem(xs, training=training, pool=self.pool, s2d=True)
         else:
-            x = images
-        if FUSE_STEM:  # BN + ReLU + MaxPool in one pass (ops.conv_bn_maxpool)
-            x = self.stem(x, training=training, pool=self.pool)
-        else:
-            x = self.stem(x, training=training)
-            x = self.pool(x)
+            if nchw:
+                x = ops.image_to_nhwc_bf16(images.float() if not images.is_floating_point() else images,
+                                           self.in_pad)
+            else:
+                x = images
+            if FUSE_STEM:  # BN + ReLU + MaxPool in one pass (ops.conv_bn_maxpool)
+                x = self.stem(x, training=training, pool=self.pool)
+            else:
+                x = self.stem(x, training=training)
+                x = self.pool(x)
         for b in self.blocks:
             x = b(x, training=training)
         x = self.gap(x)

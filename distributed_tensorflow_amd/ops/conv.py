@@ -335,20 +335,26 @@ class _ConvBNPoolFn(torch.autograd.Function):
     apply passes, instead of writing the pool gradient and re-reading it twice."""
 
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, rmean, rvar, stride, pad, dil, momentum, eps, training, pk, ps, pp):
+    def forward(ctx, x, w, gamma, beta, rmean, rvar, stride, pad, dil, momentum, eps, training, pk, ps, pp,
+                s2d=False):
         x = x.contiguous()
-        g = _geom(x, w, stride, pad, dil)
+        w16 = bf16_shadow(w)
+        if s2d:  # x: image_to_s2d_bf16 output; w: the 7x7 filter, run as its 4x4 space-to-depth form
+            w16 = stem_s2d_filter(w16)
+            g = _geom(x, w16, (1, 1), (0, 0), (1, 1))
+        else:
+            g = _geom(x, w, stride, pad, dil)
         N, H, W, C, K, R, S, P, Q = g[:9]
         M = N * P * Q
         dev = x.device
         work = torch.empty(4 * K, dtype=F32, device=dev)  # scale shift mean invstd
         scale, shift, mean, invstd = work[:K], work[K:2 * K], work[2 * K:3 * K], work[3 * K:]
         if training:
-            yc, part, rows = conv_fwd_raw(x, bf16_shadow(w), g, stats=True)
+            yc, part, rows = conv_fwd_raw(x, w16, g, stats=True)
             call("dtf_bn_finalize", ptr(part), rows, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, K,
                  float(momentum), float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
         else:
-            yc = conv_fwd_raw(x, bf16_shadow(w), g)
+            yc = conv_fwd_raw(x, w16, g)
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
                  ptr(shift), stream())
         P2, Q2 = out_size(P, pk[0], ps[0], pp[0]), out_size(Q, pk[1], ps[1], pp[1])
@@ -360,6 +366,7 @@ class _ConvBNPoolFn(torch.autograd.Function):
         ctx.bn_params = (gamma, beta)
         ctx.g = g
         ctx.pool = (P2, Q2, pk, ps, pp)
+        ctx.s2d = s2d
         return y
 
     @staticmethod
@@ -381,25 +388,96 @@ class _ConvBNPoolFn(torch.autograd.Function):
              ptr(work), stream())
         dx = dw = None
         if ctx.needs_input_grad[0]:
+            if ctx.s2d:
+                raise NotImplementedError("no input gradient through the space-to-depth stem (image input)")
             dx = conv_dgrad_raw(dyc, w, g)
         if ctx.needs_input_grad[1]:
             tw = direct_grad(w)
-            dw = conv_wgrad_raw(x, dyc, g, out=tw)
+            if ctx.s2d:
+                dw = stem_s2d_filter_grad(conv_wgrad_raw(x, dyc, g), w.shape)
+                if tw is not None:
+                    tw.add_(dw)
+            else:
+                dw = conv_wgrad_raw(x, dyc, g, out=tw)
             if tw is not None:
                 dw = None
         if direct_bn:
             dgamma = dbeta = None
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
+
+
+_S2D_IDX = {}
+
+
+def _s2d_index(Cp, device):
+    """Column maps between a 7x7 stem filter [K, 7, 7, Cp] (flattened per output channel, plus one trailing
+    zero column) and its space-to-depth form [K, 4, 4, 16]: s2d tap (a, b), channel (dh*2 + dw)*4 + c holds
+    filter tap (2a + dh - 1, 2b + dw - 1), channel c (zero outside the 7x7 window or for c >= Cp)."""
+    key = (Cp, str(device))
+    if key not in _S2D_IDX:
+        zero = 49 * Cp
+        fwd = torch.full((4 * 4 * 16,), zero, dtype=torch.long)
+        back = torch.full((49 * Cp,), 4 * 4 * 16, dtype=torch.long)
+        for a in range(4):
+            for b in range(4):
+                for k in range(16):
+                    dh, dw, c = k >> 3, (k >> 2) & 1, k & 3
+                    kh, kw = 2 * a + dh - 1, 2 * b + dw - 1
+                    if 0 <= kh < 7 and 0 <= kw < 7 and c < Cp:
+                        fwd[(a * 4 + b) * 16 + k] = (kh * 7 + kw) * Cp + c
+                        back[(kh * 7 + kw) * Cp + c] = (a * 4 + b) * 16 + k
+        _S2D_IDX[key] = (fwd.to(device), back.to(device))
+    return _S2D_IDX[key]
+
+
+def stem_s2d_filter(w):
+    """[K, 7, 7, Cp] -> [K, 4, 4, 16]: the 7x7/2 pad-3 filter as a 4x4/1 filter over image_to_s2d_bf16 output."""
+    K, R, S, Cp = w.shape
+    assert (R, S) == (7, 7)
+    fwd, _ = _s2d_index(Cp, w.device)
+    wz = torch.cat([w.reshape(K, -1), w.new_zeros(K, 1)], 1)
+    return wz.index_select(1, fwd).reshape(K, 4, 4, 16).contiguous()
+
+
+def stem_s2d_filter_grad(dw2, shape):
+    """Gradient of stem_s2d_filter: [K, 4, 4, 16] -> [K, 7, 7, Cp] (every filter entry appears once; the padded
+    colour channels c >= 4 get zero)."""
+    K, R, S, Cp = shape
+    _, back = _s2d_index(Cp, dw2.device)
+    dz = torch.cat([dw2.reshape(K, -1), dw2.new_zeros(K, 1)], 1)
+    return dz.index_select(1, back).reshape(K, R, S, Cp)
+
+
+def image_to_s2d_bf16(x_nchw):
+    """f32 NCHW images (<= 4 channels, even H, W) -> bf16 2x2 space-to-depth [N, H/2+3, W/2+3, 16] (zero padding
+    baked in) for the space-to-depth stem (conv_bn_maxpool(..., s2d=True))."""
+    N, C, H, W = x_nchw.shape
+    if on_gpu(x_nchw):
+        y = torch.empty((N, H // 2 + 3, W // 2 + 3, 16), dtype=BF16, device=x_nchw.device)
+        call("dtf_nchw_to_s2d", ptr(x_nchw.float().contiguous()), ptr(y), N, C, H, W, stream())
+        return y
+    xp = torch.zeros((N, 4, H + 6, W + 6), dtype=x_nchw.dtype)
+    xp[:, :C, 4:H + 4, 4:W + 4] = x_nchw
+    # [N, 4, Hs, 2, Ws, 2] -> [N, Hs, Ws, dh, dw, c]
+    t = xp.reshape(N, 4, (H + 6) // 2, 2, (W + 6) // 2, 2).permute(0, 2, 4, 3, 5, 1)
+    return t.reshape(N, (H + 6) // 2, (W + 6) // 2, 16)
 
 
 def conv_bn_maxpool(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1), momentum=0.9, eps=1e-5,
-                    training=True, pool_size=(3, 3), pool_strides=(2, 2), pool_pad=(1, 1)):
-    """MaxPool(ReLU(FusedBatchNorm(Conv2D(x)))), NHWC — the ResNet stem fused (see _ConvBNPoolFn)."""
+                    training=True, pool_size=(3, 3), pool_strides=(2, 2), pool_pad=(1, 1), s2d=False):
+    """MaxPool(ReLU(FusedBatchNorm(Conv2D(x)))), NHWC — the ResNet stem fused (see _ConvBNPoolFn).
+    s2d=True: x is image_to_s2d_bf16(images) and w the [K, 7, 7, Cp] filter of a 7x7/2 pad-3 conv (run as the
+    equivalent 4x4/1 conv over the space-to-depth image: 256 instead of 392 MACs per output, no padded taps)."""
     stride, pad, dil = tuple(stride), tuple(pad), tuple(dil)
     pk, ps, pp = tuple(pool_size), tuple(pool_strides), tuple(pool_pad)
+    if s2d:
+        assert tuple(w.shape[1:3]) == (7, 7) and stride == (2, 2) and pad == (3, 3) and dil == (1, 1)
     if on_gpu(x) and w.shape[0] % 8 == 0 and pk[0] * pk[1] <= 127:
         return _ConvBNPoolFn.apply(x.to(BF16), w, gamma, beta, rmean, rvar, stride, pad, dil, float(momentum),
-                                   float(eps), bool(training), pk, ps, pp)
+                                   float(eps), bool(training), pk, ps, pp, bool(s2d))
+    if s2d:
+        w = stem_s2d_filter(w)
+        stride, pad = (1, 1), (0, 0)
     from .nn import max_pool2d
     y = conv_bn(x, w, gamma, beta, rmean, rvar, stride, pad, dil, relu=True, momentum=momentum, eps=eps,
                 training=training)

@@ -195,3 +195,46 @@ def test_fused_stem_matches_f32_reference(cuda):
     (gw,) = torch.autograd.grad((y.float() * dyv.to(cuda)).sum(), [wd])
     assert (y.float().cpu() - yr).abs().max().item() < 0.05 * yr.abs().max().item()
     assert (gw.cpu() - gwr).abs().max().item() < 0.03 * gwr.abs().max().item()
+
+
+def test_s2d_stem_filter_is_exact_cpu():
+    """CPU: the 2x2 space-to-depth image + 4x4 filter reproduce the 7x7/2 pad-3 conv, and the filter-gradient
+    fold is the adjoint of the filter gather (padded colour channels get zero gradient)."""
+    torch.manual_seed(0)
+    x = torch.randn(2, 3, 16, 16)
+    w = torch.randn(8, 7, 7, 8)
+    xn = torch.zeros(2, 16, 16, 8)
+    xn[..., :3] = x.permute(0, 2, 3, 1)
+    ref = OC._ref_conv(xn, w, None, (2, 2), (3, 3), (1, 1))
+    out = OC._ref_conv(OC.image_to_s2d_bf16(x), OC.stem_s2d_filter(w), None, (1, 1), (0, 0), (1, 1))
+    assert (ref - out).abs().max().item() < 1e-4
+    g = torch.randn(8, 4, 4, 16)
+    back = OC.stem_s2d_filter_grad(g, w.shape)
+    assert abs((OC.stem_s2d_filter(w) * g).sum().item() - (w * back).sum().item()) < 1e-3
+    assert back[..., 4:].abs().max().item() == 0
+
+
+@pytest.mark.gpu
+def test_s2d_stem_matches_direct_stem(cuda):
+    """GPU: the space-to-depth stem (image_to_s2d_bf16 + 4x4/1 conv) against the direct 7x7/2 conv over the
+    8-channel NHWC image, both through the fused BN + ReLU + MaxPool: same bf16 products, different f32
+    summation order, so outputs and filter gradients agree to bf16 rounding."""
+    g = torch.Generator().manual_seed(19)
+    img = torch.randn(4, 3, 64, 64, generator=g).to(cuda)
+    w = (torch.randn(64, 7, 7, 8, generator=g) * 0.05).to(cuda)
+    gamma = (torch.rand(64, generator=g) + 0.5).to(cuda)
+    beta = (torch.randn(64, generator=g) * 0.1).to(cuda)
+    dyv = torch.randn(4, 16, 16, 64, generator=g).to(cuda)
+    outs = []
+    for s2d in (False, True):
+        wd = w.clone().requires_grad_(True)
+        rm, rv = torch.zeros(64, device=cuda), torch.ones(64, device=cuda)
+        x = ops.image_to_s2d_bf16(img) if s2d else ops.image_to_nhwc_bf16(img, 8)
+        y = ops.conv_bn_maxpool(x, wd, gamma, beta, rm, rv, stride=(2, 2), pad=(3, 3), s2d=s2d)
+        (gw,) = torch.autograd.grad((y.float() * dyv).sum(), [wd])
+        outs.append((y.float().cpu(), gw.cpu(), rm.cpu()))
+    (y0, g0, m0), (y1, g1, m1) = outs
+    assert (y0 - y1).abs().max().item() < 0.02 * y0.abs().max().item()
+    assert (g0 - g1).abs().max().item() < 0.03 * g0.abs().max().item()
+    assert (m0 - m1).abs().max().item() < 1e-3 * m0.abs().max().item() + 1e-6
+    assert g1[..., 3:].abs().max().item() == 0  # zero-padded colour channels
