@@ -230,6 +230,58 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   // ---- epilogue (no glds outstanding: the last tile drained with vmcnt(0)) ----
   const float alpha = a.scales ? a.alpha * a.scales[0] * a.scales[1] : a.alpha;
   const long cbase = a.slab > 0 ? (long)z * a.slab : (long)bz * a.sC;
+  // bf16 outputs (and the optional pre-activation side output) go through LDS, one 128-row half of the tile at
+  // a time, so the global stores are whole 16-B chunks of 512-B row segments instead of 8-B pieces of 16 rows
+  const bool staged = !a.out_f32 && a.beta == 0.f && a.slab == 0 && !(a.N & 7) && !(a.ldc & 7) &&
+                      !(reinterpret_cast<uintptr_t>(a.C) & 15) && !(reinterpret_cast<uintptr_t>(a.aux) & 15);
+  if (staged) {
+    constexpr int CS = 256 + 8;  // LDS row stride (elements): conflict-free 8-B fragment writes
+    bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
+    __syncthreads();  // every wave is done with the operand buffers
+    for (int o = 0; o < (a.aux ? 2 : 1); ++o) {
+      bf16_t* dst = (o ? a.aux : reinterpret_cast<bf16_t*>(a.C)) + cbase;
+      for (int h = 0; h < 2; ++h) {
+        if (wr == h) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int nl = wc * 64 + j * 16 + (lane >> 4) * 4;
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
+              if (a.bias && n0 + nl < a.N) {
+                float4 b = *reinterpret_cast<const float4*>(a.bias + n0 + nl);
+                v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+              }
+              if (o == 0 && a.act == 1) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+              } else if (o == 0 && a.act == 2) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+              }
+              uint2 pk;
+              pk.x = pack2bf(v[0], v[1]);
+              pk.y = pack2bf(v[2], v[3]);
+              *reinterpret_cast<uint2*>(ct + (i * 16 + (lane & 15)) * CS + nl) = pk;
+            }
+          }
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int c = threadIdx.x; c < 128 * 32; c += NT2) {
+          const int row = c >> 5, c8 = c & 31;
+          const int m = m0 + h * 128 + row, n = n0 + c8 * 8;
+          if (m < a.M && n < a.N)
+            *reinterpret_cast<uint4*>(dst + (long)m * a.ldc + n) =
+                *reinterpret_cast<const uint4*>(ct + row * CS + c8 * 8);
+        }
+        __syncthreads();
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);

@@ -129,10 +129,11 @@ __device__ __forceinline__ void stat_acc(const GemmArgs& a, long mrow, int n, co
   }
 }
 
+// 0.5 x (1 + tanh(u)) == x * sigmoid(2u): one exp and one reciprocal instead of a libm tanhf
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
 }
 
 // Bit mask over the taps (kh * S + kw) of an R x S filter with kh in [h0, h1] and kw in [w0, w1] (empty when

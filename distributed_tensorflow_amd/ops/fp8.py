@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 
 from ._util import BF16, F32, bf16_shadow, call, direct_grad, ptr, stream, weights_epoch, workspace
-from .linalg import colsum, gemm
+from .linalg import colsum, dense_dgrad, dense_wgrad, gemm
 
 E4M3_MAX = 448.0
 
@@ -86,14 +86,14 @@ class _DenseFP8(torch.autograd.Function):
             g = torch.empty_like(dz)
             call("dtf_act", ptr(pre), ptr(dz), ptr(g), g.numel(), ctx.act, 1, stream())
             dz = g
-        dx = gemm(dz, bf16_shadow(w), b_kouter=True).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
+        dx = dense_dgrad(dz, bf16_shadow(w)).reshape(ctx.shp) if ctx.needs_input_grad[0] else None
         dw = db = None
         if ctx.needs_input_grad[1]:  # inside Model.train_step: accumulate into the arena gradient directly
             tw = direct_grad(w)
             if tw is not None:
-                gemm(dz, x2, a_kouter=True, b_kouter=True, out=tw, beta=1.0)
+                dense_wgrad(dz, x2, out=tw)
             else:
-                dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
+                dw = dense_wgrad(dz, x2)
         if ctx.has_b and ctx.needs_input_grad[2]:
             tb = direct_grad(ctx.b_param)
             if tb is not None:

@@ -124,6 +124,34 @@ def colsum(x2d, out=None, accumulate=False):
     return out
 
 
+# Plain (epilogue-free) backward GEMMs may go to hipBLASLt (torch.mm), the library GEMM of the platform: measured
+# faster than the MFMA kernel for every data-gradient shape of BERT-base / GPT-2-medium (1.1-1.55x) and for the
+# large weight gradients (out*in >= 4M: GPT-2 FFN and LM head); the split-K weight gradients of BERT's 768-wide
+# layers stay on the MFMA kernel, which is faster there (tools/bench_blas_plain.py). DTF_PLAIN_BLAS=0: all MFMA.
+_PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "1") != "0"
+_BLAS_WGRAD_MIN = 4 << 20
+
+
+def dense_dgrad(dz, w16):
+    """dX[T, in] = dZ[T, out] W[out, in] (bf16)."""
+    if _PLAIN_BLAS:
+        return torch.mm(dz, w16)
+    return gemm(dz, w16, b_kouter=True)
+
+
+def dense_wgrad(dz, x2, out=None):
+    """dW[out, in] = dZ^T X in f32; accumulated into `out` (an arena gradient view) when given."""
+    o, i = dz.shape[1], x2.shape[1]
+    if _PLAIN_BLAS and o * i >= _BLAS_WGRAD_MIN:
+        if out is not None and out.is_contiguous():
+            return torch.ops.aten.addmm.dtype_out(out, dz.t(), x2, F32, beta=1, alpha=1, out=out)
+        r = torch.mm(dz.t(), x2, out_dtype=F32)
+        return r if out is None else out.add_(r)
+    if out is not None:
+        return gemm(dz, x2, a_kouter=True, b_kouter=True, out=out, beta=1.0)
+    return gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
+
+
 def _act_ref(x, act):
     if act == ACT_RELU:
         return torch.relu(x)
@@ -165,15 +193,15 @@ class _DenseFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             # dx[t,i] = sum_o dz[t,o] W[o,i]  -> B stored [K=out][N=in] (k-outer)
-            dx = gemm(dz, bf16_shadow(w), b_kouter=True).reshape(ctx.shp)
+            dx = dense_dgrad(dz, bf16_shadow(w)).reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
             # dW[o,i] = sum_t dz[t,o] x[t,i]  -> both operands k-outer, f32 out; inside Model.train_step
             # accumulated straight into the arena gradient (beta = 1) instead of returned
             tw = direct_grad(w)
             if tw is not None and tw.dim() == 2:
-                gemm(dz, x2, a_kouter=True, b_kouter=True, out=tw, beta=1.0)
+                dense_wgrad(dz, x2, out=tw)
             else:
-                dw = gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
+                dw = dense_wgrad(dz, x2)
         if ctx.has_b and ctx.needs_input_grad[2]:
             tb = direct_grad(ctx.b_param)
             if tb is not None:
