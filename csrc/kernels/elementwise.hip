@@ -344,6 +344,94 @@ __global__ void __launch_bounds__(256) softmax_ce_kernel(const void* __restrict_
   }
 }
 
+// Two-pass softmax cross-entropy (the gradient is produced in the backward, where dloss is known):
+//   fwd: one online pass per row -> loss[r], lse[r];  bwd: dlogits = (exp(x - lse) - target) * dloss[r].
+// bf16 rows are read with 16-B vector loads between a scalar head (rows of odd length V start at any element
+// offset) and a scalar tail; one 256-thread block per row.
+__device__ __forceinline__ void ce_online(float v, float& m, float& s) {
+  if (v > m) {
+    s = s * __expf(m - v) + 1.f;
+    m = v;
+  } else {
+    s += __expf(v - m);
+  }
+}
+
+__global__ void __launch_bounds__(256) softmax_ce_fwd_kernel(const void* __restrict__ logits, int in_f32,
+                                                             const long* __restrict__ labels, float* __restrict__ loss,
+                                                             float* __restrict__ lse_out, int V, float smooth) {
+  __shared__ float red[16];
+  const long r = blockIdx.x;
+  const int t = threadIdx.x;
+  float m = -INFINITY, s = 0.f, sx = 0.f;
+  if (in_f32) {
+    const float* xf = reinterpret_cast<const float*>(logits) + r * V;
+    for (int i = t; i < V; i += blockDim.x) { const float v = xf[i]; ce_online(v, m, s); sx += v; }
+  } else {
+    const bf16_t* xb = reinterpret_cast<const bf16_t*>(logits) + r * V;
+    const int head = min(V, (int)((8 - ((reinterpret_cast<uintptr_t>(xb) >> 1) & 7)) & 7));
+    const int nvec = (V - head) >> 3;
+    if (t < head) { const float v = bf2f(xb[t]); ce_online(v, m, s); sx += v; }
+    const bf16_t* xv = xb + head;
+    for (int c = t; c < nvec; c += blockDim.x) {
+      float f[8];
+      load8(xv + c * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { ce_online(f[j], m, s); sx += f[j]; }
+    }
+    for (int i = head + nvec * 8 + t; i < V; i += blockDim.x) { const float v = bf2f(xb[i]); ce_online(v, m, s); sx += v; }
+  }
+  const float M = block_max(m, red);
+  const float S = block_sum(m == -INFINITY ? 0.f : s * __expf(m - M), red);
+  const float SX = block_sum(sx, red);
+  if (t == 0) {
+    const float lse = M + __logf(S);
+    const long lab = labels[r];
+    float l = 0.f;
+    if (lab >= 0) {
+      const float xl = in_f32 ? reinterpret_cast<const float*>(logits)[r * V + lab]
+                              : bf2f(reinterpret_cast<const bf16_t*>(logits)[r * V + lab]);
+      l = (1.f - smooth) * (lse - xl) + smooth * (lse - SX / V);
+    }
+    loss[r] = l;
+    lse_out[r] = lse;
+  }
+}
+
+__global__ void __launch_bounds__(256) softmax_ce_bwd_kernel(const void* __restrict__ logits, int in_f32,
+                                                             const long* __restrict__ labels,
+                                                             const float* __restrict__ lse_in,
+                                                             const float* __restrict__ dloss, void* __restrict__ dl,
+                                                             int V, float smooth) {
+  const long r = blockIdx.x;
+  const int t = threadIdx.x;
+  const long lab = labels[r];
+  const float g = lab >= 0 ? dloss[r] : 0.f, lse = lse_in[r];
+  const float off = smooth / V, hit = 1.f - smooth;
+  auto grad = [&](float v, int i) { return (__expf(v - lse) - ((i == lab ? hit : 0.f) + off)) * g; };
+  if (in_f32) {
+    const float* xf = reinterpret_cast<const float*>(logits) + r * V;
+    float* o = reinterpret_cast<float*>(dl) + r * V;
+    for (int i = t; i < V; i += blockDim.x) o[i] = grad(xf[i], i);
+    return;
+  }
+  const bf16_t* xb = reinterpret_cast<const bf16_t*>(logits) + r * V;
+  bf16_t* ob = reinterpret_cast<bf16_t*>(dl) + r * V;
+  const int head = min(V, (int)((8 - ((reinterpret_cast<uintptr_t>(xb) >> 1) & 7)) & 7));
+  const bool vec = ((reinterpret_cast<uintptr_t>(ob) ^ reinterpret_cast<uintptr_t>(xb)) & 15) == 0;
+  const int nvec = vec ? (V - head) >> 3 : 0;
+  if (vec && t < head) ob[t] = f2bf(grad(bf2f(xb[t]), t));
+  for (int c = t; c < nvec; c += blockDim.x) {
+    float f[8];
+    const int i0 = head + c * 8;
+    load8(xb + i0, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = grad(f[j], i0 + j);
+    store8(ob + i0, f);
+  }
+  for (int i = (vec ? head + nvec * 8 : 0) + t; i < V; i += blockDim.x) ob[i] = f2bf(grad(bf2f(xb[i]), i));
+}
+
 // Row softmax over bf16 scores with scale and optional causal mask (attention probabilities).
 // rows are [batch][Sq] with row length Sk; causal: col > (row % Sq) + (Sk - Sq) masked.
 __global__ void __launch_bounds__(256) softmax_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
@@ -490,6 +578,20 @@ DTF_API int dtf_softmax_ce(const void* logits, int in_f32, const long* labels, f
                            int grad_f32, long rows, int V, float gscale, float smooth, void* stream) {
   hipLaunchKernelGGL(softmax_ce_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, logits, in_f32, labels, loss,
                      dlogits, grad_f32, V, gscale, smooth);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_softmax_ce_fwd(const void* logits, int in_f32, const long* labels, float* loss, float* lse, long rows,
+                               int V, float smooth, void* stream) {
+  if ((reinterpret_cast<uintptr_t>(logits) & 1) || rows <= 0) return rows <= 0 ? 0 : -1;
+  hipLaunchKernelGGL(softmax_ce_fwd_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, logits, in_f32, labels, loss,
+                     lse, V, smooth);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_softmax_ce_bwd(const void* logits, int in_f32, const long* labels, const float* lse,
+                               const float* dloss, void* dl, long rows, int V, float smooth, void* stream) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(softmax_ce_bwd_kernel, dim3(rows), dim3(256), 0, (hipStream_t)stream, logits, in_f32, labels, lse,
+                     dloss, dl, V, smooth);
   return (int)hipGetLastError();
 }
 DTF_API int dtf_softmax_fwd(const void* x, void* y, long rows, int Sq, int Sk, float scale, int causal,

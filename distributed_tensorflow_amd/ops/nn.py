@@ -225,24 +225,33 @@ def embedding(ids, table, pos_table=None, type_ids=None, type_table=None):
 
 # ------------------------------------------------------------------ softmax / losses
 class _SoftmaxCEFn(torch.autograd.Function):
+    """Forward: one online pass per row (loss, logsumexp); backward: ONE pass writing
+    (softmax - target) * dloss[row] — the logits are read twice and the gradient written once in total."""
+
     @staticmethod
     def forward(ctx, logits, labels, smooth):
         logits = logits.contiguous()
+        labels = labels.contiguous().long()
         V = logits.shape[-1]
         rows = logits.numel() // V
         loss = torch.empty(rows, dtype=F32, device=logits.device)
-        dl = torch.empty_like(logits)
-        call("dtf_softmax_ce", ptr(logits), int(logits.dtype == F32), ptr(labels.contiguous().long()), ptr(loss),
-             ptr(dl), int(dl.dtype == F32), rows, V, 1.0, float(smooth), stream())
-        ctx.save_for_backward(dl)
+        lse = torch.empty(rows, dtype=F32, device=logits.device)
+        call("dtf_softmax_ce_fwd", ptr(logits), int(logits.dtype == F32), ptr(labels), ptr(loss), ptr(lse), rows, V,
+             float(smooth), stream())
+        ctx.save_for_backward(logits, labels, lse)
+        ctx.smooth = float(smooth)
         return loss.reshape(logits.shape[:-1])
 
     @staticmethod
     def backward(ctx, dloss):
-        (dl,) = ctx.saved_tensors
-        g = dloss.reshape(-1, 1).to(dl.dtype)
-        V = dl.shape[-1]
-        return (dl.reshape(-1, V) * g).reshape(dl.shape), None, None
+        logits, labels, lse = ctx.saved_tensors
+        V = logits.shape[-1]
+        rows = logits.numel() // V
+        g = dloss.reshape(-1).to(F32).expand(rows).contiguous()
+        dl = torch.empty_like(logits)
+        call("dtf_softmax_ce_bwd", ptr(logits), int(logits.dtype == F32), ptr(labels), ptr(lse), ptr(g), ptr(dl),
+             rows, V, ctx.smooth, stream())
+        return dl, None, None
 
 
 def sparse_softmax_cross_entropy(logits, labels, label_smoothing=0.0):

@@ -200,6 +200,25 @@ def test_softmax_ce(cuda):
     close(logits.grad, lg.grad, 1e-4)
 
 
+def test_softmax_ce_bf16_odd_vocab(cuda):
+    """bf16 logits with an odd vocabulary (rows start at every element offset mod 8: vector body + scalar
+    head/tail), label smoothing, an ignored row (label -1) and per-row loss weights, vs f32 PyTorch."""
+    rows, V = 37, 1001
+    logits = (torch.randn(rows, V, device=cuda) * 3).to(BF).requires_grad_(True)
+    labels = torch.randint(0, V, (rows,), device=cuda)
+    labels[5] = -1
+    wts = torch.rand(rows, device=cuda)
+    l = ops.sparse_softmax_cross_entropy(logits, labels, label_smoothing=0.1)
+    lf = logits.detach().float().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(lf, labels.clamp(min=0), reduction="none", label_smoothing=0.1)
+    lr = torch.where(labels >= 0, lr, torch.zeros_like(lr))
+    close(l, lr, 1e-3)
+    (l * wts).sum().backward()
+    (lr * wts).sum().backward()
+    close(logits.grad, lf.grad, 2e-2)
+    assert logits.grad[5].float().abs().max().item() == 0
+
+
 def test_layernorm(cuda):
     x = rnd(512, 768, dev=cuda).requires_grad_(True)
     g = (torch.rand(768, device=cuda) + 0.5).requires_grad_(True)
