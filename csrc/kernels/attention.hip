@@ -141,13 +141,9 @@ __device__ __forceinline__ void store4(bf16_t* p, const v4f& v, float s) {
 // ------------------------------------------------------------------------------------------------ forward
 // block: 4 waves x (16 QT) queries; grid (cdiv(Sq, 64 QT), B*H)
 template <int QT>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char sk[64 * 128];
-  __shared__ __attribute__((aligned(16))) char sv[64 * 128];
-  __shared__ float smask[64];
+__device__ __forceinline__ void attn_fwd_body(const AttnArgs& a, const int qblk, char* sk, char* sv, float* smask) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qblk = gridDim.x - 1 - blockIdx.x;  // heavy (causal) blocks first
   const int BM = 64 * QT;
   const int q0 = qblk * BM + w * 16 * QT;
   const bf16_t* Q = a.q + b * a.qsb + h * a.qsh;
@@ -277,6 +273,31 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// Causal launches pair the logical block x with nblk - 1 - x in one workgroup (heavy block first), so every
+// workgroup walks the same number of tiles; otherwise block x is logical block nblk - 1 - x.
+__device__ __forceinline__ int pair_block(int causal, int nblk, int pass) {
+  const int x = blockIdx.x;
+  if (!causal) return pass == 0 ? nblk - 1 - x : -1;
+  const int heavy = nblk - 1 - x, light = x;
+  return pass == 0 ? heavy : (light < heavy ? light : -1);
+}
+__host__ __forceinline__ unsigned pair_grid(int causal, int nblk) {
+  return (unsigned)(causal ? (nblk + 1) / 2 : nblk);
+}
+
+template <int QT>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a, int nblk) {
+  __shared__ __attribute__((aligned(16))) char sk[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sv[64 * 128];
+  __shared__ float smask[64];
+  for (int pass = 0; pass < 2; ++pass) {
+    const int blk = pair_block(a.causal, nblk, pass);
+    if (blk < 0) break;
+    if (pass) __syncthreads();  // the previous block's last tile is no longer read
+    attn_fwd_body<QT>(a, blk, sk, sv, smask);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ backward
 // D[q] = sum_d dO[q][d] * O[q][d]; one thread per (bh, q) row
 __global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
@@ -302,14 +323,11 @@ __global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
 // dK, dV: block = 4 waves x (16 KT) keys, loop over 64-query tiles; grid (cdiv(Sk, 64 KT), B*H).
 // Query subtiles are processed in pairs (one 32-query MFMA k-step) so only 2 x KT score tiles are live.
 template <int KT>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char sq[64 * 128];
-  __shared__ __attribute__((aligned(16))) char sdo[64 * 128];
-  __shared__ float slse[64], sdv[64];
+__device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk, char* sq, char* sdo, float* slse,
+                                               float* sdv) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int BN = 64 * KT;
-  const int kblk = blockIdx.x;
   const int k0w = kblk * BN + w * 16 * KT;
   const long hb = b * a.qsb + h * a.qsh, kb = b * a.ksb + h * a.ksh, ob = b * a.osb + h * a.osh;
   const bf16_t* Q = a.q + hb;
@@ -447,15 +465,26 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
   }
 }
 
+// key block kblk walks the query tiles from its diagonal on (causal): heavy = small kblk
+template <int KT>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a, int nblk) {
+  __shared__ __attribute__((aligned(16))) char sq[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sdo[64 * 128];
+  __shared__ float slse[64], sdv[64];
+  for (int pass = 0; pass < 2; ++pass) {
+    int blk = pair_block(a.causal, nblk, pass);
+    if (blk < 0) break;
+    blk = nblk - 1 - blk;  // (pair_block orders by descending index; here the heavy blocks are the low ones)
+    if (pass) __syncthreads();
+    attn_dkdv_body<KT>(a, blk, sq, sdo, slse, sdv);
+  }
+}
+
 // dQ: block = 4 waves x (16 QT) queries, loop over 64-key tiles; grid (cdiv(Sq, 64 QT), B*H)
 template <int QT>
-__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char sk[64 * 128];
-  __shared__ __attribute__((aligned(16))) char sv[64 * 128];
-  __shared__ float smask[64];
+__device__ __forceinline__ void attn_dq_body(const AttnArgs& a, const int qblk, char* sk, char* sv, float* smask) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qblk = gridDim.x - 1 - blockIdx.x;
   const int BM = 64 * QT;
   const int q0 = qblk * BM + w * 16 * QT;
   const long hb = b * a.qsb + h * a.qsh, kb = b * a.ksb + h * a.ksh, ob = b * a.osb + h * a.osh;
@@ -563,6 +592,19 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
+template <int QT>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a, int nblk) {
+  __shared__ __attribute__((aligned(16))) char sk[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sv[64 * 128];
+  __shared__ float smask[64];
+  for (int pass = 0; pass < 2; ++pass) {
+    const int blk = pair_block(a.causal, nblk, pass);
+    if (blk < 0) break;
+    if (pass) __syncthreads();
+    attn_dq_body<QT>(a, blk, sk, sv, smask);
+  }
+}
+
 AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, const void* o,
                    const void* dout, const long* ostr, int B, int H, int Sq, int Sk, float scale, float dropout,
                    unsigned long long seed, int causal, const float* kmask) {
@@ -612,8 +654,9 @@ DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long
   if (dropout < 0.f || dropout >= 1.f) return -1;
   AttnArgs a = make_args(q, k, v, qstr, kstr, o, nullptr, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
   a.lse = lse;
-  dim3 grid((unsigned)((Sq + 127) / 128), (unsigned)(B * H));
-  hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  const int nqb = (Sq + 127) / 128;
+  dim3 grid(pair_grid(causal, nqb), (unsigned)(B * H));
+  hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(256), 0, (hipStream_t)stream, a, nqb);
   return (int)hipGetLastError();
 }
 
@@ -637,9 +680,10 @@ DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long
   const long rows = (long)B * H * Sq;
   hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)std::min<long>((rows + 255) / 256, 4096)), dim3(256), 0, st,
                      a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3((unsigned)((Sk + 127) / 128), (unsigned)(B * H)), dim3(256), 0,
-                     st, a);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, dim3((unsigned)((Sq + 127) / 128), (unsigned)(B * H)), dim3(256), 0,
-                     st, a);
+  const int nkb = (Sk + 127) / 128, nqb = (Sq + 127) / 128;
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0, st, a,
+                     nkb);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, dim3(pair_grid(causal, nqb), (unsigned)(B * H)), dim3(256), 0, st, a,
+                     nqb);
   return (int)hipGetLastError();
 }
