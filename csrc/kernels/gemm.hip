@@ -209,6 +209,25 @@ static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st
   else if (amode == OP_DGRAD_T && bmode == OP_KCONTIG) launch_modes<OP_DGRAD_T, OP_KCONTIG>(a, tile, st);
   else if (amode == OP_KOUTER && bmode == OP_WGRADX) launch_modes<OP_KOUTER, OP_WGRADX>(a, tile, st);
   else if (amode == OP_KOUTER_R && bmode == OP_WGRADX_R) launch_modes<OP_KOUTER_R, OP_WGRADX_R>(a, tile, st);
+  else if (amode == OP_WGRADX_R && bmode == OP_KOUTER_R) launch_modes<OP_WGRADX_R, OP_KOUTER_R>(a, tile, st);
+}
+
+// dst[c][r] (+)= src[r][c] for an f32 [R][C] matrix (the transposed weight gradient of dtf_conv_wgrad)
+__global__ void __launch_bounds__(256) transpose_acc_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                            int R, int C, int accumulate) {
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8)
+    if (r0 + y < R && c0 + tx < C) tile[y][tx] = src[(long)(r0 + y) * C + c0 + tx];
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < C && r < R) {
+      float* d = dst + (long)c * R + r;
+      *d = accumulate ? *d + tile[tx][y] : tile[tx][y];
+    }
+  }
 }
 
 static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw,
@@ -497,6 +516,34 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   const bool use_glds = small && wgrad_glds_on() && (tile >= 7 || (tile < 0 && R * S > 1));
   // row-mapped / LDS-DMA loaders: one pixel decode per lane per K-tile row (spatial filters), buffer loads
   const bool rowmap = small && (use_glds || (!pointwise && rowmap_ok()));
+  // Kout <= 64 spatial filters (ResNet's 56x56 stage and stem): a 128-row tile over Kout would be half empty;
+  // compute dW^T [R*S*C][Kout] with the operands swapped on 128x64 tiles and transpose it into dW
+  static const bool swap_on = [] {
+    const char* e = getenv("DTF_WGRAD_SWAP");
+    return !(e && e[0] == '0');
+  }();
+  if (swap_on && use_glds && tile < 0 && K <= 64 && R * S > 1 && ws != nullptr) {
+    GemmArgs b = a;
+    b.A = (const bf16_t*)X; b.B = (const bf16_t*)dY;
+    b.M = R * S * C; b.N = K;
+    b.lda = C; b.ldb = K; b.ldc = K;
+    const long mnT = (long)b.M * b.N;
+    int sk = choose_splitk(b.M, b.N, b.K, 128, 64, 1);
+    if ((long)(sk + 1) * mnT > ws_elems) sk = (int)(ws_elems / mnT) - 1;
+    if (sk >= 1) {
+      b.splitk = sk;
+      b.kchunk = ((b.K + sk - 1) / sk + BK - 1) / BK * BK;
+      b.C = ws;
+      b.slab = mnT;
+      b.beta = 0.f;
+      dispatch(b, OP_WGRADX_R, OP_KOUTER_R, 8, st);
+      float* dwt = ws + (long)sk * mnT;
+      dtf_sum_rows(ws, mnT, sk, mnT, dwt, 0, st);
+      hipLaunchKernelGGL(transpose_acc_kernel, dim3(cdiv(b.N, 32), cdiv(b.M, 32)), dim3(256), 0, st, dwt, dW, b.M,
+                         b.N, accumulate);
+      return (int)hipGetLastError();
+    }
+  }
   if (tile < 0 && use_glds) tile = 7;
   if (tile < 0) {  // measured on ResNet-50's filters (tools/conv_roofline.py --only wgrad --tiles)
     if (a.M <= 64) tile = pointwise && a.N >= 256 ? 4 : 3;  // Kout = 64: no half-empty 128-row tiles
