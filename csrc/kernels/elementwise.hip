@@ -173,6 +173,21 @@ __global__ void dropout_kernel(const bf16_t* x, bf16_t* y, long n8, float keep, 
   }
 }
 
+// Residual add of a dropped-out branch: y = x + dropout(f) in one pass, the same mask as dropout_kernel(f)
+// (so the backward of the branch is dropout_kernel(dy) with the same seed) and the same bf16 rounding as the
+// two-kernel form (the dropped branch value is rounded before the add).
+__global__ void add_dropout_kernel(const bf16_t* x, const bf16_t* f, bf16_t* y, long n8, float keep, uint64_t seed) {
+  const float inv = 1.f / keep;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float a[8], b[8];
+    load8(x + i * 8, a);
+    load8(f + i * 8, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += uhash(seed, i * 8 + j) < keep ? bf2f(f2bf(b[j] * inv)) : 0.f;
+    store8(y + i * 8, a);
+  }
+}
+
 // Column partial sums of a bf16 [M][N] matrix (BiasAddGrad core), N % 8 == 0. Block (bx, by) owns columns
 // [256 bx, 256 bx + 256) (32 lanes x 8 columns, 512 contiguous bytes per row) and rows [by rpb, by rpb + rpb)
 // (8 row-threads); it writes its partial sums to part[by][N]. No atomics: dtf_sum_rows finishes the reduction
@@ -517,6 +532,13 @@ DTF_API int dtf_add_bf16(const void* a, const void* b, void* y, long n, float al
 DTF_API int dtf_act(const void* x, const void* dy, void* y, long n, int act, int bwd, void* stream) {
   if (n & 7) return -1;
   hipLaunchKernelGGL(act_kernel, GRID(n / 8), (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)y, n / 8, act, bwd);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_add_dropout(const void* x, const void* f, void* y, long n, float keep, unsigned long long seed,
+                            void* stream) {
+  if (n & 7) return -1;
+  hipLaunchKernelGGL(add_dropout_kernel, GRID(n / 8), (const bf16_t*)x, (const bf16_t*)f, (bf16_t*)y, n / 8, keep,
+                     (uint64_t)seed);
   return (int)hipGetLastError();
 }
 DTF_API int dtf_dropout(const void* x, void* y, long n, float keep, unsigned long long seed, void* stream) {

@@ -36,6 +36,7 @@ _KERNEL_SIGS = {
     "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],
     "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "dtf_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
+    "dtf_add_dropout": [P, P, P, L, F, U, P],
     "dtf_softmax_ce_fwd": [P, I, P, P, P, L, I, F, P],
     "dtf_softmax_ce_bwd": [P, I, P, P, P, P, L, I, F, P],
     "dtf_nchw_to_s2d": [P, P, I, I, I, I, P],

@@ -62,10 +62,8 @@ class BertLayer(KL.Layer):
         self.dropout = dropout
 
     def call(self, x, mask=None, training=None):
-        a = ops.dropout(self.att(x, mask, training=training), self.dropout, training=bool(training))
-        x = self.ln1(ops.add(x, a))
-        f = ops.dropout(self.ff2(self.ff1(x)), self.dropout, training=bool(training))
-        return self.ln2(ops.add(x, f))
+        x = self.ln1(ops.add_dropout(x, self.att(x, mask, training=training), self.dropout, bool(training)))
+        return self.ln2(ops.add_dropout(x, self.ff2(self.ff1(x)), self.dropout, bool(training)))
 
 
 class BertModel(Model):
@@ -135,8 +133,8 @@ class GPT2Block(KL.Layer):
         self.dropout = dropout
 
     def call(self, x, training=None):
-        x = ops.add(x, ops.dropout(self.att(self.ln1(x), training=training), self.dropout, training=bool(training)))
-        return ops.add(x, ops.dropout(self.proj(self.fc(self.ln2(x))), self.dropout, training=bool(training)))
+        x = ops.add_dropout(x, self.att(self.ln1(x), training=training), self.dropout, bool(training))
+        return ops.add_dropout(x, self.proj(self.fc(self.ln2(x))), self.dropout, bool(training))
 
 
 class GPT2(Model):

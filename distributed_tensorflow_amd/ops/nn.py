@@ -131,6 +131,41 @@ def dropout(x, rate, training=True, seed=None):
     return torch.nn.functional.dropout(x, rate, True)
 
 
+_FUSE_ADD_DROPOUT = __import__("os").environ.get("DTF_FUSE_ADD_DROPOUT", "1") != "0"
+
+
+class _AddDropoutFn(torch.autograd.Function):
+    """y = x + dropout(f): one pass forward; backward dx = dy, df = dropout(dy) with the same mask."""
+
+    @staticmethod
+    def forward(ctx, x, f, keep, seed):
+        x, f = x.contiguous(), f.contiguous()
+        y = torch.empty_like(x)
+        call("dtf_add_dropout", ptr(x), ptr(f), ptr(y), x.numel(), float(keep), int(seed), stream())
+        ctx.keep, ctx.seed = keep, seed
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.to(BF16).contiguous()
+        df = torch.empty_like(dy)
+        call("dtf_dropout", ptr(dy), ptr(df), dy.numel(), float(ctx.keep), int(ctx.seed), stream())
+        return dy, df, None, None
+
+
+def add_dropout(x, f, rate, training=True, seed=None):
+    """Residual connection around a dropped-out branch: x + dropout(f, rate) (fused on GPU)."""
+    if not training or rate <= 0.0:
+        return add(x, f)
+    if _FUSE_ADD_DROPOUT and on_gpu(x) and x.dtype == BF16 and f.dtype == BF16 and x.shape == f.shape \
+            and x.numel() % 8 == 0:
+        if seed is None:
+            _seed_counter[0] += 1
+            seed = _seed_counter[0] * 0x9E3779B1
+        return _AddDropoutFn.apply(x, f, 1.0 - rate, seed & 0xFFFFFFFFFFFFFFFF)
+    return add(x, dropout(f, rate, training, seed))
+
+
 def add(a, b):
     if on_gpu(a) and a.dtype == BF16 and b.dtype == BF16 and a.numel() % 8 == 0 and a.shape == b.shape:
         return _AddFn.apply(a, b)

@@ -501,3 +501,18 @@ def test_conv_wgrad_lds_dma_matches(cuda, case, tile, monkeypatch):
     wr = torch.zeros(K, Cin, R, S, device=cuda, requires_grad=True)
     torch.nn.functional.conv2d(xr, wr, stride=st, padding=pd).backward(dy.float().permute(0, 3, 1, 2))
     close(got.permute(0, 3, 1, 2), wr.grad, 1e-2)
+
+
+def test_add_dropout_matches_two_kernel_form(cuda):
+    """x + dropout(f) in one pass == add(x, dropout(f)) with the same seed, bit for bit, forward and backward;
+    the realised keep rate matches."""
+    x = rnd(64, 768, dev=cuda).requires_grad_(True)
+    f = rnd(64, 768, dev=cuda).requires_grad_(True)
+    dy = rnd(64, 768, dev=cuda)
+    y1 = ops.add_dropout(x, f, 0.1, training=True, seed=1234)
+    gx1, gf1 = torch.autograd.grad(y1, [x, f], dy)
+    y2 = ops.add(x, ops.dropout(f, 0.1, training=True, seed=1234))
+    gx2, gf2 = torch.autograd.grad(y2, [x, f], dy)
+    assert torch.equal(y1, y2) and torch.equal(gx1, gx2) and torch.equal(gf1, gf2)
+    kept = (gf1 != 0).float().mean().item()
+    assert abs(kept - 0.9) < 0.01
