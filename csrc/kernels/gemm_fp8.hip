@@ -13,33 +13,61 @@ namespace {
 
 __device__ __forceinline__ float fp8_max() { return 448.f; }
 
-// 8 bf16 -> 8 e4m3 bytes; scale_inv = 1/scale
+// 8 bf16 -> 8 e4m3 bytes (x * inv, saturated to +-448)
+__device__ __forceinline__ uint2 quant8(const float* f, float inv) {
+  uint32_t w[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float a0 = fminf(fmaxf(f[4 * h + 0] * inv, -fp8_max()), fp8_max());
+    float a1 = fminf(fmaxf(f[4 * h + 1] * inv, -fp8_max()), fp8_max());
+    float a2 = fminf(fmaxf(f[4 * h + 2] * inv, -fp8_max()), fp8_max());
+    float a3 = fminf(fmaxf(f[4 * h + 3] * inv, -fp8_max()), fp8_max());
+    int r = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
+    w[h] = (uint32_t)r;
+  }
+  return make_uint2(w[0], w[1]);
+}
+
+// Grid-stride passes over 8-element chunks, QU chunks per thread per trip with every load issued before any use
+// (a trip keeps 4 x 16 B per lane in flight: the pass is HBM-latency bound otherwise).
+constexpr int QU = 4;
+
+// x (bf16) -> e4m3 with scale; amax(|x|) of the pass is max-ed into *amax (delayed scaling)
 __global__ void __launch_bounds__(256) quant_fp8_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q, long n8,
                                                         const float* __restrict__ scale, float* __restrict__ amax) {
   __shared__ float red[16];
   const float inv = 1.f / fmaxf(scale[0], 1e-30f);
   float m = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (QU - 1) * stride < n8; i += QU * stride) {
+    float f[QU][8];
+#pragma unroll
+    for (int u = 0; u < QU; ++u) load8(x + (i + u * stride) * 8, f[u]);
+#pragma unroll
+    for (int u = 0; u < QU; ++u) {
+      *reinterpret_cast<uint2*>(q + (i + u * stride) * 8) = quant8(f[u], inv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[u][j]));
+    }
+  }
+  for (; i < n8; i += stride) {
     float f[8];
     load8(x + i * 8, f);
-    uint32_t w[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float a0 = fminf(fmaxf(f[4 * h + 0] * inv, -fp8_max()), fp8_max());
-      float a1 = fminf(fmaxf(f[4 * h + 1] * inv, -fp8_max()), fp8_max());
-      float a2 = fminf(fmaxf(f[4 * h + 2] * inv, -fp8_max()), fp8_max());
-      float a3 = fminf(fmaxf(f[4 * h + 3] * inv, -fp8_max()), fp8_max());
-      int r = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
-      r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
-      w[h] = (uint32_t)r;
-    }
+    *reinterpret_cast<uint2*>(q + i * 8) = quant8(f, inv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[j]));
-    *reinterpret_cast<uint2*>(q + i * 8) = make_uint2(w[0], w[1]);
   }
   if (amax) {
     m = block_max(m, red);
-    if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+    // only blocks that can raise the running maximum issue the atomic: thousands of same-address atomics
+    // serialise at the memory side, and most blocks' maxima are below the first few published ones
+    if (threadIdx.x == 0) {
+      unsigned int* a = reinterpret_cast<unsigned int*>(amax);
+      const unsigned int cur = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__float_as_uint(m) > cur) atomicMax(a, __float_as_uint(m));
+    }
   }
 }
 
@@ -56,7 +84,18 @@ __global__ void __launch_bounds__(256) absmax_part_kernel(const bf16_t* __restri
                                                           float* __restrict__ part) {
   __shared__ float red[16];
   float m = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (QU - 1) * stride < n8; i += QU * stride) {
+    float f[QU][8];
+#pragma unroll
+    for (int u = 0; u < QU; ++u) load8(x + (i + u * stride) * 8, f[u]);
+#pragma unroll
+    for (int u = 0; u < QU; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[u][j]));
+  }
+  for (; i < n8; i += stride) {
     float f[8];
     load8(x + i * 8, f);
 #pragma unroll
@@ -77,21 +116,19 @@ __global__ void __launch_bounds__(256) quant_fp8_exact_kernel(const bf16_t* __re
   const float scale = fmaxf(m, 1e-12f) / fp8_max();
   if (blockIdx.x == 0 && threadIdx.x == 0) scale_out[0] = scale;
   const float inv = 1.f / scale;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (QU - 1) * stride < n8; i += QU * stride) {
+    float f[QU][8];
+#pragma unroll
+    for (int u = 0; u < QU; ++u) load8(x + (i + u * stride) * 8, f[u]);
+#pragma unroll
+    for (int u = 0; u < QU; ++u) *reinterpret_cast<uint2*>(q + (i + u * stride) * 8) = quant8(f[u], inv);
+  }
+  for (; i < n8; i += stride) {
     float f[8];
     load8(x + i * 8, f);
-    uint32_t w[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float a0 = fminf(fmaxf(f[4 * h + 0] * inv, -fp8_max()), fp8_max());
-      float a1 = fminf(fmaxf(f[4 * h + 1] * inv, -fp8_max()), fp8_max());
-      float a2 = fminf(fmaxf(f[4 * h + 2] * inv, -fp8_max()), fp8_max());
-      float a3 = fminf(fmaxf(f[4 * h + 3] * inv, -fp8_max()), fp8_max());
-      int r = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
-      r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
-      w[h] = (uint32_t)r;
-    }
-    *reinterpret_cast<uint2*>(q + i * 8) = make_uint2(w[0], w[1]);
+    *reinterpret_cast<uint2*>(q + i * 8) = quant8(f, inv);
   }
 }
 
@@ -109,20 +146,18 @@ DTF_API int dtf_quant_fp8(const void* x, void* q, long n, const float* scale, fl
   if (n & 7) return -1;
   hipStream_t st = (hipStream_t)stream;
   if (amax && zero_amax) (void)hipMemsetAsync(amax, 0, sizeof(float), st);
-  int grid = stream_grid(n / 8, 256);
-  if (grid > 1024) grid = 1024;
+  int grid = stream_grid(n / 8 / QU, 256);
   hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, (uint8_t*)q, n / 8, scale,
                      amax);
   return (int)hipGetLastError();
 }
 
 // Exact per-tensor quantization (weights): scale_out = amax(|x|)/448 computed on the device, two launches,
-// ws >= 1024 floats of scratch for the per-block partials.
+// ws >= 2048 floats of scratch for the per-block partials.
 DTF_API int dtf_quant_fp8_exact(const void* x, void* q, long n, float* scale_out, float* ws, void* stream) {
   if (n & 7) return -1;
   hipStream_t st = (hipStream_t)stream;
-  int grid = stream_grid(n / 8, 256);
-  if (grid > 1024) grid = 1024;
+  int grid = stream_grid(n / 8 / QU, 256);  // <= 2048 partials
   hipLaunchKernelGGL(absmax_part_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, n / 8, ws);
   hipLaunchKernelGGL(quant_fp8_exact_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, (uint8_t*)q, n / 8, ws,
                      grid, scale_out);
