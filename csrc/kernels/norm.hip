@@ -253,19 +253,33 @@ __device__ __forceinline__ void bn_apply_row(const bf16_t* __restrict__ x, const
   }
 }
 
+// rscale/rshift (optional): the residual is itself a BatchNorm input (a projection shortcut's conv output) whose
+// affine normalisation is applied here, so the shortcut's BN output is never materialised.
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
-                                                       long M, int C, int relu, uint8_t* __restrict__ mbits) {
+                                                       long M, int C, int relu, uint8_t* __restrict__ mbits,
+                                                       const float* __restrict__ rscale,
+                                                       const float* __restrict__ rshift) {
   const ColGeo g = colgeo(C);
   const int t = threadIdx.x;
   if (t >= g.TPR * g.RPB) return;
   const int rsub = t / g.TPR;
   const long rstep = (long)gridDim.x * g.RPB;
   for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
-    float sc[8], sh[8];
+    float sc[8], sh[8], rsc[8], rsh[8];
     load_coef8(scale + cc * 8, sc);
     load_coef8(shift + cc * 8, sh);
+    if (rscale) {
+      load_coef8(rscale + cc * 8, rsc);
+      load_coef8(rshift + cc * 8, rsh);
+    }
+    auto raff = [&](float* rv) {
+      if (rscale) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rv[j] = fmaf(rv[j], rsc[j], rsh[j]);
+      }
+    };
     long r = (long)blockIdx.x * g.RPB + rsub;
     for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
       float f[EU][8], rv[EU][8];
@@ -276,14 +290,19 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
         if (res) load8(res + i8 * 8, rv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < EU; ++u)
+      for (int u = 0; u < EU; ++u) {
+        if (res) raff(rv[u]);
         bn_apply_row(x, res, y, mbits, (r + u * rstep) * g.cols8 + cc, f[u], rv[u], sc, sh, relu);
+      }
     }
     for (; r < M; r += rstep) {
       float f[8], rv[8];
       const long i8 = r * g.cols8 + cc;
       load8(x + i8 * 8, f);
-      if (res) load8(res + i8 * 8, rv);
+      if (res) {
+        load8(res + i8 * 8, rv);
+        raff(rv);
+      }
       bn_apply_row(x, res, y, mbits, i8, f, rv, sc, sh, relu);
     }
   }
@@ -865,12 +884,13 @@ DTF_API int dtf_bn_infer_coeff(const float* gamma, const float* beta, const floa
 }
 
 // mbits (optional, relu only): 1-bit ReLU mask, M*C/8 bytes, consumed by dtf_bn_bwd instead of re-reading y
+// rscale/rshift (optional, with res): res is a BN input; res * rscale + rshift is added (see bn_apply_kernel)
 DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, const void* res, void* y, long M,
-                         int C, int relu, void* mbits, void* stream) {
-  if (C & 7) return -1;
+                         int C, int relu, void* mbits, const float* rscale, const float* rshift, void* stream) {
+  if ((C & 7) || ((rscale == nullptr) != (rshift == nullptr))) return -1;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M, C)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, M, C, relu,
-                     relu ? (uint8_t*)mbits : nullptr);
+                     relu ? (uint8_t*)mbits : nullptr, res ? rscale : nullptr, res ? rshift : nullptr);
   return (int)hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ _KERNEL_SIGS = {
     "dtf_bn_stats": [P, L, I, P, P, P],
     "dtf_bn_finalize": [P, I, P, P, P, P, L, I, F, F, P, P, P, P, P],
     "dtf_bn_infer_coeff": [P, P, P, P, I, F, P, P, P],
-    "dtf_bn_apply": [P, P, P, P, P, L, I, I, P, P],
+    "dtf_bn_apply": [P, P, P, P, P, L, I, I, P, P, P, P],
     "dtf_bn_bwd": [P, P, P, P, P, P, P, L, I, P, P, P, P, I, P, P],
     "dtf_layernorm_fwd": [P, P, P, P, P, P, L, I, F, P],
     "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],

@@ -205,6 +205,7 @@ class _BNSource:
 
 _FUSE_BN_BWD = __import__("os").environ.get("DTF_FUSE_BN_BWD", "1") != "0"
 _LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
+_DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -233,12 +234,20 @@ class _ConvBNFn(torch.autograd.Function):
             yc = conv_fwd_raw(x, bf16_shadow(w), g)
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
                  ptr(shift), stream())
-        out = torch.empty_like(yc)
+        raff = getattr(res, "_dtf_affine", None) if res is not None else None
         if res is not None:
             res = res.contiguous()
         mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if relu else None
-        call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
-             stream())
+        if role == "proj" and not relu and _DEFER_PROJ_BN:
+            # projection shortcut: its BN output is consumed only as the residual of the block's last ConvBN,
+            # whose apply pass normalises the conv output on the fly (res * scale + shift) — hand autograd the
+            # conv output tagged with the affine instead of materialising the BN output
+            out = yc
+            out._dtf_affine = (scale, shift)
+        else:
+            out = torch.empty_like(yc)
+            call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
+                 ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, stream())
         # backward needs the conv output and a 1-bit ReLU mask, not the bf16 BN output
         ctx.save_for_backward(x, w, gamma, yc, mbits, mean, invstd)
         ctx.bn_params = (gamma, beta)

@@ -50,7 +50,7 @@ class _BNFn(torch.autograd.Function):
             res = res.to(BF16).contiguous()
         mbits = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if relu else None
         call("dtf_bn_apply", ptr(x), ptr(scale), ptr(shift), ptr(res), ptr(out), M, C, int(relu), ptr(mbits),
-             stream())
+             None, None, stream())
         ctx.save_for_backward(x, gamma, mbits, mean, invstd)
         ctx.relu = relu
         ctx.has_res = res is not None

@@ -31,7 +31,13 @@ def _emu_conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=
     y = rnd(OC._ref_conv(rnd(x), rnd(w), None, tuple(stride), tuple(pad), tuple(dil)))
     y = batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training)
     if residual is not None:
-        y = y + rnd(residual)
+        y = y + (residual if getattr(residual, "_emu_unrounded", False) else rnd(residual))
+    if role == "proj" and not relu and OC._DEFER_PROJ_BN:
+        # the GPU never stores the projection's BN output: the block's last BN apply normalises the projection
+        # conv output on the fly (ops.conv._DEFER_PROJ_BN), so the residual it adds is not bf16-rounded
+        y = y.clone()
+        y._emu_unrounded = True
+        return y
     return rnd(torch.relu(y) if relu else y)
 
 

@@ -37,9 +37,9 @@ def main():
         work = torch.empty((2 * 1024 + 3) * C, device=dev)
         n = M * C * 2  # bytes of one bf16 tensor
         t_copy = timeit(lambda: y.copy_(x))
-        t_app = timeit(lambda: call("dtf_bn_apply", ptr(x), ptr(sc), ptr(sh), None, ptr(y), M, C, 1, ptr(mb),
+        t_app = timeit(lambda: call("dtf_bn_apply", ptr(x), ptr(sc), ptr(sh), None, ptr(y), M, C, 1, ptr(mb), None, None,
                                     stream()))
-        t_res = timeit(lambda: call("dtf_bn_apply", ptr(x), ptr(sc), ptr(sh), ptr(res), ptr(y), M, C, 1, ptr(mb),
+        t_res = timeit(lambda: call("dtf_bn_apply", ptr(x), ptr(sc), ptr(sh), ptr(res), ptr(y), M, C, 1, ptr(mb), None, None,
                                     stream()))
         t_bwd = timeit(lambda: call("dtf_bn_bwd", ptr(dy), None, ptr(mb), ptr(x), ptr(mean), ptr(inv), ptr(gm), M, C,
                                     ptr(dx), None, ptr(dg), ptr(db), 0, ptr(work), stream()))
