@@ -427,23 +427,45 @@ __device__ __forceinline__ void bn_bwd_apply_row(const float* d, const float* xv
 
 // dx = a*dz + b*x + c per channel (coefficients from bn_bwd_finalize); dz_out: the masked dz for the
 // residual branch (only when a ReLU mask is given)
+// SC: the masked dz (dz_out, the residual gradient) also feeds a projection shortcut's BatchNorm whose input is
+// x2 (mean2): its backward reduction (sum dz, sum dz*(x2 - mean2), over the bf16-rounded dz that is stored) is
+// taken here as one partial row per block into part2 — the shortcut's own reduce pass disappears.
+// (host: C/8 <= 256 and 256 % (C/8) == 0, so every thread owns exactly one channel chunk)
+template <bool SC>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ ymask,
                                                            const uint8_t* __restrict__ mbits,
                                                            const bf16_t* __restrict__ x,
                                                            const float* __restrict__ coef, long M, int C,
-                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out) {
+                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out,
+                                                           const bf16_t* __restrict__ x2,
+                                                           const float* __restrict__ mean2,
+                                                           float* __restrict__ part2) {
   const ColGeo g = colgeo(C);
   const int t = threadIdx.x;
-  if (t >= g.TPR * g.RPB) return;
+  if (!SC && t >= g.TPR * g.RPB) return;
   const int rsub = t / g.TPR;
   const long rstep = (long)gridDim.x * g.RPB;
   if (!ymask && !mbits) dz_out = nullptr;
+  float s2[8] = {0}, q2[8] = {0}, mu2[8];
+  auto sc_acc = [&](const float* d, long i8) {
+    if constexpr (SC) {
+      float x2v[8];
+      load8(x2 + i8 * 8, x2v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dz = bf2f(f2bf(d[j]));
+        s2[j] += dz;
+        q2[j] = fmaf(dz, x2v[j] - mu2[j], q2[j]);
+      }
+    }
+  };
   for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
     float ka[8], kb[8], kc[8];
     load_coef8(coef + cc * 8, ka);
     load_coef8(coef + C + cc * 8, kb);
     load_coef8(coef + 2 * C + cc * 8, kc);
+    if constexpr (SC) load_coef8(mean2 + cc * 8, mu2);
     long r = (long)blockIdx.x * g.RPB + rsub;
     for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
       float d[EU][8], xv[EU][8];
@@ -455,7 +477,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
         relu_mask8(d[u], ymask, mbits, i8);
       }
 #pragma unroll
-      for (int u = 0; u < EU; ++u) bn_bwd_apply_row(d[u], xv[u], ka, kb, kc, dx, dz_out, (r + u * rstep) * g.cols8 + cc);
+      for (int u = 0; u < EU; ++u) {
+        bn_bwd_apply_row(d[u], xv[u], ka, kb, kc, dx, dz_out, (r + u * rstep) * g.cols8 + cc);
+        sc_acc(d[u], (r + u * rstep) * g.cols8 + cc);
+      }
     }
     for (; r < M; r += rstep) {
       float d[8], xv[8];
@@ -464,7 +489,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
       load8(x + i8 * 8, xv);
       relu_mask8(d, ymask, mbits, i8);
       bn_bwd_apply_row(d, xv, ka, kb, kc, dx, dz_out, i8);
+      sc_acc(d, i8);
     }
+  }
+  if constexpr (SC) {
+    __shared__ float red[4096];
+    block_col_partials(s2, q2, 0, g.TPR, g.RPB, C, part2 + (long)blockIdx.x * 2 * C, red);
   }
 }
 
@@ -894,17 +924,26 @@ DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, 
   return (int)hipGetLastError();
 }
 
+struct ShortcutStats {  // optional fused projection-shortcut BN reduction (bn_bwd_apply_kernel<true>)
+  const void* x2;
+  const float* mean2;
+  float* part2;
+  int* rows2;
+};
 static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
-                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st);
+                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,
+                       const ShortcutStats* sc = nullptr);
 
 // work: (2*1024 + 3) * C floats (partials + coefficients)
 // ReLU mask from mbits (1 bit/element, preferred) or from the bf16 output ymask; neither = no ReLU
 DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd,
                        const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma, float* dbeta,
-                       int accumulate, float* work, void* stream) {
+                       int accumulate, float* work, const void* x2, const float* mean2, float* part2, int* rows2,
+                       void* stream) {
   if (C & 7) return -1;
+  const ShortcutStats sc{x2, mean2, part2, rows2};
   hipStream_t st = (hipStream_t)stream;
   float* coef = work;
   float* part = work + 3 * C;
@@ -912,7 +951,7 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
                      (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part);
   return bn_bwd_tail(dy, ymask, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, G,
-                     coef, st);
+                     coef, st, &sc);
 }
 
 // Backward with the reduction already done by the GEMM that produced dy (dtf_conv_dgrad's fused BN-backward
@@ -920,10 +959,11 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
 DTF_API int dtf_bn_bwd_partials(const void* dy, const void* mbits, const void* x, const float* mean,
                                 const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out,
                                 float* dgamma, float* dbeta, int accumulate, float* part, int T, float* coef,
-                                void* stream) {
+                                const void* x2, const float* mean2, float* part2, int* rows2, void* stream) {
   if ((C & 7) || T < 1) return -1;
+  const ShortcutStats sc{x2, mean2, part2, rows2};
   return bn_bwd_tail(dy, nullptr, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, T,
-                     coef, (hipStream_t)stream);
+                     coef, (hipStream_t)stream, &sc);
 }
 
 // Sum the G partial rows [G][2C] of a BN backward reduction and finalize: dgamma/dbeta and the apply
@@ -948,11 +988,22 @@ static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const 
 
 static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
-                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st) {
+                       float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,
+                       const ShortcutStats* sc) {
   bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(M, C)), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                     (bf16_t*)dz_out);
+  const ColGeo geo = colgeo(C);
+  const int grid = ew_grid(M, C);
+  const bool fuse_sc = sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&
+                       geo.TPR * geo.RPB == 256;
+  if (sc && sc->rows2) *sc->rows2 = fuse_sc ? grid : 0;
+  if (fuse_sc)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
+                       (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
+                       (bf16_t*)dz_out, nullptr, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 

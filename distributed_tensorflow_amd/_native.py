@@ -25,13 +25,13 @@ _KERNEL_SIGS = {
     "dtf_gemm": [P, P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, L, L, L, F, F, I, I, I, I, P, L, P],
     "dtf_conv_fwd": [P, P, P, P, P, P] + [I] * 15 + [I, I, I, P],
     "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P, L, P, P, P, P, P, P, P],
-    "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P],
+    "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P],
     "dtf_conv_wgrad": [P, P, P] + [I] * 15 + [I, I, I, P, L, P],
     "dtf_bn_stats": [P, L, I, P, P, P],
     "dtf_bn_finalize": [P, I, P, P, P, P, L, I, F, F, P, P, P, P, P],
     "dtf_bn_infer_coeff": [P, P, P, P, I, F, P, P, P],
     "dtf_bn_apply": [P, P, P, P, P, L, I, I, P, P, P, P],
-    "dtf_bn_bwd": [P, P, P, P, P, P, P, L, I, P, P, P, P, I, P, P],
+    "dtf_bn_bwd": [P, P, P, P, P, P, P, L, I, P, P, P, P, I, P, P, P, P, P, P],
     "dtf_layernorm_fwd": [P, P, P, P, P, P, L, I, F, P],
     "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],
     "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],

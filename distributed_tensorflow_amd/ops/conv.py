@@ -235,6 +235,8 @@ class _ConvBNFn(torch.autograd.Function):
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
                  ptr(shift), stream())
         raff = getattr(res, "_dtf_affine", None) if res is not None else None
+        # the deferred projection BN (its input + mean): its backward reduction is taken in our apply pass
+        res_src = getattr(res, "_dtf_bnsrc", None) if raff is not None else None
         if res is not None:
             res = res.contiguous()
         mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if relu else None
@@ -257,6 +259,7 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.training = training
         ctx.link, ctx.role = link, role
         ctx.in_src = in_src if (ctx.needs_input_grad[0] and _FUSE_BN_BWD) else None
+        ctx.res_src = res_src if (training and _FUSE_BN_BWD) else None
         ctx.src = None
         if training and _FUSE_BN_BWD and any(ctx.needs_input_grad):
             src = _BNSource(yc, mbits, mean)
@@ -283,15 +286,23 @@ class _ConvBNFn(torch.autograd.Function):
         dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
         dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
         fused = ctx.src.take(dout) if ctx.src is not None else None
+        rsrc = ctx.res_src if dres is not None else None
+        sc = (None, None, None, None)
+        if rsrc is not None:  # projection shortcut BN: its backward reduction rides on our apply pass
+            part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=yc.device), IntOut()
+            sc = (ptr(rsrc.yc), ptr(rsrc.mean), ptr(part2), rows2.addr)
         if fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
             coef = torch.empty(3 * K, dtype=F32, device=yc.device)
             call("dtf_bn_bwd_partials", ptr(dout), ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
                  ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(fused[0]), fused[1], ptr(coef),
-                 stream())
+                 *sc, stream())
         else:
             work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
             call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
-                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), stream())
+                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), *sc, stream())
+        if rsrc is not None and rows2.value > 0:
+            rsrc.provide(dres, part2, rows2.value)
+        ctx.res_src = None
         ctx.src = None
         if ctx.has_res and not ctx.relu:
             dres = dout

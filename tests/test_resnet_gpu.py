@@ -113,9 +113,9 @@ def test_fused_bn_backward_reduction_matches_separate_pass(cuda, monkeypatch):
         runs[fuse] = _run(_blocks(), x)
         n_fused = seen.count("dtf_bn_bwd_partials")
         if fuse:
-            # bn1 and bn2 of both blocks (via the c2/c3 dgrads) and block 0's output BN (via block 1's
-            # residual-link c1 dgrad)
-            assert n_fused == 5, seen
+            # bn1 and bn2 of both blocks (via the c2/c3 dgrads), block 0's output BN (via block 1's
+            # residual-link c1 dgrad) and block 0's projection BN (via its c3 BN backward apply pass)
+            assert n_fused == 6, seen
         else:
             assert n_fused == 0
     worst = 0.0
