@@ -266,8 +266,12 @@ static bool rowmap_ok() {
 
 static int choose_splitk(long M, long N, long K, int tile_m, int tile_n, long batch) {
   long tiles = (long)cdiv(M, tile_m) * cdiv(N, tile_n) * batch;
+  static const long target = [] {
+    const char* e = getenv("DTF_SPLITK_BLOCKS");  // blocks a split-K launch aims for (2 per CU by default)
+    return e ? std::max(64L, atol(e)) : 512L;
+  }();
   if (tiles >= 256 || K <= 1024) return 1;
-  long want = (512 + tiles - 1) / tiles;
+  long want = (target + tiles - 1) / tiles;
   if (want > 256) want = 256;
   long maxs = K / 512;  // keep >= 512 of K per split
   if (want > maxs) want = maxs;
