@@ -16,6 +16,10 @@ from .. import ops
 from ..ops import mha as attn_ops
 from ..keras import layers as KL
 from ..keras.models import Model
+from ..ops.conv import ResidualGradLink
+
+# off by default: hipBLASLt's addmm (bf16 C) measured ~0.5-1% slower on BERT-base than mm + autograd's add
+RES_LINK = __import__("os").environ.get("DTF_TF_RES_LINK", "0") == "1"
 
 
 class _Proj(KL.Layer):
@@ -31,11 +35,11 @@ class _Proj(KL.Layer):
         self.bias = self.add_weight("bias", (self.units,), "zeros")
         self.built = True
 
-    def call(self, x, training=None):
+    def call(self, x, training=None, link=None):
         if self.fp8 and x.is_cuda:
             from ..ops.fp8 import dense_fp8
             return dense_fp8(x, self.kernel, self.bias, self.activation, self)
-        return ops.dense(x, self.kernel, self.bias, act=self.activation)
+        return ops.dense(x, self.kernel, self.bias, act=self.activation, link=link)
 
 
 class MultiHeadSelfAttention(KL.Layer):
@@ -45,8 +49,8 @@ class MultiHeadSelfAttention(KL.Layer):
         self.qkv = _Proj(3 * hidden, fp8=fp8)
         self.out = _Proj(hidden, fp8=fp8)
 
-    def call(self, x, mask=None, training=None):
-        o = attn_ops.attention_packed(self.qkv(x), self.heads, causal=self.causal, mask=mask,
+    def call(self, x, mask=None, training=None, link=None):
+        o = attn_ops.attention_packed(self.qkv(x, link=link), self.heads, causal=self.causal, mask=mask,
                                       dropout=self.dropout, training=training)
         return self.out(o)
 
@@ -62,8 +66,13 @@ class BertLayer(KL.Layer):
         self.dropout = dropout
 
     def call(self, x, mask=None, training=None):
-        x = self.ln1(ops.add_dropout(x, self.att(x, mask, training=training), self.dropout, bool(training)))
-        return self.ln2(ops.add_dropout(x, self.ff2(self.ff1(x)), self.dropout, bool(training)))
+        # residual gradients of x join the data-gradient GEMM of the branch's first projection (ResidualGradLink)
+        l1, l2 = (ResidualGradLink(), ResidualGradLink()) if (RES_LINK and training and x.is_cuda
+                                                              and torch.is_grad_enabled()) else (None, None)
+        a = self.att(x, mask, training=training, link=l1)
+        x = self.ln1(ops.add_dropout(x, a, self.dropout, bool(training), link=l1))
+        f = self.ff2(self.ff1(x, link=l2))
+        return self.ln2(ops.add_dropout(x, f, self.dropout, bool(training), link=l2))
 
 
 class BertModel(Model):

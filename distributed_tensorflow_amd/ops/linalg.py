@@ -132,11 +132,15 @@ _PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "1") != "0"
 _BLAS_WGRAD_MIN = 4 << 20
 
 
-def dense_dgrad(dz, w16):
-    """dX[T, in] = dZ[T, out] W[out, in] (bf16)."""
+def dense_dgrad(dz, w16, acc=None):
+    """dX[T, in] = dZ[T, out] W[out, in] (bf16); with `acc` (another gradient of the same input, [T, in]) the GEMM
+    adds it (one rounding, no separate add pass)."""
     if _PLAIN_BLAS:
-        return torch.mm(dz, w16)
-    return gemm(dz, w16, b_kouter=True)
+        return torch.mm(dz, w16) if acc is None else torch.addmm(acc, dz, w16)
+    if acc is None:
+        return gemm(dz, w16, b_kouter=True)
+    out = acc.clone()
+    return gemm(dz, w16, b_kouter=True, out=out, beta=1.0)
 
 
 def dense_wgrad(dz, x2, out=None):
@@ -162,8 +166,10 @@ def _act_ref(x, act):
 
 class _DenseFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act):
+    def forward(ctx, x, w, b, act, link=None):
         # x: [..., in] bf16 ; w: [out, in] f32 master ; b: [out] f32 or None
+        # link: ops.conv.ResidualGradLink whose parked gradient of x the data-gradient GEMM adds in
+        ctx.link = link
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if not x2.is_contiguous():
@@ -193,7 +199,9 @@ class _DenseFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             # dx[t,i] = sum_o dz[t,o] W[o,i]  -> B stored [K=out][N=in] (k-outer)
-            dx = dense_dgrad(dz, bf16_shadow(w)).reshape(ctx.shp)
+            acc = ctx.link.take()[0] if ctx.link is not None else None
+            dx = dense_dgrad(dz, bf16_shadow(w), None if acc is None else acc.reshape(dz.shape[0], -1))
+            dx = dx.reshape(ctx.shp)
         if ctx.needs_input_grad[1]:
             # dW[o,i] = sum_t dz[t,o] x[t,i]  -> both operands k-outer, f32 out; inside Model.train_step
             # accumulated straight into the arena gradient (beta = 1) instead of returned
@@ -208,16 +216,18 @@ class _DenseFn(torch.autograd.Function):
                 colsum(dz, out=tb, accumulate=True)
             else:
                 db = colsum(dz)
-        return dx, dw, db, None
+        ctx.link = None
+        return dx, dw, db, None, None
 
 
-def dense(x, w, b=None, act=None):
-    """y = act(x @ w^T + b); w is [out, in] (f32 master variable)."""
+def dense(x, w, b=None, act=None, link=None):
+    """y = act(x @ w^T + b); w is [out, in] (f32 master variable). link: ops.conv.ResidualGradLink joining x's
+    gradient from a residual connection into this layer's data-gradient GEMM."""
     a = act_code(act)
     if on_gpu(x):
         if x.dtype != BF16:
             x = x.to(BF16)
-        return _DenseFn.apply(x, w, b, a)
+        return _DenseFn.apply(x, w, b, a, link)
     y = torch.nn.functional.linear(x.to(w.dtype), w, b)
     return _act_ref(y, a)
 

@@ -138,11 +138,11 @@ class _AddDropoutFn(torch.autograd.Function):
     """y = x + dropout(f): one pass forward; backward dx = dy, df = dropout(dy) with the same mask."""
 
     @staticmethod
-    def forward(ctx, x, f, keep, seed):
+    def forward(ctx, x, f, keep, seed, link):
         x, f = x.contiguous(), f.contiguous()
         y = torch.empty_like(x)
         call("dtf_add_dropout", ptr(x), ptr(f), ptr(y), x.numel(), float(keep), int(seed), stream())
-        ctx.keep, ctx.seed = keep, seed
+        ctx.keep, ctx.seed, ctx.link = keep, seed, link
         return y
 
     @staticmethod
@@ -150,11 +150,15 @@ class _AddDropoutFn(torch.autograd.Function):
         dy = dy.to(BF16).contiguous()
         df = torch.empty_like(dy)
         call("dtf_dropout", ptr(dy), ptr(df), dy.numel(), float(ctx.keep), int(ctx.seed), stream())
-        return dy, df, None, None
+        dx = ctx.link.park(dy) if ctx.link is not None else dy  # None: the branch's first GEMM adds it
+        ctx.link = None
+        return dx, df, None, None, None
 
 
-def add_dropout(x, f, rate, training=True, seed=None):
-    """Residual connection around a dropped-out branch: x + dropout(f, rate) (fused on GPU)."""
+def add_dropout(x, f, rate, training=True, seed=None, link=None):
+    """Residual connection around a dropped-out branch: x + dropout(f, rate) (fused on GPU). link: a
+    ResidualGradLink shared with the branch's first Dense layer (ops.dense(..., link=)): the residual gradient
+    of x is then added inside that layer's data-gradient GEMM instead of by autograd."""
     if not training or rate <= 0.0:
         return add(x, f)
     if _FUSE_ADD_DROPOUT and on_gpu(x) and x.dtype == BF16 and f.dtype == BF16 and x.shape == f.shape \
@@ -162,7 +166,7 @@ def add_dropout(x, f, rate, training=True, seed=None):
         if seed is None:
             _seed_counter[0] += 1
             seed = _seed_counter[0] * 0x9E3779B1
-        return _AddDropoutFn.apply(x, f, 1.0 - rate, seed & 0xFFFFFFFFFFFFFFFF)
+        return _AddDropoutFn.apply(x, f, 1.0 - rate, seed & 0xFFFFFFFFFFFFFFFF, link)
     return add(x, dropout(f, rate, training, seed))
 
 

@@ -516,3 +516,27 @@ def test_add_dropout_matches_two_kernel_form(cuda):
     assert torch.equal(y1, y2) and torch.equal(gx1, gx2) and torch.equal(gf1, gf2)
     kept = (gf1 != 0).float().mean().item()
     assert abs(kept - 0.9) < 0.01
+
+
+def test_bert_layer_residual_grad_link(cuda, monkeypatch):
+    """BERT layer with the residual gradients joined inside the branch projections' data-gradient GEMMs
+    (ResidualGradLink through ops.add_dropout / ops.dense) == autograd summing them: same gradients up to the one
+    bf16 rounding of the sum."""
+    from distributed_tensorflow_amd.keras import initializers
+    from distributed_tensorflow_amd.models import transformer as T
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 64, 128, generator=g).to(cuda).to(BF)
+    dy = torch.randn(2, 64, 128, generator=g).to(cuda)
+    res = {}
+    for link in (False, True):
+        monkeypatch.setattr(T, "RES_LINK", link)
+        from distributed_tensorflow_amd.ops import mha as _mha, nn as _nn
+        _nn._seed_counter[0], _mha._seed_counter[0] = 0x5EED, 0  # same dropout masks in both runs
+        initializers.set_seed(7)
+        layer = T.BertLayer(hidden=128, heads=2, ffn=256, dropout=0.1)
+        xx = x.clone().requires_grad_(True)
+        y = layer(xx, training=True)
+        grads = torch.autograd.grad((y.float() * dy).sum(), [xx] + list(layer.trainable_weights))
+        res[link] = [t.float().cpu() for t in grads]
+    for a, b in zip(res[False], res[True]):
+        assert (a - b).abs().max().item() <= 2e-2 * a.abs().max().item() + 1e-6
