@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--allreduce-dtype", default=None, choices=["f32", "bf16"],
+                    help="gradient all-reduce payload type (default f32; bf16 halves the xGMI bytes)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture the whole train step in a hipGraph (compile(jit_compile=True))")
     args = ap.parse_args()
@@ -104,10 +106,11 @@ def main():
 
     from distributed_tensorflow_amd import parallel
 
+    co = parallel.CommunicationOptions(wire_dtype=args.allreduce_dtype)
     if args.model == "bert_base":
-        strategy = parallel.MultiWorkerMirroredStrategy(bucket_mb=args.bucket_mb)
+        strategy = parallel.MultiWorkerMirroredStrategy(communication_options=co, bucket_mb=args.bucket_mb)
     else:
-        strategy = parallel.MirroredStrategy(bucket_mb=args.bucket_mb)
+        strategy = parallel.MirroredStrategy(bucket_mb=args.bucket_mb, communication_options=co)
     rank = strategy.worker_index
     dev = strategy.device
     model, data, unit, cfg = build(args, strategy, dev, rank)
@@ -125,6 +128,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    bucketers = list(getattr(strategy, "_bucketers", {}).values())
+    for b in bucketers:
+        b.timing = hasattr(b, "exposed_ms")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         logs = step()
@@ -133,11 +139,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    exposed = [b.exposed_ms() for b in bucketers if hasattr(b, "exposed_ms")]
+    exposed = [e for e in exposed if e is not None]
     loss = float(logs["loss"])
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt, sum(exposed) if exposed else 0.0], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # slowest rank's clock and exposed communication
+    dt, exposed_max = float(t[0].item()), float(t[1].item())
     ms = dt / args.steps * 1e3
     global_batch = args.batch * world
     per_sample = getattr(args, "tokens_per_sample", 1)
@@ -159,11 +167,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / ref) if ref else None,
-            "dtype": "bf16",
+            "dtype": "bf16+fp8" if args.model.endswith("fp8") else "bf16",
             "data": "synthetic (random inputs + labels resident on GPU; random-init weights)",
             "config": dict(cfg, global_batch=global_batch, per_gpu_batch=args.batch, parallelism=f"dp{world}",
                            strategy=type(strategy).__name__ + " (1 process/GPU, RCCL)",
-                           optimizer=type(model.optimizer).__name__, final_loss=round(loss, 4)),
+                           optimizer=type(model.optimizer).__name__, final_loss=round(loss, 4),
+                           allreduce_dtype=args.allreduce_dtype or "f32",
+                           exposed_comm_ms_per_step=round(exposed_max, 3)),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

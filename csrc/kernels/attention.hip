@@ -44,6 +44,7 @@ struct AttnArgs {
   uint32_t thr;     // keep threshold on 16-bit uniforms (65536 = no dropout)
   float inv_keep;   // 65536 / thr
   uint32_t seed;
+  const unsigned long long* seedctr;  // optional device step counter (per-step masks under hipGraph replay)
   int nkq;          // (Sk + 3) / 4 hash blocks per query row
   int causal;
 };
@@ -57,7 +58,12 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   return h;
 }
 __device__ __forceinline__ uint32_t drop_salt(const AttnArgs& a, int bh) {
-  return fmix32(a.seed ^ ((uint32_t)bh * 0x9E3779B9u));
+  uint32_t s = a.seed;
+  if (a.seedctr) {
+    const unsigned long long c = *a.seedctr * 0xD1B54A32D192ED03ull;
+    s ^= (uint32_t)(c ^ (c >> 32));
+  }
+  return fmix32(s ^ ((uint32_t)bh * 0x9E3779B9u));
 }
 // 4 x 16-bit uniforms for keys 4 kq .. 4 kq + 3 of query q
 __device__ __forceinline__ uint2 drop_bits(const AttnArgs& a, uint32_t salt, int q, int kq) {
@@ -607,7 +613,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a, int nblk) 
 
 AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, const void* o,
                    const void* dout, const long* ostr, int B, int H, int Sq, int Sk, float scale, float dropout,
-                   unsigned long long seed, int causal, const float* kmask) {
+                   unsigned long long seed, int causal, const float* kmask,
+                   const unsigned long long* seedctr) {
   AttnArgs a{};
   a.q = (const bf16_t*)q;
   a.k = (const bf16_t*)k;
@@ -633,6 +640,7 @@ AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr
   a.thr = (uint32_t)thr;
   a.inv_keep = 65536.f / (float)thr;
   a.seed = (uint32_t)(seed ^ (seed >> 32));
+  a.seedctr = dropout > 0.f ? seedctr : nullptr;
   a.nkq = (Sk + 3) / 4;
   a.causal = causal;
   a.kmask = kmask;
@@ -648,11 +656,13 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // negative drop). dropout: probability of zeroing an attention weight (training).
 DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, void* o,
                          const long* ostr, float* lse, const float* kmask, int B, int H, int Sq, int Sk, int D,
-                         float scale, float dropout, unsigned long long seed, int causal, void* stream) {
+                         float scale, float dropout, unsigned long long seed, int causal, const void* seedctr,
+                         void* stream) {
   if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o)) return -1;
   if ((qstr[0] | qstr[1] | qstr[2] | kstr[0] | kstr[1] | kstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
   if (dropout < 0.f || dropout >= 1.f) return -1;
-  AttnArgs a = make_args(q, k, v, qstr, kstr, o, nullptr, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
+  AttnArgs a = make_args(q, k, v, qstr, kstr, o, nullptr, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask,
+                         (const unsigned long long*)seedctr);
   a.lse = lse;
   const int nqb = (Sq + 127) / 128;
   dim3 grid(pair_grid(causal, nqb), (unsigned)(B * H));
@@ -664,14 +674,15 @@ DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long
 DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long* qstr, const long* kstr,
                          const void* o, const void* dout, const long* ostr, const float* lse, float* dvec, void* dq,
                          void* dk, void* dv, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
-                         float dropout, unsigned long long seed, int causal, void* stream) {
+                         float dropout, unsigned long long seed, int causal, const void* seedctr, void* stream) {
   if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
       !aligned16(dq) || !aligned16(dk) || !aligned16(dv))
     return -1;
   if ((qstr[0] | qstr[1] | qstr[2] | kstr[0] | kstr[1] | kstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
   if (dropout < 0.f || dropout >= 1.f) return -1;
   hipStream_t st = (hipStream_t)stream;
-  AttnArgs a = make_args(q, k, v, qstr, kstr, o, dout, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask);
+  AttnArgs a = make_args(q, k, v, qstr, kstr, o, dout, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask,
+                         (const unsigned long long*)seedctr);
   a.lse = const_cast<float*>(lse);
   a.dvec = dvec;
   a.dq = (bf16_t*)dq;

@@ -161,9 +161,19 @@ __global__ void act_kernel(const bf16_t* x, const bf16_t* dy, bf16_t* y, long n8
   }
 }
 
+// Per-step dropout stream: the host seed identifies the call site within a step, the device counter `ctr`
+// (advanced once per training step by dtf_rng_advance, inside the captured graph when the step is a hipGraph)
+// identifies the step, so a replayed graph draws fresh masks although its kernel arguments are frozen.
+__device__ __forceinline__ uint64_t step_seed(uint64_t seed, const uint64_t* ctr) {
+  return ctr ? seed ^ (*ctr * 0xD1B54A32D192ED03ull) : seed;
+}
+
+__global__ void rng_advance_kernel(uint64_t* ctr) { *ctr += 1; }
+
 // dropout: y = x * mask / keep ; mask regenerated from (seed, index)
-__global__ void dropout_kernel(const bf16_t* x, bf16_t* y, long n8, float keep, uint64_t seed) {
+__global__ void dropout_kernel(const bf16_t* x, bf16_t* y, long n8, float keep, uint64_t seed, const uint64_t* ctr) {
   const float inv = 1.f / keep;
+  seed = step_seed(seed, ctr);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     float f[8];
     load8(x + i * 8, f);
@@ -176,8 +186,10 @@ __global__ void dropout_kernel(const bf16_t* x, bf16_t* y, long n8, float keep, 
 // Residual add of a dropped-out branch: y = x + dropout(f) in one pass, the same mask as dropout_kernel(f)
 // (so the backward of the branch is dropout_kernel(dy) with the same seed) and the same bf16 rounding as the
 // two-kernel form (the dropped branch value is rounded before the add).
-__global__ void add_dropout_kernel(const bf16_t* x, const bf16_t* f, bf16_t* y, long n8, float keep, uint64_t seed) {
+__global__ void add_dropout_kernel(const bf16_t* x, const bf16_t* f, bf16_t* y, long n8, float keep, uint64_t seed,
+                                   const uint64_t* ctr) {
   const float inv = 1.f / keep;
+  seed = step_seed(seed, ctr);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     float a[8], b[8];
     load8(x + i * 8, a);
@@ -534,16 +546,23 @@ DTF_API int dtf_act(const void* x, const void* dy, void* y, long n, int act, int
   hipLaunchKernelGGL(act_kernel, GRID(n / 8), (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)y, n / 8, act, bwd);
   return (int)hipGetLastError();
 }
+// ctr: optional device step counter (see step_seed); nullptr = the host seed alone
 DTF_API int dtf_add_dropout(const void* x, const void* f, void* y, long n, float keep, unsigned long long seed,
-                            void* stream) {
+                            const void* ctr, void* stream) {
   if (n & 7) return -1;
   hipLaunchKernelGGL(add_dropout_kernel, GRID(n / 8), (const bf16_t*)x, (const bf16_t*)f, (bf16_t*)y, n / 8, keep,
-                     (uint64_t)seed);
+                     (uint64_t)seed, (const uint64_t*)ctr);
   return (int)hipGetLastError();
 }
-DTF_API int dtf_dropout(const void* x, void* y, long n, float keep, unsigned long long seed, void* stream) {
+DTF_API int dtf_dropout(const void* x, void* y, long n, float keep, unsigned long long seed, const void* ctr,
+                        void* stream) {
   if (n & 7) return -1;
-  hipLaunchKernelGGL(dropout_kernel, GRID(n / 8), (const bf16_t*)x, (bf16_t*)y, n / 8, keep, (uint64_t)seed);
+  hipLaunchKernelGGL(dropout_kernel, GRID(n / 8), (const bf16_t*)x, (bf16_t*)y, n / 8, keep, (uint64_t)seed,
+                     (const uint64_t*)ctr);
+  return (int)hipGetLastError();
+}
+DTF_API int dtf_rng_advance(void* ctr, void* stream) {
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, (uint64_t*)ctr);
   return (int)hipGetLastError();
 }
 // Column sums (BiasAddGrad): partial rows into ws, then a deterministic row reduction into out.

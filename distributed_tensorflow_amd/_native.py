@@ -36,7 +36,7 @@ _KERNEL_SIGS = {
     "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],
     "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "dtf_maxpool_bwd": [P, P, P] + [I] * 12 + [P],
-    "dtf_add_dropout": [P, P, P, L, F, U, P],
+    "dtf_add_dropout": [P, P, P, L, F, U, P, P],
     "dtf_softmax_ce_fwd": [P, I, P, P, P, L, I, F, P],
     "dtf_softmax_ce_bwd": [P, I, P, P, P, P, L, I, F, P],
     "dtf_nchw_to_s2d": [P, P, I, I, I, I, P],
@@ -53,11 +53,12 @@ _KERNEL_SIGS = {
     "dtf_filters_to_crsk": [P, I, I, P],
     "dtf_add_bf16": [P, P, P, L, F, F, P],
     "dtf_act": [P, P, P, L, I, I, P],
-    "dtf_dropout": [P, P, L, F, U, P],
+    "dtf_dropout": [P, P, L, F, U, P, P],
+    "dtf_rng_advance": [P, P],
     "dtf_gemm256": [P, P, P, I, I, I, L, L, L, I, I, I, I, P, L, P],
     "dtf_quant_fp8_exact": [P, P, L, P, P, P],
-    "dtf_attn_fwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
-    "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P],
+    "dtf_attn_fwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],
+    "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],
     "dtf_colsum": [P, L, I, P, I, P, L, P],
     "dtf_embed_fwd": [P, P, P, P, P, P, P, L, I, I, P],
     "dtf_embed_bwd_sorted": [P, P, P, P, L, I, P],

@@ -7,8 +7,9 @@ issued by ONE graph launch. Inputs are copied into static buffers; per-step scal
 cannot bake in (bias-corrected learning rate, gradient scale) are published by
 ``Optimizer.graph_prestep`` into the pinned buffers the captured memcpy nodes read; derived weight
 layouts are invalidated after every replay. Restrictions (as for any graph capture): static shapes,
-no host reads of device values inside the step, and dropout masks repeat every replay (seeds are
-baked at capture).
+no host reads of device values inside the step. Dropout stays random across replays: automatically seeded
+dropout kernels also read a device step counter that Model.train_step advances with a captured kernel
+(ops._util.advance_rng).
 """
 from __future__ import annotations
 

@@ -25,7 +25,7 @@ import torch
 
 from .. import context
 from .. import profiler as prof
-from ..ops._util import direct_grads
+from ..ops._util import advance_rng, direct_grads
 from ..data import Dataset
 from ..parallel import strategy as S
 from . import callbacks as cbs
@@ -172,6 +172,9 @@ class Model(Layer):
                 with torch.no_grad():
                     self(_head(x), training=False)
             self._ensure_arena()
+        dev = self._device()
+        if dev.type == "cuda":
+            advance_rng(dev)  # fresh dropout masks for this step, also under hipGraph replay
         with prof.phase("forward"):
             y_pred = self(x, training=True)
             loss = self.compute_loss(x, y, y_pred, sw)

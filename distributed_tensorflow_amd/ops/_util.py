@@ -47,6 +47,34 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+# ---------------------------------------------------------------- per-step dropout stream
+# Dropout kernels hash (host seed, device step counter, element index). An automatically drawn host seed names
+# the call site within a step; the device counter names the step and is advanced by `advance_rng` at the start
+# of every Model.train_step, as a kernel, so a hipGraph-captured step (whose kernel arguments are frozen at
+# capture) still draws a fresh mask on every replay. Explicit user seeds bypass the counter (stateless ops:
+# the same seed gives the same mask).
+_RNG = {}
+
+
+def rng_counter(device):
+    """Device pointer of the step counter for `device` (created on first use, never inside a capture)."""
+    key = (device.type, device.index)
+    t = _RNG.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dropout RNG counter first used inside a hipGraph capture: run an eager step first")
+        t = torch.zeros(1, dtype=torch.int64, device=device)
+        _RNG[key] = t
+    return t.data_ptr()
+
+
+def advance_rng(device):
+    """Next training step: new dropout masks everywhere (no-op until a dropout kernel has run on `device`)."""
+    t = _RNG.get((device.type, device.index))
+    if t is not None and device.type == "cuda":
+        call("dtf_rng_advance", t.data_ptr(), stream())
+
+
 def on_gpu(*ts) -> bool:
     for t in ts:
         if t is not None and isinstance(t, torch.Tensor):

@@ -14,16 +14,19 @@ import math
 
 import torch
 
-from ._util import BF16, F32, call, on_gpu, ptr, stream
+from ._util import BF16, F32, call, on_gpu, ptr, rng_counter, stream
 from .linalg import bmm
 from .nn import softmax
 
 _seed_counter = [0]
 
 
-def _next_seed():
+def _next_seed(seed, device):
+    """(host seed, device step-counter pointer or None): see ops.nn._auto_seed."""
+    if seed is not None:
+        return seed, None
     _seed_counter[0] += 1
-    return (_seed_counter[0] * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    return (_seed_counter[0] * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF, rng_counter(device)
 
 
 def _strides3(b, s, h):
@@ -33,7 +36,7 @@ def _strides3(b, s, h):
 
 class _FlashPackedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, kmask, heads, causal, scale, dropout, seed):
+    def forward(ctx, qkv, kmask, heads, causal, scale, dropout, seed, ctr):
         qkv = qkv.contiguous()
         B, S, T = qkv.shape
         D = T // (3 * heads)
@@ -44,15 +47,15 @@ class _FlashPackedFn(torch.autograd.Function):
         os_, osp = _strides3(S * HD, HD, D)
         base = qkv.data_ptr()
         call("dtf_attn_fwd", base, base + 2 * HD, base + 4 * HD, qsp, qsp, ptr(o), osp, ptr(lse), ptr(kmask), B, heads, S,
-             S, D, float(scale), float(dropout), seed, int(causal), stream())
+             S, D, float(scale), float(dropout), seed, int(causal), ctr, stream())
         ctx.save_for_backward(qkv, o, lse, kmask)
-        ctx.cfg = (heads, causal, scale, dropout, seed)
+        ctx.cfg = (heads, causal, scale, dropout, seed, ctr)
         return o
 
     @staticmethod
     def backward(ctx, do):
         qkv, o, lse, kmask = ctx.saved_tensors
-        heads, causal, scale, dropout, seed = ctx.cfg
+        heads, causal, scale, dropout, seed, ctr = ctx.cfg
         do = do.to(BF16).contiguous()
         B, S, T = qkv.shape
         D = T // (3 * heads)
@@ -64,15 +67,15 @@ class _FlashPackedFn(torch.autograd.Function):
         base, gb = qkv.data_ptr(), dqkv.data_ptr()
         call("dtf_attn_bwd", base, base + 2 * HD, base + 4 * HD, qsp, qsp, ptr(o), ptr(do), osp, ptr(lse), ptr(dvec),
              gb, gb + 2 * HD, gb + 4 * HD, ptr(kmask), B, heads, S, S, D, float(scale), float(dropout), seed,
-             int(causal), stream())
-        return dqkv, None, None, None, None, None, None
+             int(causal), ctr, stream())
+        return dqkv, None, None, None, None, None, None, None
 
 
 class _FlashFn(torch.autograd.Function):
     """Separate q, k, v tensors in [B, H, S, D] layout."""
 
     @staticmethod
-    def forward(ctx, q, k, v, kmask, causal, scale, dropout, seed):
+    def forward(ctx, q, k, v, kmask, causal, scale, dropout, seed, ctr):
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         B, H, Sq, D = q.shape
         Sk = k.shape[2]
@@ -81,15 +84,15 @@ class _FlashFn(torch.autograd.Function):
         qs, qsp = _strides3(H * Sq * D, D, Sq * D)
         ks, ksp = _strides3(H * Sk * D, D, Sk * D)
         call("dtf_attn_fwd", ptr(q), ptr(k), ptr(v), qsp, ksp, ptr(o), qsp, ptr(lse), ptr(kmask), B, H, Sq, Sk, D,
-             float(scale), float(dropout), seed, int(causal), stream())
+             float(scale), float(dropout), seed, int(causal), ctr, stream())
         ctx.save_for_backward(q, k, v, o, lse, kmask)
-        ctx.cfg = (causal, scale, dropout, seed)
+        ctx.cfg = (causal, scale, dropout, seed, ctr)
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse, kmask = ctx.saved_tensors
-        causal, scale, dropout, seed = ctx.cfg
+        causal, scale, dropout, seed, ctr = ctx.cfg
         do = do.to(BF16).contiguous()
         B, H, Sq, D = q.shape
         Sk = k.shape[2]
@@ -99,8 +102,8 @@ class _FlashFn(torch.autograd.Function):
         ks, ksp = _strides3(H * Sk * D, D, Sk * D)
         call("dtf_attn_bwd", ptr(q), ptr(k), ptr(v), qsp, ksp, ptr(o), ptr(do), qsp, ptr(lse), ptr(dvec), ptr(dq),
              ptr(dk), ptr(dv), ptr(kmask), B, H, Sq, Sk, D, float(scale), float(dropout), seed, int(causal),
-             stream())
-        return dq, dk, dv, None, None, None, None, None
+             ctr, stream())
+        return dq, dk, dv, None, None, None, None, None, None
 
 
 def _kmask(mask, B, Sk):
@@ -117,9 +120,9 @@ def attention(q, k, v, causal=False, mask=None, scale=None, dropout=0.0, trainin
     rate = float(dropout) if (dropout and training) else 0.0
     if on_gpu(q):
         if D == 64 and k.shape[2] == v.shape[2]:
-            seed = _next_seed() if seed is None else seed
+            seed, ctr = _next_seed(seed, q.device)
             return _FlashFn.apply(q.to(BF16), k.to(BF16), v.to(BF16), _kmask(mask, B, Sk), bool(causal),
-                                  float(scale), rate, seed)
+                                  float(scale), rate, seed, ctr)
         return _composed(q, k, v, causal, mask, scale, rate)
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
     if causal:
@@ -140,8 +143,8 @@ def attention_packed(qkv, heads, causal=False, mask=None, scale=None, dropout=0.
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     rate = float(dropout) if (dropout and training) else 0.0
     if on_gpu(qkv) and D == 64 and qkv.dtype == BF16:
-        seed = _next_seed() if seed is None else seed
-        return _FlashPackedFn.apply(qkv, _kmask(mask, B, S), heads, bool(causal), float(scale), rate, seed)
+        seed, ctr = _next_seed(seed, qkv.device)
+        return _FlashPackedFn.apply(qkv, _kmask(mask, B, S), heads, bool(causal), float(scale), rate, seed, ctr)
     q, k, v = split_qkv(qkv, heads)
     return merge_heads(attention(q, k, v, causal, mask, scale, dropout, training))
 

@@ -4,7 +4,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, call, direct_grad, on_gpu, ptr, stream, workspace
+from ._util import BF16, F32, call, direct_grad, on_gpu, ptr, rng_counter, stream, workspace
 from .conv import out_size
 
 
@@ -101,22 +101,31 @@ def gelu(x):
 
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, keep, seed):
+    def forward(ctx, x, keep, seed, ctr):
         x = x.contiguous()
         y = torch.empty_like(x)
-        call("dtf_dropout", ptr(x), ptr(y), x.numel(), float(keep), int(seed), stream())
-        ctx.keep, ctx.seed = keep, seed
+        call("dtf_dropout", ptr(x), ptr(y), x.numel(), float(keep), int(seed), ctr, stream())
+        ctx.keep, ctx.seed, ctx.ctr = keep, seed, ctr
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dy = dy.to(BF16).contiguous()
         dx = torch.empty_like(dy)
-        call("dtf_dropout", ptr(dy), ptr(dx), dy.numel(), float(ctx.keep), int(ctx.seed), stream())
-        return dx, None, None
+        call("dtf_dropout", ptr(dy), ptr(dx), dy.numel(), float(ctx.keep), int(ctx.seed), ctx.ctr, stream())
+        return dx, None, None, None
 
 
 _seed_counter = [0x5EED]
+
+
+def _auto_seed(seed, device):
+    """(host seed, device step-counter pointer or None): explicit seeds are stateless, automatic ones follow
+    the per-step device counter (see _util.rng_counter)."""
+    if seed is not None:
+        return seed & 0xFFFFFFFFFFFFFFFF, None
+    _seed_counter[0] += 1
+    return (_seed_counter[0] * 0x9E3779B1) & 0xFFFFFFFFFFFFFFFF, rng_counter(device)
 
 
 def dropout(x, rate, training=True, seed=None):
@@ -124,10 +133,8 @@ def dropout(x, rate, training=True, seed=None):
         return x
     keep = 1.0 - rate
     if on_gpu(x) and x.dtype == BF16 and x.numel() % 8 == 0:
-        if seed is None:
-            _seed_counter[0] += 1
-            seed = _seed_counter[0] * 0x9E3779B1
-        return _DropoutFn.apply(x, keep, seed & 0xFFFFFFFFFFFFFFFF)
+        s, ctr = _auto_seed(seed, x.device)
+        return _DropoutFn.apply(x, keep, s, ctr)
     return torch.nn.functional.dropout(x, rate, True)
 
 
@@ -138,21 +145,21 @@ class _AddDropoutFn(torch.autograd.Function):
     """y = x + dropout(f): one pass forward; backward dx = dy, df = dropout(dy) with the same mask."""
 
     @staticmethod
-    def forward(ctx, x, f, keep, seed, link):
+    def forward(ctx, x, f, keep, seed, ctr, link):
         x, f = x.contiguous(), f.contiguous()
         y = torch.empty_like(x)
-        call("dtf_add_dropout", ptr(x), ptr(f), ptr(y), x.numel(), float(keep), int(seed), stream())
-        ctx.keep, ctx.seed, ctx.link = keep, seed, link
+        call("dtf_add_dropout", ptr(x), ptr(f), ptr(y), x.numel(), float(keep), int(seed), ctr, stream())
+        ctx.keep, ctx.seed, ctx.ctr, ctx.link = keep, seed, ctr, link
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dy = dy.to(BF16).contiguous()
         df = torch.empty_like(dy)
-        call("dtf_dropout", ptr(dy), ptr(df), dy.numel(), float(ctx.keep), int(ctx.seed), stream())
+        call("dtf_dropout", ptr(dy), ptr(df), dy.numel(), float(ctx.keep), int(ctx.seed), ctx.ctr, stream())
         dx = ctx.link.park(dy) if ctx.link is not None else dy  # None: the branch's first GEMM adds it
         ctx.link = None
-        return dx, df, None, None, None
+        return dx, df, None, None, None, None
 
 
 def add_dropout(x, f, rate, training=True, seed=None, link=None):
@@ -163,10 +170,8 @@ def add_dropout(x, f, rate, training=True, seed=None, link=None):
         return add(x, f)
     if _FUSE_ADD_DROPOUT and on_gpu(x) and x.dtype == BF16 and f.dtype == BF16 and x.shape == f.shape \
             and x.numel() % 8 == 0:
-        if seed is None:
-            _seed_counter[0] += 1
-            seed = _seed_counter[0] * 0x9E3779B1
-        return _AddDropoutFn.apply(x, f, 1.0 - rate, seed & 0xFFFFFFFFFFFFFFFF, link)
+        s, ctr = _auto_seed(seed, x.device)
+        return _AddDropoutFn.apply(x, f, 1.0 - rate, s, ctr, link)
     return add(x, dropout(f, rate, training, seed))
 
 

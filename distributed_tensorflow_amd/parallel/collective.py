@@ -25,6 +25,9 @@ import torch
 import torch.distributed as dist
 
 _DEFAULT_BUCKET_MB = float(os.environ.get("DTF_BUCKET_MB", "32"))
+# wire dtype of the gradient all-reduce: "f32" (default) or "bf16" (half the bytes on the xGMI links; each
+# bucket is cast to bf16 before and back to f32 after the collective, the optimizer still accumulates in f32)
+_DEFAULT_WIRE = os.environ.get("DTF_ALLREDUCE_DTYPE", "f32")
 
 
 def backend_for(device_type: str) -> str:
@@ -61,10 +64,17 @@ def world():
 class GradientBucketer:
     """Bucketed, backward-overlapped SUM all-reduce of a ParamArena's gradient buffer."""
 
-    def __init__(self, arena, group=None, bucket_mb=None, average=False):
+    def __init__(self, arena, group=None, bucket_mb=None, average=False, wire_dtype=None):
         self.arena = arena
         self.group = group
         self.average = average
+        self.wire = (wire_dtype or _DEFAULT_WIRE).lower()
+        if self.wire not in ("f32", "bf16"):
+            raise ValueError(f"all-reduce wire dtype {self.wire!r} (f32 or bf16)")
+        self._wirebuf = None
+        # exposed-communication timing (bench): events around the wait for the last buckets, per step
+        self.timing = False
+        self._timed = []
         cap = int((bucket_mb if bucket_mb is not None else _DEFAULT_BUCKET_MB) * (1 << 20) / 4)
         nv = len(arena.variables)
         self.buckets = []          # [start, end) element ranges of arena.grad
@@ -132,6 +142,12 @@ class GradientBucketer:
     def _launch(self, b):
         lo, hi = self.buckets[b]
         t = self.arena.grad[lo:hi]
+        if self.wire == "bf16":
+            if self._wirebuf is None:
+                self._wirebuf = torch.empty(self.arena.grad.numel(), dtype=torch.bfloat16, device=t.device)
+            w = self._wirebuf[lo:hi]
+            _cast(t, w)
+            t = w
         self._works[b] = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finalize(self):
@@ -139,12 +155,44 @@ class GradientBucketer:
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
+        ev0 = None
+        if self.timing and self.arena.grad.is_cuda:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()  # backward compute is done here; what follows on this stream is waiting on RCCL
         for w in self._works:
             if w is not None:
                 w.wait()
+        if self.wire == "bf16":
+            for lo, hi in self.buckets:
+                _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._timed.append((ev0, ev1))
         if self.average:
             self.arena.grad.div_(dist.get_world_size(self.group))
         self.reset()
+
+    def exposed_ms(self, clear=True):
+        """Mean device time per timed step between the end of the backward compute and the completion of the
+        last gradient bucket (communication the backward overlap did not hide); None if nothing was timed."""
+        if not self._timed:
+            return None
+        torch.cuda.synchronize()
+        v = sum(a.elapsed_time(b) for a, b in self._timed) / len(self._timed)
+        if clear:
+            self._timed = []
+        return v
+
+
+def _cast(src, dst):
+    """f32 <-> bf16 conversion of one bucket (HIP cast kernels on GPU)."""
+    if src.is_cuda:
+        from ..ops._util import call, stream
+        name = "dtf_cast_f32_bf16" if src.dtype == torch.float32 else "dtf_cast_bf16_f32"
+        call(name, src.data_ptr(), dst.data_ptr(), src.numel(), stream())
+    else:
+        dst.copy_(src)
 
 
 class ShmAllReduce:

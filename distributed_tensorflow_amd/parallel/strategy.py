@@ -158,11 +158,27 @@ class OneDeviceStrategy(Strategy):
         return self._device
 
 
+class CommunicationOptions:
+    """tf.distribute.experimental.CommunicationOptions: ``bytes_per_pack`` is the gradient bucket cap (0 = the
+    framework default, DTF_BUCKET_MB); ``wire_dtype`` ("f32" / "bf16", an extension) the all-reduce payload
+    type; ``implementation`` is accepted for API compatibility (the collective is always RCCL on GPUs)."""
+
+    def __init__(self, bytes_per_pack=0, timeout_seconds=None, implementation=None, wire_dtype=None):
+        self.bytes_per_pack = int(bytes_per_pack or 0)
+        self.timeout_seconds = timeout_seconds
+        self.implementation = implementation
+        self.wire_dtype = wire_dtype
+
+
 class MultiWorkerMirroredStrategy(Strategy):
     """Synchronous collective all-reduce data parallelism, one process per device."""
 
     def __init__(self, cluster_resolver=None, communication_options=None, bucket_mb=None):
         super().__init__()
+        co = communication_options
+        if bucket_mb is None and co is not None and co.bytes_per_pack:
+            bucket_mb = co.bytes_per_pack / float(1 << 20)
+        self.wire_dtype = getattr(co, "wire_dtype", None)
         self.bucket_mb = bucket_mb
         if cluster_resolver is None:
             if TorchrunClusterResolver.active():
@@ -189,7 +205,10 @@ class MultiWorkerMirroredStrategy(Strategy):
         else:
             dev = torch.device("cpu")
         self._device = dev
-        if self._world > 1:
+        # DTF_FORCE_COLLECTIVE=1: run the collective path (process group + bucketed all-reduce) even with one
+        # replica — how the RCCL code path and its hipGraph capture are exercised on a 1-GPU box
+        self._force = os.environ.get("DTF_FORCE_COLLECTIVE", "0") == "1"
+        if self._world > 1 or self._force:
             collective.init_process_group(self._rank, self._world, addr, port, dev.type)
 
     @property
@@ -213,7 +232,7 @@ class MultiWorkerMirroredStrategy(Strategy):
         return self._rank == 0
 
     def setup_model(self, model, arena):
-        if self._world <= 1:
+        if self._world <= 1 and not getattr(self, "_force", False):
             return
         # identical initial state everywhere: one broadcast of the whole master arena + non-trainables
         collective.broadcast_tensors([arena.flat] + [v.data for v in model.non_trainable_weights], src=0)
@@ -230,7 +249,8 @@ class MultiWorkerMirroredStrategy(Strategy):
             dist.broadcast_object_list(obj, src=0)
             b = collective.ShmAllReduce(arena, self._rank, self._world, obj[0])
         else:
-            b = collective.GradientBucketer(arena, bucket_mb=self.bucket_mb).install()
+            b = collective.GradientBucketer(arena, bucket_mb=self.bucket_mb,
+                                            wire_dtype=getattr(self, "wire_dtype", None)).install()
         self._bucketers[id(arena)] = b
 
     def backward(self, loss, arena):
@@ -269,8 +289,9 @@ class MirroredStrategy(MultiWorkerMirroredStrategy):
     devices=None under a multi-process launch: one replica per process (RCCL).
     devices=[...] in one process: in-process replicas over those devices."""
 
-    def __init__(self, devices=None, cross_device_ops=None, bucket_mb=None):
+    def __init__(self, devices=None, cross_device_ops=None, bucket_mb=None, communication_options=None):
         self._devices = [context.parse_device(d) for d in devices] if devices else None
+        self.wire_dtype = getattr(communication_options, "wire_dtype", None)
         if self._devices and len(self._devices) > 1 and not TorchrunClusterResolver.active():
             Strategy.__init__(self)
             self.bucket_mb = bucket_mb
@@ -288,9 +309,9 @@ class MirroredStrategy(MultiWorkerMirroredStrategy):
             self.cluster_resolver = None
             return
         if TorchrunClusterResolver.active():
-            super().__init__(TorchrunClusterResolver(), bucket_mb=bucket_mb)
+            super().__init__(TorchrunClusterResolver(), communication_options, bucket_mb=bucket_mb)
         else:
-            super().__init__(TFConfigClusterResolver(tf_config={}), bucket_mb=bucket_mb)
+            super().__init__(TFConfigClusterResolver(tf_config={}), communication_options, bucket_mb=bucket_mb)
 
     @property
     def extended_devices(self):

@@ -124,3 +124,54 @@ def test_two_rank_resnet_replicas_stay_identical(cuda):
     for a, b in zip(res[0][1], res[1][1]):
         assert (a == b).all(), "replicas diverged"
     assert all(x == x for x in res[0][2])
+
+
+def _worker_rccl1(port, jit, wire, q):
+    """One replica on the REAL RCCL backend (world size 1, DTF_FORCE_COLLECTIVE): process group, bucketed
+    all-reduces from post-accumulate hooks, optionally the bf16 wire and hipGraph capture of the whole step."""
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      DTF_FORCE_COLLECTIVE="1")
+    os.environ.pop("DTF_COLLECTIVE_BACKEND", None)
+    try:
+        import torch.distributed as dist
+        from distributed_tensorflow_amd import parallel
+        s = parallel.MultiWorkerMirroredStrategy(bucket_mb=0.25,
+                                                 communication_options=parallel.CommunicationOptions(
+                                                     wire_dtype=wire))
+        assert dist.get_backend() == "nccl"
+        with s.scope():
+            m = _gpt2(100)
+        m._jit = jit
+        fn = m.make_train_function(force=True)
+        losses = [float(fn((x, y))["loss"]) for x, y in _batches("gpt2", s.device, steps=5)]
+        torch.cuda.synchronize()
+        b = s._bucketers[id(m._arena)]
+        q.put((type(fn).__name__, [w.detach().float().cpu().numpy() for w in m.trainable_variables], losses,
+               len(b.buckets)))
+        dist.destroy_process_group()
+    except Exception:
+        q.put((None, None, traceback.format_exc(), 0))
+
+
+@pytest.mark.parametrize("jit,wire", [(False, "f32"), (True, "f32"), (False, "bf16")])
+def test_rccl_bucketer_world1_matches_single_process(cuda, jit, wire):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl1, args=(_port(), jit, wire, q))
+    p.start()
+    try:
+        kind, ws, losses, nb = q.get(timeout=100)
+    finally:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    assert ws is not None, losses
+    assert nb > 3 and kind == ("CapturedStep" if jit else "method")
+    m = _gpt2(100)
+    ref = [float(m.train_step((x, y))["loss"]) for x, y in _batches("gpt2", cuda, steps=5)]
+    torch.cuda.synchronize()
+    tol = dict(rtol=2e-3, atol=2e-4) if wire == "f32" else dict(rtol=3e-2, atol=3e-3)
+    for a, b in zip(losses, ref):
+        assert abs(a - b) <= tol["rtol"] * abs(b) + 1e-4, (losses, ref)
+    for a, w in zip(ws, m.trainable_variables):
+        torch.testing.assert_close(torch.from_numpy(a), w.detach().float().cpu(), **tol)

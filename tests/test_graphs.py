@@ -62,3 +62,25 @@ def test_captured_step_matches_eager(cuda):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), (l0, l1)
     for a, b in zip(w0, w1):
         torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+def test_captured_step_draws_fresh_dropout_masks(cuda):
+    """A hipGraph-captured step of a model with dropout (residual, attention and FFN dropout of a tiny GPT-2)
+    must not replay one frozen mask: with lr = 0 the weights never change, so the per-step losses differ only
+    through the masks — eager steps differ from each other, and so must the replays."""
+    from distributed_tensorflow_amd.graphs import CapturedStep
+    from distributed_tensorflow_amd.keras import initializers
+    from distributed_tensorflow_amd.models.transformer import GPT2
+    ids = torch.randint(0, 512, (4, 64), device=cuda)
+    seen = {}
+    for jit in (False, True):
+        initializers.set_seed(5)
+        model = GPT2(vocab=512, ctx=64, hidden=128, layers=2, heads=2, dropout=0.3)
+        model.compile(optimizer=optimizers.SGD(0.0), loss=losses.SparseCategoricalCrossentropy(from_logits=True),
+                      jit_compile=jit)
+        fn = model.make_train_function(force=True)
+        assert isinstance(fn, CapturedStep) == jit
+        seen[jit] = [float(fn((ids, ids))["loss"]) for _ in range(6)]
+    for jit, ls in seen.items():
+        assert len({round(v, 6) for v in ls[2:]}) >= 3, (jit, ls)  # replays (steps 3..6) differ too
