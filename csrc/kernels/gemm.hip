@@ -149,6 +149,18 @@ static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
 }
 
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8 = 0);  // gemm256.hip
+int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool force);  // conv256.hip
+bool conv256_on();
+
+// The 256-row pipelined LDS-DMA kernel (conv256.hip) for a convolution GEMM: forced by tiles 11-14 (variant
+// tile - 11, see conv256.hip launch_cfg); by default whenever it is eligible and fills the chip. True if launched.
+static bool try_conv256(GemmArgs& a, int am, int bm, int& tile, hipStream_t st) {
+  if (tile >= 11 && tile <= 14) {
+    if (conv256_try(a, am, bm, tile - 11, st, true) == 0) return true;
+    tile = -1;
+  }
+  return tile < 0 && conv256_try(a, am, bm, -1, st, false) == 0;
+}
 
 // 256x256 (1 block/CU, ~1.12-1.24x faster per tile, more so at long K) vs 128x128 (2 blocks/CU): compare the
 // wave-quantisation efficiency of both tilings on 256 CUs.
@@ -373,8 +385,10 @@ DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bi
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
-  if (tile < 0) tile = pick_glds_tile(a, am, OP_KCONTIG);
-  dispatch(a, am, OP_KCONTIG, tile, (hipStream_t)stream);
+  if (!try_conv256(a, am, OP_KCONTIG, tile, (hipStream_t)stream)) {
+    if (tile < 0) tile = pick_glds_tile(a, am, OP_KCONTIG);
+    dispatch(a, am, OP_KCONTIG, tile, (hipStream_t)stream);
+  }
   if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();
 }
@@ -439,7 +453,8 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
     bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
-    dispatch(a, am, OP_KCONTIG, tile < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : tile, st);
+    int t = tile;
+    if (!try_conv256(a, am, OP_KCONTIG, t, st)) dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
     if (bnrows) *bnrows = bnx ? a.tiles_m : 0;
     return (int)hipGetLastError();
   }
@@ -483,7 +498,9 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
       const bool pointwise = nkh == 1 && nkw == 1 && ch == 0 && cw == 0 && Hs == P && Ws == Q;
       const int am = pointwise ? OP_KCONTIG
                      : tap_uniform(K, nkh * nkw, (long)N * P * Q * K) ? OP_DGRAD_T : OP_DGRAD;
-      dispatch(a, am, OP_KCONTIG, tile < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : tile, st);
+      int t = tile;
+      if (!try_conv256(a, am, OP_KCONTIG, t, st))
+        dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
       prow += a.tiles_m;
     }
   }
@@ -526,6 +543,44 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
     const char* e = getenv("DTF_WGRAD_SWAP");
     return !(e && e[0] == '0');
   }();
+  // conv256: dW^T [R*S*C][Kout] = X^T . dY on the 256-row pipelined kernel (M = filter taps x channels, the long
+  // dimension; N = Kout), split-K over the pixels into f32 slabs, reduced and transposed into dW
+  static const bool c256w = [] {
+    const char* e = getenv("DTF_CONV256_WGRAD");  // opt-in: slower than gemm_core.h on every ResNet-50 filter
+    return e && e[0] == '1';
+  }();
+  const bool c256_forced = tile >= 11 && tile <= 14;
+  if (small && ws != nullptr && (c256_forced || (tile < 0 && c256w && conv256_on())) &&
+      (pointwise || (C % 8 == 0 && (dh == 1 && dw == 1)))) {
+    GemmArgs b = a;
+    b.A = (const bf16_t*)X; b.B = (const bf16_t*)dY;
+    b.M = R * S * C; b.N = K;
+    b.lda = C; b.ldb = K; b.ldc = K;
+    const int cfg = c256_forced ? tile - 11 : (K <= 64 ? 2 : K >= 256 ? 1 : 0);
+    const int bn = cfg == 1 ? 256 : cfg == 2 ? 64 : 128;
+    const long mnT = (long)b.M * b.N;
+    const long tiles = (long)cdiv(b.M, 256) * cdiv(b.N, bn);
+    // ~2 rounds of 1-block/CU tiles, >= 16 K-tiles (1024 pixels) per split
+    long sk = std::max<long>(1, (512 + tiles - 1) / tiles);
+    sk = std::min<long>(sk, std::max<long>(1, (long)b.K / 1024));
+    if ((sk + 1) * mnT > ws_elems) sk = ws_elems / mnT - 1;
+    if (sk >= 1) {
+      b.splitk = (int)sk;
+      b.kchunk = (int)(((b.K + sk - 1) / sk + BK - 1) / BK * BK);
+      b.C = ws;
+      b.slab = mnT;
+      b.beta = 0.f;
+      b.atomic_out = 0;
+      if (conv256_try(b, pointwise ? OP_KOUTER : OP_WGRADX_R, OP_KOUTER_R, cfg, st, true) == 0) {
+        float* dwt = ws + (long)b.splitk * mnT;
+        dtf_sum_rows(ws, mnT, b.splitk, mnT, dwt, 0, st);
+        hipLaunchKernelGGL(transpose_acc_kernel, dim3(cdiv(b.N, 32), cdiv(b.M, 32)), dim3(256), 0, st, dwt, dW,
+                           b.M, b.N, accumulate);
+        return (int)hipGetLastError();
+      }
+    }
+  }
+  if (c256_forced) tile = -1;
   if (swap_on && use_glds && tile < 0 && K <= 64 && R * S > 1 && ws != nullptr) {
     GemmArgs b = a;
     b.A = (const bf16_t*)X; b.B = (const bf16_t*)dY;

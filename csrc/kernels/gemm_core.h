@@ -681,6 +681,257 @@ __device__ __forceinline__ long frag_fp8(const char* lds, int rb, int kk, int la
   return *reinterpret_cast<const long*>(lds + row * 128 + pc * 16 + (G & 1) * 8);
 }
 
+// Shared epilogue of the MFMA GEMM kernels (gemm_kernel here, conv256_kernel in conv256.hip): the block's
+// BM x BN accumulator tile is held by WM x WN waves as acc[TM][TN] 16x16 fragments (wave (wm, wn) = (wave / WN,
+// wave % WN) owns rows wm*BM/WM.., cols wn*BN/WN..); NTH threads; SMEMB bytes of LDS at smem are free.
+// Fused: alpha/beta (+ deferred-ReLU beta mask), bias, activation, pre-activation side output, forward BN
+// statistics or backward BN statistics (bnx), split-K slabs, f32 atomics, row remap.
+template <int BM, int BN, int WM, int WN, int NTH, int SMEMB>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM / WM / 16][BN / WN / 16], char* smem,
+                                              int m0, int n0, int tile_m, int z, int bz) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  // ---- epilogue: lane owns row m = ..+(lane&15), cols n = ..+(lane>>4)*4 + r ----
+  const long cbase = a.slab > 0 ? (long)z * a.slab : (long)bz * a.sC;
+  const float alpha = a.scales ? a.alpha * a.scales[0] * a.scales[1] : a.alpha;
+  float csum[TN][4], csq[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) csum[j][r] = csq[j][r] = 0.f;
+
+  // bf16 outputs without beta/atomics: the tile goes through LDS so that the global stores are whole
+  // 16-B chunks of contiguous row segments (a lane's MFMA fragment covers 4 columns x 1 row, i.e. 8-B
+  // pieces of 16 different rows per store instruction). The main loop ended on a barrier: LDS is free.
+  constexpr int CS = BN + 8;  // LDS row stride (elements): 16-B pad keeps the fragment writes conflict-free
+  constexpr bool can_stage = BM * CS * 2 <= SMEMB;  // the C tile fits the LDS buffers
+  // beta != 0 (accumulate into C) is staged too when there is no bias/activation/aux: the bf16 product goes
+  // through LDS and the old C is added in the coalesced store pass (one extra bf16 rounding of the product).
+  const bool staged = can_stage && !a.atomic_out && !a.out_f32 && !(a.N & 7) && !(a.ldc & 7) &&
+                      !(reinterpret_cast<uintptr_t>(a.C) & 15) &&
+                      (a.beta == 0.f || (!a.bias && !a.act && !a.aux && (!a.stats || a.bnx)));
+  // BN-backward statistics are taken in the store pass from whole 16-B chunks (coalesced reads of the BN
+  // input and one mask byte per 8 channels) instead of per fragment
+  const bool bn_bwd = a.stats != nullptr && a.bnx != nullptr;
+  if (staged) {
+    bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WTM + i * 16 + (lane & 15);
+      const int m = m0 + ml;
+      const bool mv = m < a.M;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4;
+        const int n = n0 + nl;
+        const bool nv = n < a.N;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
+        if (a.bias && nv) {
+          float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        if (a.aux && mv && nv) {
+          uint2 o;
+          o.x = pack2bf(v[0], v[1]);
+          o.y = pack2bf(v[2], v[3]);
+          *reinterpret_cast<uint2*>(a.aux + cbase + out_row(a, m) * a.ldc + n) = o;
+        }
+        if (a.act == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        } else if (a.act == 2) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+        }
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(ct + ml * CS + nl) = o;
+        if (a.stats && !bn_bwd && a.beta == 0.f && mv && nv) {  // statistics of the stored (bf16) values
+          v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);
+          v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
+          stat_acc(a, out_row(a, m), n, v, csum[j], csq[j]);
+        }
+      }
+    }
+    __syncthreads();
+    constexpr int C8 = BN / 8;
+    static_assert(NTH % C8 == 0, "a thread's channel chunk must stay fixed across the store pass");
+    const int c8t = threadIdx.x % C8;  // this thread's 8-channel chunk (constant over the pass)
+    float bs[8], bq[8], bmu[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) bs[r] = bq[r] = bmu[r] = 0.f;
+    if (bn_bwd && n0 + c8t * 8 < a.N) {
+      const float4 m0v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8);
+      const float4 m1v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8 + 4);
+      bmu[0] = m0v.x; bmu[1] = m0v.y; bmu[2] = m0v.z; bmu[3] = m0v.w;
+      bmu[4] = m1v.x; bmu[5] = m1v.y; bmu[6] = m1v.z; bmu[7] = m1v.w;
+    }
+#pragma unroll 4
+    for (int c = threadIdx.x; c < BM * C8; c += NTH) {
+      const int ml = c / C8;
+      const int m = m0 + ml, n = n0 + c8t * 8;
+      if (m >= a.M || n >= a.N) continue;
+      uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8t * 8);
+      const long e = out_row(a, m) * a.ldc + n;
+      bf16_t* cp = reinterpret_cast<bf16_t*>(a.C) + cbase + e;
+      if (a.beta != 0.f) {
+        const uint4 old = *reinterpret_cast<const uint4*>(cp);
+        float f[8], g[8];
+        const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, ow[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f[2 * q] = __uint_as_float(vw[q] << 16); f[2 * q + 1] = __uint_as_float(vw[q] & 0xffff0000u);
+          g[2 * q] = __uint_as_float(ow[q] << 16); g[2 * q + 1] = __uint_as_float(ow[q] & 0xffff0000u);
+        }
+        // betamask: the old C is a BN(+ReLU) output gradient whose ReLU mask was not applied yet (the
+        // residual shortcut's gradient, taken lazily instead of materialised by the BN backward)
+        const uint32_t bm = a.betamask ? (uint32_t)a.betamask[(e + cbase) >> 3] : 0xFFu;  // e % 8 == 0
+#pragma unroll
+        for (int r = 0; r < 8; ++r) f[r] = ((bm >> r) & 1u) ? fmaf(a.beta, g[r], f[r]) : f[r];
+        val.x = pack2bf(f[0], f[1]); val.y = pack2bf(f[2], f[3]);
+        val.z = pack2bf(f[4], f[5]); val.w = pack2bf(f[6], f[7]);
+      }
+      *reinterpret_cast<uint4*>(cp) = val;
+      if (bn_bwd) {
+        const uint4 xr = *reinterpret_cast<const uint4*>(a.bnx + e);
+        const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3] : 0xFFu;  // e % 8 == 0
+        const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int r = 2 * q + h;
+            const float dv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
+            const float xv = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
+            const float dz = ((bits >> r) & 1u) ? dv : 0.f;
+            bs[r] += dz;
+            bq[r] = fmaf(dz, xv - bmu[r], bq[r]);
+          }
+        }
+      }
+    }
+    if (bn_bwd) {
+      // reduce the NTH/C8 threads that share a channel chunk (fixed order: deterministic), one partial row
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) { red[threadIdx.x * 16 + r] = bs[r]; red[threadIdx.x * 16 + 8 + r] = bq[r]; }
+      __syncthreads();
+      float* prow = a.stats + (long)tile_m * 2 * a.N;
+      for (int nl = threadIdx.x; nl < BN; nl += NTH) {
+        const int n = n0 + nl;
+        if (n >= a.N) continue;
+        float sv = 0.f, qv = 0.f;
+        for (int t = nl >> 3; t < NTH; t += C8) { sv += red[t * 16 + (nl & 7)]; qv += red[t * 16 + 8 + (nl & 7)]; }
+        prow[n] = sv;
+        prow[a.N + n] = qv;
+      }
+    } else if (a.stats) {
+      __syncthreads();  // the statistics reduction below reuses the LDS
+    }
+  } else
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WTM + i * 16 + (lane & 15);
+    const bool mv = m < a.M;
+    const long mrow = out_row(a, mv ? m : 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WTN + j * 16 + (lane >> 4) * 4;
+      if (!mv || n >= a.N) continue;  // N % 4 == 0 is required by the host
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
+      const long off = cbase + mrow * a.ldc + n;
+      if (a.atomic_out) {
+        float* Cf = reinterpret_cast<float*>(a.C) + off;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(Cf + r, v[r]);
+        continue;
+      }
+      if (a.beta != 0.f) {
+        if (a.out_f32) {
+          float4 o = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(a.C) + off);
+          v[0] += a.beta * o.x; v[1] += a.beta * o.y; v[2] += a.beta * o.z; v[3] += a.beta * o.w;
+        } else {
+          uint2 o = *reinterpret_cast<const uint2*>(reinterpret_cast<bf16_t*>(a.C) + off);
+          if (a.betamask) {  // zero the old values whose ReLU bit is clear (see the staged path)
+            const uint32_t bm = ((uint32_t)a.betamask[off >> 3] >> (off & 4)) & 0xFu;  // off % 4 == 0
+            o.x &= ((bm & 1u) ? 0x0000ffffu : 0u) | ((bm & 2u) ? 0xffff0000u : 0u);
+            o.y &= ((bm & 4u) ? 0x0000ffffu : 0u) | ((bm & 8u) ? 0xffff0000u : 0u);
+          }
+          v[0] += a.beta * __uint_as_float(o.x << 16); v[1] += a.beta * __uint_as_float(o.x & 0xffff0000u);
+          v[2] += a.beta * __uint_as_float(o.y << 16); v[3] += a.beta * __uint_as_float(o.y & 0xffff0000u);
+        }
+      }
+      if (a.bias) {
+        float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (a.aux) {
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(a.aux + off) = o;
+      }
+      if (a.act == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      } else if (a.act == 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+      }
+      if (a.out_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.C) + off) = o;
+        if (a.stats) {  // statistics of the stored (bf16-rounded) values
+          v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);
+          v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
+        }
+      }
+      if (a.stats) stat_acc(a, mrow, n, v, csum[j], csq[j]);
+    }
+  }
+  if (a.stats && !(staged && bn_bwd)) {
+    // Deterministic BN statistics: reduce the 16 rows of a lane group by shuffles, the WM wave rows of
+    // the tile through LDS, then write ONE partial row per M-tile: stats[tile_m][0,N) = sum,
+    // stats[tile_m][N,2N) = sum of squares (bn_finalize sums the tiles_m rows). No atomics.
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = row16_sum(csum[j][r]), q = row16_sum(csq[j][r]);
+        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4 + r;
+        if ((lane & 15) == 0) {
+          red[wm * BN + nl] = s;
+          red[WM * BN + wm * BN + nl] = q;
+        }
+      }
+    }
+    __syncthreads();
+    float* prow = a.stats + (long)tile_m * 2 * a.N;
+    for (int nl = threadIdx.x; nl < BN; nl += NTH) {
+      const int n = n0 + nl;
+      if (n >= a.N) continue;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) { s += red[w * BN + nl]; q += red[WM * BN + w * BN + nl]; }
+      prow[n] = s;
+      prow[a.N + n] = q;
+    }
+  }
+}
+
 // Staging pipeline (PIPE):
 //  1: register-staged, ONE LDS buffer (a second barrier before each restage) — half the LDS per block, so
 //     twice the blocks (and bytes in flight) per CU; the default for 128-row tiles.
@@ -827,243 +1078,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
     }
   }
 
-  // ---- epilogue: lane owns row m = ..+(lane&15), cols n = ..+(lane>>4)*4 + r ----
-  const long cbase = a.slab > 0 ? (long)z * a.slab : (long)bz * a.sC;
-  const float alpha = a.scales ? a.alpha * a.scales[0] * a.scales[1] : a.alpha;
-  float csum[TN][4], csq[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) csum[j][r] = csq[j][r] = 0.f;
-
-  // bf16 outputs without beta/atomics: the tile goes through LDS so that the global stores are whole
-  // 16-B chunks of contiguous row segments (a lane's MFMA fragment covers 4 columns x 1 row, i.e. 8-B
-  // pieces of 16 different rows per store instruction). The main loop ended on a barrier: LDS is free.
-  constexpr int CS = BN + 8;  // LDS row stride (elements): 16-B pad keeps the fragment writes conflict-free
-  constexpr bool can_stage = BM * CS * 2 <= NBUF * (A_BYTES + B_BYTES);  // the C tile fits the LDS buffers
-  // beta != 0 (accumulate into C) is staged too when there is no bias/activation/aux: the bf16 product goes
-  // through LDS and the old C is added in the coalesced store pass (one extra bf16 rounding of the product).
-  const bool staged = can_stage && !a.atomic_out && !a.out_f32 && !(a.N & 7) && !(a.ldc & 7) &&
-                      !(reinterpret_cast<uintptr_t>(a.C) & 15) &&
-                      (a.beta == 0.f || (!a.bias && !a.act && !a.aux && (!a.stats || a.bnx)));
-  // BN-backward statistics are taken in the store pass from whole 16-B chunks (coalesced reads of the BN
-  // input and one mask byte per 8 channels) instead of per fragment
-  const bool bn_bwd = a.stats != nullptr && a.bnx != nullptr;
-  if (staged) {
-    bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int ml = wm * WTM + i * 16 + (lane & 15);
-      const int m = m0 + ml;
-      const bool mv = m < a.M;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4;
-        const int n = n0 + nl;
-        const bool nv = n < a.N;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
-        if (a.bias && nv) {
-          float4 b = *reinterpret_cast<const float4*>(a.bias + n);
-          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-        }
-        if (a.aux && mv && nv) {
-          uint2 o;
-          o.x = pack2bf(v[0], v[1]);
-          o.y = pack2bf(v[2], v[3]);
-          *reinterpret_cast<uint2*>(a.aux + cbase + out_row(a, m) * a.ldc + n) = o;
-        }
-        if (a.act == 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        } else if (a.act == 2) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-        }
-        uint2 o;
-        o.x = pack2bf(v[0], v[1]);
-        o.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(ct + ml * CS + nl) = o;
-        if (a.stats && !bn_bwd && a.beta == 0.f && mv && nv) {  // statistics of the stored (bf16) values
-          v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);
-          v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
-          stat_acc(a, out_row(a, m), n, v, csum[j], csq[j]);
-        }
-      }
-    }
-    __syncthreads();
-    constexpr int C8 = BN / 8;
-    static_assert(NT % C8 == 0, "a thread's channel chunk must stay fixed across the store pass");
-    const int c8t = threadIdx.x % C8;  // this thread's 8-channel chunk (constant over the pass)
-    float bs[8], bq[8], bmu[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) bs[r] = bq[r] = bmu[r] = 0.f;
-    if (bn_bwd && n0 + c8t * 8 < a.N) {
-      const float4 m0v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8);
-      const float4 m1v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8 + 4);
-      bmu[0] = m0v.x; bmu[1] = m0v.y; bmu[2] = m0v.z; bmu[3] = m0v.w;
-      bmu[4] = m1v.x; bmu[5] = m1v.y; bmu[6] = m1v.z; bmu[7] = m1v.w;
-    }
-#pragma unroll 4
-    for (int c = threadIdx.x; c < BM * C8; c += NT) {
-      const int ml = c / C8;
-      const int m = m0 + ml, n = n0 + c8t * 8;
-      if (m >= a.M || n >= a.N) continue;
-      uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8t * 8);
-      const long e = out_row(a, m) * a.ldc + n;
-      bf16_t* cp = reinterpret_cast<bf16_t*>(a.C) + cbase + e;
-      if (a.beta != 0.f) {
-        const uint4 old = *reinterpret_cast<const uint4*>(cp);
-        float f[8], g[8];
-        const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, ow[4] = {old.x, old.y, old.z, old.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f[2 * q] = __uint_as_float(vw[q] << 16); f[2 * q + 1] = __uint_as_float(vw[q] & 0xffff0000u);
-          g[2 * q] = __uint_as_float(ow[q] << 16); g[2 * q + 1] = __uint_as_float(ow[q] & 0xffff0000u);
-        }
-        // betamask: the old C is a BN(+ReLU) output gradient whose ReLU mask was not applied yet (the
-        // residual shortcut's gradient, taken lazily instead of materialised by the BN backward)
-        const uint32_t bm = a.betamask ? (uint32_t)a.betamask[(e + cbase) >> 3] : 0xFFu;  // e % 8 == 0
-#pragma unroll
-        for (int r = 0; r < 8; ++r) f[r] = ((bm >> r) & 1u) ? fmaf(a.beta, g[r], f[r]) : f[r];
-        val.x = pack2bf(f[0], f[1]); val.y = pack2bf(f[2], f[3]);
-        val.z = pack2bf(f[4], f[5]); val.w = pack2bf(f[6], f[7]);
-      }
-      *reinterpret_cast<uint4*>(cp) = val;
-      if (bn_bwd) {
-        const uint4 xr = *reinterpret_cast<const uint4*>(a.bnx + e);
-        const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3] : 0xFFu;  // e % 8 == 0
-        const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int r = 2 * q + h;
-            const float dv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
-            const float xv = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
-            const float dz = ((bits >> r) & 1u) ? dv : 0.f;
-            bs[r] += dz;
-            bq[r] = fmaf(dz, xv - bmu[r], bq[r]);
-          }
-        }
-      }
-    }
-    if (bn_bwd) {
-      // reduce the NT/C8 threads that share a channel chunk (fixed order: deterministic), one partial row
-      __syncthreads();
-      float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) { red[threadIdx.x * 16 + r] = bs[r]; red[threadIdx.x * 16 + 8 + r] = bq[r]; }
-      __syncthreads();
-      float* prow = a.stats + (long)tile_m * 2 * a.N;
-      for (int nl = threadIdx.x; nl < BN; nl += NT) {
-        const int n = n0 + nl;
-        if (n >= a.N) continue;
-        float sv = 0.f, qv = 0.f;
-        for (int t = nl >> 3; t < NT; t += C8) { sv += red[t * 16 + (nl & 7)]; qv += red[t * 16 + 8 + (nl & 7)]; }
-        prow[n] = sv;
-        prow[a.N + n] = qv;
-      }
-    } else if (a.stats) {
-      __syncthreads();  // the statistics reduction below reuses the LDS
-    }
-  } else
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * WTM + i * 16 + (lane & 15);
-    const bool mv = m < a.M;
-    const long mrow = out_row(a, mv ? m : 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WTN + j * 16 + (lane >> 4) * 4;
-      if (!mv || n >= a.N) continue;  // N % 4 == 0 is required by the host
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
-      const long off = cbase + mrow * a.ldc + n;
-      if (a.atomic_out) {
-        float* Cf = reinterpret_cast<float*>(a.C) + off;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd(Cf + r, v[r]);
-        continue;
-      }
-      if (a.beta != 0.f) {
-        if (a.out_f32) {
-          float4 o = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(a.C) + off);
-          v[0] += a.beta * o.x; v[1] += a.beta * o.y; v[2] += a.beta * o.z; v[3] += a.beta * o.w;
-        } else {
-          uint2 o = *reinterpret_cast<const uint2*>(reinterpret_cast<bf16_t*>(a.C) + off);
-          if (a.betamask) {  // zero the old values whose ReLU bit is clear (see the staged path)
-            const uint32_t bm = ((uint32_t)a.betamask[off >> 3] >> (off & 4)) & 0xFu;  // off % 4 == 0
-            o.x &= ((bm & 1u) ? 0x0000ffffu : 0u) | ((bm & 2u) ? 0xffff0000u : 0u);
-            o.y &= ((bm & 4u) ? 0x0000ffffu : 0u) | ((bm & 8u) ? 0xffff0000u : 0u);
-          }
-          v[0] += a.beta * __uint_as_float(o.x << 16); v[1] += a.beta * __uint_as_float(o.x & 0xffff0000u);
-          v[2] += a.beta * __uint_as_float(o.y << 16); v[3] += a.beta * __uint_as_float(o.y & 0xffff0000u);
-        }
-      }
-      if (a.bias) {
-        float4 b = *reinterpret_cast<const float4*>(a.bias + n);
-        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-      }
-      if (a.aux) {
-        uint2 o;
-        o.x = pack2bf(v[0], v[1]);
-        o.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(a.aux + off) = o;
-      }
-      if (a.act == 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      } else if (a.act == 2) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-      }
-      if (a.out_f32) {
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        uint2 o;
-        o.x = pack2bf(v[0], v[1]);
-        o.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.C) + off) = o;
-        if (a.stats) {  // statistics of the stored (bf16-rounded) values
-          v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);
-          v[2] = __uint_as_float(o.y << 16); v[3] = __uint_as_float(o.y & 0xffff0000u);
-        }
-      }
-      if (a.stats) stat_acc(a, mrow, n, v, csum[j], csq[j]);
-    }
-  }
-  if (a.stats && !(staged && bn_bwd)) {
-    // Deterministic BN statistics: reduce the 16 rows of a lane group by shuffles, the WM wave rows of
-    // the tile through LDS, then write ONE partial row per M-tile: stats[tile_m][0,N) = sum,
-    // stats[tile_m][N,2N) = sum of squares (bn_finalize sums the tiles_m rows). No atomics.
-    float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = row16_sum(csum[j][r]), q = row16_sum(csq[j][r]);
-        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4 + r;
-        if ((lane & 15) == 0) {
-          red[wm * BN + nl] = s;
-          red[WM * BN + wm * BN + nl] = q;
-        }
-      }
-    }
-    __syncthreads();
-    float* prow = a.stats + (long)tile_m * 2 * a.N;
-    for (int nl = threadIdx.x; nl < BN; nl += NT) {
-      const int n = n0 + nl;
-      if (n >= a.N) continue;
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) { s += red[w * BN + nl]; q += red[WM * BN + w * BN + nl]; }
-      prow[n] = s;
-      prow[a.N + n] = q;
-    }
-  }
+  gemm_epilogue<BM, BN, WM, WN, NT, NBUF * (A_BYTES + B_BYTES)>(a, acc, smem, m0, n0, tile_m, z, bz);
 }
 
 }  // namespace dtf

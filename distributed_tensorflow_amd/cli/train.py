@@ -72,6 +72,18 @@ def _step(model, loss_fn, x, y):
     return loss
 
 
+def _graph_def(model, opt):
+    """The training GraphDef (reference FileWriter(output_path, sess.graph), trainer/task.py:80,228)."""
+    from ..saved_model.graph_def import model_graph
+    return model_graph(model, training=True, optimizer=opt)[0].graph_def()
+
+
+def _meta_graph(model, opt):
+    """model.ckpt-N.meta next to every checkpoint (the Supervisor's Saver writes it in TF)."""
+    from ..saved_model.graph_def import training_meta_graph
+    return training_meta_graph(model, optimizer=opt)
+
+
 def run_standalone():
     from .. import context, summary
     from ..models.linear import LinearRegression
@@ -84,7 +96,7 @@ def run_standalone():
     loss_fn = LinearRegression.reference_loss()
     arena = opt.arena_for(model.trainable_variables)
     print("Save tensorboard files into: {}".format(FLAGS.output_path))
-    writer = summary.FileWriter(FLAGS.output_path, graph="linear_regression: y = X*weight + bias")
+    writer = summary.FileWriter(FLAGS.output_path, graph=_graph_def(model, opt))
     X = torch.as_tensor(train_X, device=dev).reshape(-1, 1, 1)
     Y = torch.as_tensor(train_Y, device=dev).reshape(-1, 1, 1)
     print("Run training with epoch number: {}".format(FLAGS.max_epochs))
@@ -131,7 +143,8 @@ def run_distributed(resolver):
         strategy.pull()
         global_step.assign(strategy.global_step())
 
-    saver = Saver({"weight": model.weight, "bias": model.bias, "global_step": global_step})
+    saver = Saver({"weight": model.weight, "bias": model.bias, "global_step": global_step},
+                  meta_graph_def=lambda: _meta_graph(model, opt))
     mt = ManagedTraining(is_chief, FLAGS.checkpoint_path, saver, global_step=lambda: strategy.global_step(),
                          save_model_secs=FLAGS.save_model_secs, before_save=before_save)
     with mt:
@@ -140,7 +153,7 @@ def run_distributed(resolver):
             print("Restored from {} at global_step {}".format(mt.restored_from, int(global_step.item())))
         strategy.setup_model(model, arena, opt)
         print("Save tensorboard files into: {}".format(FLAGS.output_path))
-        writer = summary.FileWriter(FLAGS.output_path) if is_chief else None
+        writer = summary.FileWriter(FLAGS.output_path, graph=_graph_def(model, opt)) if is_chief else None
         X = torch.as_tensor(train_X, device=dev).reshape(-1, 1, 1)
         Y = torch.as_tensor(train_Y, device=dev).reshape(-1, 1, 1)
         print("Run training with epoch number: {}".format(FLAGS.max_epochs))

@@ -6,8 +6,12 @@ Layout (reference trainer/task.py:264-291 writes ``saved_model_path/<model_versi
                                   holds ``serving_default`` (method ``tensorflow/serving/predict``)
   <dir>/variables/variables.{index,data-00000-of-00001}   tensor bundle (native writer)
   <dir>/dtf_model.json            how to rebuild the computation in this framework (class + init args +
-                                  build shape + signature -> method), since the graph runs on our kernels
-                                  rather than as a TF GraphDef (the MetaGraphDef's graph_def is empty).
+                                  build shape + signature -> method): this framework runs the model on its
+                                  own kernels. The MetaGraphDef also holds a real TF GraphDef (graph_def.py):
+                                  every variable as VariableV2 + initializer, the V2 Saver subgraph and its
+                                  SaverDef, the variables collections, and — for models that describe their
+                                  computation (the reference's linear model: Placeholder, Identity, Mul,
+                                  Add) — the serving graph whose tensors the signature names.
 The reference's legacy ``session_bundle`` exporter (trainer/task.py:294-307) is superseded by this
 format.
 """
@@ -65,22 +69,23 @@ def _map_entry(f, key, value_bytes):
     return _ld(f, _ld(1, key.encode()) + _ld(2, value_bytes))
 
 
-def signature_def(inputs, outputs, method_name=PREDICT_METHOD_NAME):
-    """inputs/outputs: {key: (dtype, shape)} -> serialized SignatureDef."""
+def signature_def(inputs, outputs, method_name=PREDICT_METHOD_NAME, tensor_names=None):
+    """inputs/outputs: {key: (dtype, shape)} -> serialized SignatureDef. tensor_names: {"inputs": {key: "node:0"},
+    "outputs": {...}} — the graph tensors the keys bind to (default "<key>:0")."""
+    tn = tensor_names or {}
     b = b""
     for k, (dt, shp) in sorted(inputs.items()):
-        b += _map_entry(1, k, _tensor_info(f"{k}:0", dt, shp))
+        b += _map_entry(1, k, _tensor_info(tn.get("inputs", {}).get(k, f"{k}:0"), dt, shp))
     for k, (dt, shp) in sorted(outputs.items()):
-        b += _map_entry(2, k, _tensor_info(f"{k}:0", dt, shp))
+        b += _map_entry(2, k, _tensor_info(tn.get("outputs", {}).get(k, f"{k}:0"), dt, shp))
     b += _ld(3, method_name.encode())
     return b
 
 
-def saved_model_proto(signatures, tags=(SERVING,)):
-    meta_info = _ld(1, b"dtf-1") + b"".join(_ld(4, t.encode()) for t in tags) + _ld(5, b"distributed_tensorflow_amd")
-    mg = _ld(1, meta_info) + _ld(2, b"")
-    for k, sig in sorted(signatures.items()):
-        mg += _map_entry(5, k, sig)
+def saved_model_proto(signatures, tags=(SERVING,), graph_def=b"", saver_def=None, collections=None):
+    from .graph_def import meta_graph_def
+    mg = meta_graph_def(graph_def, tags=tags, signature_defs=signatures, saver_def=saver_def,
+                        collections=collections)
     return _vi(1, 1) + _ld(2, mg)
 
 
@@ -216,8 +221,12 @@ def save(model, export_dir, signatures=None):
     os.makedirs(os.path.join(export_dir, "variables"), exist_ok=True)
     sig = signatures or (model.serving_signature() if hasattr(model, "serving_signature") else
                          _default_signature(model))
+    from .graph_def import model_graph
+    g, tensor_names, _ = model_graph(model, training=False)
+    saver_def = g.saver()
     sig_defs = {DEFAULT_SERVING_SIGNATURE_DEF_KEY: signature_def(sig["inputs"], sig["outputs"],
-                                                                 sig.get("method_name", PREDICT_METHOD_NAME))}
+                                                                 sig.get("method_name", PREDICT_METHOD_NAME),
+                                                                 tensor_names)}
     w = BundleWriter(os.path.join(export_dir, "variables", "variables"))
     for v in model.weights:
         w.add(v.name, v.detach())
@@ -230,7 +239,8 @@ def save(model, export_dir, signatures=None):
         json.dump(spec, f, indent=1)
     tmp = os.path.join(export_dir, "saved_model.pb.tmp")
     with open(tmp, "wb") as f:
-        f.write(saved_model_proto(sig_defs))
+        f.write(saved_model_proto(sig_defs, graph_def=g.graph_def(), saver_def=saver_def,
+                                  collections=g.collections()))
     os.replace(tmp, os.path.join(export_dir, "saved_model.pb"))
     return export_dir
 

@@ -147,9 +147,16 @@ def create_file_writer(logdir, **kw):
 
 
 def FileWriter(logdir, graph=None):
-    """TF1 tf.summary.FileWriter(logdir, graph)."""
+    """TF1 tf.summary.FileWriter(logdir, graph). `graph`: a serialized GraphDef, a graph_def.GraphBuilder, or a
+    Model (its TF training graph, saved_model.graph_def.model_graph) — written as the Event.graph_def record that
+    TensorBoard's graph dashboard renders."""
     w = SummaryWriter(logdir)
     if graph is not None:
+        if hasattr(graph, "graph_def"):
+            graph = graph.graph_def()
+        elif hasattr(graph, "weights") and hasattr(graph, "trainable_variables"):
+            from ..saved_model.graph_def import model_graph
+            graph = model_graph(graph, training=True)[0].graph_def()
         w.add_graph(graph if isinstance(graph, (str, bytes)) else repr(graph))
     return w
 
@@ -177,8 +184,8 @@ def histogram(name, data, step=None):
     return True
 
 
-def read_events(path):
-    """Parse an event file back into [(wall_time, step, {tag: value})] (used by tests and tooling)."""
+def read_event_records(path):
+    """The raw serialized Event protos of an event file, in order (TFRecord framing and CRCs checked)."""
     import ctypes
     lib = _native.runtime()
     h = lib.dtfrt_tfrecord_reader_open(path.encode())
@@ -194,10 +201,15 @@ def read_events(path):
                 break
             if rc < 0:
                 raise IOError(err(lib))
-            out.append(_parse_event(ctypes.string_at(data.value, n.value)))
+            out.append(ctypes.string_at(data.value, n.value))
     finally:
         lib.dtfrt_tfrecord_reader_close(h)
     return out
+
+
+def read_events(path):
+    """Parse an event file back into [(wall_time, step, {tag: value})] (used by tests and tooling)."""
+    return [_parse_event(r) for r in read_event_records(path)]
 
 
 def _read_varint(b, p):

@@ -261,7 +261,10 @@ class Saver:
     """tf.train.Saver: name-keyed variables, optional sharding (one data file per PS shard)."""
 
     def __init__(self, var_list=None, sharded=False, num_shards=None, shard_of=None, max_to_keep=5,
-                 async_write=False):
+                 async_write=False, meta_graph_def=None):
+        """meta_graph_def: serialized MetaGraphDef (or a callable returning it) written as `<prefix>.meta` next to
+        every checkpoint, like TF's Saver.save(write_meta_graph=True) (saved_model.graph_def.training_meta_graph)."""
+        self.meta_graph_def = meta_graph_def
         if isinstance(var_list, dict):
             self.var_map = dict(var_list)
         else:
@@ -280,16 +283,21 @@ class Saver:
             return int(self.shard_of(name)) % self.num_shards
         return i % self.num_shards
 
-    def save(self, sess=None, save_path="model.ckpt", global_step=None, write_state=True):
+    def save(self, sess=None, save_path="model.ckpt", global_step=None, write_state=True, write_meta_graph=True):
         prefix = save_path if global_step is None else f"{save_path}-{int(_as_int(global_step))}"
         names = list(self.var_map)
         snap = _snapshot({k: self._value(v) for k, v in self.var_map.items()})
+        meta = self.meta_graph_def() if callable(self.meta_graph_def) else self.meta_graph_def
 
         def write():
             w = BundleWriter(prefix, self.num_shards)
             for i, k in enumerate(names):
                 w.add(k, snap[k], self._shard(k, i))
             w.finish()
+            if write_meta_graph and meta:
+                with open(prefix + ".meta.tmp", "wb") as f:
+                    f.write(meta)
+                os.replace(prefix + ".meta.tmp", prefix + ".meta")
             if write_state:
                 d = os.path.dirname(prefix) or "."
                 self._kept = [p for p in self._kept if p != prefix] + [prefix]

@@ -404,7 +404,8 @@ def test_conv_bn_direct_arena_grads(cuda):
 @pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 3, 3, 1, 1), (2, 16, 16, 64, 128, 3, 3, 2, 1),
                                   (2, 12, 12, 256, 64, 1, 1, 1, 0), (4, 8, 8, 16, 32, 3, 3, 1, 1)])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
-def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta):
+@pytest.mark.parametrize("tile", [-1, 11])
+def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta, tile):
     """dtf_conv_dgrad's BN-backward epilogue: partial rows of sum(dz), sum(dz*(x-mean)) with dz = dX*mask."""
     from distributed_tensorflow_amd.ops import conv as C
     from distributed_tensorflow_amd.ops._util import IntOut, call, crsk_shadow, ptr, stream, workspace
@@ -425,7 +426,7 @@ def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta):
     ws = workspace(cuda)
     wc = crsk_shadow(w, K, R * S, Cin)
     call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, Cin, K, R, S, g[7], g[8], st, st, pd, pd, 1, 1, 0,
-         beta, -1, ptr(ws), 2 * ws.numel(), ptr(yc), ptr(bits), ptr(mean), ptr(part), rows.addr, None, stream())
+         beta, tile, ptr(ws), 2 * ws.numel(), ptr(yc), ptr(bits), ptr(mean), ptr(part), rows.addr, None, stream())
     T = rows.value
     assert T >= 1
     p = part[:T * 2 * Cin].view(T, 2 * Cin).sum(0)
@@ -436,12 +437,13 @@ def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta):
     close(p[Cin:], q_ref, 1e-3)
 
 
-@pytest.mark.parametrize("tile", [0, 2, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("tile", [0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 9, 128, 64, 1, 1, 1, 0),
-                                  (2, 15, 15, 64, 64, 3, 3, 2, 1)])
+                                  (2, 15, 15, 64, 64, 3, 3, 2, 1), (5, 13, 11, 128, 192, 3, 3, 1, 1)])
 def test_conv_staging_pipelines_agree(cuda, case, tile):
-    """Every staging pipeline (register-staged single/double LDS buffer, LDS-DMA single/double buffer) and
-    tile shape computes bitwise the same conv forward and data gradient (same per-element K order)."""
+    """Every staging pipeline (register-staged single/double LDS buffer, LDS-DMA single/double buffer, the
+    256-row triple-buffered conv256 kernel: tiles 11-13) and tile shape computes bitwise the same conv forward
+    and data gradient (same per-element K order)."""
     from distributed_tensorflow_amd.ops import conv as C
     from distributed_tensorflow_amd.ops._util import call, crsk_shadow, ptr, stream, workspace
     N, H, W, Cin, K, R, S, st, pd = case
@@ -540,3 +542,46 @@ def test_bert_layer_residual_grad_link(cuda, monkeypatch):
         res[link] = [t.float().cpu() for t in grads]
     for a, b in zip(res[False], res[True]):
         assert (a - b).abs().max().item() <= 2e-2 * a.abs().max().item() + 1e-6
+
+
+@pytest.mark.parametrize("tile", [11, 12, 13, 14])
+@pytest.mark.parametrize("case", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 9, 128, 64, 1, 1, 1, 0),
+                                  (2, 15, 15, 64, 64, 3, 3, 2, 1), (2, 12, 12, 64, 256, 1, 1, 2, 0),
+                                  (4, 7, 9, 16, 64, 4, 4, 1, 0)])
+def test_conv_wgrad_conv256_matches_reference(cuda, case, tile):
+    """Weight gradient on the 256-row pipelined kernel (dW^T = X^T dY over split-K slabs, reduced and
+    transposed; forced tiles 11-13) against the f32 reference, accumulating into an existing gradient."""
+    from distributed_tensorflow_amd.ops import conv as C
+    from distributed_tensorflow_amd.ops._util import call, ptr, stream, workspace
+    N, H, W, Cin, K, R, S, st, pd = case
+    x = rnd(N, H, W, Cin, dev=cuda)
+    g = C._geom(x, torch.empty(K, R, S, Cin), (st, st), (pd, pd), (1, 1))
+    P, Q = g[7], g[8]
+    dy = rnd(N, P, Q, K, dev=cuda)
+    ws = workspace(cuda)
+    base = torch.randn(K, R, S, Cin, device=cuda)
+    dw = base.clone()
+    call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw), N, H, W, Cin, K, R, S, P, Q, st, st, pd, pd, 1, 1, 1, 0, tile,
+         ptr(ws), ws.numel(), stream())
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = torch.zeros(K, Cin, R, S, device=cuda, requires_grad=True)
+    torch.nn.functional.conv2d(xr, wr, stride=st, padding=pd).backward(dy.float().permute(0, 3, 1, 2))
+    close((dw - base).permute(0, 3, 1, 2), wr.grad, 1e-2)
+
+
+def test_conv256_default_path_bn_stats(cuda):
+    """A layer on the default conv256 route (>= 192 blocks of 256 rows, N >= 256, K >= 1024: ResNet-50 stage 3):
+    forward with the BN statistics epilogue against the f32 reference, partial rows summing to the column sums /
+    sums of squares."""
+    from distributed_tensorflow_amd.ops import conv as C
+    N, H, W, Cin, K = 64, 28, 28, 128, 256
+    x = rnd(N, H, W, Cin, dev=cuda)
+    w = torch.randn(K, 3, 3, Cin, device=cuda) / math.sqrt(9 * Cin)
+    g = C._geom(x, w, (1, 1), (1, 1), (1, 1))
+    y, part, rows = C.conv_fwd_raw(x, w.to(BF), g, stats=True)
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.to(BF).float().permute(0, 3, 1, 2), padding=1)
+    close(y.permute(0, 3, 1, 2).float(), yr, 1e-2)
+    p = part[:rows * 2 * K].view(rows, 2 * K).sum(0)
+    yf = y.float().reshape(-1, K)
+    close(p[:K], yf.sum(0), 1e-3)
+    close(p[K:], (yf * yf).sum(0), 1e-3)
