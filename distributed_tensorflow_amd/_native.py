@@ -70,6 +70,10 @@ _KERNEL_SIGS = {
     "dtf_quant_fp8": [P, P, L, P, P, I, P],
     "dtf_fp8_update_scale": [P, P, F, P],
     "dtf_group_rows_once": [P, L, I, L, I, P, P],
+    "dtf_ipc_export": [P, P, P],
+    "dtf_ipc_open": [P, P],
+    "dtf_ipc_close": [P],
+    "dtf_memcpy_async": [P, P, L, P],
 }
 
 

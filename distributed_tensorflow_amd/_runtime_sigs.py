@@ -59,6 +59,17 @@ SIGS = {
     "dtfrt_ps_push": (I, [P, I, U64, P, U64, P]),
     "dtfrt_ps_var_bytes": (I64, [P, I]),
     "dtfrt_ps_close": (None, [P]),
+    # intra-node PS mailbox + shared-memory regions (ps_mailbox.cc)
+    "dtfrt_mbox_create": (P, [S, I]),
+    "dtfrt_mbox_open": (P, [S, I]),
+    "dtfrt_mbox_post": (I64, [P, I, I, U64]),
+    "dtfrt_mbox_wait": (I, [P, I, I64, I]),
+    "dtfrt_mbox_next": (I, [P, I, P, P, P, P]),
+    "dtfrt_mbox_complete": (I, [P, I, I64, I]),
+    "dtfrt_mbox_close": (None, [P, I]),
+    "dtfrt_shmem_create": (P, [S, U64]),
+    "dtfrt_shmem_open": (P, [S, U64, I]),
+    "dtfrt_shmem_close": (None, [P, U64, S, I]),
     # shared-memory CPU all-reduce
     "dtfrt_shm_open": (P, [S, I, I, U64]),
     "dtfrt_shm_allreduce_f32": (I, [P, P, U64]),

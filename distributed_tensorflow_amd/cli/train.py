@@ -34,7 +34,8 @@ flags.DEFINE_string("optimizer", "sgd", "Optimizer to train")
 flags.DEFINE_string("saved_model_path", "./saved_model/", "The path of the saved model")
 flags.DEFINE_integer("model_version", 1, "The version of the model")
 flags.DEFINE_integer("seed", -1, "Data seed (-1: unseeded like the reference)")
-flags.DEFINE_string("device", "cpu", "Compute device for the linear model (cpu, cuda:0, /GPU:0)")
+flags.DEFINE_string("device", "cpu", "Compute device for the linear model (cpu, cuda:0, /GPU:0; auto = the task's "
+                                     "GPU when one is visible, else the CPU)")
 flags.DEFINE_integer("save_model_secs", 60, "Chief checkpoint interval in seconds")
 flags.DEFINE_boolean("export_standalone", False, "Also export a SavedModel in standalone mode")
 flags.DEFINE_boolean("ps_join_forever", False, "PS never exits (trainer/task.py server.join())")
@@ -72,6 +73,11 @@ def _step(model, loss_fn, x, y):
     return loss
 
 
+def _device():
+    from .. import context
+    return context.default_device() if FLAGS.device == "auto" else context.parse_device(FLAGS.device)
+
+
 def _graph_def(model, opt):
     """The training GraphDef (reference FileWriter(output_path, sess.graph), trainer/task.py:80,228)."""
     from ..saved_model.graph_def import model_graph
@@ -90,7 +96,7 @@ def run_standalone():
     train_X, train_Y = _data()
     start = datetime.datetime.now()
     opt = _optimizer()
-    dev = context.parse_device(FLAGS.device)
+    dev = _device()
     with context.device(dev):
         model = LinearRegression()
     loss_fn = LinearRegression.reference_loss()
@@ -130,13 +136,14 @@ def run_distributed(resolver):
     train_X, train_Y = _data()
     start = datetime.datetime.now()
     opt = _optimizer()
-    dev = context.parse_device(FLAGS.device)
+    dev = _device()
     strategy = ParameterServerStrategy(resolver, variable_partitioner=FLAGS.partitioner, device=dev)
+    print("PS data plane: {}".format(strategy.transport), flush=True)
     is_chief = strategy.is_chief
     with strategy.scope():
         model = LinearRegression()
     loss_fn = LinearRegression.reference_loss()
-    arena = opt.arena_for(model.trainable_variables)
+    arena = opt.arena_for(strategy.order_variables(model.trainable_variables))
     global_step = Variable(0, trainable=False, name="global_step", dtype=torch.int64)
 
     def before_save():  # checkpoint the PS state (the Saver runs on the PS shards in TF)
@@ -192,12 +199,10 @@ def main(argv=None):
     r = TFConfigClusterResolver()
     if r.is_ps:
         from ..parallel.parameter_server import ParameterServer
-        if FLAGS.ps_join_forever:
-            ps = ParameterServer(r, device=FLAGS.device)
-            ps.num_trainers = 1 << 30  # never "all done": plain server.join()
-            ps.serve()
-            return 0
-        ParameterServer(r, device=FLAGS.device).serve()
+        ps = ParameterServer(r, device=_device())
+        print("PS data plane: {}".format(ps.transport), flush=True)
+        ps.serve(forever=bool(FLAGS.ps_join_forever))  # forever: plain server.join() (no auto-stop)
+        print("PS applied {} updates".format(ps.applies))
         print("PS exits after all workers done")
         return 0
     if r.task_type in ("worker", "master", "chief"):

@@ -26,8 +26,11 @@ def _stack():
 
 
 def default_device() -> torch.device:
+    """DTF_DEVICE_ORDINAL (set per task by cli.launch: every GPU stays visible so PS tasks and trainers can map each
+    other's memory), else LOCAL_RANK (torchrun), else GPU 0; the CPU when no GPU is visible."""
     if torch.cuda.is_available():
-        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+        idx = os.environ.get("DTF_DEVICE_ORDINAL", os.environ.get("LOCAL_RANK", "0"))
+        return torch.device("cuda", int(idx) % max(1, torch.cuda.device_count()))
     return torch.device("cpu")
 
 

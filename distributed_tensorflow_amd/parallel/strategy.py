@@ -95,6 +95,11 @@ class Strategy:
             _tls.strategy = prev
 
     # ---- training-loop hooks
+    def order_variables(self, variables):
+        """The order of the trainable variables in the model's parameter arena (identity by default;
+        ParameterServerStrategy groups them by PS shard)."""
+        return list(variables)
+
     def setup_model(self, model, arena):
         """Called once after the trainable arena exists (broadcast initial state, install hooks)."""
 

@@ -154,13 +154,18 @@ def test_parameter_server_strategy_keras_fit(tmp_path):
 
 
 @pytest.mark.slow
-def test_ps_runbook_collective_transport(tmp_path):
-    """The PS runbook over the torch.distributed point-to-point transport (gloo here; RCCL between GPUs):
-    2 PS + 1 worker + master, per-pair groups, shard-parallel push/pull, DONE-driven PS exit."""
+@pytest.mark.parametrize("transport", ["", "tcp"])
+def test_ps_runbook_negotiated_transport(tmp_path, transport):
+    """The PS runbook with the data plane the chief negotiates for the whole cluster (unset: every task on one host
+    -> 'shm', direct copies into the PS's memory + the native mailbox) or forced to 'tcp' through the chief's
+    environment: 2 PS + 1 worker + master, ASSIGN/PUSH/pull per shard, DONE-driven PS exit, export, checkpoint."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, DTF_PS_TRANSPORT="collective")
+    env = dict(os.environ)
+    env.pop("DTF_PS_TRANSPORT", None)
+    if transport:
+        env["DTF_PS_TRANSPORT"] = transport
     env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     cmd = [sys.executable, "-m", "distributed_tensorflow_amd.cli.launch", "--ps", "2", "--workers", "1", "--chief",
            "1", "--timeout", "240", "--", sys.executable, "-m", "distributed_tensorflow_amd.cli.train", "--seed=0",
@@ -170,9 +175,40 @@ def test_ps_runbook_collective_transport(tmp_path):
     assert r.returncode == 0, out[-4000:]
     assert out.count("PS exits after all workers done") == 2
     assert "Exported SavedModel" in out
+    assert f"PS data plane: {transport or 'shm'}" in out
     from distributed_tensorflow_amd.train import checkpoint as C
     ck = C.latest_checkpoint(str(tmp_path / "checkpoint"))
     names = dict(C.list_variables(ck))
     assert {"weight", "bias", "global_step"} <= set(names)
     w = float(C.load_variable(ck, "weight"))
     assert 1.0 < w < 3.0, w
+
+
+@pytest.mark.slow
+def test_ps_shm_two_ps_six_trainers(tmp_path):
+    """BASELINE config 4's topology (2 PS + 6 trainers) on the CPU through ONE serve loop per PS: 6 trainers
+    (master + 5 workers) push/pull concurrently through the shared-memory mailbox; every update is applied
+    (global_step counts all of them) and the model converges (async SGD, reference trainer/task.py:232-236)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("DTF_PS_TRANSPORT", None)
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    cmd = [sys.executable, "-m", "distributed_tensorflow_amd.cli.launch", "--ps", "2", "--workers", "5", "--chief",
+           "1", "--timeout", "280", "--", sys.executable, "-m", "distributed_tensorflow_amd.cli.train", "--seed=0",
+           "--max_epochs=2", "--optimizer=sgd", "--learning_rate=0.01"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=320)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert out.count("PS exits after all workers done") == 2
+    assert out.count("PS data plane: shm") >= 8
+    from distributed_tensorflow_amd.train import checkpoint as C
+    ck = C.latest_checkpoint(str(tmp_path / "checkpoint"))
+    gs = int(C.load_variable(ck, "global_step"))
+    assert 2 * 100 <= gs <= 6 * 2 * 100, gs  # the chief saved while the other trainers were still stepping
+    import re
+    applied = [int(m) for m in re.findall(r"PS applied (\d+) updates", out)]
+    assert applied == [6 * 2 * 100] * 2, applied  # every trainer's every push reached both shards
+    w, b = float(C.load_variable(ck, "weight")), float(C.load_variable(ck, "bias"))
+    assert 1.5 < w < 2.5 and 9.5 < b < 10.5, (w, b)

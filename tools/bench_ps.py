@@ -3,12 +3,15 @@
 
     python tools/bench_ps.py --gpus 8 [--steps 20 --warmup 5 --batch 256]
 
-Without TF_CONFIG it launches the local cluster itself (cli.launch: one process per task, one GPU each,
-ps tasks included, launcher-hosted coordination store): P = max(1, gpus // 4) parameter servers holding
-the variable shards in their HBM, the rest trainers (the first is the chief). The data plane is the
-collective transport (RCCL point-to-point between GPUs; gloo + host staging when the PS runs on the CPU,
-`--ps_cpu`, which is also what a 1-GPU box needs). Training is asynchronous as in the reference: every
-trainer pushes its gradients to the PS shards after each step and continues with the returned values.
+Without TF_CONFIG it launches the local cluster itself (cli.launch: one process per task, every GPU visible, the
+task's own GPU by ordinal, launcher-hosted coordination store): `--ps` parameter servers (default
+max(1, gpus // 4)) holding the variable shards in their HBM, `--trainers` trainers (default the remaining GPUs; the
+first is the chief). Tasks are assigned GPUs round-robin over `--gpus`, so `--gpus 1 --ps 1 --trainers 3` rehearses
+the whole data plane on one GPU. The data plane is the one the chief negotiates — on one node `shm`: gradients are
+copied into per-trainer inboxes in the PS's HBM (HIP IPC, xGMI between GPUs) and parameters copied back out, a
+shared-memory mailbox carries the requests (parallel/ps_shm.py); `--ps_cpu` keeps the shards in host shared memory.
+Training is asynchronous as in the reference: every trainer pushes its gradients to the PS shards after each step
+and continues with the values it pulls.
 Each trainer times its own `--steps` steps after `--warmup`; the chief sums the trainers' images/sec and
 prints one JSON line (metric: images/sec whole node, async PS).
 """
@@ -29,27 +32,24 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--depth", type=int, default=50)
-    ap.add_argument("--ps_cpu", action="store_true", help="PS shards in host memory (gloo transport)")
+    ap.add_argument("--ps", type=int, default=None, help="PS tasks (default max(1, gpus // 4))")
+    ap.add_argument("--trainers", type=int, default=None, help="trainer tasks (default: the remaining GPUs)")
+    ap.add_argument("--ps_cpu", action="store_true", help="PS shards in host shared memory")
     ap.add_argument("--timeout", type=float, default=1500)
     return ap.parse_args()
 
 
 def launch(a):
     from distributed_tensorflow_amd.cli.launch import launch as run_cluster
-    n_ps = 1 if a.ps_cpu else max(1, a.gpus // 4)
-    n_tr = a.gpus if a.ps_cpu else a.gpus - n_ps
+    n_ps = a.ps if a.ps is not None else (1 if a.ps_cpu else max(1, a.gpus // 4))
+    n_tr = a.trainers if a.trainers is not None else (a.gpus if a.ps_cpu else a.gpus - n_ps)
     if n_tr < 1:
-        raise SystemExit("need at least one trainer GPU (use --ps_cpu on a 1-GPU box)")
-    gpus = ",".join(str(i) for i in range(a.gpus))
-    env = {"DTF_PS_TRANSPORT": "collective", "DTF_BENCH_PS_CPU": "1" if a.ps_cpu else "0"}
+        raise SystemExit("need at least one trainer (pass --trainers on a 1-GPU box)")
+    env = {"DTF_BENCH_PS_CPU": "1" if a.ps_cpu else "0"}
     cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
-    if a.ps_cpu:
-        rc, _ = run_cluster(cmd, num_ps=n_ps, num_workers=n_tr - 1, num_chief=1, gpus=gpus, ps_gpus=False, env=env,
-                            timeout=a.timeout, host_kv=True)
-    else:  # PS tasks take the first GPUs
-        order = [str(i) for i in range(a.gpus)]
-        rc, _ = run_cluster(cmd, num_ps=n_ps, num_workers=n_tr - 1, num_chief=1, gpus=",".join(order), ps_gpus=True,
-                            env=env, timeout=a.timeout, host_kv=True)
+    gpus = ",".join(str(i) for i in range(a.gpus))  # PS tasks first, then trainers, round-robin
+    rc, _ = run_cluster(cmd, num_ps=n_ps, num_workers=n_tr - 1, num_chief=1, gpus=gpus, ps_gpus=not a.ps_cpu,
+                        env=env, timeout=a.timeout, host_kv=True)
     return rc
 
 
@@ -59,12 +59,13 @@ def task(a):
     from distributed_tensorflow_amd.parallel.parameter_server import ParameterServerStrategy, run_parameter_server
     r = TFConfigClusterResolver()
     ps_cpu = os.environ.get("DTF_BENCH_PS_CPU") == "1"
+    from distributed_tensorflow_amd import context
     if r.is_ps:
-        return run_parameter_server(r, device="cpu" if ps_cpu else "cuda:0")
+        return run_parameter_server(r, device="cpu" if ps_cpu else context.default_device())
     from distributed_tensorflow_amd.data import synthetic_imagenet
     from distributed_tensorflow_amd.keras import losses, optimizers
     from distributed_tensorflow_amd.models import ResNet
-    dev = torch.device("cuda:0")
+    dev = context.default_device()
     strat = ParameterServerStrategy(r, variable_partitioner="balanced", device=dev)
     with strat.scope():
         model = ResNet(a.depth, num_classes=1000)
