@@ -25,7 +25,7 @@ import torch
 
 from .. import context
 from .. import profiler as prof
-from ..ops._util import advance_rng, direct_grads
+from ..ops._util import advance_rng, direct_grads, join_side_streams
 from ..data import Dataset
 from ..parallel import strategy as S
 from . import callbacks as cbs
@@ -181,6 +181,7 @@ class Model(Layer):
         arena = self._ensure_arena()
         with prof.phase("backward"), direct_grads():  # includes the overlapped bucket all-reduces
             strat.backward(loss, arena)
+            join_side_streams()  # weight gradients issued on the side stream are in the arena
         with prof.phase("optimizer"):
             strat.apply_gradients(self.optimizer, arena)
         return self._update_metrics(loss, y, y_pred)

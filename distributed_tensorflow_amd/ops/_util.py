@@ -34,13 +34,67 @@ WS_ELEMS = 32 << 20  # 128 MiB of f32 split-K slabs per device
 
 
 def workspace(device, nelem=WS_ELEMS):
-    """Persistent per-device f32 scratch (split-K slabs). Stream-ordered reuse only."""
-    key = (device.type, device.index)
+    """Persistent f32 scratch (split-K slabs) per device AND stream: stream-ordered reuse only, so kernels on
+    the weight-gradient side stream (side_stream) get their own buffer."""
+    sid = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
+    key = (device.type, device.index, sid)
     w = _WS.get(key)
     if w is None or w.numel() < nelem:
         w = torch.empty(nelem, dtype=torch.float32, device=device)
         _WS[key] = w
     return w
+
+
+# ---------------------------------------------------------------- weight-gradient side stream
+# In a backward pass the weight gradient of a layer (dW = X^T dY) and its data gradient (dX = dY W^T) are
+# independent: only dX is on the critical path to the earlier layers. With direct arena accumulation the weight
+# gradient runs on a second HIP stream, concurrently with the dgrad chain: it fills the tail waves of the dgrad
+# GEMMs and the latency-bound BatchNorm reduction launches that otherwise leave CUs idle. The side stream joins the
+# main stream before anything reads the gradient arena (bucket all-reduce, optimizer: join_side_streams).
+_SIDE = {}
+_SIDE_USED = set()
+SIDE_STREAM_ON = __import__("os").environ.get("DTF_WGRAD_STREAM", "1") != "0"
+
+
+def side_stream(device):
+    s = _SIDE.get(device.index)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _SIDE[device.index] = s
+    return s
+
+
+def fork_side(device, *tensors):
+    """Make the side stream wait for the main stream's work so far; the tensors it reads stay allocated until
+    the side stream is done with them. Returns the stream context to issue side work in."""
+    side = side_stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    for t in tensors:
+        if t is not None:
+            t.record_stream(side)
+    _SIDE_USED.add(device.index)
+    return torch.cuda.stream(side)
+
+
+def comm_stream_ctx(device):
+    """Where to issue a collective over arena gradients: on the side stream (after it has also waited for the
+    main stream) when weight gradients are in flight there — the collective then waits for both without
+    blocking the main stream's dgrad chain — else the current stream."""
+    import contextlib
+    if device.type != "cuda" or device.index not in _SIDE_USED:
+        return contextlib.nullcontext()
+    side = _SIDE[device.index]
+    side.wait_stream(torch.cuda.current_stream(device))
+    return torch.cuda.stream(side)
+
+
+def join_side_streams():
+    """Main stream waits for every side-stream weight gradient issued so far."""
+    if not _SIDE_USED:
+        return
+    for idx in list(_SIDE_USED):
+        torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
+    _SIDE_USED.clear()
 
 
 def stream():

@@ -11,8 +11,8 @@ from __future__ import annotations
 
 import torch
 
-from ._util import (BF16, F32, IntOut, bf16_shadow, call, crsk_shadow, direct_grad, on_gpu, ptr,
-                    stream, workspace)
+from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, bf16_shadow, call, crsk_shadow, direct_grad, fork_side,
+                    on_gpu, ptr, stream, workspace)
 
 
 def out_size(h, k, s, p, d=1):
@@ -311,6 +311,16 @@ class _ConvBNFn(torch.autograd.Function):
         elif link is not None and role == "res":
             dres = link.park(dres)
         dx = dw = None
+        if ctx.needs_input_grad[1]:
+            tw = direct_grad(w)
+            if tw is not None and SIDE_STREAM_ON:
+                with fork_side(x.device, x, dyc):  # off the critical path: overlaps the dgrad chain
+                    conv_wgrad_raw(x, dyc, g, out=tw)
+            else:
+                dw = conv_wgrad_raw(x, dyc, g, out=tw)
+            if tw is not None:
+                dw = None  # (autograd still runs the parameter's AccumulateGrad node with an undefined
+                #            gradient, so its post-accumulate hooks — gradient bucketing — fire as usual)
         if ctx.needs_input_grad[0]:
             acc, acc_mask = link.take() if (link is not None and role == "acc") else (None, None)
             src = ctx.in_src
@@ -320,12 +330,6 @@ class _ConvBNFn(torch.autograd.Function):
             ctx.in_src = None
             if link is not None and role == "proj":
                 dx = link.park(dx)
-        if ctx.needs_input_grad[1]:
-            tw = direct_grad(w)
-            dw = conv_wgrad_raw(x, dyc, g, out=tw)
-            if tw is not None:
-                dw = None  # (autograd still runs the parameter's AccumulateGrad node with an undefined
-                #            gradient, so its post-accumulate hooks — gradient bucketing — fire as usual)
         if direct_bn:
             dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None

@@ -142,16 +142,25 @@ class GradientBucketer:
     def _launch(self, b):
         lo, hi = self.buckets[b]
         t = self.arena.grad[lo:hi]
-        if self.wire == "bf16":
-            if self._wirebuf is None:
-                self._wirebuf = torch.empty(self.arena.grad.numel(), dtype=torch.bfloat16, device=t.device)
-            w = self._wirebuf[lo:hi]
-            _cast(t, w)
-            t = w
-        self._works[b] = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        import contextlib
+        ctx = contextlib.nullcontext()
+        if t.is_cuda:  # the bucket's weight gradients may still be in flight on the side stream
+            from ..ops._util import comm_stream_ctx
+            ctx = comm_stream_ctx(t.device)
+        with ctx:
+            if self.wire == "bf16":
+                if self._wirebuf is None:
+                    self._wirebuf = torch.empty(self.arena.grad.numel(), dtype=torch.bfloat16, device=t.device)
+                w = self._wirebuf[lo:hi]
+                _cast(t, w)
+                t = w
+            self._works[b] = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finalize(self):
         """Issue buckets whose variables got no gradient (in order), then wait for all of them."""
+        if self.arena.grad.is_cuda:
+            from ..ops._util import join_side_streams
+            join_side_streams()
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
