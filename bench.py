@@ -94,6 +94,9 @@ def main():
                     help="gradient all-reduce payload type (default f32; bf16 halves the xGMI bytes)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture the whole train step in a hipGraph (compile(jit_compile=True))")
+    ap.add_argument("--hiprio", type=int, default=0,
+                    help="1: issue the train step on a high-priority HIP stream (the weight-gradient side stream "
+                         "keeps normal priority, so the dgrad critical path wins block dispatch)")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
@@ -113,10 +116,15 @@ def main():
         strategy = parallel.MirroredStrategy(bucket_mb=args.bucket_mb, communication_options=co)
     rank = strategy.worker_index
     dev = strategy.device
+    if args.hiprio:
+        hs = torch.cuda.Stream(device=dev, priority=-1)
+        hs.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(hs)
     model, data, unit, cfg = build(args, strategy, dev, rank)
     model._jit = bool(args.graph)
     train_fn = model.make_train_function(force=True)
     cfg["hipgraph"] = type(train_fn).__name__ == "CapturedStep"
+    cfg["hiprio"] = bool(args.hiprio)
 
     def step():
         x, y = next(data)

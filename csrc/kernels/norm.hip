@@ -12,6 +12,8 @@
 //   write one partial row per block (no same-address atomics: deterministic).
 #include "common.h"
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 
 namespace {
 
@@ -151,6 +153,10 @@ __device__ __forceinline__ void bn_bwd_finalize_channel(int c, int C, float sdz,
 // Partial-row reduction and per-channel finalize in ONE launch: block (x, g) sums rows [g*sg, (g+1)*sg) of
 // the 64 channels [64x, 64x+64) (both the [0,C) and [C,2C) halves) into the group's leader row; the last-
 // arriving group of channel block x sums the leader rows in order (deterministic) and finalizes.
+// Thread layout: 32 float4 columns (16 channel quads of each half) x 8 row lanes; every thread keeps up to
+// 8 independent 16-B loads in flight, so a pass over ~sqrt(T) rows is one or two memory latencies.
+constexpr int RF_LANES = 8;
+
 template <bool BWD>
 __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restrict__ part, int T, long rs, int sg,
                                                                  int C, long M, const float* __restrict__ gamma,
@@ -158,53 +164,81 @@ __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restri
                                                                  float* rm_or_invstd, float* running_var,
                                                                  float momentum, float eps, float* o0, float* o1,
                                                                  float* o2, float* o3, int accumulate, int* tickets) {
-  __shared__ float red[2][4][64];
+  __shared__ float4 red[RF_LANES][32];
   __shared__ int flag;
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int r0 = blockIdx.y * sg, r1 = min(T, r0 + sg);
-  // 4 independent accumulator pairs: 8 partial-row loads in flight per thread (the pass is L2-latency bound)
-  float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (c < C) {
-    int r = r0 + grp;
-    for (; r + 12 < r1; r += 16) {
+  const int col = threadIdx.x & 31, lane = threadIdx.x >> 5;
+  const int c = blockIdx.x * 64 + (col & 15) * 4;     // first channel of this thread's quad
+  const long off = (col < 16 ? 0 : C) + c;            // sum half / sum-of-squares half
+  const bool cv = c < C;
+  // sum rows r0 + lane, r0 + lane + 8, ... < r1 with row stride `stride` (in rows of rs floats)
+  auto sweep = [&](int r0, int r1, long stride) {
+    float4 acc[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a4[u] += part[(long)(r + 4 * u) * rs + c];
-        b4[u] += part[(long)(r + 4 * u) * rs + C + c];
+    for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (cv) {
+      int r = r0 + lane;
+      for (; r + 7 * RF_LANES < r1; r += 8 * RF_LANES) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(part + (long)(r + u * RF_LANES) * stride * rs + off);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc[u & 3].x += v[u].x; acc[u & 3].y += v[u].y; acc[u & 3].z += v[u].z; acc[u & 3].w += v[u].w;
+        }
+      }
+      for (int u = 0; r < r1; r += RF_LANES, ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(part + (long)r * stride * rs + off);
+        acc[u & 3].x += v.x; acc[u & 3].y += v.y; acc[u & 3].z += v.z; acc[u & 3].w += v.w;
       }
     }
-    for (; r < r1; r += 4) { a4[0] += part[(long)r * rs + c]; b4[0] += part[(long)r * rs + C + c]; }
-  }
-  red[0][grp][cl] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-  red[1][grp][cl] = (b4[0] + b4[1]) + (b4[2] + b4[3]);
-  __syncthreads();
-  if (grp == 0 && c < C) {
-    part[(long)r0 * rs + c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
-    part[(long)r0 * rs + C + c] = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
-  }
+    float4 t;
+    t.x = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x);
+    t.y = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
+    t.z = (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z);
+    t.w = (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w);
+    red[lane][col] = t;
+    __syncthreads();
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane == 0) {
+#pragma unroll
+      for (int l = 0; l < RF_LANES; ++l) {
+        const float4 q = red[l][col];
+        s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
+      }
+    }
+    return s;
+  };
+  const int r0 = blockIdx.y * sg, r1 = min(T, r0 + sg);
+  const float4 grp = sweep(r0, r1, 1);
+  if (lane == 0 && cv) *reinterpret_cast<float4*>(part + (long)r0 * rs + off) = grp;
   if (!last_arriver(tickets + blockIdx.x, gridDim.y, &flag)) return;
-  const int G = gridDim.y;
-  float a = 0.f, b = 0.f;
-  if (c < C)
-    for (int g = grp; g < G; g += 4) { a += part[(long)g * sg * rs + c]; b += part[(long)g * sg * rs + C + c]; }
+  const float4 tot = sweep(0, gridDim.y, sg);  // the leader rows: row g*sg
   __syncthreads();
-  red[0][grp][cl] = a;
-  red[1][grp][cl] = b;
+  if (lane == 0) red[0][col] = tot;
   __syncthreads();
-  if (grp != 0 || c >= C) return;
-  a = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
-  b = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
-  if constexpr (BWD)
-    bn_bwd_finalize_channel(c, C, a, b, gamma, beta_or_mean, rm_or_invstd, M, o0, o1, accumulate, o2);
-  else
-    bn_finalize_channel(c, a, b, gamma, beta_or_mean, rm_or_invstd, running_var, M, momentum, eps, o0, o1, o2, o3);
+  if (threadIdx.x >= 16 || !cv) return;
+  const float4 a = red[0][threadIdx.x], b = red[0][threadIdx.x + 16];
+  const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if constexpr (BWD)
+      bn_bwd_finalize_channel(c + j, C, av[j], bv[j], gamma, beta_or_mean, rm_or_invstd, M, o0, o1, accumulate, o2);
+    else
+      bn_finalize_channel(c + j, av[j], bv[j], gamma, beta_or_mean, rm_or_invstd, running_var, M, momentum, eps, o0,
+                          o1, o2, o3);
+  }
 }
 
-// groups for bn_reduce_finalize_kernel: <= 32 (each group's agent-scope release costs an L2 write-back, so
-// few large groups beat many small ones; measured on ResNet-50's 53 BN layers)
+// groups for bn_reduce_finalize_kernel: about sqrt(T) rows per group and sqrt(T) groups (<= 128), so both the
+// group pass and the leader-row pass are ~sqrt(T)/8 loads per thread (each group's agent-scope release costs
+// an L2 write-back, so the group count stays bounded)
 static inline int bn_groups(int T, int* sg) {
-  int G = std::min(32, std::max(1, (T + 31) / 32));
+  static const int gmax = [] {
+    const char* e = getenv("DTF_BN_GROUPS");  // tuning knob: fixed group cap instead of the sqrt rule
+    return e ? atoi(e) : 0;
+  }();
+  int G = gmax > 0 ? std::min(gmax, (T + 31) / 32) : (int)std::sqrt((double)T);
+  G = std::min(128, std::max(1, G));
   *sg = (T + G - 1) / G;
   return (T + *sg - 1) / *sg;
 }
@@ -260,7 +294,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
                                                        long M, int C, int relu, uint8_t* __restrict__ mbits,
                                                        const float* __restrict__ rscale,
-                                                       const float* __restrict__ rshift) {
+                                                       const float* __restrict__ rshift, int rev) {
   const ColGeo g = colgeo(C);
   const int t = threadIdx.x;
   if (t >= g.TPR * g.RPB) return;
@@ -285,19 +319,20 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
       float f[EU][8], rv[EU][8];
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
-        const long i8 = (r + u * rstep) * g.cols8 + cc;
+        const long i8 = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
         load8(x + i8 * 8, f[u]);
         if (res) load8(res + i8 * 8, rv[u]);
       }
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
         if (res) raff(rv[u]);
-        bn_apply_row(x, res, y, mbits, (r + u * rstep) * g.cols8 + cc, f[u], rv[u], sc, sh, relu);
+        bn_apply_row(x, res, y, mbits, (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc, f[u], rv[u],
+                     sc, sh, relu);
       }
     }
     for (; r < M; r += rstep) {
       float f[8], rv[8];
-      const long i8 = r * g.cols8 + cc;
+      const long i8 = (rev ? M - 1 - r : r) * g.cols8 + cc;
       load8(x + i8 * 8, f);
       if (res) {
         load8(res + i8 * 8, rv);
@@ -440,7 +475,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out,
                                                            const bf16_t* __restrict__ x2,
                                                            const float* __restrict__ mean2,
-                                                           float* __restrict__ part2) {
+                                                           float* __restrict__ part2, int rev) {
   const ColGeo g = colgeo(C);
   const int t = threadIdx.x;
   if (!SC && t >= g.TPR * g.RPB) return;
@@ -471,20 +506,21 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
       float d[EU][8], xv[EU][8];
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
-        const long i8 = (r + u * rstep) * g.cols8 + cc;
+        const long i8 = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
         load8(dy + i8 * 8, d[u]);
         load8(x + i8 * 8, xv[u]);
         relu_mask8(d[u], ymask, mbits, i8);
       }
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
-        bn_bwd_apply_row(d[u], xv[u], ka, kb, kc, dx, dz_out, (r + u * rstep) * g.cols8 + cc);
-        sc_acc(d[u], (r + u * rstep) * g.cols8 + cc);
+        const long i8 = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
+        bn_bwd_apply_row(d[u], xv[u], ka, kb, kc, dx, dz_out, i8);
+        sc_acc(d[u], i8);
       }
     }
     for (; r < M; r += rstep) {
       float d[8], xv[8];
-      const long i8 = r * g.cols8 + cc;
+      const long i8 = (rev ? M - 1 - r : r) * g.cols8 + cc;
       load8(dy + i8 * 8, d);
       load8(x + i8 * 8, xv);
       relu_mask8(d, ymask, mbits, i8);
@@ -860,6 +896,28 @@ int red_grid(long M, int C) {
   return (int)blocks;
 }
 
+// BN statistic reduce + finalize as ONE launch (last-arriver hand-off) or two (group pass, finalize pass):
+// the agent-scope fences of the one-launch form cost more than the second launch boundary, mostly in the backward
+// where the side-stream weight gradients keep the CUs busy. DTF_BN_ONE_LAUNCH=1 selects the one-launch form.
+static bool bn_one_launch() {
+  static const bool on = [] {
+    const char* e = getenv("DTF_BN_ONE_LAUNCH");  // two launches measured 1.9 % faster on ResNet-50 (b256)
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// Elementwise passes that consume a GEMM output sweep the rows last-to-first: the GEMM wrote them first-to-last,
+// so the most recently written rows (still in the 256 MiB Infinity Cache) are read first; the next GEMM then
+// reads this pass's output in its own first-to-last order, again most recent first. DTF_EW_REVERSE=1: on.
+static int ew_reverse() {
+  static const int on = [] {
+    const char* e = getenv("DTF_EW_REVERSE");  // opt-in: no measurable effect on ResNet-50 (b256)
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return on;
+}
+
 // elementwise channels-last passes: enough blocks to fill the chip, each with >= EU row trips when possible
 int ew_grid(long M, int C) {
   ColGeo g = colgeo(C);
@@ -891,7 +949,7 @@ DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float*
   {
     int sg = 0;
     const int G = bn_groups(T, &sg);
-    int* tk = dtf_tickets(cdiv(C, 64));
+    int* tk = bn_one_launch() ? dtf_tickets(cdiv(C, 64)) : nullptr;
     if (tk) {
       hipLaunchKernelGGL((bn_reduce_finalize_kernel<false>), dim3(cdiv(C, 64), G), dim3(256), 0,
                          (hipStream_t)stream, part, T, rs, sg, C, M, gamma, beta, running_mean, running_var, momentum,
@@ -920,7 +978,7 @@ DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, 
   if ((C & 7) || ((rscale == nullptr) != (rshift == nullptr))) return -1;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M, C)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, M, C, relu,
-                     relu ? (uint8_t*)mbits : nullptr, res ? rscale : nullptr, res ? rshift : nullptr);
+                     relu ? (uint8_t*)mbits : nullptr, res ? rscale : nullptr, res ? rshift : nullptr, ew_reverse());
   return (int)hipGetLastError();
 }
 
@@ -974,7 +1032,7 @@ static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const 
   long rs = 2L * C;
   int sg = 0;
   const int G2 = bn_groups(G, &sg);
-  int* tk = dtf_tickets(cdiv(C, 64));
+  int* tk = bn_one_launch() ? dtf_tickets(cdiv(C, 64)) : nullptr;
   if (tk) {
     hipLaunchKernelGGL((bn_reduce_finalize_kernel<true>), dim3(cdiv(C, 64), G2), dim3(256), 0, st, part, G, rs, sg,
                        C, M, gamma, mean, const_cast<float*>(invstd), nullptr, 0.f, 0.f, dgamma, dbeta, coef, nullptr,
@@ -999,11 +1057,11 @@ static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, con
   if (fuse_sc)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                       (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2);
+                       (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse());
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                       (bf16_t*)dz_out, nullptr, nullptr, nullptr);
+                       (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse());
   return (int)hipGetLastError();
 }
 

@@ -150,7 +150,24 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) atomicAdd(out, s);
 }
 
+// hipGraph replays: hp = table[ctr % R], then ctr += 1. The host fills slot k % R of the (pinned) table before
+// replay k and reuses a slot only after the replay that read it has finished, so consecutive replays need no
+// host synchronisation (graphs.CapturedStep; the captured table copy reads the pinned ring at replay time).
+__global__ void hp_ring_select_kernel(const float* __restrict__ table, int R, int n, int* ctr,
+                                      float* __restrict__ hp) {
+  const int k = *ctr;
+  if ((int)threadIdx.x < n) hp[threadIdx.x] = table[(k % R) * n + threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) *ctr = k + 1;
+}
+
 }  // namespace
+
+DTF_API int dtf_hp_ring_select(const float* table, int R, int n, int* ctr, float* hp, void* stream) {
+  if (R < 1 || n < 1 || n > 64) return -1;
+  hipLaunchKernelGGL(hp_ring_select_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, table, R, n, ctr, hp);
+  return (int)hipGetLastError();
+}
 
 DTF_API int dtf_optim_apply(int kind, float* p, float* g, float* s1, float* s2, void* p16, long n, float b1,
                             float b2, float eps, float wd, float mom, float l1, float l2, int nesterov,

@@ -46,6 +46,7 @@ _KERNEL_SIGS = {
     "dtf_gap_bwd": [P, I, P, I, I, I, P],
     "dtf_optim_apply": [I, P, P, P, P, P, L, F, F, F, F, F, F, F, I, I, P, P, P],
     "dtf_sumsq": [P, L, P, I, P],
+    "dtf_hp_ring_select": [P, I, I, P, P, P],
     "dtf_cast_f32_bf16": [P, P, L, P],
     "dtf_cast_bf16_f32": [P, P, L, P],
     "dtf_nchw_to_nhwc_pad": [P, P, I, I, I, I, P],

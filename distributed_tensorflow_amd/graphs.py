@@ -48,7 +48,6 @@ class CapturedStep:
         self.calls = 0
         self.static_in = None
         self.out = None
-        self._done_ev = None
 
     def _capture(self, args):
         from .ops import _util
@@ -65,7 +64,6 @@ class CapturedStep:
         # keep the raw (device) log values: each replay hands out a fresh lazy view of them
         self._log_type = type(out) if isinstance(out, dict) else None
         self.out = {k: dict.__getitem__(out, k) for k in out.keys()} if self._log_type else out
-        self._done_ev = torch.cuda.Event()
         # the capture did not execute anything: roll the host step back so the first replay is step t
         for o in self.optimizers:
             o._host_iter -= 1
@@ -88,12 +86,12 @@ class CapturedStep:
             for s, t in zip(self.static_in, _flat(args, [])):
                 if s.data_ptr() != t.data_ptr():
                     s.copy_(t, non_blocking=True)
-        # the previous replay must have consumed the pinned scalars before they are rewritten
-        self._done_ev.synchronize()
+        # per-step scalars go to a pinned ring (Optimizer.graph_prestep): no host sync between replays
         for o in self.optimizers:
             o.graph_prestep()
         self.graph.replay()
-        self._done_ev.record()
+        for o in self.optimizers:
+            o.graph_poststep()
         from .ops import _util
         _util.bump_weights_epoch()
         return self._log_type(self.out) if self._log_type else self.out

@@ -32,6 +32,9 @@ from ..variables import ParamArena, Variable
 from ..ops import _util
 from ..ops.optim import optim_apply, sumsq as _sumsq
 
+# rows of the pinned per-step scalar ring of a hipGraph-captured step (how far the host may run ahead)
+GRAPH_RING = 8
+
 _SLOTS = {
     "sgd": [],
     "momentum": [("Momentum", 0.0)],
@@ -213,12 +216,16 @@ class Optimizer:
         hp = self._hp.get(id(a))
         vals = self._hp_values(lr)
         if self._graph is not None:
-            # inside a capture: a fixed pinned buffer whose contents the capturer rewrites before
-            # every replay (graph_prestep); the captured memcpy node reads it at replay time
-            pinned = self._graph.get(id(a))
-            if pinned is None or hp is None:
+            # inside a capture: a pinned ring of GRAPH_RING scalar rows that the host fills before each replay
+            # (graph_prestep); the captured copy brings the ring to the device at replay time and a captured
+            # select kernel picks row (replay count % GRAPH_RING) with a device counter
+            ring = self._graph.get(id(a))
+            if ring is None or hp is None:
                 raise RuntimeError("optimizer arena was not prepared for graph capture (graph_prepare())")
-            hp.copy_(pinned, non_blocking=True)
+            pinned, dev_table, ctr = ring
+            dev_table.copy_(pinned, non_blocking=True)
+            _util.call("dtf_hp_ring_select", _util.ptr(dev_table), GRAPH_RING, 4, _util.ptr(ctr), _util.ptr(hp),
+                       _util.stream())
             return hp
         if hp is None:
             hp = torch.tensor(vals, dtype=torch.float32, device=a.device)
@@ -275,24 +282,45 @@ class Optimizer:
         """Allocate (outside the capture: pinned allocation is not capturable) the fixed pinned
         scalar buffer and device hp tensor of every arena, and switch `_hp_tensor` to graph mode."""
         self._graph = {}
+        self._graph_replays = 0
+        self._graph_events = [None] * GRAPH_RING
         for a in self._arenas.values():
             if a.device.type != "cuda":
                 continue
-            self._graph[id(a)] = torch.zeros(4, dtype=torch.float32).pin_memory()
+            self._graph[id(a)] = (torch.zeros(GRAPH_RING, 4, dtype=torch.float32).pin_memory(),
+                                  torch.zeros(GRAPH_RING, 4, dtype=torch.float32, device=a.device),
+                                  torch.zeros(1, dtype=torch.int32, device=a.device))
             if id(a) not in self._hp:
                 self._hp[id(a)] = torch.zeros(4, dtype=torch.float32, device=a.device)
 
     def graph_prestep(self):
         """Before a hipGraph replay of a captured step: advance the host step and publish the step's
-        scalars (bias-corrected lr, grad scale, clip) into the pinned buffers the graph copies from."""
+        scalars (bias-corrected lr, grad scale, clip) into this replay's row of the pinned ring. The host
+        blocks only when it is GRAPH_RING replays ahead of the GPU (the row's previous reader not done)."""
         t = self.host_iterations() + 1
         lr = self._effective_lr(t)
-        for buf in (self._graph or {}).values():
-            buf.copy_(torch.tensor(self._hp_values(lr)))
+        slot = self._graph_replays % GRAPH_RING
+        ev = self._graph_events[slot]
+        if ev is not None:
+            ev.synchronize()
+        vals = torch.tensor(self._hp_values(lr))
+        for pinned, _, _ in (self._graph or {}).values():
+            pinned[slot].copy_(vals)
         self._host_iter = t
         if not self.iterations.is_cuda:  # host-resident counter: the capture ran its add_ only once
             with torch.no_grad():
                 self.iterations.fill_(t)
+
+    def graph_poststep(self):
+        """After a replay was issued: mark its ring row busy until the replay has run."""
+        if self._graph is None:
+            return
+        slot = self._graph_replays % GRAPH_RING
+        ev = self._graph_events[slot]
+        if ev is None:
+            ev = self._graph_events[slot] = torch.cuda.Event()
+        ev.record()
+        self._graph_replays += 1
 
     def apply_gradients(self, grads_and_vars, zero_grad=True):
         gv = [(g, v) for g, v in grads_and_vars if g is not None]
