@@ -224,14 +224,10 @@ __global__ void __launch_bounds__(NW * 64, 1) conv256_kernel(GemmArgs a) {
 
   // ---- block -> tile: XCD-aware bijective remap, N-tiles of one M-tile adjacent (they share the A rows) ----
   const int nwg = a.tiles_m * a.tiles_n;
-  int bid = blockIdx.x;
-  {
-    int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  }
+  int bid, z;
+  xcd_block(nwg, bid, z);
   const int tile_m = bid / a.tiles_n, tile_n = bid % a.tiles_n;
   const int m0 = tile_m * BMC, n0 = tile_n * BN;
-  const int z = blockIdx.z;
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);

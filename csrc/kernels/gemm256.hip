@@ -66,11 +66,8 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
 
   // ---- block -> tile (XCD-aware bijective remap, grouped order) ----
   const int nwg = a.tiles_m * a.tiles_n;
-  int bid = blockIdx.x;
-  {
-    int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  }
+  int bid, z;
+  xcd_block(nwg, bid, z);
   constexpr int GROUP = 4;
   const int per_group = GROUP * a.tiles_n;
   const int grp = bid / per_group;
@@ -80,7 +77,6 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   const int tile_m = first_m + in_g % gsize;
   const int tile_n = in_g / gsize;
   const int m0 = tile_m * 256, n0 = tile_n * 256;
-  const int z = blockIdx.z;
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);

@@ -932,6 +932,19 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
   }
 }
 
+// Block -> (tile, z) over a grid of nwg tiles x gridDim.z (split-K slices / batch entries), gridDim.y == 1. The
+// hardware deals workgroups to the 8 XCDs round-robin in dispatch order (x fastest, then z): the flat id is
+// remapped bijectively so that each XCD gets one contiguous range of (z, tile) pairs — the tiles of one split
+// (which read the same operand rows) share an XCD's L2 instead of being spread over all eight.
+__device__ __forceinline__ void xcd_block(int nwg, int& bid, int& z) {
+  const int total = nwg * (int)gridDim.z;
+  int L = (int)blockIdx.z * nwg + (int)blockIdx.x;
+  const int xcd = L & 7, qq = total >> 3, rr = total & 7;
+  L = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (L >> 3);
+  z = L / nwg;
+  bid = L - z * nwg;
+}
+
 // Staging pipeline (PIPE):
 //  1: register-staged, ONE LDS buffer (a second barrier before each restage) — half the LDS per block, so
 //     twice the blocks (and bytes in flight) per CU; the default for 128-row tiles.
@@ -952,11 +965,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
   // ---- block -> tile (XCD-aware bijective remap, then grouped order) ----
   const int nwg = a.tiles_m * a.tiles_n;
-  int bid = blockIdx.x;
-  {
-    int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    bid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  }
+  int bid, z;
+  xcd_block(nwg, bid, z);
   constexpr int GROUP = 8;
   const int per_group = GROUP * a.tiles_n;
   const int grp = bid / per_group;
@@ -967,7 +977,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const int tile_n = in_g / gsize;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  const int z = blockIdx.z;
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
