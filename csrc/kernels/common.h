@@ -16,6 +16,7 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 typedef short v8s __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef int v8i __attribute__((ext_vector_type(8)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 

@@ -123,10 +123,10 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  // bf16: 2 k-substeps of 32 per 64-wide K-tile (16-B fragments); fp8 (OCP e4m3, K-tile = 128 bytes): 4
-  // k-substeps of 32 (8-B fragments) on v_mfma_f32_16x16x32_fp8_fp8 — same LDS image, half the bytes per FLOP
-  using FragT = typename std::conditional<FP8 != 0, long, v8bf>::type;
-  constexpr int KS = FP8 ? 4 : 2;
+  // bf16: 2 k-substeps of 32 per 64-wide K-tile (16-B fragments); fp8 (OCP e4m3, K-tile = 128 bytes, same LDS image)
+  // fp8: ONE block-scaled 16x16x128 MFMA per fragment pair and K-tile (32-B fragments, 2x the bf16 FLOP rate)
+  using FragT = typename std::conditional<FP8 != 0, v8i, v8bf>::type;
+  constexpr int KS = FP8 ? 1 : 2;
   FragT fa[4][KS], fb0[2][KS], fb1[2][KS];
 
   auto read_a = [&](int buf, int h) {
@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
-        if constexpr (FP8) fa[i][kk] = frag_fp8(base, wr * 64 + i * 16, kk, lane);
+        if constexpr (FP8) fa[i][kk] = frag_fp8x128(base, wr * 64 + i * 16, lane);
         else if constexpr (AM == OP_KOUTER) fa[i][kk] = frag_ko(base, wr * 64 + i * 16, kk, lane);
         else fa[i][kk] = frag_kcontig(base, wr * 64 + i * 16, kk, lane);
       }
@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
-        if constexpr (FP8) fb[j][kk] = frag_fp8(base, wc * 32 + j * 16, kk, lane);
+        if constexpr (FP8) fb[j][kk] = frag_fp8x128(base, wc * 32 + j * 16, lane);
         else if constexpr (BMD == OP_KOUTER) fb[j][kk] = frag_ko(base, wc * 32 + j * 16, kk, lane);
         else fb[j][kk] = frag_kcontig(base, wc * 32 + j * 16, kk, lane);
       }
@@ -160,8 +160,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if constexpr (FP8)
-            acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(
-                fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+            acc[ha * 4 + i][hb * 2 + j] = mfma_fp8x128(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j]);
           else
             acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);

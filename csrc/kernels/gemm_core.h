@@ -671,14 +671,21 @@ __device__ __forceinline__ v8bf frag(const char* lds, int rb, int kk, int lane) 
   else return frag_kcontig(lds, rb, kk, lane);
 }
 
-// FP8 (OCP e4m3) fragment: lane holds 8 consecutive k bytes of row (rb + lane&15) for k-substep kk (0..3)
-// of a [R][128 fp8] tile (same byte geometry and swizzle as the bf16 [R][64] tile).
-__device__ __forceinline__ long frag_fp8(const char* lds, int rb, int kk, int lane) {
-  int row = rb + (lane & 15);
-  int G = lane >> 4;
-  int c = 2 * kk + (G >> 1);
-  int pc = c ^ ((row >> 1) & 7);
-  return *reinterpret_cast<const long*>(lds + row * 128 + pc * 16 + (G & 1) * 8);
+// FP8 (OCP e4m3) 128-deep fragment for the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4: lane (G, i) holds the
+// 32 consecutive k bytes 32 G .. 32 G + 31 of row rb + i of a [R][128 fp8] tile (two swizzled 16-B chunks). Any
+// assignment of the 128 k values to the 4 lane groups x 32 bytes is a valid MFMA operand as long as A and B use
+// the same one (the product sums over k): this one costs two ds_read_b128 per fragment.
+__device__ __forceinline__ v8i frag_fp8x128(const char* lds, int rb, int lane) {
+  const int row = rb + (lane & 15), G = lane >> 4, sw = (row >> 1) & 7;
+  const uint4 lo = *reinterpret_cast<const uint4*>(lds + row * 128 + (((2 * G) ^ sw) << 4));
+  const uint4 hi = *reinterpret_cast<const uint4*>(lds + row * 128 + (((2 * G + 1) ^ sw) << 4));
+  return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+// e4m3 x e4m3 over 128 k with unit block scales (E8M0 127 = 2^0): twice the FLOP rate of the non-scaled fp8 and
+// bf16 16x16 MFMAs (MI355X_MICROARCH.md, Matrix cores)
+__device__ __forceinline__ v4f mfma_fp8x128(const v8i& a, const v8i& b, const v4f& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
 }
 
 // Shared epilogue of the MFMA GEMM kernels (gemm_kernel here, conv256_kernel in conv256.hip): the block's
@@ -1004,21 +1011,16 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
   auto compute = [&](const char* cA, const char* cB) {
     if constexpr (FP8) {
-      // 128 fp8 of K per tile: four 16x16x32 fp8 MFMA k-substeps (same rate as bf16 per MFMA,
-      // half the staged bytes per FLOP)
+      // 128 fp8 of K per tile: ONE block-scaled 16x16x128 MFMA per fragment pair (2x the bf16 FLOP rate)
+      v8i fa[TM], fb[TN];
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        long fa[TM], fb[TN];
+      for (int i = 0; i < TM; ++i) fa[i] = frag_fp8x128(cA, wm * WTM + i * 16, lane);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = frag_fp8(cA, wm * WTM + i * 16, kk, lane);
+      for (int j = 0; j < TN; ++j) fb[j] = frag_fp8x128(cB, wn * WTN + j * 16, lane);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = frag_fp8(cB, wn * WTN + j * 16, kk, lane);
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(fb[j], fa[i], acc[i][j], 0, 0, 0);
-      }
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_fp8x128(fb[j], fa[i], acc[i][j]);
     } else
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
