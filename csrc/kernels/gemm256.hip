@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if constexpr (FP8)
-            acc[ha * 4 + i][hb * 2 + j] = mfma_fp8x128(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j]);
+            acc[ha * 4 + i][hb * 2 + j] = mfma_fp8_ab<FP8>(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j]);
           else
             acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
@@ -343,7 +343,8 @@ int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8) {
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
   if (fp8) {
     if (amode != OP_KCONTIG || bmode != OP_KCONTIG) return 1;
-    hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT2), 0, st, a);
+    if (fp8 == 2) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 2>), grid, dim3(NT2), 0, st, a);
+    else hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT2), 0, st, a);
   } else if (amode == OP_KCONTIG && bmode == OP_KCONTIG)
     hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
   else if (amode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KOUTER>), grid, dim3(NT2), 0, st, a);

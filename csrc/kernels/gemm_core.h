@@ -682,10 +682,18 @@ __device__ __forceinline__ v8i frag_fp8x128(const char* lds, int rb, int lane) {
   return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
 }
 
-// e4m3 x e4m3 over 128 k with unit block scales (E8M0 127 = 2^0): twice the FLOP rate of the non-scaled fp8 and
-// bf16 16x16 MFMAs (MI355X_MICROARCH.md, Matrix cores)
+// 8-bit float operands over 128 k with unit block scales (E8M0 127 = 2^0): twice the FLOP rate of the non-scaled
+// fp8 and bf16 16x16 MFMAs (MI355X_MICROARCH.md, Matrix cores). Format codes (cbsz for the first operand, blgp for
+// the second): 0 = e4m3 (OCP fp8), 1 = e5m2 (bf8).
+template <int FA = 0, int FB = 0>
 __device__ __forceinline__ v4f mfma_fp8x128(const v8i& a, const v8i& b, const v4f& c) {
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+}
+// FP8 template code of the GEMM kernels: 0 = bf16; 1 = A e4m3 x B e4m3; 2 = A e5m2 (gradients) x B e4m3.
+// (the kernels issue the MFMA with (B, A) swapped, so B's format goes first)
+template <int FP8>
+__device__ __forceinline__ v4f mfma_fp8_ab(const v8i& fb, const v8i& fa, const v4f& c) {
+  return mfma_fp8x128<0, FP8 == 2 ? 1 : 0>(fb, fa, c);
 }
 
 // Shared epilogue of the MFMA GEMM kernels (gemm_kernel here, conv256_kernel in conv256.hip): the block's
@@ -1020,7 +1028,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_fp8x128(fb[j], fa[i], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_fp8_ab<FP8>(fb[j], fa[i], acc[i][j]);
     } else
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {

@@ -132,7 +132,163 @@ __global__ void __launch_bounds__(256) quant_fp8_exact_kernel(const bf16_t* __re
   }
 }
 
+// ---- transposing quantizer (fp8 backward) ----
+// One pass over a [M][N] bf16 tensor (M, N multiples of 64) produces any of: the row-major fp8 copy q [M][N], the
+// transposed fp8 copy qT [N][M] (the K-contiguous operand of a weight-gradient GEMM over M), per-64-row-tile
+// column sums of the f32 values (bias gradient partials) and the running amax (delayed scaling). With `pre` the
+// value is dy * act'(pre) (the activation backward folded in: the bf16 gradient is never written).
+struct QtArgs {
+  const bf16_t* x;
+  const bf16_t* pre;
+  uint8_t* q;
+  uint8_t* qT;
+  float* colpart;
+  const float* scale;
+  float* amax;
+  const float* part;  // exact scaling: per-block absmax partials of x (scale = max / fmax, written to scale_out)
+  int nparts;
+  float* scale_out;
+  int M, N, act;
+};
+
+__device__ __forceinline__ float gelu_grad_q(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+template <int FMT>
+__device__ __forceinline__ uint32_t cvt4(float a0, float a1, float a2, float a3) {
+  int r;
+  if constexpr (FMT == 1) {
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a0, a1, 0, false);
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a2, a3, r, true);
+  } else {
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
+  }
+  return (uint32_t)r;
+}
+
+// block (x, y) = columns [64x, 64x+64) x rows [QT_ROWS y, QT_ROWS (y+1)), walked as 64-row tiles; thread (wave w,
+// lane l): row 16w + (l & 15) of each tile, the 16 columns 16 (l >> 4) .. +15 (the 16 lanes of a DPP row share
+// the columns: the column sums, kept in registers over the strip, are row16_sum reductions at the end). The next
+// tile's loads are issued before this tile's quantize / transpose.
+constexpr int QT_ROWS = 256;
+
+template <int FMT>
+__global__ void __launch_bounds__(256) quant_t_kernel(QtArgs a) {
+  constexpr float FMAX = FMT == 1 ? 57344.f : 448.f;
+  constexpr int LDT = 80;  // transposed tile row stride (bytes): 16-B aligned rows
+  __shared__ __attribute__((aligned(16))) uint8_t sT[2][64 * LDT];
+  __shared__ float red[4][64];
+  __shared__ float redm[16];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, cc = l >> 4, r = 16 * w + (l & 15);
+  const int n0 = blockIdx.x * 64, mb = blockIdx.y * QT_ROWS;
+  const int ntile = min(QT_ROWS, a.M - mb) / 64;
+  float scale;
+  if (a.part) {
+    float m = 0.f;
+    for (int i = t; i < a.nparts; i += 256) m = fmaxf(m, a.part[i]);
+    m = block_max(m, redm);
+    scale = fmaxf(m, 1e-12f) / FMAX;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0) a.scale_out[0] = scale;
+  } else {
+    scale = fmaxf(a.scale[0], 1e-30f);
+  }
+  const float inv = 1.f / scale;
+  float cs[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) cs[j] = 0.f;
+  float mx = 0.f;
+  uint4 xr[2], pr[2];
+  auto load = [&](int tile) {
+    const long e = (long)(mb + 64 * tile + r) * a.N + n0 + 16 * cc;
+    xr[0] = *reinterpret_cast<const uint4*>(a.x + e);
+    xr[1] = *reinterpret_cast<const uint4*>(a.x + e + 8);
+    if (a.pre) {
+      pr[0] = *reinterpret_cast<const uint4*>(a.pre + e);
+      pr[1] = *reinterpret_cast<const uint4*>(a.pre + e + 8);
+    }
+  };
+  load(0);
+  for (int tile = 0; tile < ntile; ++tile) {
+    const int m0 = mb + 64 * tile;
+    float f[16];
+    {
+      const uint32_t xw[8] = {xr[0].x, xr[0].y, xr[0].z, xr[0].w, xr[1].x, xr[1].y, xr[1].z, xr[1].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        f[2 * k] = __uint_as_float(xw[k] << 16);
+        f[2 * k + 1] = __uint_as_float(xw[k] & 0xffff0000u);
+      }
+      if (a.pre) {
+        const uint32_t pw[8] = {pr[0].x, pr[0].y, pr[0].z, pr[0].w, pr[1].x, pr[1].y, pr[1].z, pr[1].w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float p0 = __uint_as_float(pw[k] << 16), p1 = __uint_as_float(pw[k] & 0xffff0000u);
+          f[2 * k] *= a.act == 1 ? (p0 > 0.f ? 1.f : 0.f) : gelu_grad_q(p0);
+          f[2 * k + 1] *= a.act == 1 ? (p1 > 0.f ? 1.f : 0.f) : gelu_grad_q(p1);
+        }
+      }
+    }
+    if (tile + 1 < ntile) load(tile + 1);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      mx = fmaxf(mx, fabsf(f[j]));
+      cs[j] += f[j];
+    }
+    uint32_t qw[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fminf(fmaxf(f[4 * h + j] * inv, -FMAX), FMAX);
+      qw[h] = cvt4<FMT>(v[0], v[1], v[2], v[3]);
+    }
+    const long e = (long)(m0 + r) * a.N + n0 + 16 * cc;
+    if (a.q) *reinterpret_cast<uint4*>(a.q + e) = make_uint4(qw[0], qw[1], qw[2], qw[3]);
+    if (a.qT) {
+      uint8_t* st = sT[tile & 1];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) st[(16 * cc + j) * LDT + r] = (uint8_t)(qw[j >> 2] >> (8 * (j & 3)));
+      __syncthreads();  // (double-buffered: the tile before last is no longer read)
+      const int c = t >> 2, rq = (t & 3) * 16;
+      *reinterpret_cast<uint4*>(a.qT + (long)(n0 + c) * a.M + m0 + rq) =
+          *reinterpret_cast<const uint4*>(st + c * LDT + rq);
+    }
+  }
+  if (a.colpart) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float sj = row16_sum(cs[j]);
+      if ((l & 15) == 0) red[w][16 * cc + j] = sj;
+    }
+    __syncthreads();
+    if (t < 64) a.colpart[(long)blockIdx.y * a.N + n0 + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  }
+  if (a.amax) {
+    mx = block_max(mx, redm);
+    if (t == 0) {
+      unsigned int* am = reinterpret_cast<unsigned int*>(a.amax);
+      const unsigned int cur = __hip_atomic_load(am, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__float_as_uint(mx) > cur) atomicMax(am, __float_as_uint(mx));
+    }
+  }
+}
+
+// scale <- amax / fmax * 2^margin (unchanged when amax is 0), prev (optional) <- the replaced scale, amax <- 0
+__global__ void fp8_update_scale2_kernel(float* amax, float* scale, float* prev, float fmax, float margin) {
+  const float am = amax[0], old = scale[0];
+  if (prev) prev[0] = old;
+  scale[0] = am > 0.f ? am / fmax * exp2f(margin) : old;
+  amax[0] = 0.f;
+}
+
 }  // namespace
+
+DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream);
 
 namespace dtf {
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8);  // gemm256.hip
@@ -166,6 +322,86 @@ DTF_API int dtf_quant_fp8_exact(const void* x, void* q, long n, float* scale_out
 
 DTF_API int dtf_fp8_update_scale(float* amax, float* scale, float margin, void* stream) {
   hipLaunchKernelGGL(fp8_update_scale_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, amax, scale, margin);
+  return (int)hipGetLastError();
+}
+
+// Transposing quantizer (see quant_t_kernel; column-sum partials: one row per 256 rows of x). fmt 0 = e4m3, 1 = e5m2. exact: the scale is amax(|x|)/fmax computed
+// on the device (two launches; ws >= 2048 floats; written to scale_out), else x is quantized with *scale and
+// amax (optional) records max |value|. pre (optional, exact = 0 only): x is dy of act(pre), act 1 relu / 2 gelu.
+DTF_API int dtf_quant_fp8_t(const void* x, const void* pre, int act, void* q, void* qT, float* colpart,
+                            const float* scale, float* amax, int M, int N, int fmt, int exact, float* ws,
+                            float* scale_out, void* stream) {
+  if ((M & 63) || (N & 63) || M <= 0 || N <= 0 || (exact && (pre || !ws || !scale_out))) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  QtArgs a{};
+  a.x = (const bf16_t*)x; a.pre = (const bf16_t*)pre; a.act = act;
+  a.q = (uint8_t*)q; a.qT = (uint8_t*)qT; a.colpart = colpart;
+  a.scale = scale; a.amax = amax; a.M = M; a.N = N;
+  if (exact) {
+    const long n8 = (long)M * N / 8;
+    const int grid = stream_grid(n8 / QU, 256);
+    hipLaunchKernelGGL(absmax_part_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, n8, ws);
+    a.part = ws; a.nparts = grid; a.scale_out = scale_out;
+  }
+  dim3 g(N / 64, (M + QT_ROWS - 1) / QT_ROWS);
+  if (fmt == 1) hipLaunchKernelGGL(quant_t_kernel<1>, g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(quant_t_kernel<0>, g, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// out[W] (+)= sum of nrows rows [nrows][stride] (deterministic; the bias-gradient partials of dtf_quant_fp8_t)
+DTF_API int dtf_reduce_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream) {
+  dtf_sum_rows(rows, stride, nrows, W, out, accumulate, stream);
+  return (int)hipGetLastError();
+}
+
+DTF_API int dtf_fp8_update_scale2(float* amax, float* scale, float* prev, float fmax, float margin, void* stream) {
+  hipLaunchKernelGGL(fp8_update_scale2_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, amax, scale, prev, fmax,
+                     margin);
+  return (int)hipGetLastError();
+}
+
+// General fp8 GEMM: C[M][N] = (s0*s1) * A_q[M][K] . B_q[N][K]^T; A e4m3 (fmt_a 0) or e5m2 (fmt_a 1, gradients), B
+// e4m3. bf16 out (+bias, act, aux) or f32 out with beta in {0, 1}; splitk > 1 (f32 out only) goes through f32
+// slabs in ws (>= splitk*M*N floats) reduced by dtf_sum_rows (accumulating into C when beta = 1).
+DTF_API int dtf_gemm_fp8_ex(const void* A, const void* B, void* C, void* aux, const float* bias, const float* scales,
+                            int M, int N, int K, long lda, long ldb, long ldc, int act, int fmt_a, int out_f32,
+                            float beta, int splitk, float* ws, long ws_elems, void* stream) {
+  if ((N & 7) || (K & 127) || (lda & 15) || (ldb & 15) || M <= 0) return -1;
+  if (beta != 0.f && beta != 1.f) return -2;
+  if (!out_f32 && (beta != 0.f || splitk > 1)) return -3;
+  hipStream_t st = (hipStream_t)stream;
+  const int fp8 = fmt_a == 1 ? 2 : 1;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.aux = (bf16_t*)aux;
+  a.bias = bias; a.scales = scales;
+  a.M = M; a.N = N; a.K = K / 2;
+  a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
+  a.batch = 1; a.alpha = 1.f; a.beta = beta; a.act = act; a.out_f32 = out_f32;
+  if (splitk < 1) splitk = 1;
+  if (splitk > 1) {
+    if (!ws || ws_elems < (long)splitk * M * N || ldc != N || bias || act || aux) return -4;
+    a.splitk = splitk;
+    a.kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;
+    a.C = ws;
+    a.slab = (long)M * N;
+    a.beta = 0.f;
+    if (gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8)) return -5;
+    dtf_sum_rows(ws, (long)M * N, splitk, (long)M * N, (float*)C, beta != 0.f ? 1 : 0, stream);
+    return (int)hipGetLastError();
+  }
+  a.splitk = 1;
+  a.kchunk = (a.K + BK - 1) / BK * BK;
+  if (prefer256(M, N, 2L * K, 1) && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8) == 0) return (int)hipGetLastError();
+  const long b128 = (long)cdiv(M, 128) * cdiv(N, 128);
+  const bool big = b128 >= 256;
+  a.tiles_m = cdiv(M, 128);
+  a.tiles_n = cdiv(N, big ? 128 : 64);
+  dim3 grid(a.tiles_m * a.tiles_n, 1, 1);
+  if (big && fp8 == 2) hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, OP_KCONTIG, OP_KCONTIG, 2>), grid, dim3(NT), 0, st, a);
+  else if (big) hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT), 0, st, a);
+  else if (fp8 == 2) hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, OP_KCONTIG, OP_KCONTIG, 2>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -70,6 +70,10 @@ _KERNEL_SIGS = {
     "dtf_gemm_fp8": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, P],
     "dtf_quant_fp8": [P, P, L, P, P, I, P],
     "dtf_fp8_update_scale": [P, P, F, P],
+    "dtf_quant_fp8_t": [P, P, I, P, P, P, P, P, I, I, I, I, P, P, P],
+    "dtf_fp8_update_scale2": [P, P, P, F, F, P],
+    "dtf_reduce_rows": [P, L, I, L, P, I, P],
+    "dtf_gemm_fp8_ex": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, F, I, P, L, P],
     "dtf_group_rows_once": [P, L, I, L, I, P, P],
     "dtf_ipc_export": [P, P, P],
     "dtf_ipc_open": [P, P],

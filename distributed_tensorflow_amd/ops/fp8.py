@@ -1,20 +1,37 @@
-"""FP8 (OCP e4m3) projections for GPT-2-medium (csrc/kernels/gemm_fp8.hip).
+"""FP8 (OCP e4m3 / e5m2) projections for GPT-2-medium (csrc/kernels/gemm_fp8.hip).
 
-Forward: activations and weights are quantized to e4m3 with per-tensor scales and multiplied on the
-gfx950 fp8 MFMA (``v_mfma_f32_16x16x32_fp8_fp8``), f32 accumulate, dequant + bias + GELU fused in the
-epilogue. Activation scales use delayed scaling (the quantize pass of step t records amax(|x|), which
-sets the scale of step t+1: no extra reduction pass); weight scales are exact (recomputed once per
-optimizer step). Backward runs in bf16 against the bf16 weight copies (fp8 forward / bf16 backward
-recipe), so master weights, optimizer and gradients are unchanged.
+Every GEMM of an fp8 Dense layer runs on the gfx950 block-scaled MFMA
+(``v_mfma_scale_f32_16x16x128_f8f6f4``, unit block scales + per-tensor scales folded into the epilogue,
+f32 accumulate) — forward AND backward:
+
+* forward  ``y = x W^T``:  x e4m3 (delayed scaling: the quantize pass of step t records amax(|x|), which sets
+  the scale of step t+1), W e4m3 (exact per-tensor scale, requantized once per optimizer step); dequant, bias
+  and GELU fused in the epilogue. The same quantize pass writes x^T in fp8 for the weight gradient, so the
+  layer saves 1 byte per activation instead of 2.
+* backward ``dX = dZ W`` and ``dW += dZ^T X``:  the incoming gradient is quantized to e5m2 (the wider-range
+  format; delayed scaling with its own amax) by ONE transposing pass that also folds in the GELU derivative
+  and produces the bias-gradient column sums, so the bf16 dZ is never written. dX runs e5m2 x e4m3 (W^T is kept
+  in fp8 next to W), dW runs e5m2 x e4m3 over the tokens with split-K f32 slabs accumulated straight into the
+  f32 gradient arena.
+
+Master weights, optimizer and the gradient arena stay f32 (the "fp8 compute / high-precision state" recipe).
+DTF_FP8_BWD=0 keeps the backward in bf16 against the bf16 weight copies (forward-only fp8).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from ._util import BF16, F32, bf16_shadow, call, direct_grad, ptr, stream, weights_epoch, workspace
-from .linalg import colsum, dense_dgrad, dense_wgrad, gemm
+from .linalg import colsum, dense_dgrad, dense_wgrad
 
 E4M3_MAX = 448.0
+E5M2_MAX = 57344.0
+_FP8_BWD = os.environ.get("DTF_FP8_BWD", "1") != "0"
+
+# state buffer slots (f32, per layer): adjacent pairs are the (s_a, s_b) dequant scales of the three GEMMs
+X_SCALE, W_SCALE, G_SCALE, X_USED, X_AMAX, G_AMAX = range(6)
 
 
 def quantize(x, scale, amax=None, zero_amax=True):
@@ -23,11 +40,55 @@ def quantize(x, scale, amax=None, zero_amax=True):
     return q
 
 
+def quantize_t(x, scale=None, amax=None, *, fmt=0, pre=None, act=0, rowmajor=True, transposed=True, colsums=False,
+               exact_out=None):
+    """One transposing pass over a [M, N] bf16 matrix (M, N multiples of 64): returns (q [M,N] | None,
+    qT [N,M] | None, column-sum partials [ceil(M/256), N] | None). fmt 0 = e4m3, 1 = e5m2. exact_out: compute the
+    exact per-tensor scale on the device and store it there (weights); else quantize with `scale` and record
+    amax. pre/act: x is the gradient of act(pre) (the activation backward is applied in the pass)."""
+    M, N = x.shape
+    dev = x.device
+    q = torch.empty((M, N), dtype=torch.uint8, device=dev) if rowmajor else None
+    qT = torch.empty((N, M), dtype=torch.uint8, device=dev) if transposed else None
+    cp = torch.empty((-(-M // 256), N), dtype=F32, device=dev) if colsums else None
+    ws = workspace(dev) if exact_out is not None else None
+    call("dtf_quant_fp8_t", ptr(x), ptr(pre), int(act), ptr(q), ptr(qT), ptr(cp), ptr(scale), ptr(amax), M, N,
+         int(fmt), int(exact_out is not None), ptr(ws), ptr(exact_out), stream())
+    return q, qT, cp
+
+
+def gemm_fp8(a, b, scales, out, *, fmt_a=0, out_f32=False, beta=0.0, splitk=1):
+    """out[M,N] (=|+=) s0*s1 * a[M,K] . b[N,K]^T for fp8 a (fmt_a 0 e4m3 / 1 e5m2) and e4m3 b (K-contiguous)."""
+    M, K = a.shape
+    N = b.shape[0]
+    ws = workspace(a.device) if splitk > 1 else None
+    call("dtf_gemm_fp8_ex", ptr(a), ptr(b), ptr(out), None, None, ptr(scales), M, N, K, a.stride(0), b.stride(0),
+         out.stride(0), 0, int(fmt_a), int(out_f32), float(beta), int(splitk), ptr(ws),
+         ws.numel() if ws is not None else 0, stream())
+    return out
+
+
+_WGRAD_SPLIT_MAX = int(os.environ.get("DTF_FP8_WGRAD_SPLITS", "4"))
+
+
+def _wgrad_splits(M, N, K, ws_elems):
+    """Split-K factor for the fp8 weight gradient (M x N output, K tokens) on the 256x256 kernel: about one
+    round of 1-block/CU tiles, >= 1024 tokens per split, at most DTF_FP8_WGRAD_SPLITS (the f32 slabs cost a
+    reduction pass), slabs within the workspace."""
+    tiles = -(-M // 256) * -(-N // 256)
+    s = max(1, min(256 // max(tiles, 1), K // 1024, _WGRAD_SPLIT_MAX))
+    while s > 1 and s * M * N > ws_elems:
+        s -= 1
+    return s
+
+
 class _Fp8State:
     def __init__(self, dev):
-        self.buf = torch.zeros(4, dtype=F32, device=dev)  # [x_scale, w_scale, x_amax, w_amax]
+        self.buf = torch.zeros(8, dtype=F32, device=dev)
+        self.buf[W_SCALE] = 1.0
         self.x_ready = False
-        self.wq = None
+        self.g_ready = False
+        self.wq = self.wqT = None
         self.w_key = None
 
 
@@ -39,18 +100,28 @@ def _state(layer, dev):
     return st
 
 
-def _weight_fp8(st, w):
-    key = (weights_epoch(), w._version)
+def _weight_fp8(st, w, need_t):
+    key = (weights_epoch(), w._version, need_t)
     if st.wq is not None and st.w_key == key:
-        return st.wq
+        return st.wq, st.wqT
     w16 = bf16_shadow(w)
-    if st.wq is None:
-        st.wq = torch.empty(w16.shape, dtype=torch.uint8, device=w16.device)
-    # exact per-tensor weight scale (amax/448) computed and applied on the device: 2 launches, no host sync
-    ws = workspace(w16.device)
-    call("dtf_quant_fp8_exact", ptr(w16), ptr(st.wq), w16.numel(), ptr(st.buf[1:2]), ptr(ws), stream())
+    N, K = w16.shape
+    if need_t:
+        # exact per-tensor scale (amax/448) computed on the device; W and W^T from one transposing pass
+        st.wq, st.wqT, _ = quantize_t(w16, exact_out=st.buf[W_SCALE:W_SCALE + 1])
+    else:
+        if st.wq is None or st.wq.shape != w16.shape:
+            st.wq = torch.empty(w16.shape, dtype=torch.uint8, device=w16.device)
+        ws = workspace(w16.device)
+        call("dtf_quant_fp8_exact", ptr(w16), ptr(st.wq), w16.numel(), ptr(st.buf[W_SCALE:W_SCALE + 1]), ptr(ws),
+             stream())
+        st.wqT = None
     st.w_key = key
-    return st.wq
+    return st.wq, st.wqT
+
+
+def _fp8_bwd_ok(M, K, N):
+    return _FP8_BWD and M % 128 == 0 and K % 128 == 0 and N % 128 == 0
 
 
 class _DenseFP8(torch.autograd.Function):
@@ -58,27 +129,77 @@ class _DenseFP8(torch.autograd.Function):
     def forward(ctx, x, w, b, act, st):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).contiguous()
-        if not st.x_ready:  # bootstrap the delayed activation scale once
-            st.buf[0:1].copy_(x2.abs().amax().float().clamp_min(1e-12) / E4M3_MAX)
-            st.x_ready = True
-        xq = quantize(x2, st.buf[0:1], st.buf[2:3], zero_amax=False)  # reset by the scale update below
-        wq = _weight_fp8(st, w)
         M, K = x2.shape
         N = w.shape[0]
+        buf = st.buf
+        fbwd = _fp8_bwd_ok(M, K, N)
+        if not st.x_ready:  # bootstrap the delayed activation scale once
+            buf[X_SCALE:X_SCALE + 1].copy_(x2.abs().amax().float().clamp_min(1e-12) / E4M3_MAX)
+            st.x_ready = True
+        xs, xa = buf[X_SCALE:X_SCALE + 1], buf[X_AMAX:X_AMAX + 1]
+        if fbwd:
+            xq, xqT, _ = quantize_t(x2, xs, xa)
+        else:
+            xq, xqT = quantize(x2, xs, xa, zero_amax=False), None
+        wq, wqT = _weight_fp8(st, w, fbwd)
         y = torch.empty((M, N), dtype=BF16, device=x.device)
         pre = torch.empty((M, N), dtype=BF16, device=x.device) if act else None
-        call("dtf_gemm_fp8", ptr(xq), ptr(wq), ptr(y), ptr(pre), ptr(b), ptr(st.buf), M, N, K, K, K, N, int(act), -1,
-             stream())
-        call("dtf_fp8_update_scale", ptr(st.buf[2:3]), ptr(st.buf[0:1]), 0.0, stream())  # next step's x scale
-        ctx.save_for_backward(x2, w, pre)
+        call("dtf_gemm_fp8", ptr(xq), ptr(wq), ptr(y), ptr(pre), ptr(b), ptr(buf[X_SCALE:X_SCALE + 2]), M, N, K, K, K,
+             N, int(act), -1, stream())
+        # next step's x scale from this pass's amax; the scale this pass used is kept for the weight gradient
+        call("dtf_fp8_update_scale2", ptr(xa), ptr(xs), ptr(buf[X_USED:X_USED + 1]), E4M3_MAX, 0.0, stream())
+        ctx.fbwd = fbwd
+        if fbwd:
+            ctx.save_for_backward(xqT, w, pre)
+        else:
+            ctx.save_for_backward(x2, w, pre)
+        ctx.st = st
         ctx.b_param = b
         ctx.act = act
         ctx.has_b = b is not None
         ctx.shp = shp
+        ctx.MKN = (M, K, N)
         return y.reshape(*shp[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
+        if not ctx.fbwd:
+            return _DenseFP8._backward_bf16(ctx, dy)
+        xqT, w, pre = ctx.saved_tensors
+        st, (M, K, N) = ctx.st, ctx.MKN
+        buf = st.buf
+        dy2 = dy.reshape(-1, N).to(BF16).contiguous()
+        gs, ga = buf[G_SCALE:G_SCALE + 1], buf[G_AMAX:G_AMAX + 1]
+        if not st.g_ready:  # bootstrap the delayed gradient scale once (GELU' <= 1.13)
+            gs.copy_(dy2.abs().amax().float().clamp_min(1e-30) * (1.2 if ctx.act else 1.0) / E5M2_MAX)
+            st.g_ready = True
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        need_db = ctx.has_b and ctx.needs_input_grad[2]
+        dzq, dzqT, cp = quantize_t(dy2, gs, ga, fmt=1, pre=pre if ctx.act else None, act=ctx.act, rowmajor=need_dx,
+                                   transposed=need_dw, colsums=need_db)
+        dx = dw = db = None
+        if need_dx:
+            _, wqT = _weight_fp8(st, w, True)
+            dx = torch.empty((M, K), dtype=BF16, device=dy.device)
+            gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1)  # scales (s_w, s_g)
+            dx = dx.reshape(ctx.shp)
+        if need_dw:  # dW[N, K] (+)= dZ^T X over the M tokens; inside Model.train_step straight into the arena
+            tw = direct_grad(w)
+            out = tw if tw is not None else torch.empty((N, K), dtype=F32, device=dy.device)
+            sk = _wgrad_splits(N, K, M, workspace(dy.device).numel())
+            gemm_fp8(dzqT, xqT, buf[G_SCALE:G_SCALE + 2], out, fmt_a=1, out_f32=True,
+                     beta=1.0 if tw is not None else 0.0, splitk=sk)  # scales (s_g, s_x used)
+            dw = None if tw is not None else out
+        if need_db:
+            tb = direct_grad(ctx.b_param)
+            out = tb if tb is not None else torch.empty(N, dtype=F32, device=dy.device)
+            call("dtf_reduce_rows", ptr(cp), N, cp.shape[0], N, ptr(out), int(tb is not None), stream())
+            db = None if tb is not None else out
+        call("dtf_fp8_update_scale2", ptr(ga), ptr(gs), None, E5M2_MAX, 0.0, stream())
+        return dx, dw, db, None, None
+
+    @staticmethod
+    def _backward_bf16(ctx, dy):
         x2, w, pre = ctx.saved_tensors
         N = w.shape[0]
         dz = dy.reshape(-1, N).to(BF16).contiguous()

@@ -585,3 +585,75 @@ def test_conv256_default_path_bn_stats(cuda):
     yf = y.float().reshape(-1, K)
     close(p[:K], yf.sum(0), 1e-3)
     close(p[K:], (yf * yf).sum(0), 1e-3)
+
+
+@pytest.mark.parametrize("fmt,act", [(0, 0), (1, 0), (1, 2)])
+def test_fp8_transposing_quantizer(cuda, fmt, act):
+    """dtf_quant_fp8_t: q, q^T, bias-gradient column sums and amax in one pass (e4m3 / e5m2, GELU backward)."""
+    from distributed_tensorflow_amd.ops import fp8
+    M, N = 256, 192
+    x = rnd(M, N, dev=cuda)
+    pre = rnd(M, N, dev=cuda) if act else None
+    v = x.float()
+    if act:
+        p = pre.float()
+        t = torch.tanh(0.7978845608028654 * (p + 0.044715 * p ** 3))
+        v = v * (0.5 * (1 + t) + 0.5 * p * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * p * p))
+    fmax = 57344.0 if fmt else 448.0
+    scale = (v.abs().max() / fmax).reshape(1)
+    amax = torch.zeros(1, device=cuda)
+    q, qT, cp = fp8.quantize_t(x, scale, amax, fmt=fmt, pre=pre, act=act, colsums=True)
+    dt = torch.float8_e5m2 if fmt else torch.float8_e4m3fn
+    dq = q.view(dt).float() * scale
+    assert (dq - v).abs().max().item() <= (0.13 if fmt else 0.07) * v.abs().max().item()
+    assert torch.equal(qT, q.t().contiguous())
+    close(cp.sum(0), v.sum(0), 1e-3)
+    assert abs(amax.item() - v.abs().max().item()) <= 1e-6 * v.abs().max().item() + 1e-12
+
+
+def test_fp8_backward_matches_bf16(cuda):
+    """The fp8 backward (e5m2 gradients x e4m3 weights / activations on the scaled MFMA) against the bf16 backward
+    of the same fp8 forward (same layer, same delayed scales): dX, dW, db within e5m2 quantization error."""
+    from distributed_tensorflow_amd.models.transformer import _Proj
+    from distributed_tensorflow_amd.ops import fp8
+    torch.manual_seed(0)
+    x0 = rnd(512, 256, dev=cuda)
+    g = torch.randn(512, 384, device=cuda).to(BF)
+    layer = _Proj(384, activation="gelu", fp8=True)
+    layer(x0)  # build + bootstrap the activation scale
+    outs = []
+    for bwd in (False, True):
+        fp8._FP8_BWD = bwd
+        try:
+            layer.kernel.grad = layer.bias.grad = None
+            x = x0.clone().requires_grad_(True)
+            y = layer(x)
+            y.backward(g)
+            outs.append((y.float(), x.grad.float(), layer.kernel.grad.float(), layer.bias.grad.float()))
+        finally:
+            fp8._FP8_BWD = True
+    rels = [((a - b).norm() / a.norm()).item() for a, b in zip(outs[0], outs[1])]
+    assert rels[0] < 1e-6 and max(rels) < 0.06, rels
+
+
+@pytest.mark.parametrize("fmt_a,out_f32,splitk,M,N,K", [(0, False, 1, 256, 128, 256), (1, False, 1, 256, 128, 256),
+                                                        (1, False, 1, 1024, 1024, 1024),
+                                                        (1, True, 1, 256, 128, 512), (1, True, 4, 512, 512, 4096)])
+def test_fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K):
+    """dtf_gemm_fp8_ex: e4m3 / e5m2 A x e4m3 B on the scaled MFMA vs the torch decode of the same bytes."""
+    from distributed_tensorflow_amd.ops import fp8
+    torch.manual_seed(0)
+    da = torch.float8_e5m2 if fmt_a else torch.float8_e4m3fn
+    a = (torch.randn(M, K, device=cuda) * 4).to(da)
+    b = (torch.randn(N, K, device=cuda) * 4).to(torch.float8_e4m3fn)
+    scales = torch.tensor([0.5, 0.25], device=cuda)
+    ref = (a.float() @ b.float().t()) * 0.125
+    if out_f32:
+        out = torch.full((M, N), 1.0, device=cuda)
+        fp8.gemm_fp8(a.view(torch.uint8), b.view(torch.uint8), scales, out, fmt_a=fmt_a, out_f32=True, beta=1.0,
+                     splitk=splitk)
+        ref = ref + 1.0
+    else:
+        out = torch.empty((M, N), dtype=BF, device=cuda)
+        fp8.gemm_fp8(a.view(torch.uint8), b.view(torch.uint8), scales, out, fmt_a=fmt_a)
+    close(out, ref, 1e-2)
