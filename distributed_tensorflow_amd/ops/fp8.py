@@ -23,8 +23,10 @@ import os
 
 import torch
 
-from ._util import BF16, F32, bf16_shadow, call, direct_grad, ptr, stream, weights_epoch, workspace
-from .linalg import colsum, dense_dgrad, dense_wgrad
+import contextlib
+
+from ._util import BF16, F32, bf16_shadow, call, direct_grad, fork_side, ptr, stream, weights_epoch, workspace
+from .linalg import DENSE_SIDE_ON, colsum, dense_dgrad, dense_wgrad
 
 E4M3_MAX = 448.0
 E5M2_MAX = 57344.0
@@ -183,19 +185,25 @@ class _DenseFP8(torch.autograd.Function):
             dx = torch.empty((M, K), dtype=BF16, device=dy.device)
             gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1)  # scales (s_w, s_g)
             dx = dx.reshape(ctx.shp)
-        if need_dw:  # dW[N, K] (+)= dZ^T X over the M tokens; inside Model.train_step straight into the arena
-            tw = direct_grad(w)
-            out = tw if tw is not None else torch.empty((N, K), dtype=F32, device=dy.device)
-            sk = _wgrad_splits(N, K, M, workspace(dy.device).numel())
-            gemm_fp8(dzqT, xqT, buf[G_SCALE:G_SCALE + 2], out, fmt_a=1, out_f32=True,
-                     beta=1.0 if tw is not None else 0.0, splitk=sk)  # scales (s_g, s_x used)
-            dw = None if tw is not None else out
-        if need_db:
-            tb = direct_grad(ctx.b_param)
-            out = tb if tb is not None else torch.empty(N, dtype=F32, device=dy.device)
-            call("dtf_reduce_rows", ptr(cp), N, cp.shape[0], N, ptr(out), int(tb is not None), stream())
-            db = None if tb is not None else out
-        call("dtf_fp8_update_scale2", ptr(ga), ptr(gs), None, E5M2_MAX, 0.0, stream())
+        tw = direct_grad(w) if need_dw else None
+        tb = direct_grad(ctx.b_param) if need_db else None
+        # arena-accumulated weight / bias gradients go to the side stream (off the dgrad critical path)
+        side = (fork_side(dy.device, dzqT, xqT, cp, buf) if (tw is not None and DENSE_SIDE_ON)
+                else contextlib.nullcontext())
+        with side:
+            if need_dw:  # dW[N, K] (+)= dZ^T X over the M tokens; inside Model.train_step straight into the arena
+                out = tw if tw is not None else torch.empty((N, K), dtype=F32, device=dy.device)
+                sk = _wgrad_splits(N, K, M, workspace(dy.device).numel())
+                gemm_fp8(dzqT, xqT, buf[G_SCALE:G_SCALE + 2], out, fmt_a=1, out_f32=True,
+                         beta=1.0 if tw is not None else 0.0, splitk=sk)  # scales (s_g, s_x used)
+                dw = None if tw is not None else out
+            if need_db:
+                out = tb if tb is not None else torch.empty(N, dtype=F32, device=dy.device)
+                call("dtf_reduce_rows", ptr(cp), N, cp.shape[0], N, ptr(out), int(tb is not None), stream())
+                db = None if tb is not None else out
+            # next step's gradient scale: on the stream of the last reader of this step's scale (the weight
+            # gradient), which was forked after the data gradient was issued
+            call("dtf_fp8_update_scale2", ptr(ga), ptr(gs), None, E5M2_MAX, 0.0, stream())
         return dx, dw, db, None, None
 
     @staticmethod

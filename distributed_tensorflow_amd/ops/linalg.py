@@ -8,7 +8,8 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, IntOut, bf16_shadow, call, direct_grad, on_gpu, ptr, stream, workspace
+from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, bf16_shadow, call, direct_grad, fork_side, on_gpu, ptr,
+                    stream, workspace)
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 _ACTS = {None: 0, "linear": 0, "relu": 1, "gelu": 2}
@@ -129,6 +130,8 @@ def colsum(x2d, out=None, accumulate=False):
 # large weight gradients (out*in >= 4M: GPT-2 FFN and LM head); the split-K weight gradients of BERT's 768-wide
 # layers stay on the MFMA kernel, which is faster there (tools/bench_blas_plain.py). DTF_PLAIN_BLAS=0: all MFMA.
 _PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "1") != "0"
+# Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream
+DENSE_SIDE_ON = SIDE_STREAM_ON and __import__("os").environ.get("DTF_DENSE_WGRAD_STREAM", "1") != "0"
 _BLAS_WGRAD_MIN = 4 << 20
 
 
@@ -202,16 +205,27 @@ class _DenseFn(torch.autograd.Function):
             acc = ctx.link.take()[0] if ctx.link is not None else None
             dx = dense_dgrad(dz, bf16_shadow(w), None if acc is None else acc.reshape(dz.shape[0], -1))
             dx = dx.reshape(ctx.shp)
+        tw = direct_grad(w) if ctx.needs_input_grad[1] else None
+        tb = direct_grad(ctx.b_param) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        if tw is not None and tw.dim() == 2 and DENSE_SIDE_ON and dz.is_cuda:
+            # arena-accumulated weight / bias gradients on the side stream: off the dgrad critical path, and their
+            # blocks fill the partial last wave of the data-gradient GEMMs (and vice versa)
+            with fork_side(dz.device, dz, x2):
+                dense_wgrad(dz, x2, out=tw)
+                if tb is not None:
+                    colsum(dz, out=tb, accumulate=True)
+            if ctx.has_b and ctx.needs_input_grad[2] and tb is None:
+                db = colsum(dz)
+            ctx.link = None
+            return dx, dw, db, None, None
         if ctx.needs_input_grad[1]:
             # dW[o,i] = sum_t dz[t,o] x[t,i]  -> both operands k-outer, f32 out; inside Model.train_step
             # accumulated straight into the arena gradient (beta = 1) instead of returned
-            tw = direct_grad(w)
             if tw is not None and tw.dim() == 2:
                 dense_wgrad(dz, x2, out=tw)
             else:
                 dw = dense_wgrad(dz, x2)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            tb = direct_grad(ctx.b_param)
             if tb is not None:
                 colsum(dz, out=tb, accumulate=True)
             else:
