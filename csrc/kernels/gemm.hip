@@ -148,7 +148,7 @@ static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
   return 3;
 }
 
-int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8 = 0);  // gemm256.hip
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8 = 0, int bn = 256);  // gemm256.hip
 int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool force);  // conv256.hip
 bool conv256_on();
 
@@ -162,16 +162,31 @@ static bool try_conv256(GemmArgs& a, int am, int bm, int& tile, hipStream_t st) 
   return tile < 0 && conv256_try(a, am, bm, -1, st, false) == 0;
 }
 
-// 256x256 (1 block/CU, ~1.12-1.24x faster per tile, more so at long K) vs 128x128 (2 blocks/CU): compare the
-// wave-quantisation efficiency of both tilings on 256 CUs.
-bool prefer256(long M, long N, long K, long batch) {
-  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch, t128 = (long)cdiv(M, 128) * cdiv(N, 128) * batch;
-  if (t256 < 128) return false;
-  const double e256 = (double)t256 / (double)(((t256 + 255) / 256) * 256);
-  const double e128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
+// 256-row pipelined tiles (1 block/CU, ~1.12-1.24x faster per tile than 128x128, more so at long K) vs the
+// 128x128 kernel (2 blocks/CU): compare the wave-quantisation efficiency of the tilings on 256 CUs. Returns the
+// 256-row tile width to use (256 or 128), or 0 for the 128x128 kernel.
+int pick256(long M, long N, long K, long batch) {
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch, t2x1 = (long)cdiv(M, 256) * cdiv(N, 128) * batch,
+             t128 = (long)cdiv(M, 128) * cdiv(N, 128) * batch;
+  static const long force_min = [] {  // tuning knob: take 256x256 whenever it has at least this many tiles
+    const char* e = getenv("DTF_G256_MIN");
+    return e ? atol(e) : 0L;
+  }();
+  static const int narrow = [] {  // opt-in (DTF_G256_NARROW=1): the 256x128 tiles are LDS-read bound with the 2x4
+    const char* e = getenv("DTF_G256_NARROW");  // wave layout: GPT-2-medium 218.5k -> 210.4k tok/s with them on
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  if (force_min > 0) return t256 >= force_min ? 256 : 0;
+  auto eff = [](long t, long slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
   const double base = 1.12 + 0.12 * (double)std::min<long>(K, 4096) / 4096.0;
-  return base * e256 > e128;
+  const double s256 = t256 >= 128 ? base * eff(t256, 256) : 0.0;
+  const double s2x1 = (narrow && t2x1 >= 128) ? 0.96 * base * eff(t2x1, 256) : 0.0;  // half the B reuse per tile
+  const double s128 = eff(t128, 512);
+  if (s256 >= s2x1 && s256 > s128) return 256;
+  if (s2x1 > s128) return 128;
+  return 0;
 }
+bool prefer256(long M, long N, long K, long batch) { return pick256(M, N, K, batch) == 256; }
 
 // LDS-DMA staged tiles for K-contiguous operands (both operand images filled by buffer_load ... lds):
 // 128x64 synchronous (occupancy hides the DMA) almost everywhere, 128x128 double-buffered when there are
@@ -359,8 +374,9 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
   }
   if (stats && (a.batch > 1 || a.splitk > 1)) return -7;
   // large K-contiguous problems: the 256x256 glds-pipelined kernel when it fills the chip
-  if (tile < 0 && !stats && a.splitk == 1 && prefer256(M, N, K, a.batch) &&
-      gemm256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream) == 0)
+  const int bn256 = (tile < 0 && !stats && a.splitk == 1) ? pick256(M, N, K, a.batch) : 0;
+  if (bn256 && gemm256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream,
+                           0, bn256) == 0)
     return (int)hipGetLastError();
   const int am = a_kouter ? OP_KOUTER : OP_KCONTIG, bm = b_kouter ? OP_KOUTER : OP_KCONTIG;
   if (tile < 0 && dense_glds_on() && a.batch == 1) tile = pick_glds_tile(a, am, bm);

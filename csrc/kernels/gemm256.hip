@@ -24,12 +24,19 @@ namespace dtf {
 namespace {
 
 constexpr int NT2 = 512;
-constexpr int HALF = 128 * 128;  // bytes of one half-tile image (128 rows x 64 bf16)
-constexpr int BUF = 4 * HALF;    // A0 | A1 | B0 | B1
+constexpr int HALF = 128 * 128;  // bytes of one A half-tile image (128 rows x 64 bf16)
+// B half-tile image: BN/2 rows x 64 bf16; buffer = A0 | A1 | B0 | B1
+template <int BN> constexpr int half_b() { return BN * 64; }
+template <int BN> constexpr int buf_bytes() { return 2 * HALF + 2 * half_b<BN>(); }
+template <int BN> constexpr int half_off(int h) { return h < 2 ? h * HALF : 2 * HALF + (h - 2) * half_b<BN>(); }
 
-// LDS image row -> block-tile row (A: two 64-row slices per M-wave; B: two 32-col slices per N-wave)
+// LDS image row -> block-tile row (A: two 64-row slices per M-wave; B: two BN/8-col slices per N-wave)
 __device__ __forceinline__ int a_row(int r, int h) { return (r >> 6) * 128 + h * 64 + (r & 63); }
-__device__ __forceinline__ int b_row(int r, int h) { return (r >> 5) * 64 + h * 32 + (r & 31); }
+template <int BN>
+__device__ __forceinline__ int b_row(int r, int h) {
+  constexpr int S = BN / 8;  // columns of one N-wave in one half
+  return (r / S) * (2 * S) + h * S + (r % S);
+}
 
 // K-outer half image [64 k][128 cols]: physical 16-B chunk of logical chunk c in k-row k
 __device__ __forceinline__ int ko_swz(int k) { return (k & 3) << 1; }
@@ -58,8 +65,12 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int AM, int BMD, int FP8 = 0>
+// BN = 256 (each wave 128x64: 8x4 fragments) or 128 (each wave 128x32: 8x2 fragments; 256x128 tiles fill the
+// chip where 256x256 would leave half of it idle, e.g. M = 8192 x N = 1024)
+template <int AM, int BMD, int FP8 = 0, int BN = 256>
 __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
+  constexpr int BUF = buf_bytes<BN>();
+  constexpr int JN = BN / 128;           // B fragments per wave per half (and glds instructions per B half)
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 2, wc = w & 3;
@@ -76,7 +87,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   const int in_g = bid - grp * per_group;
   const int tile_m = first_m + in_g % gsize;
   const int tile_n = in_g / gsize;
-  const int m0 = tile_m * 256, n0 = tile_n * 256;
+  const int m0 = tile_m * 256, n0 = tile_n * BN;
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
@@ -94,43 +105,49 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     const long ld = isA ? a.lda : a.ldb;
     const int lim = isA ? a.M : a.N;
     const int o0 = isA ? m0 : n0;
+    const bool narrow = !isA && BN == 128;  // 64-row B half
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      if (!ko) {  // [128 rows][64 k] image, 8 lanes per 128-B row
+      if (!ko) {  // [rows][64 k] image, 8 lanes per 128-B row
         const int r = 8 * (u * 8 + w) + (lane >> 3);
         const int lc = (lane & 7) ^ ((r >> 1) & 7);
-        const int g = min(o0 + (isA ? a_row(r, h) : b_row(r, h - 2)), lim - 1);
+        const int g = min(o0 + (isA ? a_row(r, h) : b_row<BN>(r, h - 2)), lim - 1);
         src[h][u] = P + (long)g * ld + kbeg + lc * 8;
-      } else {    // [64 k][128 cols] image, 16 lanes per 256-B k-row
+      } else if (!narrow) {  // [64 k][128 cols] image, 16 lanes per 256-B k-row
         const int k = 4 * (u * 8 + w) + (lane >> 4);
         const int lc = (lane & 15) ^ ko_swz(k);
         const int col = lc * 8;
-        const int g = min(o0 + (isA ? a_row(col, h) : b_row(col, h - 2)), lim - 8);
+        const int g = min(o0 + (isA ? a_row(col, h) : b_row<BN>(col, h - 2)), lim - 8);
         src[h][u] = P + (long)(kbeg + k) * ld + g;
+      } else {  // [64 k][64 cols] image, 8 lanes per 128-B k-row (gemm_core.h K-outer swizzle, R = 64)
+        const int k = 8 * (u * 8 + w) + (lane >> 3);
+        const int lc = (lane & 7) ^ (kouter_swz<64>(k & 63) << 1);
+        const int g = min(o0 + b_row<BN>(lc * 8, h - 2), lim - 8);
+        src[h][u] = P + (long)(kbeg + (k & 63)) * ld + g;
       }
     }
     kstep[h] = ko ? (long)BK * ld : (long)BK;
   }
   auto issue = [&](int h, int t, int buf) {
     const long ko = (long)t * kstep[h];
-    char* d = smem + buf * BUF + h * HALF + w * 1024;
+    char* d = smem + buf * BUF + half_off<BN>(h) + w * 1024;
     glds16(src[h][0] + ko, d);
-    glds16(src[h][1] + ko, d + 8 * 1024);
+    if (h < 2 || JN == 2) glds16(src[h][1] + ko, d + 8 * 1024);
   };
 
-  v4f acc[8][4];
+  v4f acc[8][2 * JN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2 * JN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
   // bf16: 2 k-substeps of 32 per 64-wide K-tile (16-B fragments); fp8 (OCP e4m3, K-tile = 128 bytes, same LDS image)
   // fp8: ONE block-scaled 16x16x128 MFMA per fragment pair and K-tile (32-B fragments, 2x the bf16 FLOP rate)
   using FragT = typename std::conditional<FP8 != 0, v8i, v8bf>::type;
   constexpr int KS = FP8 ? 1 : 2;
-  FragT fa[4][KS], fb0[2][KS], fb1[2][KS];
+  FragT fa[4][KS], fb0[JN][KS], fb1[JN][KS];
 
   auto read_a = [&](int buf, int h) {
-    const char* base = smem + buf * BUF + h * HALF;
+    const char* base = smem + buf * BUF + half_off<BN>(h);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -140,30 +157,32 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
         else fa[i][kk] = frag_kcontig(base, wr * 64 + i * 16, kk, lane);
       }
   };
-  auto read_b = [&](FragT (&fb)[2][KS], int buf, int h) {
-    const char* base = smem + buf * BUF + (2 + h) * HALF;
+  auto read_b = [&](FragT (&fb)[JN][KS], int buf, int h) {
+    const char* base = smem + buf * BUF + half_off<BN>(2 + h);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < JN; ++j)
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
-        if constexpr (FP8) fb[j][kk] = frag_fp8x128(base, wc * 32 + j * 16, lane);
-        else if constexpr (BMD == OP_KOUTER) fb[j][kk] = frag_ko(base, wc * 32 + j * 16, kk, lane);
-        else fb[j][kk] = frag_kcontig(base, wc * 32 + j * 16, kk, lane);
+        const int cb = wc * (BN / 8) + j * 16;
+        if constexpr (FP8) fb[j][kk] = frag_fp8x128(base, cb, lane);
+        else if constexpr (BMD == OP_KOUTER && BN == 128) fb[j][kk] = frag_kouter<64>(base, cb, kk, lane);
+        else if constexpr (BMD == OP_KOUTER) fb[j][kk] = frag_ko(base, cb, kk, lane);
+        else fb[j][kk] = frag_kcontig(base, cb, kk, lane);
       }
   };
-  auto mma = [&](const FragT (&fb)[2][KS], int ha, int hb) {
+  auto mma = [&](const FragT (&fb)[JN][KS], int ha, int hb) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < JN; ++j) {
           if constexpr (FP8)
-            acc[ha * 4 + i][hb * 2 + j] = mfma_fp8_ab<FP8>(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j]);
+            acc[ha * 4 + i][hb * JN + j] = mfma_fp8_ab<FP8>(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * JN + j]);
           else
-            acc[ha * 4 + i][hb * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+            acc[ha * 4 + i][hb * JN + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * JN + j], 0, 0, 0);
         }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -175,6 +194,9 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   // one phase apart (group 1 passes one extra barrier first), so group 1's MFMAs overlap group 0's LDS reads
   // and barrier waits on every SIMD. With that stagger a barrier must also publish the NEXT phase's halves,
   // so the wait before phase x covers the halves due at x and x+1: vmcnt(4|4|6|4).
+  // counted waits: an A half is 2 glds per thread, a B half JN; the wait before phase x leaves in flight exactly
+  // the halves issued after the ones due at phases x and x+1 (JN = 2: 6 | 4 4 6 4)
+  constexpr int WP = JN + 4, W0 = 4, W1 = 2 + JN, W2 = 2 + 2 * JN, W3 = JN + 2;
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
   if (nk > 0) {
     issue(0, 0, 0);
@@ -184,7 +206,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   }
   if (nk > 1) issue(0, 1, 1);
   if (wr == 1) {
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WP) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
   }
@@ -192,7 +214,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     const int buf = t & 1, nb = buf ^ 1;
     const bool more = t + 1 < nk, more2 = t + 2 < nk;
     // phase 0: (A0, B0)
-    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W0) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     read_a(buf, 0);
@@ -200,21 +222,21 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     if (more) issue(2, t + 1, nb);
     mma(fb0, 0, 0);
     // phase 1: (A0, B1)
-    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W1) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     read_b(fb1, buf, 1);
     if (more) issue(3, t + 1, nb);
     mma(fb1, 0, 1);
     // phase 2: (A1, B1)
-    if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W2) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     read_a(buf, 1);
     if (more) issue(1, t + 1, nb);
     mma(fb1, 1, 1);
     // phase 3: (A1, B0) from registers
-    if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W3) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     if (more2) issue(0, t + 2, buf);
@@ -230,7 +252,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   const bool staged = !a.out_f32 && a.beta == 0.f && a.slab == 0 && !(a.N & 7) && !(a.ldc & 7) &&
                       !(reinterpret_cast<uintptr_t>(a.C) & 15) && !(reinterpret_cast<uintptr_t>(a.aux) & 15);
   if (staged) {
-    constexpr int CS = 256 + 8;  // LDS row stride (elements): conflict-free 8-B fragment writes
+    constexpr int CS = BN + 8;  // LDS row stride (elements): conflict-free 8-B fragment writes
     bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
     __syncthreads();  // every wave is done with the operand buffers
     for (int o = 0; o < (a.aux ? 2 : 1); ++o) {
@@ -240,8 +262,8 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int nl = wc * 64 + j * 16 + (lane >> 4) * 4;
+            for (int j = 0; j < 2 * JN; ++j) {
+              const int nl = wc * (BN / 4) + j * 16 + (lane >> 4) * 4;
               float v[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
@@ -265,8 +287,8 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
         }
         __syncthreads();
 #pragma unroll 4
-        for (int c = threadIdx.x; c < 128 * 32; c += NT2) {
-          const int row = c >> 5, c8 = c & 31;
+        for (int c = threadIdx.x; c < 128 * (BN / 8); c += NT2) {
+          const int row = c / (BN / 8), c8 = c % (BN / 8);
           const int m = m0 + h * 128 + row, n = n0 + c8 * 8;
           if (m < a.M && n < a.N)
             *reinterpret_cast<uint4*>(dst + (long)m * a.ldc + n) =
@@ -282,8 +304,8 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);
     if (m >= a.M) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + (lane >> 4) * 4;
+    for (int j = 0; j < 2 * JN; ++j) {
+      const int n = n0 + wc * (BN / 4) + j * 16 + (lane >> 4) * 4;
       if (n >= a.N) continue;  // N % 4 == 0 (host)
       float v[4];
 #pragma unroll
@@ -328,28 +350,36 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   }
 }
 
+template <int BN>
+void launch256(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8) {
+  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
+  if (fp8 == 2) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 2, BN>), grid, dim3(NT2), 0, st, a);
+  else if (fp8) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 1, BN>), grid, dim3(NT2), 0, st, a);
+  else if (amode == OP_KCONTIG && bmode == OP_KCONTIG)
+    hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 0, BN>), grid, dim3(NT2), 0, st, a);
+  else if (amode == OP_KCONTIG)
+    hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KOUTER, 0, BN>), grid, dim3(NT2), 0, st, a);
+  else if (bmode == OP_KCONTIG)
+    hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KCONTIG, 0, BN>), grid, dim3(NT2), 0, st, a);
+  else hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KOUTER, 0, BN>), grid, dim3(NT2), 0, st, a);
+}
+
 }  // namespace
 
-// Used by dtf_gemm for eligible problems; returns 0 if launched, 1 if not eligible.
-int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8) {
+// Used by dtf_gemm for eligible problems; returns 0 if launched, 1 if not eligible. bn: 256 or 128 (tile width).
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int bn) {
   if (a.kchunk % BK || a.kchunk < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.stats || a.atomic_out || a.crm)
     return 1;
   if ((a.splitk > 1 && a.K % a.kchunk && (a.K % a.kchunk) % BK) || a.K % BK) return 1;
   if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return 1;
   if ((amode == OP_KOUTER && (a.M & 7)) || (bmode == OP_KOUTER && (a.N & 7))) return 1;
   if ((amode != OP_KCONTIG && amode != OP_KOUTER) || (bmode != OP_KCONTIG && bmode != OP_KOUTER)) return 1;
+  if (bn != 256 && bn != 128) return 1;
+  if (fp8 && (amode != OP_KCONTIG || bmode != OP_KCONTIG)) return 1;
   a.tiles_m = cdiv(a.M, 256);
-  a.tiles_n = cdiv(a.N, 256);
-  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
-  if (fp8) {
-    if (amode != OP_KCONTIG || bmode != OP_KCONTIG) return 1;
-    if (fp8 == 2) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 2>), grid, dim3(NT2), 0, st, a);
-    else hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT2), 0, st, a);
-  } else if (amode == OP_KCONTIG && bmode == OP_KCONTIG)
-    hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
-  else if (amode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KOUTER>), grid, dim3(NT2), 0, st, a);
-  else if (bmode == OP_KCONTIG) hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KCONTIG>), grid, dim3(NT2), 0, st, a);
-  else hipLaunchKernelGGL((gemm256_kernel<OP_KOUTER, OP_KOUTER>), grid, dim3(NT2), 0, st, a);
+  a.tiles_n = cdiv(a.N, bn);
+  if (bn == 256) launch256<256>(a, amode, bmode, st, fp8);
+  else launch256<128>(a, amode, bmode, st, fp8);
   return 0;
 }
 
@@ -373,8 +403,23 @@ DTF_API int dtf_gemm256(const void* A, const void* B, void* C, int M, int N, int
     a.slab = (long)M * N;
   }
   if (dtf::gemm256_try(a, a_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG, b_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG,
-                       st, 0))
+                       st, 0, 256))
     return -2;
   if (a.splitk > 1) dtf_sum_rows(ws, (long)M * N, a.splitk, (long)M * N, (float*)C, 0, stream);
+  return (int)hipGetLastError();
+}
+
+// Direct entry with an explicit tile width (256 or 128) for tests and tile sweeps (no split-K).
+DTF_API int dtf_gemm256_bn(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
+                           int a_kouter, int b_kouter, int out_f32, int bn, void* stream) {
+  dtf::GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.batch = 1; a.splitk = 1; a.alpha = 1.f; a.beta = 0.f; a.out_f32 = out_f32;
+  if (N & 3) return -1;
+  a.kchunk = (K + dtf::BK - 1) / dtf::BK * dtf::BK;
+  if (dtf::gemm256_try(a, a_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG, b_kouter ? dtf::OP_KOUTER : dtf::OP_KCONTIG,
+                       (hipStream_t)stream, 0, bn))
+    return -2;
   return (int)hipGetLastError();
 }

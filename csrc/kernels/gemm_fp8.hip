@@ -291,8 +291,8 @@ __global__ void fp8_update_scale2_kernel(float* amax, float* scale, float* prev,
 DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream);
 
 namespace dtf {
-int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8);  // gemm256.hip
-bool prefer256(long M, long N, long K, long batch);                           // gemm.hip
+int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int bn);  // gemm256.hip
+int pick256(long M, long N, long K, long batch);                                      // gemm.hip
 }  // namespace dtf
 
 using namespace dtf;
@@ -386,13 +386,14 @@ DTF_API int dtf_gemm_fp8_ex(const void* A, const void* B, void* C, void* aux, co
     a.C = ws;
     a.slab = (long)M * N;
     a.beta = 0.f;
-    if (gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8)) return -5;
+    if (gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8, 256)) return -5;
     dtf_sum_rows(ws, (long)M * N, splitk, (long)M * N, (float*)C, beta != 0.f ? 1 : 0, stream);
     return (int)hipGetLastError();
   }
   a.splitk = 1;
   a.kchunk = (a.K + BK - 1) / BK * BK;
-  if (prefer256(M, N, 2L * K, 1) && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8) == 0) return (int)hipGetLastError();
+  const int bn = pick256(M, N, 2L * K, 1);
+  if (bn && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8, bn) == 0) return (int)hipGetLastError();
   const long b128 = (long)cdiv(M, 128) * cdiv(N, 128);
   const bool big = b128 >= 256;
   a.tiles_m = cdiv(M, 128);
@@ -418,7 +419,8 @@ DTF_API int dtf_gemm_fp8(const void* A, const void* B, void* C, void* aux, const
   a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = 0;
   // the 256x256 glds pipeline when its tiling fills the chip (fp8 halves its staged bytes per FLOP)
-  if (tile < 0 && prefer256(M, N, 2L * K, 1) && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, (hipStream_t)stream, 1) == 0)
+  const int bn = tile < 0 ? pick256(M, N, 2L * K, 1) : 0;
+  if (bn && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, (hipStream_t)stream, 1, bn) == 0)
     return (int)hipGetLastError();
   if (tile < 0) {
     long b128 = (long)cdiv(M, 128) * cdiv(N, 128);

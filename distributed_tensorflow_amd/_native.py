@@ -57,6 +57,7 @@ _KERNEL_SIGS = {
     "dtf_dropout": [P, P, L, F, U, P, P],
     "dtf_rng_advance": [P, P],
     "dtf_gemm256": [P, P, P, I, I, I, L, L, L, I, I, I, I, P, L, P],
+    "dtf_gemm256_bn": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
     "dtf_quant_fp8_exact": [P, P, L, P, P, P],
     "dtf_attn_fwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],
     "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],

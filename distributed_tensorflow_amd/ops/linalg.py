@@ -125,11 +125,11 @@ def colsum(x2d, out=None, accumulate=False):
     return out
 
 
-# Plain (epilogue-free) backward GEMMs may go to hipBLASLt (torch.mm), the library GEMM of the platform: measured
-# faster than the MFMA kernel for every data-gradient shape of BERT-base / GPT-2-medium (1.1-1.55x) and for the
-# large weight gradients (out*in >= 4M: GPT-2 FFN and LM head); the split-K weight gradients of BERT's 768-wide
-# layers stay on the MFMA kernel, which is faster there (tools/bench_blas_plain.py). DTF_PLAIN_BLAS=0: all MFMA.
-_PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "1") != "0"
+# Every GEMM runs on the hand-written MFMA kernels by default. DTF_PLAIN_BLAS=1 sends the plain (epilogue-free)
+# backward GEMMs to hipBLASLt (torch.mm) instead: standalone it is faster on the data-gradient shapes
+# (tools/bench_blas_plain.py), but with the weight gradients overlapped on the side stream the end-to-end numbers
+# are BERT-base 789k (ours) vs 777k tok/s (hipBLASLt), GPT-2-medium 219k vs 225k, fp8 226k vs 228k.
+_PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "0") == "1"
 # Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream
 DENSE_SIDE_ON = SIDE_STREAM_ON and __import__("os").environ.get("DTF_DENSE_WGRAD_STREAM", "1") != "0"
 _BLAS_WGRAD_MIN = 4 << 20

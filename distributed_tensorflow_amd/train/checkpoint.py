@@ -409,7 +409,9 @@ class Checkpoint:
         out["save_counter" + _ATTR] = self.save_counter
         return out
 
-    def write(self, file_prefix, async_write=False):
+    def write(self, file_prefix, async_write=False, after=None):
+        """Write the bundle; `after` (optional) runs once the bundle is complete (in the writer thread when
+        asynchronous), e.g. to publish it in the `checkpoint` state file."""
         snap = _snapshot(self._tensors())
         meta = json.dumps({"keys": sorted(snap), "format": "dtf-object-graph-v1", "time": time.time()})
 
@@ -419,20 +421,26 @@ class Checkpoint:
                 bw.add(k, snap[k])
             bw.add_string("_DTF_OBJECT_GRAPH_JSON", meta)
             bw.finish()
+            if after is not None:
+                after()
         if async_write:
             self._async.submit(w)
         else:
             w()
         return file_prefix
 
+    MAX_STATE_PATHS = 100  # all_model_checkpoint_paths kept in the state file (most recent)
+
     def save(self, file_prefix, async_write=False):
         self.save_counter.assign_add(1)
         p = f"{file_prefix}-{int(self.save_counter.item())}"
-        self.write(p, async_write)
         d = os.path.dirname(p) or "."
-        st = get_checkpoint_state(d)
-        allp = (st["all_model_checkpoint_paths"] if st else []) + [p]
-        update_checkpoint_state(d, p, allp)
+
+        def publish():  # only after the bundle is on disk: a crash mid-write keeps the previous good checkpoint
+            st = get_checkpoint_state(d)
+            allp = [q for q in (st["all_model_checkpoint_paths"] if st else []) if q != p] + [p]
+            update_checkpoint_state(d, p, allp[-self.MAX_STATE_PATHS:])
+        self.write(p, async_write, after=publish)
         return p
 
     def sync(self):

@@ -10,6 +10,7 @@ from distributed_tensorflow_amd.ops import _util
 pytestmark = pytest.mark.gpu
 
 BF = torch.bfloat16
+F32 = torch.float32
 
 
 def rnd(*shape, dev, scale=1.0):
@@ -657,3 +658,20 @@ def test_fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K):
         out = torch.empty((M, N), dtype=BF, device=cuda)
         fp8.gemm_fp8(a.view(torch.uint8), b.view(torch.uint8), scales, out, fmt_a=fmt_a)
     close(out, ref, 1e-2)
+
+
+@pytest.mark.parametrize("ak,bk", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 512), (4096, 1096, 384)])
+def test_gemm256_narrow_tiles(cuda, ak, bk, M, N, K):
+    """256x128 tiles of the pipelined kernel (picked when 256x256 would leave half the chip idle) in all four
+    operand layouts vs an fp32 reference."""
+    torch.manual_seed(0)
+    a = rnd(K, M, dev=cuda) if ak else rnd(M, K, dev=cuda)
+    b = rnd(K, N, dev=cuda) if bk else rnd(N, K, dev=cuda)
+    out = torch.empty(M, N, dtype=F32, device=cuda)
+    from distributed_tensorflow_amd.ops._util import call, ptr, stream
+    call("dtf_gemm256_bn", ptr(a), ptr(b), ptr(out), M, N, K, a.stride(0), b.stride(0), N, int(ak), int(bk), 1, 128,
+         stream())  # (raises on a non-zero status)
+    A = a.float().t() if ak else a.float()
+    B = b.float() if bk else b.float().t()
+    close(out, A @ B, 2e-2)
