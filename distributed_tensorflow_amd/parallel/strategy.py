@@ -292,11 +292,21 @@ class MirroredStrategy(MultiWorkerMirroredStrategy):
     """Single-node synchronous data parallelism.
 
     devices=None under a multi-process launch: one replica per process (RCCL).
-    devices=[...] in one process: in-process replicas over those devices."""
+    devices=[...] in one process: in-process replicas over those devices (host devices, e.g. the reference's
+    CPU:0 / CPU:1 plumbing config). Several GPUs in ONE process are rejected: on MI355X every GPU gets its own
+    process (its own HIP runtime queues, RCCL rank and Python interpreter), launched by
+    ``python -m distributed_tensorflow_amd.cli.launch --gpus N ...`` or ``torchrun --nproc-per-node N``; the
+    same ``MirroredStrategy()`` then finds its replica through the launcher's environment."""
 
     def __init__(self, devices=None, cross_device_ops=None, bucket_mb=None, communication_options=None):
         self._devices = [context.parse_device(d) for d in devices] if devices else None
         self.wire_dtype = getattr(communication_options, "wire_dtype", None)
+        gpus = {d for d in (self._devices or []) if d.type == "cuda"}
+        if len(gpus) > 1 and not TorchrunClusterResolver.active():
+            raise ValueError(
+                f"MirroredStrategy over {len(gpus)} GPUs in one process is not supported: run one process per GPU "
+                "(python -m distributed_tensorflow_amd.cli.launch --gpus N <script>, or torchrun --nproc-per-node N) "
+                "and construct MirroredStrategy() without devices in each process")
         if self._devices and len(self._devices) > 1 and not TorchrunClusterResolver.active():
             Strategy.__init__(self)
             self.bucket_mb = bucket_mb

@@ -212,3 +212,11 @@ def test_ps_shm_two_ps_six_trainers(tmp_path):
     assert applied == [6 * 2 * 100] * 2, applied  # every trainer's every push reached both shards
     w, b = float(C.load_variable(ck, "weight")), float(C.load_variable(ck, "bias"))
     assert 1.5 < w < 2.5 and 9.5 < b < 10.5, (w, b)
+
+
+def test_mirrored_rejects_several_gpus_in_one_process():
+    """Several GPUs in ONE process are rejected with a pointer to the one-process-per-GPU launch."""
+    import pytest
+    from distributed_tensorflow_amd import parallel
+    with pytest.raises(ValueError, match="one process per GPU"):
+        parallel.MirroredStrategy(["GPU:0", "GPU:1"])
