@@ -312,14 +312,41 @@ using namespace dtf;
 // Generic (batched) GEMM: C[b][m][n] = alpha * sum_k A(m,k) B(n,k) + beta*C (+bias, act)
 //   a_kouter: A stored [K][M] (ld=lda) instead of [M][K]; b_kouter: B stored [K][N] instead of [N][K].
 // stats (optional): per-M-tile partial rows [tiles_m][2N] (capacity ceil(M/64) rows); *stat_rows = tiles_m.
+static int gemm_impl(const void* A, const void* B, void* C, void* aux, const float* bias, float* stats,
+                     int* stat_rows, int M, int N, int K, long lda, long ldb, long ldc, int a_kouter, int b_kouter,
+                     int batch, long sA, long sB, long sC, float alpha, float beta, int act, int out_f32,
+                     int splitk, int tile, float* ws, long ws_elems, void* stream, const void* dact_src = nullptr,
+                     int dact = 0);
+
 DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const float* bias, float* stats,
                      int* stat_rows, int M, int N, int K, long lda, long ldb, long ldc, int a_kouter, int b_kouter,
                      int batch, long sA, long sB, long sC, float alpha, float beta, int act, int out_f32,
                      int splitk, int tile, float* ws, long ws_elems, void* stream) {
+  return gemm_impl(A, B, C, aux, bias, stats, stat_rows, M, N, K, lda, ldb, ldc, a_kouter, b_kouter, batch, sA, sB,
+                   sC, alpha, beta, act, out_f32, splitk, tile, ws, ws_elems, stream);
+}
+
+// Data-gradient GEMM with the activation backward fused: C[M][N] (bf16) = (A . B^T) * act'(pre), pre [M][N] with
+// row stride ldc (act 1 relu, 2 gelu-tanh). The product is rounded to bf16 before the multiply, exactly as the
+// unfused GEMM + dtf_act pair would.
+DTF_API int dtf_gemm_dact(const void* A, const void* B, void* C, const void* pre, int act, int M, int N, int K, long lda,
+                          long ldb, long ldc, int a_kouter, int b_kouter, void* stream) {
+  if (!pre || (act != 1 && act != 2)) return -1;
+  return gemm_impl(A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, a_kouter, b_kouter, 1, 0, 0, 0,
+                   1.f, 0.f, 0, 0, 1, -1, nullptr, 0, stream, pre, act);
+}
+
+static int gemm_impl(const void* A, const void* B, void* C, void* aux, const float* bias, float* stats,
+                     int* stat_rows, int M, int N, int K, long lda, long ldb, long ldc, int a_kouter, int b_kouter,
+                     int batch, long sA, long sB, long sC, float alpha, float beta, int act, int out_f32,
+                     int splitk, int tile, float* ws, long ws_elems, void* stream, const void* dact_src, int dact) {
   if ((N & 3) || (K & 7) || M <= 0 || N <= 0) return -1;
   if (a_kouter && (M & 7)) return -2;
   if (b_kouter && (N & 7)) return -3;
+  if (dact && (out_f32 || beta != 0.f || act || aux || splitk > 1 || batch > 1)) return -8;
   GemmArgs a{};
+  a.dact_src = (const bf16_t*)dact_src;
+  a.dact = dact;
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.aux = (bf16_t*)aux;
   a.bias = bias; a.stats = stats;
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;

@@ -290,9 +290,11 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
         for (int c = threadIdx.x; c < 128 * (BN / 8); c += NT2) {
           const int row = c / (BN / 8), c8 = c % (BN / 8);
           const int m = m0 + h * 128 + row, n = n0 + c8 * 8;
-          if (m < a.M && n < a.N)
-            *reinterpret_cast<uint4*>(dst + (long)m * a.ldc + n) =
-                *reinterpret_cast<const uint4*>(ct + row * CS + c8 * 8);
+          if (m < a.M && n < a.N) {
+            uint4 val = *reinterpret_cast<const uint4*>(ct + row * CS + c8 * 8);
+            if (o == 0 && a.dact) val = dact8(val, *reinterpret_cast<const uint4*>(a.dact_src + (long)m * a.ldc + n), a.dact);
+            *reinterpret_cast<uint4*>(dst + (long)m * a.ldc + n) = val;
+          }
         }
         __syncthreads();
       }
@@ -344,6 +346,11 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
         uint2 o;
         o.x = pack2bf(v[0], v[1]);
         o.y = pack2bf(v[2], v[3]);
+        if (a.dact) {
+          const uint2 pr = *reinterpret_cast<const uint2*>(a.dact_src + (long)m * a.ldc + n);
+          const uint4 d = dact8(make_uint4(o.x, o.y, 0, 0), make_uint4(pr.x, pr.y, 0, 0), a.dact);
+          o.x = d.x; o.y = d.y;
+        }
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.C) + off) = o;
       }
     }

@@ -89,6 +89,10 @@ struct GemmArgs {
   const uint8_t* bnmask;
   const float* bnmean;
   const uint8_t* betamask;  // optional 1-bit mask on the beta*C term (staged bf16 epilogue only)
+  // optional activation backward applied to the (bf16-rounded) product: C = C * act'(dact_src), act 1 relu / 2 gelu
+  // (a data-gradient GEMM that produces the gradient of an activation output hands on the pre-activation's)
+  const bf16_t* dact_src;
+  int dact;
   int crm;
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
@@ -134,6 +138,29 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float u = k0 * (x + k1 * x * x * x);
   return x * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  // tanh(u) = 2 s - 1 with s = sigmoid(2u): one exp and one reciprocal instead of a libm tanhf
+  const float u = k0 * (x + k1 * x * x * x);
+  const float s = __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
+  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x * x);
+}
+// 8 bf16 products (val) times act'(pre) of the 8 matching pre-activations, re-rounded to bf16
+__device__ __forceinline__ uint4 dact8(uint4 val, uint4 pre, int act) {
+  const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, pw[4] = {pre.x, pre.y, pre.z, pre.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float f[2], p[2];
+    f[0] = __uint_as_float(vw[q] << 16); f[1] = __uint_as_float(vw[q] & 0xffff0000u);
+    p[0] = __uint_as_float(pw[q] << 16); p[1] = __uint_as_float(pw[q] & 0xffff0000u);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) f[h] *= act == 1 ? (p[h] > 0.f ? 1.f : 0.f) : gelu_tanh_grad(p[h]);
+    o[q] = pack2bf(f[0], f[1]);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // Bit mask over the taps (kh * S + kw) of an R x S filter with kh in [h0, h1] and kw in [w0, w1] (empty when
@@ -811,6 +838,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
         val.x = pack2bf(f[0], f[1]); val.y = pack2bf(f[2], f[3]);
         val.z = pack2bf(f[4], f[5]); val.w = pack2bf(f[6], f[7]);
       }
+      if (a.dact) val = dact8(val, *reinterpret_cast<const uint4*>(a.dact_src + e), a.dact);
       *reinterpret_cast<uint4*>(cp) = val;
       if (bn_bwd) {
         const uint4 xr = *reinterpret_cast<const uint4*>(a.bnx + e);
@@ -907,6 +935,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
         uint2 o;
         o.x = pack2bf(v[0], v[1]);
         o.y = pack2bf(v[2], v[3]);
+        if (a.dact) {
+          const uint2 pr = *reinterpret_cast<const uint2*>(a.dact_src + mrow * a.ldc + n);
+          const uint4 d = dact8(make_uint4(o.x, o.y, 0, 0), make_uint4(pr.x, pr.y, 0, 0), a.dact);
+          o.x = d.x; o.y = d.y;
+        }
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(a.C) + off) = o;
         if (a.stats) {  // statistics of the stored (bf16-rounded) values
           v[0] = __uint_as_float(o.x << 16); v[1] = __uint_as_float(o.x & 0xffff0000u);

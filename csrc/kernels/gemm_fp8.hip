@@ -153,9 +153,10 @@ struct QtArgs {
 
 __device__ __forceinline__ float gelu_grad_q(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  // tanh(u) = 2 s - 1 with s = sigmoid(2u): one exp and one reciprocal instead of a libm tanhf
   const float u = k0 * (x + k1 * x * x * x);
-  const float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  const float s = __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
+  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x * x);
 }
 
 template <int FMT>

@@ -58,6 +58,7 @@ _KERNEL_SIGS = {
     "dtf_rng_advance": [P, P],
     "dtf_gemm256": [P, P, P, I, I, I, L, L, L, I, I, I, I, P, L, P],
     "dtf_gemm256_bn": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
+    "dtf_gemm_dact": [P, P, P, P, I, I, I, I, L, L, L, I, I, P],
     "dtf_quant_fp8_exact": [P, P, L, P, P, P],
     "dtf_attn_fwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],
     "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],

@@ -25,9 +25,11 @@ RES_LINK = __import__("os").environ.get("DTF_TF_RES_LINK", "0") == "1"
 class _Proj(KL.Layer):
     """Dense [units, in] with optional fp8 forward."""
 
-    def __init__(self, units, activation=None, fp8=False, init_std=0.02, **kw):
+    def __init__(self, units, activation=None, fp8=False, init_std=0.02, single_consumer=False, **kw):
         super().__init__(**kw)
         self.units, self.activation, self.fp8, self.init_std = units, activation, fp8, init_std
+        # the output feeds exactly one _Proj (FFN1 -> FFN2): its activation backward may be fused downstream
+        self.single_consumer = single_consumer
 
     def build(self, input_shape):
         from ..keras.initializers import TruncatedNormal
@@ -39,7 +41,7 @@ class _Proj(KL.Layer):
         if self.fp8 and x.is_cuda:
             from ..ops.fp8 import dense_fp8
             return dense_fp8(x, self.kernel, self.bias, self.activation, self)
-        return ops.dense(x, self.kernel, self.bias, act=self.activation, link=link)
+        return ops.dense(x, self.kernel, self.bias, act=self.activation, link=link, tag_act=self.single_consumer)
 
 
 class MultiHeadSelfAttention(KL.Layer):
@@ -60,7 +62,7 @@ class BertLayer(KL.Layer):
         super().__init__(**kw)
         self.att = MultiHeadSelfAttention(hidden, heads, dropout)
         self.ln1 = KL.LayerNormalization(epsilon=1e-12)
-        self.ff1 = _Proj(ffn, activation="gelu")
+        self.ff1 = _Proj(ffn, activation="gelu", single_consumer=True)
         self.ff2 = _Proj(hidden)
         self.ln2 = KL.LayerNormalization(epsilon=1e-12)
         self.dropout = dropout
@@ -137,7 +139,7 @@ class GPT2Block(KL.Layer):
         self.ln1 = KL.LayerNormalization(epsilon=1e-5)
         self.att = MultiHeadSelfAttention(hidden, heads, dropout, causal=True, fp8=fp8)
         self.ln2 = KL.LayerNormalization(epsilon=1e-5)
-        self.fc = _Proj(4 * hidden, activation="gelu", fp8=fp8)
+        self.fc = _Proj(4 * hidden, activation="gelu", fp8=fp8, single_consumer=True)
         self.proj = _Proj(hidden, fp8=fp8)
         self.dropout = dropout
 

@@ -167,12 +167,34 @@ def _act_ref(x, act):
     return x
 
 
+class _ActSource:
+    """Attached to the output of a Dense layer with an activation (the pre-activation and the activation code): a
+    consuming Dense layer that is the output's only reader applies the activation backward inside its own
+    data-gradient GEMM epilogue (gemm_dact), and the producer then skips its activation-backward pass — the
+    gradient of the activation output is never written (cf. ops.conv._BNSource for BatchNorm)."""
+    __slots__ = ("pre", "act", "consumers", "fused_ptr", "__weakref__")
+
+    def __init__(self, pre, act):
+        self.pre, self.act = pre, act
+        self.consumers = 0
+        self.fused_ptr = None
+
+
+_FUSE_DACT = __import__("os").environ.get("DTF_FUSE_DACT", "1") != "0"
+
+
 class _DenseFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, link=None):
+    def forward(ctx, x, w, b, act, link=None, tag_act=False):
         # x: [..., in] bf16 ; w: [out, in] f32 master ; b: [out] f32 or None
         # link: ops.conv.ResidualGradLink whose parked gradient of x the data-gradient GEMM adds in
+        # tag_act: the caller guarantees the output is read by ONE Dense layer only (e.g. FFN1 -> FFN2), which may
+        # then fuse this layer's activation backward into its data-gradient GEMM (_ActSource)
         ctx.link = link
+        in_src = getattr(x, "_dtf_actsrc", None)
+        if in_src is not None:
+            in_src.consumers += 1
+        ctx.in_src = in_src
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         if not x2.is_contiguous():
@@ -185,7 +207,12 @@ class _DenseFn(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.b_param = b
         ctx.shp = shp
-        return y.reshape(*shp[:-1], w.shape[0])
+        out = y.reshape(*shp[:-1], w.shape[0])
+        ctx.src = None
+        if act and tag_act and _FUSE_DACT and pre is not None:
+            ctx.src = _ActSource(pre, act)
+            out._dtf_actsrc = ctx.src
+        return out
 
     @staticmethod
     def backward(ctx, dy):
@@ -194,16 +221,29 @@ class _DenseFn(torch.autograd.Function):
         if dy2.dtype != BF16:
             dy2 = dy2.to(BF16)
         dy2 = dy2.contiguous()
-        if ctx.act:
+        src = ctx.src
+        ctx.src = None
+        if ctx.act and not (src is not None and src.fused_ptr == dy2.data_ptr()):
             dz = torch.empty_like(dy2)
             call("dtf_act", ptr(pre), ptr(dy2), ptr(dz), dz.numel(), ctx.act, 1, stream())
         else:
-            dz = dy2
+            dz = dy2  # (the consumer's data-gradient GEMM already applied act')
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             # dx[t,i] = sum_o dz[t,o] W[o,i]  -> B stored [K=out][N=in] (k-outer)
             acc = ctx.link.take()[0] if ctx.link is not None else None
-            dx = dense_dgrad(dz, bf16_shadow(w), None if acc is None else acc.reshape(dz.shape[0], -1))
+            isrc = ctx.in_src
+            ctx.in_src = None
+            if (acc is None and isrc is not None and isrc.consumers == 1 and not _PLAIN_BLAS
+                    and isrc.pre.shape == (dz.shape[0], w.shape[1])):
+                # the producer's activation backward in this GEMM's epilogue
+                dx = torch.empty((dz.shape[0], w.shape[1]), dtype=BF16, device=dz.device)
+                w16 = bf16_shadow(w)
+                call("dtf_gemm_dact", ptr(dz), ptr(w16), ptr(dx), ptr(isrc.pre), int(isrc.act), dz.shape[0],
+                     w.shape[1], w.shape[0], dz.stride(0), w16.stride(0), dx.stride(0), 0, 1, stream())
+                isrc.fused_ptr = dx.data_ptr()
+            else:
+                dx = dense_dgrad(dz, bf16_shadow(w), None if acc is None else acc.reshape(dz.shape[0], -1))
             dx = dx.reshape(ctx.shp)
         tw = direct_grad(w) if ctx.needs_input_grad[1] else None
         tb = direct_grad(ctx.b_param) if (ctx.has_b and ctx.needs_input_grad[2]) else None
@@ -217,7 +257,7 @@ class _DenseFn(torch.autograd.Function):
             if ctx.has_b and ctx.needs_input_grad[2] and tb is None:
                 db = colsum(dz)
             ctx.link = None
-            return dx, dw, db, None, None
+            return dx, dw, db, None, None, None
         if ctx.needs_input_grad[1]:
             # dW[o,i] = sum_t dz[t,o] x[t,i]  -> both operands k-outer, f32 out; inside Model.train_step
             # accumulated straight into the arena gradient (beta = 1) instead of returned
@@ -231,17 +271,18 @@ class _DenseFn(torch.autograd.Function):
             else:
                 db = colsum(dz)
         ctx.link = None
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
-def dense(x, w, b=None, act=None, link=None):
+def dense(x, w, b=None, act=None, link=None, tag_act=False):
     """y = act(x @ w^T + b); w is [out, in] (f32 master variable). link: ops.conv.ResidualGradLink joining x's
-    gradient from a residual connection into this layer's data-gradient GEMM."""
+    gradient from a residual connection into this layer's data-gradient GEMM. tag_act: y feeds exactly one Dense
+    layer, which then applies act' inside its data-gradient GEMM (see _ActSource)."""
     a = act_code(act)
     if on_gpu(x):
         if x.dtype != BF16:
             x = x.to(BF16)
-        return _DenseFn.apply(x, w, b, a, link)
+        return _DenseFn.apply(x, w, b, a, link, bool(tag_act))
     y = torch.nn.functional.linear(x.to(w.dtype), w, b)
     return _act_ref(y, a)
 

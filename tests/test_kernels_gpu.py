@@ -675,3 +675,27 @@ def test_gemm256_narrow_tiles(cuda, ak, bk, M, N, K):
     A = a.float().t() if ak else a.float()
     B = b.float() if bk else b.float().t()
     close(out, A @ B, 2e-2)
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu"])
+def test_dense_pair_fused_activation_backward(cuda, act):
+    """FFN1 -> FFN2 with FFN1's activation backward fused into FFN2's data-gradient GEMM (dtf_gemm_dact) gives the
+    same gradients as the unfused pair (bitwise: the product is rounded to bf16 before act', as dtf_act does)."""
+    from distributed_tensorflow_amd.ops import linalg as LA
+    torch.manual_seed(0)
+    x0 = rnd(512, 256, dev=cuda)
+    w1 = (torch.randn(1024, 256, device=cuda) * 0.05).requires_grad_(True)
+    b1 = torch.zeros(1024, device=cuda, requires_grad=True)
+    w2 = (torch.randn(256, 1024, device=cuda) * 0.05).requires_grad_(True)
+    g = rnd(512, 256, dev=cuda)
+    res = []
+    for fuse in (False, True):
+        x = x0.clone().requires_grad_(True)
+        h = LA.dense(x, w1, b1, act=act, tag_act=fuse)
+        y = LA.dense(h, w2, None)
+        y.backward(g)
+        res.append((x.grad.clone(), w1.grad.clone(), b1.grad.clone(), w2.grad.clone()))
+        for t in (w1, b1, w2):
+            t.grad = None
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
