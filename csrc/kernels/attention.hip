@@ -561,7 +561,18 @@ __device__ __forceinline__ void attn_dq_body(const AttnArgs& a, const int qblk, 
       df[qt][kk] = frag_global(dO + (long)qi * a.oss + 32 * kk + 8 * G, ok);
     }
     lse[qt] = ok ? a.lse[(long)bh * a.Sq + qi] : INFINITY;
-    dd[qt] = ok ? a.dvec[(long)bh * a.Sq + qi] : 0.f;
+    // D[q] = rowsum(dO * O): the lane's 16 dims, then the 4 lane groups of the row
+    float d = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v8bf of = frag_global(a.o + ob + (long)qi * a.oss + 32 * kk + 8 * G, ok);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d = fmaf((float)df[qt][kk][j], (float)of[j], d);
+    }
+    d += __shfl_xor(d, 16, 64);
+    d += __shfl_xor(d, 32, 64);
+    dd[qt] = d;
+    if (ok && G == 0) a.dvec[(long)bh * a.Sq + qi] = d;  // for the dK/dV kernel, launched after this one
   }
   v4f dq[4][QT];
 #pragma unroll
@@ -719,7 +730,7 @@ DTF_API int dtf_attn_fwd(const void* q, const void* k, const void* v, const long
   return (int)hipGetLastError();
 }
 
-// dvec: f32 [B*H][Sq] scratch.
+// dvec: f32 [B*H][Sq] scratch (rowsum(dO * O), written by the dQ kernel, read by the dK/dV kernel).
 DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long* qstr, const long* kstr,
                          const void* o, const void* dout, const long* ostr, const float* lse, float* dvec, void* dq,
                          void* dk, void* dv, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
@@ -737,17 +748,15 @@ DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long
   a.dq = (bf16_t*)dq;
   a.dk = (bf16_t*)dk;
   a.dv = (bf16_t*)dv;
-  const long rows = (long)B * H * Sq;
-  hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)std::min<long>((rows + 255) / 256, 4096)), dim3(256), 0, st,
-                     a);
   const int nkb = (Sk + 127) / 128, nqb = (Sq + 127) / 128;
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0, st, a,
-                     nkb);
+  // dQ first: it forms D = rowsum(dO * O) per query (dvec) that the dK/dV kernel reads
   if (causal)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 1>), dim3(pair_grid(causal, nqb), (unsigned)(B * H)), dim3(256), 0, st,
                        a, nqb);
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 2>), dim3(pair_grid(causal, nqb), (unsigned)(B * H)), dim3(256), 0, st,
                        a, nqb);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0, st, a,
+                     nkb);
   return (int)hipGetLastError();
 }
