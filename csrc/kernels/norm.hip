@@ -836,16 +836,44 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
       ab[k][j] = 0.f;
     }
   }
-  for (long row = (long)blockIdx.x * 4 + w; row < M; row += (long)gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
+  // software-pipelined over the wave's rows: the next row's x / dy / statistics are loaded while this row's
+  // two wave reductions run (a row per wave is otherwise one exposed memory latency + two reduction chains)
+  const long stride = (long)gridDim.x * 4;
+  long row = (long)blockIdx.x * 4 + w;
+  uint4 nx[NC], ng[NC];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](long r) {
+    if (r >= M) return;
+    nmu = mean[r];
+    nrs = rstd[r];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + 64 * k;
+      if (c < d8) {
+        nx[k] = *reinterpret_cast<const uint4*>(x + r * D + c * 8);
+        ng[k] = *reinterpret_cast<const uint4*>(dy + r * D + c * 8);
+      }
+    }
+  };
+  fetch(row);
+  for (; row < M; row += stride) {
+    const float mu = nmu, rs = nrs;
     float xh[NC][8], g[NC][8];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const uint32_t xw[4] = {nx[k].x, nx[k].y, nx[k].z, nx[k].w}, gw[4] = {ng[k].x, ng[k].y, ng[k].z, ng[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        xh[k][2 * q] = __uint_as_float(xw[q] << 16); xh[k][2 * q + 1] = __uint_as_float(xw[q] & 0xffff0000u);
+        g[k][2 * q] = __uint_as_float(gw[q] << 16); g[k][2 * q + 1] = __uint_as_float(gw[q] & 0xffff0000u);
+      }
+    }
+    fetch(row + stride);
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       const int c = lane + 64 * k;
       if (c < d8) {
-        load8(x + row * D + c * 8, xh[k]);
-        load8(dy + row * D + c * 8, g[k]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[k][j] = (xh[k][j] - mu) * rs;
