@@ -699,3 +699,16 @@ def test_dense_pair_fused_activation_backward(cuda, act):
             t.grad = None
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b)
+
+
+def test_dropout_keep_rate_and_scale(cuda):
+    """Elementwise dropout (16-bit uniforms from chunk hashes): realised keep rate ~= keep, kept values scaled by the
+    exact inverse of the 16-bit threshold, fresh masks for different seeds."""
+    x = torch.ones(1 << 20, device=cuda).to(BF)
+    y1 = ops.dropout(x, 0.1, training=True, seed=7).float()
+    y2 = ops.dropout(x, 0.1, training=True, seed=8).float()
+    kept = (y1 != 0).float().mean().item()
+    assert abs(kept - 0.9) < 0.003, kept
+    vals = y1[y1 != 0]
+    assert torch.allclose(vals, torch.full_like(vals, 65536.0 / round(0.9 * 65536)).to(BF).float())
+    assert ((y1 != 0) != (y2 != 0)).float().mean().item() > 0.1
