@@ -88,6 +88,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   const int tile_m = first_m + in_g % gsize;
   const int tile_n = in_g / gsize;
   const int m0 = tile_m * 256, n0 = tile_n * BN;
+  if (a.zero_slot && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) *a.zero_slot = 0.f;
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);

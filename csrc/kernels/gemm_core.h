@@ -93,6 +93,7 @@ struct GemmArgs {
   // (a data-gradient GEMM that produces the gradient of an activation output hands on the pre-activation's)
   const bf16_t* dact_src;
   int dact;
+  float* zero_slot;  // optional: block 0 clears this f32 (fp8 delayed scaling: the amax slot the next step fills)
   int crm;
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
@@ -1025,6 +1026,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const int tile_n = in_g / gsize;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
+  if (a.zero_slot && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) *a.zero_slot = 0.f;
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);

@@ -148,6 +148,11 @@ struct QtArgs {
   const float* part;  // exact scaling: per-block absmax partials of x (scale = max / fmax, written to scale_out)
   int nparts;
   float* scale_out;
+  // delayed scaling without an update launch: scale = amax_prev / fmax when amax_prev > 0 (else *scale); the scale
+  // used is published to scale_used / scale_used2 (block (0, 0))
+  const float* amax_prev;
+  float* scale_used;
+  float* scale_used2;
   int M, N, act;
 };
 
@@ -196,7 +201,12 @@ __global__ void __launch_bounds__(256) quant_t_kernel(QtArgs a) {
     scale = fmaxf(m, 1e-12f) / FMAX;
     if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0) a.scale_out[0] = scale;
   } else {
-    scale = fmaxf(a.scale[0], 1e-30f);
+    const float ap = a.amax_prev ? a.amax_prev[0] : 0.f;
+    scale = ap > 0.f ? ap / FMAX : fmaxf(a.scale[0], 1e-30f);
+    if (a.scale_used && blockIdx.x == 0 && blockIdx.y == 0 && t == 0) {
+      a.scale_used[0] = scale;
+      if (a.scale_used2) a.scale_used2[0] = scale;
+    }
   }
   const float inv = 1.f / scale;
   float cs[16];
@@ -329,15 +339,31 @@ DTF_API int dtf_fp8_update_scale(float* amax, float* scale, float margin, void* 
 // Transposing quantizer (see quant_t_kernel; column-sum partials: one row per 256 rows of x). fmt 0 = e4m3, 1 = e5m2. exact: the scale is amax(|x|)/fmax computed
 // on the device (two launches; ws >= 2048 floats; written to scale_out), else x is quantized with *scale and
 // amax (optional) records max |value|. pre (optional, exact = 0 only): x is dy of act(pre), act 1 relu / 2 gelu.
+DTF_API int dtf_quant_fp8_t2(const void* x, const void* pre, int act, void* q, void* qT, float* colpart,
+                             const float* scale, float* amax, int M, int N, int fmt, int exact, float* ws,
+                             float* scale_out, const float* amax_prev, float* scale_used, float* scale_used2,
+                             void* stream);
 DTF_API int dtf_quant_fp8_t(const void* x, const void* pre, int act, void* q, void* qT, float* colpart,
                             const float* scale, float* amax, int M, int N, int fmt, int exact, float* ws,
                             float* scale_out, void* stream) {
+  return dtf_quant_fp8_t2(x, pre, act, q, qT, colpart, scale, amax, M, N, fmt, exact, ws, scale_out, nullptr, nullptr,
+                          nullptr, stream);
+}
+
+// dtf_quant_fp8_t with delayed scaling folded in: scale = amax_prev / fmax (when > 0, else *scale), published to
+// scale_used (and scale_used2); amax accumulates this pass's max for the next step (the caller's consumer GEMM
+// clears amax_prev through GemmArgs::zero_slot so that the slot can accumulate again a step later).
+DTF_API int dtf_quant_fp8_t2(const void* x, const void* pre, int act, void* q, void* qT, float* colpart,
+                             const float* scale, float* amax, int M, int N, int fmt, int exact, float* ws,
+                             float* scale_out, const float* amax_prev, float* scale_used, float* scale_used2,
+                             void* stream) {
   if ((M & 63) || (N & 63) || M <= 0 || N <= 0 || (exact && (pre || !ws || !scale_out))) return -1;
   hipStream_t st = (hipStream_t)stream;
   QtArgs a{};
   a.x = (const bf16_t*)x; a.pre = (const bf16_t*)pre; a.act = act;
   a.q = (uint8_t*)q; a.qT = (uint8_t*)qT; a.colpart = colpart;
   a.scale = scale; a.amax = amax; a.M = M; a.N = N;
+  a.amax_prev = amax_prev; a.scale_used = scale_used; a.scale_used2 = scale_used2;
   if (exact) {
     const long n8 = (long)M * N / 8;
     const int grid = stream_grid(n8 / QU, 256);
@@ -367,7 +393,7 @@ DTF_API int dtf_fp8_update_scale2(float* amax, float* scale, float* prev, float 
 // slabs in ws (>= splitk*M*N floats) reduced by dtf_sum_rows (accumulating into C when beta = 1).
 DTF_API int dtf_gemm_fp8_ex(const void* A, const void* B, void* C, void* aux, const float* bias, const float* scales,
                             int M, int N, int K, long lda, long ldb, long ldc, int act, int fmt_a, int out_f32,
-                            float beta, int splitk, float* ws, long ws_elems, void* stream) {
+                            float beta, int splitk, float* ws, long ws_elems, float* zero_slot, void* stream) {
   if ((N & 7) || (K & 127) || (lda & 15) || (ldb & 15) || M <= 0) return -1;
   if (beta != 0.f && beta != 1.f) return -2;
   if (!out_f32 && (beta != 0.f || splitk > 1)) return -3;
@@ -379,6 +405,7 @@ DTF_API int dtf_gemm_fp8_ex(const void* A, const void* B, void* C, void* aux, co
   a.M = M; a.N = N; a.K = K / 2;
   a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
   a.batch = 1; a.alpha = 1.f; a.beta = beta; a.act = act; a.out_f32 = out_f32;
+  a.zero_slot = zero_slot;
   if (splitk < 1) splitk = 1;
   if (splitk > 1) {
     if (!ws || ws_elems < (long)splitk * M * N || ldc != N || bias || act || aux) return -4;

@@ -33,7 +33,11 @@ E5M2_MAX = 57344.0
 _FP8_BWD = os.environ.get("DTF_FP8_BWD", "1") != "0"
 
 # state buffer slots (f32, per layer): adjacent pairs are the (s_a, s_b) dequant scales of the three GEMMs
+# (forward (x, w), data gradient (w, g), weight gradient (g, x)); X_AMAX / G_AMAX are double-buffered by step
+# parity: a quantize pass derives its scale from the previous step's slot and fills the other one, and the GEMM
+# that consumes it clears the previous slot for the step after (no scale-update launch)
 X_SCALE, W_SCALE, G_SCALE, X_USED, X_AMAX, G_AMAX = range(6)
+X_AMAX2, G_AMAX2 = 6, 7
 
 
 def quantize(x, scale, amax=None, zero_amax=True):
@@ -43,7 +47,7 @@ def quantize(x, scale, amax=None, zero_amax=True):
 
 
 def quantize_t(x, scale=None, amax=None, *, fmt=0, pre=None, act=0, rowmajor=True, transposed=True, colsums=False,
-               exact_out=None):
+               exact_out=None, amax_prev=None, scale_used=None, scale_used2=None):
     """One transposing pass over a [M, N] bf16 matrix (M, N multiples of 64): returns (q [M,N] | None,
     qT [N,M] | None, column-sum partials [ceil(M/256), N] | None). fmt 0 = e4m3, 1 = e5m2. exact_out: compute the
     exact per-tensor scale on the device and store it there (weights); else quantize with `scale` and record
@@ -54,19 +58,22 @@ def quantize_t(x, scale=None, amax=None, *, fmt=0, pre=None, act=0, rowmajor=Tru
     qT = torch.empty((N, M), dtype=torch.uint8, device=dev) if transposed else None
     cp = torch.empty((-(-M // 256), N), dtype=F32, device=dev) if colsums else None
     ws = workspace(dev) if exact_out is not None else None
-    call("dtf_quant_fp8_t", ptr(x), ptr(pre), int(act), ptr(q), ptr(qT), ptr(cp), ptr(scale), ptr(amax), M, N,
-         int(fmt), int(exact_out is not None), ptr(ws), ptr(exact_out), stream())
+    call("dtf_quant_fp8_t2", ptr(x), ptr(pre), int(act), ptr(q), ptr(qT), ptr(cp), ptr(scale), ptr(amax), M, N,
+         int(fmt), int(exact_out is not None), ptr(ws), ptr(exact_out), ptr(amax_prev), ptr(scale_used),
+         ptr(scale_used2), stream())
     return q, qT, cp
 
 
-def gemm_fp8(a, b, scales, out, *, fmt_a=0, out_f32=False, beta=0.0, splitk=1):
-    """out[M,N] (=|+=) s0*s1 * a[M,K] . b[N,K]^T for fp8 a (fmt_a 0 e4m3 / 1 e5m2) and e4m3 b (K-contiguous)."""
+def gemm_fp8(a, b, scales, out, *, fmt_a=0, out_f32=False, beta=0.0, splitk=1, bias=None, act=0, aux=None,
+             zero_slot=None):
+    """out[M,N] (=|+=) s0*s1 * a[M,K] . b[N,K]^T (+bias, act with the pre-activation to aux) for fp8 a (fmt_a 0
+    e4m3 / 1 e5m2) and e4m3 b (K-contiguous); zero_slot: an f32 the kernel clears (delayed-scaling amax slot)."""
     M, K = a.shape
     N = b.shape[0]
     ws = workspace(a.device) if splitk > 1 else None
-    call("dtf_gemm_fp8_ex", ptr(a), ptr(b), ptr(out), None, None, ptr(scales), M, N, K, a.stride(0), b.stride(0),
-         out.stride(0), 0, int(fmt_a), int(out_f32), float(beta), int(splitk), ptr(ws),
-         ws.numel() if ws is not None else 0, stream())
+    call("dtf_gemm_fp8_ex", ptr(a), ptr(b), ptr(out), ptr(aux), ptr(bias), ptr(scales), M, N, K, a.stride(0),
+         b.stride(0), out.stride(0), int(act), int(fmt_a), int(out_f32), float(beta), int(splitk), ptr(ws),
+         ws.numel() if ws is not None else 0, ptr(zero_slot), stream())
     return out
 
 
@@ -90,6 +97,8 @@ class _Fp8State:
         self.buf[W_SCALE] = 1.0
         self.x_ready = False
         self.g_ready = False
+        self.tx = 0  # forward / backward step counters: parity of the double-buffered amax slots
+        self.tg = 0
         self.wq = self.wqT = None
         self.w_key = None
 
@@ -138,18 +147,28 @@ class _DenseFP8(torch.autograd.Function):
         if not st.x_ready:  # bootstrap the delayed activation scale once
             buf[X_SCALE:X_SCALE + 1].copy_(x2.abs().amax().float().clamp_min(1e-12) / E4M3_MAX)
             st.x_ready = True
-        xs, xa = buf[X_SCALE:X_SCALE + 1], buf[X_AMAX:X_AMAX + 1]
-        if fbwd:
-            xq, xqT, _ = quantize_t(x2, xs, xa)
-        else:
-            xq, xqT = quantize(x2, xs, xa, zero_amax=False), None
-        wq, wqT = _weight_fp8(st, w, fbwd)
+        xs = buf[X_SCALE:X_SCALE + 1]
         y = torch.empty((M, N), dtype=BF16, device=x.device)
         pre = torch.empty((M, N), dtype=BF16, device=x.device) if act else None
-        call("dtf_gemm_fp8", ptr(xq), ptr(wq), ptr(y), ptr(pre), ptr(b), ptr(buf[X_SCALE:X_SCALE + 2]), M, N, K, K, K,
-             N, int(act), -1, stream())
-        # next step's x scale from this pass's amax; the scale this pass used is kept for the weight gradient
-        call("dtf_fp8_update_scale2", ptr(xa), ptr(xs), ptr(buf[X_USED:X_USED + 1]), E4M3_MAX, 0.0, stream())
+        if fbwd and not torch.cuda.is_current_stream_capturing():
+            # delayed scaling folded into the quantize pass (amax slots double-buffered by step parity)
+            cur, prev = (X_AMAX, X_AMAX2) if st.tx % 2 == 0 else (X_AMAX2, X_AMAX)
+            st.tx += 1
+            xq, xqT, _ = quantize_t(x2, xs, buf[cur:cur + 1], amax_prev=buf[prev:prev + 1], scale_used=xs,
+                                    scale_used2=buf[X_USED:X_USED + 1])
+            wq, wqT = _weight_fp8(st, w, True)
+            gemm_fp8(xq, wq, buf[X_SCALE:X_SCALE + 2], y, bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1])
+        else:
+            xa = buf[X_AMAX:X_AMAX + 1]
+            if fbwd:
+                xq, xqT, _ = quantize_t(x2, xs, xa)
+            else:
+                xq, xqT = quantize(x2, xs, xa, zero_amax=False), None
+            wq, wqT = _weight_fp8(st, w, fbwd)
+            call("dtf_gemm_fp8", ptr(xq), ptr(wq), ptr(y), ptr(pre), ptr(b), ptr(buf[X_SCALE:X_SCALE + 2]), M, N, K,
+                 K, K, N, int(act), -1, stream())
+            # next step's x scale from this pass's amax; the scale this pass used is kept for the weight gradient
+            call("dtf_fp8_update_scale2", ptr(xa), ptr(xs), ptr(buf[X_USED:X_USED + 1]), E4M3_MAX, 0.0, stream())
         ctx.fbwd = fbwd
         if fbwd:
             ctx.save_for_backward(xqT, w, pre)
@@ -177,13 +196,23 @@ class _DenseFP8(torch.autograd.Function):
             st.g_ready = True
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_db = ctx.has_b and ctx.needs_input_grad[2]
-        dzq, dzqT, cp = quantize_t(dy2, gs, ga, fmt=1, pre=pre if ctx.act else None, act=ctx.act, rowmajor=need_dx,
-                                   transposed=need_dw, colsums=need_db)
+        folded = need_dx and not torch.cuda.is_current_stream_capturing()
+        prev = None
+        if folded:  # delayed gradient scaling folded into the quantize pass (see forward)
+            cur, prev = (G_AMAX, G_AMAX2) if st.tg % 2 == 0 else (G_AMAX2, G_AMAX)
+            st.tg += 1
+            dzq, dzqT, cp = quantize_t(dy2, gs, buf[cur:cur + 1], fmt=1, pre=pre if ctx.act else None, act=ctx.act,
+                                       rowmajor=True, transposed=need_dw, colsums=need_db,
+                                       amax_prev=buf[prev:prev + 1], scale_used=gs)
+        else:
+            dzq, dzqT, cp = quantize_t(dy2, gs, ga, fmt=1, pre=pre if ctx.act else None, act=ctx.act,
+                                       rowmajor=need_dx, transposed=need_dw, colsums=need_db)
         dx = dw = db = None
         if need_dx:
             _, wqT = _weight_fp8(st, w, True)
             dx = torch.empty((M, K), dtype=BF16, device=dy.device)
-            gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1)  # scales (s_w, s_g)
+            gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1,  # scales (s_w, s_g)
+                     zero_slot=buf[prev:prev + 1] if folded else None)
             dx = dx.reshape(ctx.shp)
         tw = direct_grad(w) if need_dw else None
         tb = direct_grad(ctx.b_param) if need_db else None
@@ -201,9 +230,10 @@ class _DenseFP8(torch.autograd.Function):
                 out = tb if tb is not None else torch.empty(N, dtype=F32, device=dy.device)
                 call("dtf_reduce_rows", ptr(cp), N, cp.shape[0], N, ptr(out), int(tb is not None), stream())
                 db = None if tb is not None else out
-            # next step's gradient scale: on the stream of the last reader of this step's scale (the weight
-            # gradient), which was forked after the data gradient was issued
-            call("dtf_fp8_update_scale2", ptr(ga), ptr(gs), None, E5M2_MAX, 0.0, stream())
+            if not folded:
+                # next step's gradient scale: on the stream of the last reader of this step's scale (the weight
+                # gradient), which was forked after the data gradient was issued
+                call("dtf_fp8_update_scale2", ptr(ga), ptr(gs), None, E5M2_MAX, 0.0, stream())
         return dx, dw, db, None, None
 
     @staticmethod
