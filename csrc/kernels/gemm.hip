@@ -463,11 +463,38 @@ __global__ void tap_gather_kernel(const bf16_t* __restrict__ src, bf16_t* __rest
 // whose BN input is bnx [N,H,W,C] with 1-bit ReLU mask bnmask and batch mean bnmean): partial rows
 // [rows][2C] of sum(dz), sum(dz*(x-mean)) go to bnpart (capacity ceil(N*H*W/64) + sh*sw rows: a strided dgrad
 // writes one set per phase launch); *bnrows = rows.
+static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
+                           int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
+                           float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
+                           const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
+                           const void* bsrc2, void* stream);
+
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
                            void* stream) {
+  return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, out_f32, beta, tile, ws,
+                         ws_bf16, bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream);
+}
+
+// dtf_conv_dgrad of a stride-1 pointwise conv whose result also adds bsrc2: the compact [N, H/2, W/2, C] data
+// gradient of a stride-2 1x1 projection shortcut of the same input, at the even pixels (the shortcut's full-size
+// gradient, 3/4 zeros, is never written or read). H and W even.
+DTF_API int dtf_conv_dgrad_addsub2(const void* dY, const void* Wcrsk, void* dX, const void* bsrc2, int N, int H, int W,
+                                   int C, int K, int tile, void* ws, long ws_bf16, const void* bnx,
+                                   const void* bnmask, const float* bnmean, float* bnpart, int* bnrows,
+                                   void* stream) {
+  if ((H & 1) || (W & 1) || !bsrc2) return -11;
+  return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, 1, 1, H, W, 1, 1, 0, 0, 1, 1, 0, 1.f, tile, ws, ws_bf16, bnx,
+                         bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream);
+}
+
+static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
+                           int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
+                           float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
+                           const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
+                           const void* bsrc2, void* stream) {
   if ((C & 3) || (K & 7)) return -1;
   if (bnx && (out_f32 || (C & 7) || !bnpart || !bnmean || !bnrows)) return -9;
   if (betamask && (out_f32 || beta == 0.f || (C & 7) || sh > 1 || sw > 1)) return -10;
@@ -475,6 +502,13 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
   int prow = 0;  // BN partial rows written so far (strided dgrad: one set per phase)
   auto bn_args = [&](GemmArgs& a) {
     a.betamask = (const uint8_t*)betamask;
+    if (bsrc2) {
+      a.bsrc = (const bf16_t*)bsrc2;
+      a.dBhw = make_fastdiv((uint32_t)(H * W));
+      a.dBw = make_fastdiv((uint32_t)W);
+      a.bH2 = H / 2;
+      a.bW2 = W / 2;
+    }
     if (!bnx) return;
     a.stats = bnpart + (long)prow * 2 * C;
     a.bnx = (const bf16_t*)bnx;

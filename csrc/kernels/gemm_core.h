@@ -94,6 +94,12 @@ struct GemmArgs {
   const bf16_t* dact_src;
   int dact;
   float* zero_slot;  // optional: block 0 clears this f32 (fp8 delayed scaling: the amax slot the next step fills)
+  // optional beta source other than C, on a 2x-subsampled pixel grid (the compact data gradient of a stride-2 1x1
+  // projection shortcut): output row m = pixel (n, h, w) of an H x W image adds bsrc[(n, h/2, w/2)] when h and w
+  // are even, nothing otherwise (row stride ldc, same channels as C)
+  const bf16_t* bsrc;
+  FastDiv dBhw, dBw;
+  int bH2, bW2;
   int crm;
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
@@ -109,6 +115,16 @@ __device__ __forceinline__ long out_row(const GemmArgs& a, int m) {
 
 constexpr int BK = 64;
 constexpr int NT = 256;
+
+// Beta operand of output element (row m, column n): C itself, or the stride-2 compact source (nullptr: zero)
+__device__ __forceinline__ const bf16_t* beta_src(const GemmArgs& a, long m, int n, const bf16_t* cp) {
+  if (!a.bsrc) return cp;
+  uint32_t nn, hw, h, w;
+  fdivmod((uint32_t)m, a.dBhw, nn, hw);
+  fdivmod(hw, a.dBw, h, w);
+  if ((h | w) & 1u) return nullptr;
+  return a.bsrc + (((long)nn * a.bH2 + (h >> 1)) * a.bW2 + (w >> 1)) * a.ldc + n;
+}
 
 // Per-column statistics of 4 stored output values (columns n..n+3 of output pixel row mrow): forward BN
 // (sum, sum of squares) or, with a.bnx, backward BN (sum dz, sum dz*(x - mean)).
@@ -822,8 +838,9 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
       uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8t * 8);
       const long e = out_row(a, m) * a.ldc + n;
       bf16_t* cp = reinterpret_cast<bf16_t*>(a.C) + cbase + e;
-      if (a.beta != 0.f) {
-        const uint4 old = *reinterpret_cast<const uint4*>(cp);
+      const bf16_t* bp = a.beta != 0.f ? beta_src(a, out_row(a, m), n, cp) : nullptr;
+      if (bp) {
+        const uint4 old = *reinterpret_cast<const uint4*>(bp);
         float f[8], g[8];
         const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, ow[4] = {old.x, old.y, old.z, old.w};
 #pragma unroll
@@ -903,7 +920,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
           float4 o = *reinterpret_cast<const float4*>(reinterpret_cast<float*>(a.C) + off);
           v[0] += a.beta * o.x; v[1] += a.beta * o.y; v[2] += a.beta * o.z; v[3] += a.beta * o.w;
         } else {
-          uint2 o = *reinterpret_cast<const uint2*>(reinterpret_cast<bf16_t*>(a.C) + off);
+          const bf16_t* bp = beta_src(a, mrow, n, reinterpret_cast<bf16_t*>(a.C) + off);
+          uint2 o = bp ? *reinterpret_cast<const uint2*>(bp) : make_uint2(0, 0);
           if (a.betamask) {  // zero the old values whose ReLU bit is clear (see the staged path)
             const uint32_t bm = ((uint32_t)a.betamask[off >> 3] >> (off & 4)) & 0xFu;  // off % 4 == 0
             o.x &= ((bm & 1u) ? 0x0000ffffu : 0u) | ((bm & 2u) ? 0xffff0000u : 0u);

@@ -53,7 +53,7 @@ def conv_fwd_raw(x, w16, g, stats=False, bias=None, act=0):
     return y
 
 
-def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None):
+def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=None):
     """dX (bf16); with `acc` (a bf16 [N,H,W,C] gradient already holding another contribution) the epilogue
     adds into it (beta = 1) and returns it; `acc_mask` (1 bit per element) first zeroes the acc values whose
     bit is clear (a residual gradient whose ReLU mask was deferred). With `bn` (the _BNSource of the
@@ -69,11 +69,15 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None):
         # each of which may end in a partial tile
         part = torch.empty(((N * H * W + 63) // 64 + sh * sw) * 2 * C, dtype=F32, device=dy.device)
         rows = IntOut()
-    call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0,
-         0.0 if acc is None else 1.0, -1, ptr(ws), 2 * ws.numel(),
-         ptr(bn.yc) if bn is not None else None, ptr(bn.mbits) if bn is not None else None,
-         ptr(bn.mean) if bn is not None else None, ptr(part), rows.addr if rows else None,
-         ptr(acc_mask) if acc is not None else None, stream())
+    bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
+    if acc_sub2 is not None:  # + the compact gradient of a stride-2 1x1 shortcut at the even pixels
+        assert acc is None and (R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0)
+        call("dtf_conv_dgrad_addsub2", ptr(dy), ptr(wc), ptr(dx), ptr(acc_sub2), N, H, W, C, K, -1, ptr(ws),
+             2 * ws.numel(), *bn_ptrs, ptr(part), rows.addr if rows else None, stream())
+    else:
+        call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0,
+             0.0 if acc is None else 1.0, -1, ptr(ws), 2 * ws.numel(), *bn_ptrs, ptr(part),
+             rows.addr if rows else None, ptr(acc_mask) if acc is not None else None, stream())
     if bn is not None:
         bn.provide(dx, part, rows.value)
     return dx
@@ -150,29 +154,36 @@ class ResidualGradLink:
     gradient together with the ReLU mask instead of writing the masked residual gradient, and the first conv's
     epilogue applies the mask while adding (one activation-sized write saved per identity block; the parked
     tensor is overwritten in place, it has no other reader).
+
+    A stride-2 1x1 projection may park its data gradient COMPACT ([N, H/2, W/2, C], the only pixels it reaches):
+    the first conv's dgrad epilogue then adds it at the even pixels of its own full-size output, so the
+    projection's full-size gradient (3/4 zeros) is never cleared, written or read.
     """
-    __slots__ = ("buf", "mask", "closed")
+    __slots__ = ("buf", "mask", "closed", "compact")
 
     def __init__(self):
         self.buf = None
         self.mask = None
         self.closed = False
+        self.compact = False
 
-    def park(self, g, mask=None):
+    def park(self, g, mask=None, compact=False):
         """Shortcut side: returns what to hand autograd (None when parked)."""
         if self.closed or g is None:
+            assert not compact, "a compact gradient can only be parked on an open link"
             return g
-        self.buf, self.mask = g, mask
+        self.buf, self.mask, self.compact = g, mask, compact
         return None
 
     def take(self):
-        """First-conv side: (parked gradient to accumulate into, its deferred ReLU mask or None), or
-        (None, None); then the link closes."""
-        buf, mask = self.buf, self.mask
+        """First-conv side: (parked gradient to accumulate into, its deferred ReLU mask or None, compact flag), or
+        (None, None, False); then the link closes."""
+        buf, mask, compact = self.buf, self.mask, self.compact
         self.buf = self.mask = None
+        self.compact = False
         if buf is None:
             self.closed = True
-        return buf, mask
+        return buf, mask, compact
 
 
 class _BNSource:
@@ -206,6 +217,7 @@ class _BNSource:
 _FUSE_BN_BWD = __import__("os").environ.get("DTF_FUSE_BN_BWD", "1") != "0"
 _LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
 _DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
+_COMPACT_PROJ = __import__("os").environ.get("DTF_COMPACT_PROJ", "1") != "0"
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -322,14 +334,23 @@ class _ConvBNFn(torch.autograd.Function):
                 dw = None  # (autograd still runs the parameter's AccumulateGrad node with an undefined
                 #            gradient, so its post-accumulate hooks — gradient bucketing — fire as usual)
         if ctx.needs_input_grad[0]:
-            acc, acc_mask = link.take() if (link is not None and role == "acc") else (None, None)
+            acc, acc_mask, compact = link.take() if (link is not None and role == "acc") else (None, None, False)
             src = ctx.in_src
             complete = src is not None and role != "proj" and (
                 src.consumers == 1 or (role == "acc" and acc is not None and src.consumers == 2))
-            dx = conv_dgrad_raw(dyc, w, g, acc=acc, bn=src if complete else None, acc_mask=acc_mask)
+            N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw = g[:13]
+            if (role == "proj" and link is not None and not link.closed and _COMPACT_PROJ
+                    and (R, S, sh, sw, ph, pw) == (1, 1, 2, 2, 0, 0) and H == 2 * P and W == 2 * Q):
+                # stride-2 1x1 shortcut: its gradient only reaches the even pixels — a plain GEMM over dY rows
+                gc = (N, P, Q, C, K, 1, 1, P, Q, 1, 1, 0, 0, 1, 1)
+                dx = link.park(conv_dgrad_raw(dyc, w, gc), compact=True)
+            elif compact:
+                dx = conv_dgrad_raw(dyc, w, g, bn=src if complete else None, acc_sub2=acc)
+            else:
+                dx = conv_dgrad_raw(dyc, w, g, acc=acc, bn=src if complete else None, acc_mask=acc_mask)
+                if link is not None and role == "proj":
+                    dx = link.park(dx)
             ctx.in_src = None
-            if link is not None and role == "proj":
-                dx = link.park(dx)
         if direct_bn:
             dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
