@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--allreduce-dtype", default=None, choices=["f32", "bf16"],
                     help="gradient all-reduce payload type (default f32; bf16 halves the xGMI bytes)")
+    ap.add_argument("--zero", type=int, default=0,
+                    help="1: ZeRO-1 sharded optimizer update (reduce-scatter + 1/N update + all-gather of masters)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture the whole train step in a hipGraph (compile(jit_compile=True))")
     ap.add_argument("--hiprio", type=int, default=0,
@@ -111,9 +113,11 @@ def main():
 
     co = parallel.CommunicationOptions(wire_dtype=args.allreduce_dtype)
     if args.model == "bert_base":
-        strategy = parallel.MultiWorkerMirroredStrategy(communication_options=co, bucket_mb=args.bucket_mb)
+        strategy = parallel.MultiWorkerMirroredStrategy(communication_options=co, bucket_mb=args.bucket_mb,
+                                                        shard_optimizer=bool(args.zero))
     else:
-        strategy = parallel.MirroredStrategy(bucket_mb=args.bucket_mb, communication_options=co)
+        strategy = parallel.MirroredStrategy(bucket_mb=args.bucket_mb, communication_options=co,
+                                             shard_optimizer=bool(args.zero))
     rank = strategy.worker_index
     dev = strategy.device
     if args.hiprio:
@@ -180,7 +184,7 @@ def main():
             "config": dict(cfg, global_batch=global_batch, per_gpu_batch=args.batch, parallelism=f"dp{world}",
                            strategy=type(strategy).__name__ + " (1 process/GPU, RCCL)",
                            optimizer=type(model.optimizer).__name__, final_loss=round(loss, 4),
-                           allreduce_dtype=args.allreduce_dtype or "f32",
+                           allreduce_dtype=args.allreduce_dtype or "f32", zero1=bool(args.zero),
                            exposed_comm_ms_per_step=round(exposed_max, 3)),
         }
         print(json.dumps(out), flush=True)

@@ -148,6 +148,19 @@ class LearningRateScheduler(Callback):
         opt.learning_rate = float(lr)
 
 
+def _sync_sharded_state(model):
+    """Sharded (ZeRO-1) optimizer slots are current only on their owner: gather them before a save."""
+    s = getattr(model, "distribute_strategy", None)
+    if s is not None and hasattr(s, "sync_optimizer_state") and getattr(model, "optimizer", None) is not None:
+        s.sync_optimizer_state(model.optimizer)
+
+
+def _agree(model, flag):
+    """A wall-clock save trigger must fire on every replica together when the save is collective."""
+    s = getattr(model, "distribute_strategy", None)
+    return s.agree(flag) if s is not None and hasattr(s, "agree") else flag
+
+
 class ModelCheckpoint(Callback):
     """Save a tensor-bundle checkpoint every epoch, or every `save_freq` batches, or every `save_secs`
     seconds (the Supervisor's save_model_secs=60 of reference trainer/task.py:223)."""
@@ -169,6 +182,7 @@ class ModelCheckpoint(Callback):
         return self._mgr
 
     def _save(self):
+        _sync_sharded_state(self.model)  # collective under ZeRO-1: every replica reaches it
         if not getattr(self.model, "_is_chief", True):
             return
         p = self._manager().save(checkpoint_number=self.model.optimizer.host_iterations())
@@ -177,7 +191,7 @@ class ModelCheckpoint(Callback):
         self._last = time.time()
 
     def on_train_batch_end(self, batch, logs=None):
-        if self.save_secs is not None and time.time() - self._last >= self.save_secs:
+        if self.save_secs is not None and _agree(self.model, time.time() - self._last >= self.save_secs):
             self._save()
         elif isinstance(self.save_freq, int) and (batch + 1) % self.save_freq == 0:
             self._save()
@@ -216,6 +230,7 @@ class BackupAndRestore(Callback):
 
     def on_epoch_end(self, epoch, logs=None):
         self.model._ckpt_epoch.assign(epoch + 1)
+        _sync_sharded_state(self.model)
         if getattr(self.model, "_is_chief", True):
             self._manager().save(checkpoint_number=epoch + 1)
 

@@ -278,6 +278,55 @@ class Optimizer:
             self.iterations.add_(1)
         self._host_iter = t
 
+    def apply_segments(self, a, segments, reduce_sumsq=None):
+        """One update of the arena ranges this replica owns (ZeRO-1, parallel.collective.ShardedGradientBucketer):
+        ``segments`` = [(lo, hi, grad)] with ``grad`` the summed gradient of arena elements [lo, hi); masters,
+        slots and bf16 copies are updated in place over those ranges only, one fused launch per segment.
+        ``reduce_sumsq(t)`` sums a 1-element tensor over the replicas (global-norm clipping needs the norm of
+        the WHOLE gradient, of which each replica holds a part)."""
+        if self.kind == "lamb":
+            raise ValueError("LAMB's per-variable trust ratio cannot be applied to sharded optimizer state")
+        t = self.host_iterations() + 1
+        lr = self._effective_lr(t)
+        kw = self._kernel_kwargs()
+        specs = self.slot_specs()
+        s1 = a.slots[specs[0][0]] if len(specs) > 0 else None
+        s2 = a.slots[specs[1][0]] if len(specs) > 1 else None
+        sl = lambda s, lo, hi: None if s is None else s[lo:hi]  # noqa: E731
+        if a.device.type == "cuda":
+            hp = self._hp_tensor(a, lr)
+            ss = None
+            if self.global_clipnorm:
+                ss = getattr(a, "_sumsq", None)
+                if ss is None:
+                    ss = a._sumsq = torch.empty(1, dtype=torch.float32, device=a.device)
+                ss.zero_()
+                for _, _, g in segments:
+                    _sumsq(g, ss, zero=False)
+                if reduce_sumsq is not None:
+                    reduce_sumsq(ss)
+            for lo, hi, g in segments:
+                optim_apply(_KERNEL_KIND[self.kind], a.flat[lo:hi], g, sl(s1, lo, hi), sl(s2, lo, hi),
+                            sl(a.bf16, lo, hi), hp, zero_grad=True, sumsq=ss, **kw)
+            _util.bump_weights_epoch()
+        else:
+            gs = self._grad_scale / self.loss_scale
+            if self.global_clipnorm:
+                n2 = torch.zeros(1, dtype=torch.float64)
+                for _, _, g in segments:
+                    n2 += (g.double() ** 2).sum()
+                if reduce_sumsq is not None:
+                    reduce_sumsq(n2)
+                n = float(n2.sqrt()) * gs
+                if n > self.global_clipnorm:
+                    gs *= self.global_clipnorm / n
+            for lo, hi, g in segments:
+                _torch_update(_KERNEL_KIND[self.kind], a.flat[lo:hi], g, sl(s1, lo, hi), sl(s2, lo, hi), lr, gs, **kw)
+                g.zero_()
+        with torch.no_grad():
+            self.iterations.add_(1)
+        self._host_iter = t
+
     def graph_prepare(self):
         """Allocate (outside the capture: pinned allocation is not capturable) the fixed pinned
         scalar buffer and device hp tensor of every arena, and switch `_hp_tensor` to graph mode."""

@@ -194,6 +194,138 @@ class GradientBucketer:
         return v
 
 
+class ShardedGradientBucketer(GradientBucketer):
+    """ZeRO-1 data parallelism: the optimizer update is sharded across the replicas.
+
+    Same buckets, hooks and issue order as GradientBucketer, but each bucket is REDUCE-SCATTERED instead of
+    all-reduced: bucket [lo, hi) of length L is cut into ``world`` chunks of s = ceil(L / world) elements and
+    rank r receives the summed chunk r in a compact shard-gradient buffer. After backward every rank runs the
+    fused optimizer kernel over its own chunks only (1/world of the update's HBM traffic — for Adam that is
+    ~26 B/param of the step), then the updated f32 masters are ALL-GATHERED back bucket by bucket and the bf16
+    compute copies refreshed from them. The bytes on the xGMI links equal the all-reduce's (a ring all-reduce
+    IS a reduce-scatter + all-gather); the saving is the replicated optimizer work.
+
+    Optimizer slots keep their full-arena layout but only the owned chunks are current on each rank;
+    ``gather_slots()`` (a collective: every rank must call it) all-gathers them before a checkpoint is written.
+    LAMB's per-variable trust ratio does not decompose over chunks and is rejected.
+    SURVEY §2.6 "Reduce-scatter / all-gather (ZeRO-1, optional)".
+    """
+
+    def __init__(self, arena, group=None, bucket_mb=None, wire_dtype=None):
+        super().__init__(arena, group=group, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.shards = []   # per bucket: (chunk s, own_lo, own_hi, compact offset)
+        off = 0
+        for lo, hi in self.buckets:
+            s = -(-(hi - lo) // self.world)
+            own_lo = min(hi, lo + self.rank * s)
+            own_hi = min(hi, own_lo + s)
+            self.shards.append((s, own_lo, own_hi, off))
+            off += s
+        dev = arena.grad.device
+        self.sgrad = torch.zeros(off, dtype=torch.float32, device=dev)   # this rank's summed gradient chunks
+        wire_t = torch.bfloat16 if self.wire == "bf16" else torch.float32
+        # padded send images for buckets whose length is not a multiple of world (or bf16 wire), zero tails
+        self._send = {}
+        self._recv = {}
+        for b, (lo, hi) in enumerate(self.buckets):
+            s = self.shards[b][0]
+            if self.wire == "bf16" or (hi - lo) != s * self.world:
+                self._send[b] = torch.zeros(s * self.world, dtype=wire_t, device=dev)
+            if self.wire == "bf16":
+                self._recv[b] = torch.zeros(s, dtype=wire_t, device=dev)
+        self._gather = {}  # padded all-gather images (f32), allocated on first use
+
+    def _launch(self, b):
+        lo, hi = self.buckets[b]
+        s, _, _, c = self.shards[b]
+        import contextlib
+        ctx = contextlib.nullcontext()
+        g = self.arena.grad[lo:hi]
+        if g.is_cuda:
+            from ..ops._util import comm_stream_ctx
+            ctx = comm_stream_ctx(g.device)
+        with ctx:
+            inp = g
+            if b in self._send:
+                inp = self._send[b]
+                if self.wire == "bf16":
+                    _cast(g, inp[:hi - lo])
+                else:
+                    inp[:hi - lo].copy_(g)
+            out = self._recv.get(b, self.sgrad[c:c + s])
+            self._works[b] = dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group,
+                                                        async_op=True)
+
+    def finalize(self):
+        if self.arena.grad.is_cuda:
+            from ..ops._util import join_side_streams
+            join_side_streams()
+        while self._next < len(self.buckets):
+            self._launch(self._next)
+            self._next += 1
+        ev0 = None
+        if self.timing and self.arena.grad.is_cuda:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        for w in self._works:
+            if w is not None:
+                w.wait()
+        for b, r in self._recv.items():
+            s, _, _, c = self.shards[b]
+            _cast(r, self.sgrad[c:c + s])
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._timed.append((ev0, ev1))
+        # the replicated gradient arena has been consumed (the update reads the compact chunks): clear it for
+        # the next backward's accumulation
+        self.arena.grad.zero_()
+        self.reset()
+
+    def segments(self):
+        """(own_lo, own_hi, compact gradient view) of every bucket this rank updates."""
+        out = []
+        for s, lo, hi, c in self.shards:
+            if hi > lo:
+                out.append((lo, hi, self.sgrad[c:c + hi - lo]))
+        return out
+
+    def _all_gather_(self, buf):
+        """In-place all-gather of this rank's chunks of ``buf`` (an arena-shaped f32 buffer), bucket by bucket."""
+        works = []
+        for b, (lo, hi) in enumerate(self.buckets):
+            s, own_lo, own_hi, _ = self.shards[b]
+            if (hi - lo) == s * self.world:
+                # NCCL/RCCL in-place form: the input is the rank's own slice of the output
+                works.append((None, dist.all_gather_into_tensor(buf[lo:hi], buf[own_lo:own_lo + s],
+                                                                group=self.group, async_op=True)))
+            else:
+                img = self._gather.get(b)
+                if img is None:
+                    img = self._gather[b] = torch.zeros(s * self.world, dtype=buf.dtype, device=buf.device)
+                mine = torch.zeros(s, dtype=buf.dtype, device=buf.device)
+                mine[:own_hi - own_lo].copy_(buf[own_lo:own_hi])
+                works.append((b, dist.all_gather_into_tensor(img, mine, group=self.group, async_op=True)))
+        for b, w in works:
+            w.wait()
+            if b is not None:
+                lo, hi = self.buckets[b]
+                buf[lo:hi].copy_(self._gather[b][:hi - lo])
+
+    def gather_params(self):
+        """All-gather the updated f32 masters and refresh the bf16 compute copies."""
+        self._all_gather_(self.arena.flat)
+        if self.arena.bf16 is not None:
+            _cast(self.arena.flat, self.arena.bf16)
+
+    def gather_slots(self, optimizer):
+        """Make every optimizer slot current on every rank (collective; call on all ranks before a save)."""
+        for nm, _ in optimizer.slot_specs():
+            self._all_gather_(self.arena.slots[nm])
+
+
 def _cast(src, dst):
     """f32 <-> bf16 conversion of one bucket (HIP cast kernels on GPU)."""
     if src.is_cuda:

@@ -178,8 +178,14 @@ class CommunicationOptions:
 class MultiWorkerMirroredStrategy(Strategy):
     """Synchronous collective all-reduce data parallelism, one process per device."""
 
-    def __init__(self, cluster_resolver=None, communication_options=None, bucket_mb=None):
+    shard_optimizer = False
+
+    def __init__(self, cluster_resolver=None, communication_options=None, bucket_mb=None, shard_optimizer=None):
         super().__init__()
+        # ZeRO-1 (collective.ShardedGradientBucketer): reduce-scatter gradients, update 1/N of the arena per
+        # replica, all-gather the masters; DTF_ZERO=1 turns it on without code changes
+        self.shard_optimizer = bool(int(os.environ.get("DTF_ZERO", "0"))) if shard_optimizer is None \
+            else bool(shard_optimizer)
         co = communication_options
         if bucket_mb is None and co is not None and co.bytes_per_pack:
             bucket_mb = co.bytes_per_pack / float(1 << 20)
@@ -244,7 +250,10 @@ class MultiWorkerMirroredStrategy(Strategy):
         arena.refresh_bf16()
         from ..ops._util import bump_weights_epoch
         bump_weights_epoch()
-        if arena.grad.device.type == "cpu" and os.environ.get("DTF_CPU_ALLREDUCE", "shm") == "shm":
+        if self.shard_optimizer:
+            b = collective.ShardedGradientBucketer(arena, bucket_mb=self.bucket_mb,
+                                                   wire_dtype=getattr(self, "wire_dtype", None)).install()
+        elif arena.grad.device.type == "cpu" and os.environ.get("DTF_CPU_ALLREDUCE", "shm") == "shm":
             # one node, CPU arenas: shared-memory reduce-scatter/all-gather instead of gloo TCP
             name = f"ar{os.environ.get('MASTER_PORT', '0')}_{len(self._bucketers)}"
             if dist.get_rank() == 0:
@@ -266,6 +275,29 @@ class MultiWorkerMirroredStrategy(Strategy):
 
     def grad_scale(self):
         return 1.0 / self._world
+
+    def apply_gradients(self, optimizer, arena):
+        b = self._bucketers.get(id(arena))
+        if not isinstance(b, collective.ShardedGradientBucketer):
+            return super().apply_gradients(optimizer, arena)
+        optimizer.set_grad_scale(self.grad_scale())
+        optimizer.apply_segments(arena, b.segments(), reduce_sumsq=lambda t: dist.all_reduce(t))
+        b.gather_params()
+
+    def sync_optimizer_state(self, optimizer):
+        """Collective (every replica calls it): make sharded optimizer slots whole on every replica before a
+        checkpoint is written. A no-op unless the optimizer state is sharded (ZeRO-1)."""
+        for b in self._bucketers.values():
+            if isinstance(b, collective.ShardedGradientBucketer):
+                b.gather_slots(optimizer)
+
+    def agree(self, flag):
+        """Rank 0's decision (e.g. a time-based checkpoint trigger) on every replica."""
+        if self._world <= 1 or not self.shard_optimizer:
+            return flag
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=self._device)
+        dist.broadcast(t, src=0)
+        return bool(t.item())
 
     def local_batch_slice(self, n):
         per = n // self._world
@@ -298,7 +330,8 @@ class MirroredStrategy(MultiWorkerMirroredStrategy):
     ``python -m distributed_tensorflow_amd.cli.launch --gpus N ...`` or ``torchrun --nproc-per-node N``; the
     same ``MirroredStrategy()`` then finds its replica through the launcher's environment."""
 
-    def __init__(self, devices=None, cross_device_ops=None, bucket_mb=None, communication_options=None):
+    def __init__(self, devices=None, cross_device_ops=None, bucket_mb=None, communication_options=None,
+                 shard_optimizer=None):
         self._devices = [context.parse_device(d) for d in devices] if devices else None
         self.wire_dtype = getattr(communication_options, "wire_dtype", None)
         gpus = {d for d in (self._devices or []) if d.type == "cuda"}
@@ -324,9 +357,11 @@ class MirroredStrategy(MultiWorkerMirroredStrategy):
             self.cluster_resolver = None
             return
         if TorchrunClusterResolver.active():
-            super().__init__(TorchrunClusterResolver(), communication_options, bucket_mb=bucket_mb)
+            super().__init__(TorchrunClusterResolver(), communication_options, bucket_mb=bucket_mb,
+                             shard_optimizer=shard_optimizer)
         else:
-            super().__init__(TFConfigClusterResolver(tf_config={}), communication_options, bucket_mb=bucket_mb)
+            super().__init__(TFConfigClusterResolver(tf_config={}), communication_options, bucket_mb=bucket_mb,
+                             shard_optimizer=shard_optimizer)
 
     @property
     def extended_devices(self):

@@ -38,15 +38,21 @@ def _train_mlp(strategy, x, y, epochs=2, batch=64, seed=0):
 def _mwms_worker(rank, world, port, mode, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), DTF_CPU_ALLREDUCE=mode.split("_")[0], HIP_VISIBLE_DEVICES="",
-                      CUDA_VISIBLE_DEVICES="", DTF_ALLREDUCE_DTYPE="bf16" if mode.endswith("bf16") else "f32")
+                      CUDA_VISIBLE_DEVICES="", DTF_ALLREDUCE_DTYPE="bf16" if mode.endswith("bf16") else "f32",
+                      DTF_ZERO="1" if "zero" in mode else "0", DTF_BUCKET_MB="0.004" if "zero" in mode else "32")
     try:
         from distributed_tensorflow_amd import parallel
         from distributed_tensorflow_amd.models.mlp import synthetic_mnist
-        x, y = synthetic_mnist(512)
+        n, batch = (576, 96) if world == 3 else (512, 64)
+        x, y = synthetic_mnist(n)
         s = parallel.MultiWorkerMirroredStrategy()
         # every rank starts from its own random init: rank 0's must be broadcast before the first step
-        m, h = _train_mlp(s, torch.as_tensor(x), torch.as_tensor(y), seed=rank)
-        q.put((rank, [w.detach().numpy().copy() for w in m.weights], h.history["loss"]))
+        m, h = _train_mlp(s, torch.as_tensor(x), torch.as_tensor(y), seed=rank, batch=batch)
+        from distributed_tensorflow_amd.parallel.collective import ShardedGradientBucketer
+        assert ("zero" in mode) == any(isinstance(b, ShardedGradientBucketer) for b in s._bucketers.values())
+        s.sync_optimizer_state(m.optimizer)  # ZeRO-1: make every replica's slots whole (no-op otherwise)
+        slots = [m.optimizer.get_slot(v, "Momentum").detach().numpy().copy() for v in m.trainable_variables]
+        q.put((rank, [w.detach().numpy().copy() for w in m.weights] + slots, h.history["loss"]))
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
@@ -55,30 +61,38 @@ def _mwms_worker(rank, world, port, mode, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("mode", ["shm", "gloo", "gloo_bf16"])
-def test_multi_worker_mirrored_matches_single_process(mode):
+@pytest.mark.parametrize("mode,world", [("shm", 2), ("gloo", 2), ("gloo_bf16", 2), ("gloo_zero", 2),
+                                        ("gloo_zero", 3), ("gloo_zero_bf16", 2)])
+def test_multi_worker_mirrored_matches_single_process(mode, world):
     """gloo_bf16: the gradient buckets travel as bf16 (half the all-reduce bytes) and are accumulated back into
-    the f32 arena; the replicas still agree exactly and track f32 training within bf16 rounding."""
+    the f32 arena; the replicas still agree exactly and track f32 training within bf16 rounding.
+    gloo_zero: ZeRO-1 (reduce-scatter, 1/N optimizer update per replica, all-gather of the masters; tiny
+    buckets so every variable boundary case is hit; world 3 exercises the padded, non-divisible chunks) —
+    weights AND the gathered momentum slots equal single-process training."""
     from distributed_tensorflow_amd import parallel
     from distributed_tensorflow_amd.models.mlp import synthetic_mnist
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_mwms_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    ps = [ctx.Process(target=_mwms_worker, args=(r, world, port, mode, q)) for r in range(world)]
     [p.start() for p in ps]
-    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda t: t[0])
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
     [p.join(60) for p in ps]
     for r in res:
         assert r[1] is not None, r[2]
-    # both replicas hold identical weights
-    for a, b in zip(res[0][1], res[1][1]):
-        np.testing.assert_allclose(a, b, rtol=0, atol=0)
+    # all replicas hold identical weights (and slots)
+    for other in res[1:]:
+        for a, b in zip(res[0][1], other[1]):
+            np.testing.assert_allclose(a, b, rtol=0, atol=0)
     # and equal single-process training on the same global batches
-    x, y = synthetic_mnist(512)
-    m, h = _train_mlp(parallel.OneDeviceStrategy("cpu"), torch.as_tensor(x), torch.as_tensor(y))
+    n, batch = (576, 96) if world == 3 else (512, 64)
+    x, y = synthetic_mnist(n)
+    m, h = _train_mlp(parallel.OneDeviceStrategy("cpu"), torch.as_tensor(x), torch.as_tensor(y), batch=batch)
     tol = dict(rtol=2e-2, atol=2e-3) if mode.endswith("bf16") else dict(rtol=1e-4, atol=1e-5)
-    for a, w in zip(res[0][1], m.weights):
-        np.testing.assert_allclose(a, w.detach().numpy(), **tol)
+    ref = [w.detach().numpy() for w in m.weights] + [m.optimizer.get_slot(v, "Momentum").detach().numpy()
+                                                     for v in m.trainable_variables]
+    for a, w in zip(res[0][1], ref):
+        np.testing.assert_allclose(a, w, **tol)
     assert res[0][2][-1] < res[0][2][0]
 
 
