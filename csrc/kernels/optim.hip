@@ -44,55 +44,62 @@ struct OptArgs {
   const float* sumsq;
 };
 
+template <int KIND>
 __device__ __forceinline__ void upd1(const OptArgs& a, float lr, float gs, float& p, float g, float& s1,
                                      float& s2) {
   g *= gs;
-  switch (a.kind) {
-    case OPT_SGD:
-      if (a.wd != 0.f) g += a.wd * p;
-      if (a.mom != 0.f) {
-        s1 = a.mom * s1 + g;
-        p -= lr * (a.nesterov ? g + a.mom * s1 : s1);
-      } else {
-        p -= lr * g;
-      }
-      break;
-    case OPT_ADAM:
-    case OPT_LAMB:
-      s1 = a.b1 * s1 + (1.f - a.b1) * g;
-      s2 = a.b2 * s2 + (1.f - a.b2) * g * g;
-      p -= lr * (s1 / (sqrtf(s2) + a.eps) + a.wd * p);
-      break;
-    case OPT_ADAGRAD:
-      s1 += g * g;
-      p -= lr * g / (sqrtf(s1) + a.eps);
-      break;
-    case OPT_ADADELTA: {
-      s1 = a.b1 * s1 + (1.f - a.b1) * g * g;                 // accum
-      float d = sqrtf(s2 + a.eps) / sqrtf(s1 + a.eps) * g;  // update
-      s2 = a.b1 * s2 + (1.f - a.b1) * d * d;                 // accum_update
-      p -= lr * d;
-      break;
+  if constexpr (KIND == OPT_SGD) {
+    if (a.wd != 0.f) g += a.wd * p;
+    if (a.mom != 0.f) {
+      s1 = a.mom * s1 + g;
+      p -= lr * (a.nesterov ? g + a.mom * s1 : s1);
+    } else {
+      p -= lr * g;
     }
-    case OPT_FTRL: {
-      // s1 = accumulator n, s2 = linear z
-      float n_new = s1 + g * g;
-      float sigma = (sqrtf(n_new) - sqrtf(s1)) / lr;
-      s2 += g - sigma * p;
-      s1 = n_new;
-      float quad = sqrtf(n_new) / lr + 2.f * a.l2;
-      p = fabsf(s2) > a.l1 ? (copysignf(a.l1, s2) - s2) / quad : 0.f;
-      break;
-    }
-    case OPT_RMSPROP:
-      s1 = a.b1 * s1 + (1.f - a.b1) * g * g;
-      s2 = a.mom * s2 + lr * g / sqrtf(s1 + a.eps);
-      p -= s2;
-      break;
+  } else if constexpr (KIND == OPT_ADAM || KIND == OPT_LAMB) {
+    s1 = a.b1 * s1 + (1.f - a.b1) * g;
+    s2 = a.b2 * s2 + (1.f - a.b2) * g * g;
+    p -= lr * (s1 / (sqrtf(s2) + a.eps) + a.wd * p);
+  } else if constexpr (KIND == OPT_ADAGRAD) {
+    s1 += g * g;
+    p -= lr * g / (sqrtf(s1) + a.eps);
+  } else if constexpr (KIND == OPT_ADADELTA) {
+    s1 = a.b1 * s1 + (1.f - a.b1) * g * g;                 // accum
+    float d = sqrtf(s2 + a.eps) / sqrtf(s1 + a.eps) * g;  // update
+    s2 = a.b1 * s2 + (1.f - a.b1) * d * d;                 // accum_update
+    p -= lr * d;
+  } else if constexpr (KIND == OPT_FTRL) {
+    // s1 = accumulator n, s2 = linear z
+    float n_new = s1 + g * g;
+    float sigma = (sqrtf(n_new) - sqrtf(s1)) / lr;
+    s2 += g - sigma * p;
+    s1 = n_new;
+    float quad = sqrtf(n_new) / lr + 2.f * a.l2;
+    p = fabsf(s2) > a.l1 ? (copysignf(a.l1, s2) - s2) / quad : 0.f;
+  } else {  // OPT_RMSPROP
+    s1 = a.b1 * s1 + (1.f - a.b1) * g * g;
+    s2 = a.mom * s2 + lr * g / sqrtf(s1 + a.eps);
+    p -= s2;
   }
 }
 
+// streaming loads/stores: every byte of the arenas is touched exactly once per step, so keep them out of the
+// L2/MALL working set of the kernels around the update
+typedef float nt4f __attribute__((ext_vector_type(4)));
+typedef unsigned int nt2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ld_nt(const float* p, long i) {
+  const nt4f v = __builtin_nontemporal_load(reinterpret_cast<const nt4f*>(p) + i);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float* p, long i, float4 v) {
+  __builtin_nontemporal_store((nt4f){v.x, v.y, v.z, v.w}, reinterpret_cast<nt4f*>(p) + i);
+}
+
+// U float4 groups per thread per trip, all loads issued before any math (4-5 streams x U x 16 B in flight per
+// lane); the kernel kind and the slot count are template parameters so the loop body is branch-free
+template <int KIND, int NS>
 __global__ void __launch_bounds__(256) optim_kernel(OptArgs a) {
+  constexpr int U = 2;
   const float lr = a.hp[0];
   float gs = a.hp[1];
   if (a.sumsq && a.hp[2] > 0.f) {
@@ -100,38 +107,56 @@ __global__ void __launch_bounds__(256) optim_kernel(OptArgs a) {
     if (nrm > a.hp[2]) gs *= a.hp[2] / nrm;
   }
   const long n4 = a.n / 4;
-  const bool has1 = a.s1 != nullptr, has2 = a.s2 != nullptr;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 p = reinterpret_cast<float4*>(a.p)[i];
-    float4 g = reinterpret_cast<float4*>(a.g)[i];
-    float4 s1 = has1 ? reinterpret_cast<float4*>(a.s1)[i] : make_float4(0, 0, 0, 0);
-    float4 s2 = has2 ? reinterpret_cast<float4*>(a.s2)[i] : make_float4(0, 0, 0, 0);
-    upd1(a, lr, gs, p.x, g.x, s1.x, s2.x);
-    upd1(a, lr, gs, p.y, g.y, s1.y, s2.y);
-    upd1(a, lr, gs, p.z, g.z, s1.z, s2.z);
-    upd1(a, lr, gs, p.w, g.w, s1.w, s2.w);
-    reinterpret_cast<float4*>(a.p)[i] = p;
-    if (has1) reinterpret_cast<float4*>(a.s1)[i] = s1;
-    if (has2) reinterpret_cast<float4*>(a.s2)[i] = s2;
-    if (a.zero_grad) reinterpret_cast<float4*>(a.g)[i] = make_float4(0, 0, 0, 0);
-    if (a.p16) {
-      uint2 o;
-      o.x = pack2bf(p.x, p.y);
-      o.y = pack2bf(p.z, p.w);
-      reinterpret_cast<uint2*>(a.p16)[i] = o;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += U * stride) {
+    float4 p[U], g[U], s1[U], s2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + u * stride;
+      if (i < n4) {
+        p[u] = ld_nt(a.p, i);
+        g[u] = ld_nt(a.g, i);
+        s1[u] = NS > 0 ? ld_nt(a.s1, i) : make_float4(0, 0, 0, 0);
+        s2[u] = NS > 1 ? ld_nt(a.s2, i) : make_float4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n4) break;
+      upd1<KIND>(a, lr, gs, p[u].x, g[u].x, s1[u].x, s2[u].x);
+      upd1<KIND>(a, lr, gs, p[u].y, g[u].y, s1[u].y, s2[u].y);
+      upd1<KIND>(a, lr, gs, p[u].z, g[u].z, s1[u].z, s2[u].z);
+      upd1<KIND>(a, lr, gs, p[u].w, g[u].w, s1[u].w, s2[u].w);
+      st_nt(a.p, i, p[u]);
+      if (NS > 0) st_nt(a.s1, i, s1[u]);
+      if (NS > 1) st_nt(a.s2, i, s2[u]);
+      if (a.zero_grad) st_nt(a.g, i, make_float4(0, 0, 0, 0));
+      if (a.p16) {
+        __builtin_nontemporal_store((nt2u){pack2bf(p[u].x, p[u].y), pack2bf(p[u].z, p[u].w)},
+                                    reinterpret_cast<nt2u*>(a.p16) + i);
+      }
     }
   }
   // tail
   if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
     long i = n4 * 4 + threadIdx.x;
-    float p = a.p[i], g = a.g[i], s1 = has1 ? a.s1[i] : 0.f, s2 = has2 ? a.s2[i] : 0.f;
-    upd1(a, lr, gs, p, g, s1, s2);
+    float p = a.p[i], g = a.g[i], s1 = NS > 0 ? a.s1[i] : 0.f, s2 = NS > 1 ? a.s2[i] : 0.f;
+    upd1<KIND>(a, lr, gs, p, g, s1, s2);
     a.p[i] = p;
-    if (has1) a.s1[i] = s1;
-    if (has2) a.s2[i] = s2;
+    if (NS > 0) a.s1[i] = s1;
+    if (NS > 1) a.s2[i] = s2;
     if (a.zero_grad) a.g[i] = 0.f;
     if (a.p16) a.p16[i] = f2bf(p);
   }
+}
+
+template <int KIND>
+void launch_optim(const OptArgs& a, hipStream_t st) {
+  const dim3 grid(stream_grid(a.n / 8 + 1, 256)), block(256);
+  if (a.s2) hipLaunchKernelGGL((optim_kernel<KIND, 2>), grid, block, 0, st, a);
+  else if (a.s1) hipLaunchKernelGGL((optim_kernel<KIND, 1>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((optim_kernel<KIND, 0>), grid, block, 0, st, a);
 }
 
 __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ x, long n, float* __restrict__ out) {
@@ -177,7 +202,16 @@ DTF_API int dtf_optim_apply(int kind, float* p, float* g, float* s1, float* s2, 
   a.p = p; a.g = g; a.s1 = s1; a.s2 = s2; a.p16 = (bf16_t*)p16; a.n = n; a.kind = kind;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.mom = mom; a.l1 = l1; a.l2 = l2;
   a.nesterov = nesterov; a.zero_grad = zero_grad; a.hp = hp; a.sumsq = sumsq;
-  hipLaunchKernelGGL(optim_kernel, dim3(stream_grid(n / 4 + 1, 256)), dim3(256), 0, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  switch (kind) {
+    case OPT_SGD: launch_optim<OPT_SGD>(a, st); break;
+    case OPT_ADAM: case OPT_LAMB: launch_optim<OPT_ADAM>(a, st); break;
+    case OPT_ADAGRAD: launch_optim<OPT_ADAGRAD>(a, st); break;
+    case OPT_ADADELTA: launch_optim<OPT_ADADELTA>(a, st); break;
+    case OPT_FTRL: launch_optim<OPT_FTRL>(a, st); break;
+    case OPT_RMSPROP: launch_optim<OPT_RMSPROP>(a, st); break;
+    default: return -1;
+  }
   return (int)hipGetLastError();
 }
 

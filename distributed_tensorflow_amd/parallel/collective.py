@@ -219,6 +219,7 @@ class ShardedGradientBucketer(GradientBucketer):
         off = 0
         for lo, hi in self.buckets:
             s = -(-(hi - lo) // self.world)
+            s = -(-s // 16) * 16  # 64-B aligned chunks: the fused update runs 16-B vector loads on every segment
             own_lo = min(hi, lo + self.rank * s)
             own_hi = min(hi, own_lo + s)
             self.shards.append((s, own_lo, own_hi, off))

@@ -126,7 +126,7 @@ def test_two_rank_resnet_replicas_stay_identical(cuda):
     assert all(x == x for x in res[0][2])
 
 
-def _worker_rccl1(port, jit, wire, q):
+def _worker_rccl1(port, jit, wire, q, zero=False):
     """One replica on the REAL RCCL backend (world size 1, DTF_FORCE_COLLECTIVE): process group, bucketed
     all-reduces from post-accumulate hooks, optionally the bf16 wire and hipGraph capture of the whole step."""
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
@@ -137,7 +137,7 @@ def _worker_rccl1(port, jit, wire, q):
         from distributed_tensorflow_amd import parallel
         s = parallel.MultiWorkerMirroredStrategy(bucket_mb=0.25,
                                                  communication_options=parallel.CommunicationOptions(
-                                                     wire_dtype=wire))
+                                                     wire_dtype=wire), shard_optimizer=zero)
         assert dist.get_backend() == "nccl"
         with s.scope():
             m = _gpt2(100)
@@ -153,11 +153,14 @@ def _worker_rccl1(port, jit, wire, q):
         q.put((None, None, traceback.format_exc(), 0))
 
 
-@pytest.mark.parametrize("jit,wire", [(False, "f32"), (True, "f32"), (False, "bf16")])
-def test_rccl_bucketer_world1_matches_single_process(cuda, jit, wire):
+@pytest.mark.parametrize("jit,wire,zero", [(False, "f32", False), (True, "f32", False), (False, "bf16", False),
+                                           (False, "f32", True)])
+def test_rccl_bucketer_world1_matches_single_process(cuda, jit, wire, zero):
+    """zero=True: ZeRO-1 on RCCL (reduce_scatter_tensor into the compact shard gradient, segment-wise fused
+    AdamW, in-place all_gather_into_tensor of the masters, bf16 refresh)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker_rccl1, args=(_port(), jit, wire, q))
+    p = ctx.Process(target=_worker_rccl1, args=(_port(), jit, wire, q, zero))
     p.start()
     try:
         kind, ws, losses, nb = q.get(timeout=100)
