@@ -180,7 +180,8 @@ class Model(Layer):
             loss = self.compute_loss(x, y, y_pred, sw)
         arena = self._ensure_arena()
         with prof.phase("backward"), direct_grads():  # includes the overlapped bucket all-reduces
-            strat.backward(loss, arena)
+            # a hipGraph-captured step (and its eager warmups) keeps the single update after backward
+            strat.backward(loss, arena, optimizer=None if getattr(self, "_graph_step", False) else self.optimizer)
             join_side_streams()  # weight gradients issued on the side stream are in the arena
         with prof.phase("optimizer"):
             strat.apply_gradients(self.optimizer, arena)
@@ -201,6 +202,7 @@ class Model(Layer):
                 not multi or os.environ.get("DTF_GRAPH_DIST", "0") == "1"):
             from ..graphs import CapturedStep
             fn = CapturedStep(self.train_step, warmup=2, optimizers=[self.optimizer])
+        self._graph_step = fn is not self.train_step
         self._train_fn = fn
         return fn
 

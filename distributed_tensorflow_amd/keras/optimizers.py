@@ -278,6 +278,43 @@ class Optimizer:
             self.iterations.add_(1)
         self._host_iter = t
 
+    # ---- bucket-by-bucket update during backward (collective.GradientBucketer with an optimizer attached)
+    def supports_ranges(self):
+        """Elementwise update rules only: global-norm clipping needs the whole gradient first."""
+        return not self.global_clipnorm and self.kind in _KERNEL_KIND
+
+    def begin_step(self, a):
+        """Fix this step's scalars (lr, grad scale) before the first range update; the device scalar buffer is
+        filled once (in graph mode its ring row is selected once) on the current stream."""
+        t = self.host_iterations() + 1
+        lr = self._effective_lr(t)
+        hp = self._hp_tensor(a, lr) if a.device.type == "cuda" else None
+        self._range_step = (t, lr, hp)
+
+    def apply_range(self, a, lo, hi):
+        """Update arena elements [lo, hi) (whole variables) and zero their gradients."""
+        t, lr, hp = self._range_step
+        kw = self._kernel_kwargs()
+        specs = self.slot_specs()
+        s1 = a.slots[specs[0][0]][lo:hi] if len(specs) > 0 else None
+        s2 = a.slots[specs[1][0]][lo:hi] if len(specs) > 1 else None
+        if a.device.type == "cuda":
+            optim_apply(_KERNEL_KIND[self.kind], a.flat[lo:hi], a.grad[lo:hi], s1, s2,
+                        None if a.bf16 is None else a.bf16[lo:hi], hp, zero_grad=True, **kw)
+        else:
+            _torch_update(_KERNEL_KIND[self.kind], a.flat[lo:hi], a.grad[lo:hi], s1, s2, lr,
+                          self._grad_scale / self.loss_scale, **kw)
+            a.grad[lo:hi].zero_()
+
+    def end_step(self, a):
+        t = self._range_step[0]
+        self._range_step = None
+        if a.device.type == "cuda":
+            _util.bump_weights_epoch()
+        with torch.no_grad():
+            self.iterations.add_(1)
+        self._host_iter = t
+
     def apply_segments(self, a, segments, reduce_sumsq=None):
         """One update of the arena ranges this replica owns (ZeRO-1, parallel.collective.ShardedGradientBucketer):
         ``segments`` = [(lo, hi, grad)] with ``grad`` the summed gradient of arena elements [lo, hi); masters,

@@ -88,6 +88,29 @@ def comm_stream_ctx(device):
     return torch.cuda.stream(side)
 
 
+_UPD = {}
+
+
+def update_stream_ctx(device, extra_wait=None):
+    """Stream for the per-bucket optimizer updates issued during backward (collective.GradientBucketer with an
+    optimizer attached): it waits for the main stream and the weight-gradient side stream as they are now (so
+    the bucket's gradients are complete and every kernel that reads the bucket's weights was issued before
+    it), and neither of them ever waits for it until the step ends (join_update_stream)."""
+    u = _UPD.get(device.index)
+    if u is None:
+        u = _UPD[device.index] = torch.cuda.Stream(device=device)
+    u.wait_stream(torch.cuda.current_stream(device))
+    if device.index in _SIDE_USED:
+        u.wait_stream(_SIDE[device.index])
+    return torch.cuda.stream(u)
+
+
+def join_update_stream(device):
+    u = _UPD.get(device.index)
+    if u is not None:
+        torch.cuda.current_stream(device).wait_stream(u)
+
+
 def join_side_streams():
     """Main stream waits for every side-stream weight gradient issued so far."""
     if not _SIDE_USED:

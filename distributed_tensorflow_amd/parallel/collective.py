@@ -64,9 +64,13 @@ def world():
 class GradientBucketer:
     """Bucketed, backward-overlapped SUM all-reduce of a ParamArena's gradient buffer."""
 
-    def __init__(self, arena, group=None, bucket_mb=None, average=False, wire_dtype=None):
+    def __init__(self, arena, group=None, bucket_mb=None, average=False, wire_dtype=None, collective=True):
         self.arena = arena
         self.group = group
+        # collective=False: no all-reduce (one replica) — the bucketer only drives the per-bucket optimizer update
+        self.collective = collective
+        self._opt = None        # optimizer whose update runs bucket by bucket during backward (begin_step)
+        self.updated = False
         self.average = average
         self.wire = (wire_dtype or _DEFAULT_WIRE).lower()
         if self.wire not in ("f32", "bf16"):
@@ -139,6 +143,15 @@ class GradientBucketer:
             self._launch(self._next)
             self._next += 1
 
+    def begin_step(self, optimizer, grad_scale):
+        """Overlap the optimizer with backward: every bucket is updated (masters, slots, bf16 copies, gradient
+        zeroing: one fused launch over the bucket's arena range) as soon as its gradients are final — right after
+        its all-reduce, or when its last gradient lands with one replica — on a stream of its own, while backward
+        continues. The update of the last buckets is all that remains after backward (SURVEY §2.6 overlap)."""
+        optimizer.set_grad_scale(grad_scale)
+        optimizer.begin_step(self.arena)
+        self._opt = optimizer
+
     def _launch(self, b):
         lo, hi = self.buckets[b]
         t = self.arena.grad[lo:hi]
@@ -147,14 +160,31 @@ class GradientBucketer:
         if t.is_cuda:  # the bucket's weight gradients may still be in flight on the side stream
             from ..ops._util import comm_stream_ctx
             ctx = comm_stream_ctx(t.device)
+        work = None
         with ctx:
-            if self.wire == "bf16":
-                if self._wirebuf is None:
-                    self._wirebuf = torch.empty(self.arena.grad.numel(), dtype=torch.bfloat16, device=t.device)
-                w = self._wirebuf[lo:hi]
-                _cast(t, w)
-                t = w
-            self._works[b] = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if self.collective:
+                if self.wire == "bf16":
+                    if self._wirebuf is None:
+                        self._wirebuf = torch.empty(self.arena.grad.numel(), dtype=torch.bfloat16, device=t.device)
+                    w = self._wirebuf[lo:hi]
+                    _cast(t, w)
+                    t = w
+                work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if self._opt is None:
+            self._works[b] = work
+            return
+        uctx = contextlib.nullcontext()
+        if t.is_cuda:
+            from ..ops._util import update_stream_ctx
+            uctx = update_stream_ctx(t.device)
+        with uctx:
+            if work is not None:
+                work.wait()  # GPU: the update stream waits for the collective (the host does not)
+                if self.wire == "bf16":
+                    _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])
+            if self.average and self.collective:
+                self.arena.grad[lo:hi].div_(dist.get_world_size(self.group))
+            self._opt.apply_range(self.arena, lo, hi)
 
     def finalize(self):
         """Issue buckets whose variables got no gradient (in order), then wait for all of them."""
@@ -168,18 +198,26 @@ class GradientBucketer:
         if self.timing and self.arena.grad.is_cuda:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()  # backward compute is done here; what follows on this stream is waiting on RCCL
-        for w in self._works:
-            if w is not None:
-                w.wait()
-        if self.wire == "bf16":
-            for lo, hi in self.buckets:
-                _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])
+        if self._opt is not None:
+            # every bucket was updated on the update stream: the step's tail is its last updates
+            if self.arena.grad.is_cuda:
+                from ..ops._util import join_update_stream
+                join_update_stream(self.arena.grad.device)
+            self._opt = None
+            self.updated = True
+        else:
+            for w in self._works:
+                if w is not None:
+                    w.wait()
+            if self.wire == "bf16" and self.collective:
+                for lo, hi in self.buckets:
+                    _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])
+            if self.average and self.collective:
+                self.arena.grad.div_(dist.get_world_size(self.group))
         if ev0 is not None:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             self._timed.append((ev0, ev1))
-        if self.average:
-            self.arena.grad.div_(dist.get_world_size(self.group))
         self.reset()
 
     def exposed_ms(self, clear=True):

@@ -470,6 +470,9 @@ class ParameterServerStrategy(Strategy):
         return out
 
     # ---- training-loop hooks
+    def _overlap_bucketer(self, arena, optimizer):
+        return None  # the parameter servers own the update
+
     def apply_gradients(self, optimizer, arena):
         """Async step: push this worker's gradients, the PS applies them, pull fresh values."""
         self._push_all(GRAD)

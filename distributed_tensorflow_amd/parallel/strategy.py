@@ -30,6 +30,11 @@ from .cluster_resolver import TFConfigClusterResolver, TorchrunClusterResolver
 
 _tls = threading.local()
 
+# optimizer update bucket by bucket during backward (collective.GradientBucketer.begin_step); DTF_OVERLAP_UPDATE=0
+# runs it as one launch after backward instead
+# runs it as one launch after backward instead; "force" also overlaps CPU arenas (tests)
+_OVERLAP_UPDATE = os.environ.get("DTF_OVERLAP_UPDATE", "1")
+
 
 class ReduceOp(enum.Enum):
     SUM = "sum"
@@ -103,14 +108,40 @@ class Strategy:
     def setup_model(self, model, arena):
         """Called once after the trainable arena exists (broadcast initial state, install hooks)."""
 
-    def backward(self, loss, arena):
+    def _overlap_bucketer(self, arena, optimizer):
+        """The bucketer that runs ``optimizer`` bucket by bucket during backward, or None (CPU arenas, global-norm
+        clipping, sharded or in-process-replica updates)."""
+        if optimizer is None or _OVERLAP_UPDATE == "0" or not optimizer.supports_ranges():
+            return None
+        if not arena.grad.is_cuda and _OVERLAP_UPDATE != "force":
+            return None
+        if arena.grad.is_cuda and torch.cuda.is_current_stream_capturing():
+            return None  # a captured step keeps the single update after backward (measured: replays diverged)
+        b = self._bucketers.get(id(arena))
+        if b is None:  # one replica: a bucketer without collectives, only to time the bucket updates
+            b = collective.GradientBucketer(arena, collective=False).install()
+            self._bucketers[id(arena)] = b
+        return b if type(b) is collective.GradientBucketer else None
+
+    def backward(self, loss, arena, optimizer=None):
+        b = self._overlap_bucketer(arena, optimizer)
+        if b is not None:
+            b.begin_step(optimizer, self.grad_scale())
         loss.backward()
+        if b is not None:
+            b.finalize()
 
     def grad_scale(self):
         return 1.0
 
     def apply_gradients(self, optimizer, arena):
-        """Apply the (already reduced) gradient arena: one fused optimizer launch."""
+        """Apply the (already reduced) gradient arena: one fused optimizer launch — or, when the update already
+        ran bucket by bucket during backward, only close the step."""
+        b = self._bucketers.get(id(arena))
+        if b is not None and getattr(b, "updated", False):
+            b.updated = False
+            optimizer.end_step(arena)
+            return
         optimizer.set_grad_scale(self.grad_scale())
         optimizer.apply_arena(arena, zero_grad=True)
 
@@ -267,7 +298,12 @@ class MultiWorkerMirroredStrategy(Strategy):
                                             wire_dtype=getattr(self, "wire_dtype", None)).install()
         self._bucketers[id(arena)] = b
 
-    def backward(self, loss, arena):
+    def backward(self, loss, arena, optimizer=None):
+        if getattr(self, "_inproc", False):
+            return Strategy.backward(self, loss, arena)
+        ob = self._overlap_bucketer(arena, optimizer)
+        if ob is not None:
+            ob.begin_step(optimizer, self.grad_scale())
         loss.backward()
         b = self._bucketers.get(id(arena))
         if b is not None:
@@ -279,7 +315,7 @@ class MultiWorkerMirroredStrategy(Strategy):
     def apply_gradients(self, optimizer, arena):
         b = self._bucketers.get(id(arena))
         if not isinstance(b, collective.ShardedGradientBucketer):
-            return super().apply_gradients(optimizer, arena)
+            return Strategy.apply_gradients(self, optimizer, arena)
         optimizer.set_grad_scale(self.grad_scale())
         optimizer.apply_segments(arena, b.segments(), reduce_sumsq=lambda t: dist.all_reduce(t))
         b.gather_params()

@@ -39,7 +39,9 @@ def _mwms_worker(rank, world, port, mode, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), DTF_CPU_ALLREDUCE=mode.split("_")[0], HIP_VISIBLE_DEVICES="",
                       CUDA_VISIBLE_DEVICES="", DTF_ALLREDUCE_DTYPE="bf16" if mode.endswith("bf16") else "f32",
-                      DTF_ZERO="1" if "zero" in mode else "0", DTF_BUCKET_MB="0.004" if "zero" in mode else "32")
+                      DTF_ZERO="1" if "zero" in mode else "0",
+                      DTF_BUCKET_MB="0.0001" if ("zero" in mode or "ovl" in mode) else "32",
+                      DTF_OVERLAP_UPDATE="force" if "ovl" in mode else "1")
     try:
         from distributed_tensorflow_amd import parallel
         from distributed_tensorflow_amd.models.mlp import synthetic_mnist
@@ -62,13 +64,15 @@ def _mwms_worker(rank, world, port, mode, q):
 
 
 @pytest.mark.parametrize("mode,world", [("shm", 2), ("gloo", 2), ("gloo_bf16", 2), ("gloo_zero", 2),
-                                        ("gloo_zero", 3), ("gloo_zero_bf16", 2)])
+                                        ("gloo_zero", 3), ("gloo_zero_bf16", 2), ("gloo_ovl", 2), ("gloo_ovl_bf16", 2)])
 def test_multi_worker_mirrored_matches_single_process(mode, world):
     """gloo_bf16: the gradient buckets travel as bf16 (half the all-reduce bytes) and are accumulated back into
     the f32 arena; the replicas still agree exactly and track f32 training within bf16 rounding.
     gloo_zero: ZeRO-1 (reduce-scatter, 1/N optimizer update per replica, all-gather of the masters; tiny
     buckets so every variable boundary case is hit; world 3 exercises the padded, non-divisible chunks) —
-    weights AND the gathered momentum slots equal single-process training."""
+    weights AND the gathered momentum slots equal single-process training.
+    gloo_ovl: the optimizer update runs bucket by bucket inside backward, right after each bucket's all-reduce
+    (tiny buckets: many partial updates per step) — same result as the update after backward."""
     from distributed_tensorflow_amd import parallel
     from distributed_tensorflow_amd.models.mlp import synthetic_mnist
     ctx = mp.get_context("spawn")
@@ -234,3 +238,33 @@ def test_mirrored_rejects_several_gpus_in_one_process():
     from distributed_tensorflow_amd import parallel
     with pytest.raises(ValueError, match="one process per GPU"):
         parallel.MirroredStrategy(["GPU:0", "GPU:1"])
+
+
+def test_overlapped_bucket_update_matches_single_update(monkeypatch):
+    """One replica: the per-bucket optimizer update inside backward (collective-free GradientBucketer, forced on
+    for a CPU arena) trains exactly like one fused update after backward — SGD+momentum and Adam, tiny buckets."""
+    from distributed_tensorflow_amd import parallel
+    from distributed_tensorflow_amd.keras import initializers, losses, optimizers
+    from distributed_tensorflow_amd.models.mlp import MnistMLP, synthetic_mnist
+    from distributed_tensorflow_amd.parallel import collective, strategy as S
+    x, y = synthetic_mnist(256)
+    X, Y = torch.as_tensor(x), torch.as_tensor(y)
+
+    def run(mode, opt):
+        monkeypatch.setattr(S, "_OVERLAP_UPDATE", mode)
+        monkeypatch.setattr(collective, "_DEFAULT_BUCKET_MB", 0.0001)
+        initializers.set_seed(0)
+        s = parallel.OneDeviceStrategy("cpu")
+        with s.scope():
+            m = MnistMLP(hidden=32)
+            m.compile(opt(), losses.SparseCategoricalCrossentropy(from_logits=True))
+        m.fit(X, Y, batch_size=64, epochs=2, shuffle=False, verbose=0)
+        nb = len(s._bucketers[id(m._arena)].buckets) if s._bucketers else 0
+        return [w.detach().numpy().copy() for w in m.weights], int(m.optimizer.iterations.item()), nb
+
+    for opt in (lambda: optimizers.SGD(0.1, momentum=0.9), lambda: optimizers.Adam(1e-2)):
+        a, ia, nb = run("force", opt)
+        b, ib, _ = run("0", opt)
+        assert nb > 2 and ia == ib == 8
+        for u, v in zip(a, b):
+            np.testing.assert_allclose(u, v, rtol=1e-6, atol=1e-7)
