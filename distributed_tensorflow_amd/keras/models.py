@@ -202,7 +202,7 @@ class Model(Layer):
                 not multi or os.environ.get("DTF_GRAPH_DIST", "0") == "1"):
             from ..graphs import CapturedStep
             fn = CapturedStep(self.train_step, warmup=2, optimizers=[self.optimizer])
-        self._graph_step = fn is not self.train_step
+        self._graph_step = type(fn).__name__ == "CapturedStep"
         self._train_fn = fn
         return fn
 
