@@ -21,6 +21,42 @@ __global__ void __launch_bounds__(256) dtf_group_rows_kernel(float* __restrict__
   else rows[(long)r0 * stride + i] = acc;
 }
 
+// float4 form (W, stride multiples of 4, 16-B aligned rows): 4 columns per thread
+__global__ void __launch_bounds__(256) dtf_group_rows4_kernel(float* __restrict__ rows, long stride, int nrows,
+                                                              int sg, long W4, float* __restrict__ out,
+                                                              int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W4) return;
+  const int r0 = blockIdx.y * sg;
+  const int r1 = min(nrows, r0 + sg);
+  const float4* R = reinterpret_cast<const float4*>(rows);
+  const long s4 = stride / 4;
+  float4 a[4] = {};
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = R[(long)(r + u) * s4 + i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { a[u].x += v[u].x; a[u].y += v[u].y; a[u].z += v[u].z; a[u].w += v[u].w; }
+  }
+  for (; r < r1; ++r) {
+    const float4 v = R[(long)r * s4 + i];
+    a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+  }
+  float4 acc;
+  acc.x = (a[0].x + a[1].x) + (a[2].x + a[3].x);
+  acc.y = (a[0].y + a[1].y) + (a[2].y + a[3].y);
+  acc.z = (a[0].z + a[1].z) + (a[2].z + a[3].z);
+  acc.w = (a[0].w + a[1].w) + (a[2].w + a[3].w);
+  float4* dst = out ? reinterpret_cast<float4*>(out) + i : reinterpret_cast<float4*>(rows) + (long)r0 * s4 + i;
+  if (out && accumulate) {
+    const float4 o = *dst;
+    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+  }
+  *dst = acc;
+}
+
 // One launch: sum groups of rows into leader rows so that <= target leaders remain; returns their count
 // and (via out_stride) their row stride.
 DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int target, long* out_stride,
@@ -65,6 +101,15 @@ DTF_API int* dtf_tickets(int n) {
 // Returns nothing; stream-ordered.
 DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (W >= (1l << 16) && !(W & 3) && !(stride & 3) && !((uintptr_t)rows & 15) && !((uintptr_t)out & 15) &&
+      nrows <= 64) {
+    // wide rows (split-K slabs of a weight gradient): ONE float4 pass, each thread sums its 4 columns over all
+    // rows with 4 interleaved accumulators (a fixed association: deterministic)
+    const long W4 = W / 4;
+    hipLaunchKernelGGL(dtf_group_rows4_kernel, dim3((unsigned)((W4 + 255) / 256), 1), dim3(256), 0, st, rows, stride,
+                       nrows, nrows, W4, out, accumulate);
+    return;
+  }
   const int gx = (int)((W + 255) / 256);
   long s = stride;
   int n = nrows;
@@ -297,7 +342,11 @@ static int choose_splitk(long M, long N, long K, int tile_m, int tile_n, long ba
     const char* e = getenv("DTF_SPLITK_BLOCKS");  // blocks a split-K launch aims for (2 per CU by default)
     return e ? std::max(64L, atol(e)) : 512L;
   }();
-  if (tiles >= 256 || K <= 1024) return 1;
+  static const long full = [] {  // 128x128 tile count from which no split is taken (DTF_SPLITK_TILES)
+    const char* e = getenv("DTF_SPLITK_TILES");
+    return e ? std::max(16L, atol(e)) : 256L;
+  }();
+  if (tiles >= full || K <= 1024) return 1;
   long want = (target + tiles - 1) / tiles;
   if (want > 256) want = 256;
   long maxs = K / 512;  // keep >= 512 of K per split
