@@ -93,6 +93,10 @@ def _head(x, n=1):
 
 
 class Model(Layer):
+    # run the optimizer bucket by bucket during backward (parallel.strategy._OVERLAP_UPDATE); models whose
+    # backward leaves CUs idle opt in
+    overlap_update = False
+
     def __init__(self, inputs=None, outputs=None, name=None, **kw):
         super().__init__(name=name, **kw)
         self.optimizer = None
@@ -180,8 +184,12 @@ class Model(Layer):
             loss = self.compute_loss(x, y, y_pred, sw)
         arena = self._ensure_arena()
         with prof.phase("backward"), direct_grads():  # includes the overlapped bucket all-reduces
-            # a hipGraph-captured step (and its eager warmups) keeps the single update after backward
-            strat.backward(loss, arena, optimizer=None if getattr(self, "_graph_step", False) else self.optimizer)
+            # per-bucket update during backward when the model asks for it (overlap_update) or DTF_OVERLAP_UPDATE
+            # forces it; a hipGraph-captured step (and its eager warmups) keeps the single update after backward
+            from ..parallel import strategy as _S
+            ovl = _S._OVERLAP_UPDATE in ("1", "force") or (_S._OVERLAP_UPDATE == "" and self.overlap_update)
+            strat.backward(loss, arena,
+                           optimizer=self.optimizer if ovl and not getattr(self, "_graph_step", False) else None)
             join_side_streams()  # weight gradients issued on the side stream are in the arena
         with prof.phase("optimizer"):
             strat.apply_gradients(self.optimizer, arena)

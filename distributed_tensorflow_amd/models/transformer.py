@@ -152,6 +152,9 @@ class GPT2(Model):
     def __init__(self, vocab=50257, ctx=1024, hidden=1024, layers=24, heads=16, dropout=0.1, fp8=False,
                  name="gpt2", **kw):
         super().__init__(name=name, **kw)
+        # fp8: the quantize passes and fp8 GEMMs leave CUs idle along the data-gradient chain, which the
+        # per-bucket optimizer update fills (+2% measured; bf16 -1%)
+        self.overlap_update = bool(fp8)
         self.cfg = dict(vocab=vocab, ctx=ctx, hidden=hidden, layers=layers, heads=heads, fp8=fp8)
         from ..keras.initializers import TruncatedNormal
         # vocab padded to a multiple of 64 for the MFMA tiles (padded logits are masked out of the loss)

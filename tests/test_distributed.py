@@ -41,7 +41,7 @@ def _mwms_worker(rank, world, port, mode, q):
                       CUDA_VISIBLE_DEVICES="", DTF_ALLREDUCE_DTYPE="bf16" if mode.endswith("bf16") else "f32",
                       DTF_ZERO="1" if "zero" in mode else "0",
                       DTF_BUCKET_MB="0.0001" if ("zero" in mode or "ovl" in mode) else "32",
-                      DTF_OVERLAP_UPDATE="force" if "ovl" in mode else "1")
+                      DTF_OVERLAP_UPDATE="force" if "ovl" in mode else "0")
     try:
         from distributed_tensorflow_amd import parallel
         from distributed_tensorflow_amd.models.mlp import synthetic_mnist
