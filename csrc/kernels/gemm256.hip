@@ -250,8 +250,11 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   const long cbase = a.slab > 0 ? (long)z * a.slab : (long)bz * a.sC;
   // bf16 outputs (and the optional pre-activation side output) go through LDS, one 128-row half of the tile at
   // a time, so the global stores are whole 16-B chunks of 512-B row segments instead of 8-B pieces of 16 rows
-  const bool staged = !a.out_f32 && a.beta == 0.f && a.slab == 0 && !(a.N & 7) && !(a.ldc & 7) &&
-                      !(reinterpret_cast<uintptr_t>(a.C) & 15) && !(reinterpret_cast<uintptr_t>(a.aux) & 15);
+  // beta (bf16 C, no aux/act): the old C is added to the bf16-rounded product in the store pass — exactly the
+  // unfused GEMM followed by an elementwise add (a residual gradient joined in the branch's data-gradient GEMM)
+  const bool staged = !a.out_f32 && (a.beta == 0.f || (!a.aux && !a.act)) && a.slab == 0 && !(a.N & 7) &&
+                      !(a.ldc & 7) && !(reinterpret_cast<uintptr_t>(a.C) & 15) &&
+                      !(reinterpret_cast<uintptr_t>(a.aux) & 15);
   if (staged) {
     constexpr int CS = BN + 8;  // LDS row stride (elements): conflict-free 8-B fragment writes
     bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
@@ -293,6 +296,18 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
           const int m = m0 + h * 128 + row, n = n0 + c8 * 8;
           if (m < a.M && n < a.N) {
             uint4 val = *reinterpret_cast<const uint4*>(ct + row * CS + c8 * 8);
+            if (o == 0 && a.beta != 0.f) {
+              const uint4 old = *reinterpret_cast<const uint4*>(dst + (long)m * a.ldc + n);
+              const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, ow[4] = {old.x, old.y, old.z, old.w};
+              float f[8];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                f[2 * q] = fmaf(a.beta, __uint_as_float(ow[q] << 16), __uint_as_float(vw[q] << 16));
+                f[2 * q + 1] = fmaf(a.beta, __uint_as_float(ow[q] & 0xffff0000u), __uint_as_float(vw[q] & 0xffff0000u));
+              }
+              val.x = pack2bf(f[0], f[1]); val.y = pack2bf(f[2], f[3]);
+              val.z = pack2bf(f[4], f[5]); val.w = pack2bf(f[6], f[7]);
+            }
             if (o == 0 && a.dact) val = dact8(val, *reinterpret_cast<const uint4*>(a.dact_src + (long)m * a.ldc + n), a.dact);
             *reinterpret_cast<uint4*>(dst + (long)m * a.ldc + n) = val;
           }
@@ -376,7 +391,8 @@ void launch256(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8) {
 
 // Used by dtf_gemm for eligible problems; returns 0 if launched, 1 if not eligible. bn: 256 or 128 (tile width).
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int bn) {
-  if (a.kchunk % BK || a.kchunk < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.stats || a.atomic_out || a.crm)
+  if (a.kchunk % BK || a.kchunk < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.stats || a.atomic_out || a.crm ||
+      a.betamask || a.bsrc)
     return 1;
   if ((a.splitk > 1 && a.K % a.kchunk && (a.K % a.kchunk) % BK) || a.K % BK) return 1;
   if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return 1;

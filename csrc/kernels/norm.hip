@@ -821,7 +821,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, bf16_t* __restrict__ dx,
-                                                     float* __restrict__ part, long M, int D) {
+                                                     float* __restrict__ part, long M, int D,
+                                                     const bf16_t* __restrict__ res) {
   extern __shared__ float sred[];  // [4][2D]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int d8 = D / 8;
@@ -894,6 +895,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rs * (g[k][j] * gm[k][j] - a - xh[k][j] * b);
+        if (res) {  // residual gradient joined in the store: round(round(dx) + res), as LN backward + an add
+          float rv[8];
+          load8(res + row * D + c * 8, rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(o[j])) + rv[j];
+        }
         store8(dx + row * D + c * 8, o);
       }
     }
@@ -1165,17 +1172,27 @@ DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* be
   return (int)hipGetLastError();
 }
 
+DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma, const float* mean,
+                               const float* rstd, void* dx, float* dgb, float* ws, long ws_elems, long M, int D,
+                               int accumulate, const void* res, void* stream);
 // dgb = [dgamma | dbeta] (2D floats, overwritten or accumulated); ws >= min(1024, M/16 + 1) * 2D floats.
 DTF_API int dtf_layernorm_bwd(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
                               void* dx, float* dgb, float* ws, long ws_elems, long M, int D, int accumulate,
                               void* stream) {
+  return dtf_layernorm_bwd2(dy, x, gamma, mean, rstd, dx, dgb, ws, ws_elems, M, D, accumulate, nullptr, stream);
+}
+// res (optional, bf16 [M][D]): another gradient of the LayerNorm's input (the residual branch), added to dx
+DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma, const float* mean,
+                               const float* rstd, void* dx, float* dgb, float* ws, long ws_elems, long M, int D,
+                               int accumulate, const void* res, void* stream) {
   if ((D & 7) || D > 2048) return -1;
   long blocks = std::max<long>(1, std::min<long>(cdiv(M, 16), 1024));
   blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / (2L * D)));
   const size_t sh = sizeof(float) * 8 * D;
 #define LNB(NC) \
   hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3((unsigned)blocks), dim3(256), sh, (hipStream_t)stream,       \
-                      (const bf16_t*)dy, (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, ws, M, D)
+                      (const bf16_t*)dy, (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, ws, M, D,            \
+                      (const bf16_t*)res)
   DTF_LN_DISPATCH(D, LNB);
 #undef LNB
   dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, accumulate, stream);

@@ -421,8 +421,8 @@ class LayerNormalization(Layer):
         self.beta = self.add_weight("beta", (d,), "zeros")
         self.built = True
 
-    def call(self, x, training=None):
-        return ops.layer_norm(x, self.gamma, self.beta, self.epsilon)
+    def call(self, x, training=None, link=None):
+        return ops.layer_norm(x, self.gamma, self.beta, self.epsilon, link=link)
 
 
 class Embedding(Layer):

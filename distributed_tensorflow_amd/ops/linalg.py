@@ -136,14 +136,14 @@ _BLAS_WGRAD_MIN = 4 << 20
 
 
 def dense_dgrad(dz, w16, acc=None):
-    """dX[T, in] = dZ[T, out] W[out, in] (bf16); with `acc` (another gradient of the same input, [T, in]) the GEMM
-    adds it (one rounding, no separate add pass)."""
+    """dX[T, in] = dZ[T, out] W[out, in] (bf16); with `acc` (another gradient of the same input, [T, in], parked on
+    a ResidualGradLink: no other reader) the GEMM adds it in its store pass and returns it — no separate add pass,
+    the same values as the GEMM followed by an elementwise add."""
     if _PLAIN_BLAS:
         return torch.mm(dz, w16) if acc is None else torch.addmm(acc, dz, w16)
     if acc is None:
         return gemm(dz, w16, b_kouter=True)
-    out = acc.clone()
-    return gemm(dz, w16, b_kouter=True, out=out, beta=1.0)
+    return gemm(dz, w16, b_kouter=True, out=acc, beta=1.0)
 
 
 def dense_wgrad(dz, x2, out=None):

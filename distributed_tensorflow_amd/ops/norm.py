@@ -89,7 +89,10 @@ def batch_norm(x, gamma, beta, rmean, rvar, training=True, momentum=0.99, eps=1e
 
 class _LNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps):
+    def forward(ctx, x, gamma, beta, eps, link=None):
+        # link: ops.conv.ResidualGradLink on which the residual add of the same input parks its gradient; the
+        # backward adds it in its store pass (pre-LN blocks: x feeds LN and the residual connection)
+        ctx.link = link
         x = x.contiguous()
         D = x.shape[-1]
         M = x.numel() // D
@@ -110,21 +113,27 @@ class _LNFn(torch.autograd.Function):
         dy = dy.to(BF16).contiguous()
         dx = torch.empty_like(x)
         ws = workspace(x.device)
+        res = ctx.link.take()[0] if ctx.link is not None else None
+        ctx.link = None
+        if res is not None:
+            res = res.to(BF16).contiguous()
         g_p, b_p = ctx.ln_params
         tg, tb = direct_grad(g_p), direct_grad(b_p)
         if tg is not None and tb is not None and tb.data_ptr() == tg.data_ptr() + 4 * D:
             # gamma and beta are adjacent in the arena: accumulate [dgamma | dbeta] into their gradients
-            call("dtf_layernorm_bwd", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(tg), ptr(ws),
-                 ws.numel(), M, D, 1, stream())
-            return dx, None, None, None
+            call("dtf_layernorm_bwd2", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(tg), ptr(ws),
+                 ws.numel(), M, D, 1, ptr(res), stream())
+            return dx, None, None, None, None
         dgb = torch.empty(2 * D, dtype=F32, device=x.device)
-        call("dtf_layernorm_bwd", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(dgb), ptr(ws),
-             ws.numel(), M, D, 0, stream())
-        return dx, dgb[:D], dgb[D:], None
+        call("dtf_layernorm_bwd2", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(dgb), ptr(ws),
+             ws.numel(), M, D, 0, ptr(res), stream())
+        return dx, dgb[:D], dgb[D:], None, None
 
 
-def layer_norm(x, gamma, beta, eps=1e-5):
+def layer_norm(x, gamma, beta, eps=1e-5, link=None):
+    """link: a ResidualGradLink shared with the residual add of the same input (ops.add_dropout(..., link=)):
+    that add parks its gradient of x and this backward returns the sum (no autograd add kernel)."""
     if on_gpu(x) and x.shape[-1] % 8 == 0:
-        return _LNFn.apply(x.to(BF16), gamma, beta, float(eps))
+        return _LNFn.apply(x.to(BF16), gamma, beta, float(eps), link)
     return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), gamma, beta, eps).to(
         x.dtype if x.is_floating_point() else torch.float32)

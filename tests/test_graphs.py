@@ -127,3 +127,29 @@ def test_overlapped_update_bitwise_equals_single_update(cuda, model, monkeypatch
            if not torch.allclose(a, b, rtol=2.5e-7, atol=1e-9)]
     assert not bad, (len(bad), len(res[0][1]), bad[:12], res[0][0], res[1][0])
     assert res[0][0] == res[1][0]
+
+
+@pytest.mark.gpu
+def test_gpt2_layernorm_residual_join_bitwise(cuda, monkeypatch):
+    """Pre-LN blocks: the residual gradient parked by add_dropout is added in the LayerNorm backward's store pass
+    (models.transformer.LN_LINK) — the same values as the LN backward followed by autograd's add, bit for bit."""
+    from distributed_tensorflow_amd.keras import initializers
+    from distributed_tensorflow_amd.models import transformer as T
+    torch.manual_seed(0)
+    batches = [(torch.randint(0, 128, (2, 64), device=cuda), torch.randint(0, 128, (2, 64), device=cuda))
+               for _ in range(3)]
+    res = []
+    from distributed_tensorflow_amd.ops import _util, mha, nn
+    for on in (False, True):
+        monkeypatch.setattr(T, "LN_LINK", on)
+        initializers.set_seed(5)
+        nn._seed_counter[0] = mha._seed_counter[0] = 0  # same dropout seeds and step counters in both runs
+        _util._RNG.clear()
+        m = T.GPT2(vocab=128, ctx=64, hidden=128, layers=2, heads=2, dropout=0.1)
+        m.compile(optimizer=optimizers.SGD(0.05), loss=losses.SparseCategoricalCrossentropy(from_logits=True))
+        ls = [float(m.train_step(b)["loss"]) for b in batches]
+        torch.cuda.synchronize()
+        res.append((ls, [w.detach().clone() for w in m.trainable_variables]))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)

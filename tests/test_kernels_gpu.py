@@ -712,3 +712,21 @@ def test_dropout_keep_rate_and_scale(cuda):
     vals = y1[y1 != 0]
     assert torch.allclose(vals, torch.full_like(vals, 65536.0 / round(0.9 * 65536)).to(BF).float())
     assert ((y1 != 0) != (y2 != 0)).float().mean().item() > 0.1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(4096, 768, 2304), (2048, 1024, 4096), (1000, 776, 512)])
+def test_gemm_beta_bf16_equals_gemm_then_add(cuda, M, N, K):
+    """C = A.B^T + C for bf16 C (the residual-gradient join of a data-gradient GEMM, ops.linalg.dense_dgrad with
+    acc): bit-identical to the plain GEMM followed by an f32 add rounded once — on the 256x256 kernel's staged
+    store pass as on the 128x128 kernels."""
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    w = torch.randn(K, N, device=cuda).to(torch.bfloat16)  # K-outer B, as a data gradient reads W
+    c0 = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    prod = ops.gemm(a, w, b_kouter=True)
+    ref = (prod.float() + c0.float()).to(torch.bfloat16)
+    out = c0.clone()
+    ops.gemm(a, w, b_kouter=True, out=out, beta=1.0)
+    assert torch.equal(out, ref)
+    close(prod, a.float() @ w.float(), 2e-2)
