@@ -57,6 +57,64 @@ __global__ void __launch_bounds__(256) dtf_group_rows4_kernel(float* __restrict_
   *dst = acc;
 }
 
+// Narrow rows (W <= 1024 floats, W % 4 == 0: the BatchNorm / LayerNorm / bias partial rows): each block sums one
+// group of rows with ALL its 256 threads — W/4 float4 columns x 256/(W/4) row lanes, each lane striding the
+// group's rows with 4 loads in flight — and combines the row lanes through LDS in a fixed order (deterministic).
+// The one-thread-per-column form left 7/8 of a block idle and walked ~200 rows per thread serially.
+__global__ void __launch_bounds__(256) dtf_group_rows_narrow_kernel(const float* __restrict__ rows, long stride,
+                                                                    int nrows, int sg, int W4,
+                                                                    float* __restrict__ dst, long dst_stride,
+                                                                    int accumulate) {
+  __shared__ float4 red[256];
+  const int t = threadIdx.x, RL = 256 / W4, c = t % W4, rl = t / W4;
+  const int r0 = blockIdx.y * sg, r1 = min(nrows, r0 + sg);
+  float4 a[4] = {};
+  if (rl < RL) {
+    const float4* R = reinterpret_cast<const float4*>(rows);
+    const long s4 = stride / 4;
+    int r = r0 + rl;
+    for (; r + 3 * RL < r1; r += 4 * RL) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = R[(long)(r + u * RL) * s4 + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a[u].x += v[u].x; a[u].y += v[u].y; a[u].z += v[u].z; a[u].w += v[u].w; }
+    }
+    for (; r < r1; r += RL) {
+      const float4 v = R[(long)r * s4 + c];
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
+  }
+  float4 s;
+  s.x = (a[0].x + a[1].x) + (a[2].x + a[3].x);
+  s.y = (a[0].y + a[1].y) + (a[2].y + a[3].y);
+  s.z = (a[0].z + a[1].z) + (a[2].z + a[3].z);
+  s.w = (a[0].w + a[1].w) + (a[2].w + a[3].w);
+  red[t] = s;
+  __syncthreads();
+  if (t < W4) {
+    float4 acc = red[t];
+    for (int k = 1; k < RL; ++k) {
+      const float4 v = red[k * W4 + t];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float4* o = reinterpret_cast<float4*>(dst + (long)blockIdx.y * dst_stride) + t;
+    if (accumulate) {
+      const float4 p = *o;
+      acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+    }
+    *o = acc;
+  }
+}
+
+static bool narrow_rows_ok(const float* rows, long stride, long W) {
+  static const bool on = [] {
+    const char* e = getenv("DTF_NARROW_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  return on && !(W & 3) && W <= 1024 && !(stride & 3) && !((uintptr_t)rows & 15);
+}
+
 // One launch: sum groups of rows into leader rows so that <= target leaders remain; returns their count
 // and (via out_stride) their row stride.
 DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int target, long* out_stride,
@@ -65,8 +123,13 @@ DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int
   if (nrows <= target) return nrows;
   const int sg = (nrows + target - 1) / target;
   const int groups = (nrows + sg - 1) / sg;
-  hipLaunchKernelGGL(dtf_group_rows_kernel, dim3((unsigned)((W + 255) / 256), groups), dim3(256), 0,
-                     (hipStream_t)stream, rows, stride, nrows, sg, W, (float*)nullptr, 0);
+  if (narrow_rows_ok(rows, stride, W)) {
+    hipLaunchKernelGGL(dtf_group_rows_narrow_kernel, dim3(1, groups), dim3(256), 0, (hipStream_t)stream, rows,
+                       stride, nrows, sg, (int)(W / 4), rows, stride * sg, 0);
+  } else {
+    hipLaunchKernelGGL(dtf_group_rows_kernel, dim3((unsigned)((W + 255) / 256), groups), dim3(256), 0,
+                       (hipStream_t)stream, rows, stride, nrows, sg, W, (float*)nullptr, 0);
+  }
   *out_stride = stride * sg;
   return groups;
 }
@@ -113,6 +176,21 @@ DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* ou
   const int gx = (int)((W + 255) / 256);
   long s = stride;
   int n = nrows;
+  if (out && narrow_rows_ok(rows, stride, W) && !((uintptr_t)out & 15)) {
+    const int W4 = (int)(W / 4);
+    if (n > 64) {  // one pass to <= 64 leader rows (written over the group's first row), ~16+ rows per group
+      const int groups = std::min(64, std::max(1, n / 16));
+      const int sg = (n + groups - 1) / groups;
+      const int g2 = (n + sg - 1) / sg;
+      hipLaunchKernelGGL(dtf_group_rows_narrow_kernel, dim3(1, g2), dim3(256), 0, st, rows, s, n, sg, W4, rows,
+                         s * sg, 0);
+      s *= sg;
+      n = g2;
+    }
+    hipLaunchKernelGGL(dtf_group_rows_narrow_kernel, dim3(1, 1), dim3(256), 0, st, rows, s, n, n, W4, out, 0L,
+                       accumulate);
+    return;
+  }
   if (gx < 64 && n > 32) {
     // narrow rows (LayerNorm/bias partials: W of a few thousand): ONE grouping pass to <= 32 leader rows,
     // then the final pass — two launches instead of a cascade of small ones

@@ -80,6 +80,7 @@ _KERNEL_SIGS = {
     "dtf_gemm_fp8_ex": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, F, I, P, L, P, P],
     "dtf_quant_fp8_t2": [P, P, I, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P],
     "dtf_group_rows_once": [P, L, I, L, I, P, P],
+    "dtf_sum_rows": [P, L, I, L, P, I, P],  # void: the int return value is meaningless
     "dtf_ipc_export": [P, P, P],
     "dtf_ipc_open": [P, P],
     "dtf_ipc_close": [P],

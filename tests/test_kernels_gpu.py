@@ -730,3 +730,25 @@ def test_gemm_beta_bf16_equals_gemm_then_add(cuda, M, N, K):
     ops.gemm(a, w, b_kouter=True, out=out, beta=1.0)
     assert torch.equal(out, ref)
     close(prod, a.float() @ w.float(), 2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,W,stride", [(6272, 128, 128), (1568, 512, 512), (392, 1024, 1024), (100, 96, 100),
+                                        (45, 2048, 2048), (700, 4096, 4096)])
+def test_row_reductions_large(cuda, T, W, stride):
+    """Deterministic partial-row reductions at the sizes the BN statistics and bias/LN gradients produce: the
+    grouping pass (dtf_group_rows_once: <= 32 leader rows written over each group's first row) and the full
+    sum (dtf_sum_rows, with accumulate) against an f64 sum."""
+    import ctypes
+    torch.manual_seed(0)
+    rows = torch.randn(T, stride, device=cuda)
+    ref = rows[:, :W].double().sum(0)
+    r2 = rows.clone()
+    out_stride = ctypes.c_long(0)
+    n = _util.K().dtf_group_rows_once(_util.ptr(r2), stride, T, W, 32, ctypes.byref(out_stride), _util.stream())
+    s = out_stride.value
+    lead = torch.stack([r2.view(-1)[i * s:i * s + W] for i in range(n)]).double().sum(0)
+    torch.testing.assert_close(lead, ref, rtol=1e-5, atol=1e-3)
+    out = torch.ones(W, device=cuda)
+    _util.K().dtf_sum_rows(_util.ptr(rows), stride, T, W, _util.ptr(out), 1, _util.stream())
+    torch.testing.assert_close(out.double(), ref + 1.0, rtol=1e-5, atol=1e-3)
