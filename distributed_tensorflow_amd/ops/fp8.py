@@ -38,6 +38,11 @@ _FP8_BWD = os.environ.get("DTF_FP8_BWD", "1") != "0"
 # that consumes it clears the previous slot for the step after (no scale-update launch)
 X_SCALE, W_SCALE, G_SCALE, X_USED, X_AMAX, G_AMAX = range(6)
 X_AMAX2, G_AMAX2 = 6, 7
+# weights: delayed scaling too (the standard fp8 recipe) — each step's W/W^T quantize pass uses the amax the
+# previous step's pass recorded and records its own; the step's weight-gradient GEMM clears the slot just read.
+# One launch per weight and step instead of an absmax pass + the quantize pass. DTF_FP8_W_DELAYED=0: exact scale.
+W_AMAX, W_AMAX2 = 8, 9
+_W_DELAYED = os.environ.get("DTF_FP8_W_DELAYED", "1") != "0"
 
 
 def quantize(x, scale, amax=None, zero_amax=True):
@@ -95,12 +100,15 @@ def _wgrad_splits(M, N, K, ws_elems):
 
 class _Fp8State:
     def __init__(self, dev):
-        self.buf = torch.zeros(8, dtype=F32, device=dev)
+        self.buf = torch.zeros(10, dtype=F32, device=dev)
         self.buf[W_SCALE] = 1.0
         self.x_ready = False
         self.g_ready = False
-        self.tx = 0  # forward / backward step counters: parity of the double-buffered amax slots
+        self.tx = 0  # forward / backward / weight step counters: parity of the double-buffered amax slots
         self.tg = 0
+        self.tw = 0
+        self.w_ready = False
+        self.w_prev = None  # the weight amax slot this step's pass read (cleared by this step's weight gradient)
         self.wq = self.wqT = None
         self.w_key = None
 
@@ -119,7 +127,19 @@ def _weight_fp8(st, w, need_t):
         return st.wq, st.wqT
     w16 = bf16_shadow(w)
     N, K = w16.shape
-    if need_t:
+    buf = st.buf
+    if need_t and _W_DELAYED and not torch.cuda.is_current_stream_capturing():
+        cur, prev = (W_AMAX, W_AMAX2) if st.tw % 2 == 0 else (W_AMAX2, W_AMAX)
+        st.tw += 1
+        if not st.w_ready:  # bootstrap: exact scale once, recording the amax the next step scales with
+            st.wq, st.wqT, _ = quantize_t(w16, amax=buf[cur:cur + 1], exact_out=buf[W_SCALE:W_SCALE + 1])
+            st.w_ready = True
+            st.w_prev = None
+        else:
+            st.wq, st.wqT, _ = quantize_t(w16, buf[W_SCALE:W_SCALE + 1], buf[cur:cur + 1],
+                                          amax_prev=buf[prev:prev + 1], scale_used=buf[W_SCALE:W_SCALE + 1])
+            st.w_prev = prev
+    elif need_t:
         # exact per-tensor scale (amax/448) computed on the device; W and W^T from one transposing pass
         st.wq, st.wqT, _ = quantize_t(w16, exact_out=st.buf[W_SCALE:W_SCALE + 1])
     else:
@@ -225,8 +245,10 @@ class _DenseFP8(torch.autograd.Function):
             if need_dw:  # dW[N, K] (+)= dZ^T X over the M tokens; inside Model.train_step straight into the arena
                 out = tw if tw is not None else torch.empty((N, K), dtype=F32, device=dy.device)
                 sk = _wgrad_splits(N, K, M, workspace(dy.device).numel())
+                wprev, st.w_prev = st.w_prev, None
                 gemm_fp8(dzqT, xqT, buf[G_SCALE:G_SCALE + 2], out, fmt_a=1, out_f32=True,
-                         beta=1.0 if tw is not None else 0.0, splitk=sk)  # scales (s_g, s_x used)
+                         beta=1.0 if tw is not None else 0.0, splitk=sk,  # scales (s_g, s_x used)
+                         zero_slot=None if wprev is None else buf[wprev:wprev + 1])
                 dw = None if tw is not None else out
             if need_db:
                 out = tb if tb is not None else torch.empty(N, dtype=F32, device=dy.device)
