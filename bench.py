@@ -182,7 +182,9 @@ def main():
             "dtype": "bf16+fp8" if args.model.endswith("fp8") else "bf16",
             "data": "synthetic (random inputs + labels resident on GPU; random-init weights)",
             "config": dict(cfg, global_batch=global_batch, per_gpu_batch=args.batch, parallelism=f"dp{world}",
-                           strategy=type(strategy).__name__ + " (1 process/GPU, RCCL)",
+                           strategy=type(strategy).__name__ + " (1 process/GPU, %s)" % (
+                               ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend())
+                               if dist.is_initialized() else "single replica"),
                            optimizer=type(model.optimizer).__name__, final_loss=round(loss, 4),
                            allreduce_dtype=args.allreduce_dtype or "f32", zero1=bool(args.zero),
                            exposed_comm_ms_per_step=round(exposed_max, 3)),
