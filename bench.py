@@ -76,7 +76,7 @@ def build(args, strategy, dev, rank):
             S = 1024
             args.tokens_per_sample = S
             data = iter(synthetic_tokens(args.batch, S, 50257, dev, seed=rank))
-            return model, data, "tokens/sec", {"model": "GPT-2-medium" + (" fp8 (e4m3 fwd projections)" if
+            return model, data, "tokens/sec", {"model": "GPT-2-medium" + (" fp8 (e4m3 x e4m3 fwd, e5m2 x e4m3 bwd projections)" if
                                                                            m.endswith("fp8") else ""), "seq_len": S}
     raise ValueError(m)
 
