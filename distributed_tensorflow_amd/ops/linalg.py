@@ -133,7 +133,7 @@ _PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "0") == "1"
 # Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream
 DENSE_SIDE_ON = SIDE_STREAM_ON and __import__("os").environ.get("DTF_DENSE_WGRAD_STREAM", "1") != "0"
 _BLAS_WGRAD_MIN = 4 << 20
-_SPLIT_DGRAD_K = int(__import__("os").environ.get("DTF_SPLIT_DGRAD_K", "0"))  # e.g. 8192 enables the split route
+_SPLIT_DGRAD_K = int(__import__("os").environ.get("DTF_SPLIT_DGRAD_K", "8192"))  # 0 disables the split route
 
 
 def dense_dgrad(dz, w16, acc=None):
@@ -145,7 +145,7 @@ def dense_dgrad(dz, w16, acc=None):
     M, K, N = dz.shape[0], dz.shape[1], w16.shape[1]
     if acc is None and _SPLIT_DGRAD_K and K >= _SPLIT_DGRAD_K and -(-M // 128) * -(-N // 128) < 256 and dz.is_cuda:
         # few output tiles over a long K (BERT's MLM decoder: 2432 x 768 over the 30k vocabulary): split-K f32 slabs
-        # on the wide tiles instead of one bf16 pass of small tiles, then one rounding to bf16
+        # on the wide tiles instead of one bf16 pass of small tiles, then one rounding to bf16 (BERT-base +1.7%)
         o = gemm(dz, w16, b_kouter=True, out_dtype=F32)
         out = torch.empty((M, N), dtype=BF16, device=dz.device)
         call("dtf_cast_f32_bf16", ptr(o), ptr(out), o.numel(), stream())
