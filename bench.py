@@ -154,6 +154,17 @@ def main():
     exposed = [b.exposed_ms() for b in bucketers if hasattr(b, "exposed_ms")]
     exposed = [e for e in exposed if e is not None]
     loss = float(logs["loss"])
+    # proof that the N replicas trained in lock step: an exact checksum of every trainable f32 master (the bit
+    # patterns summed as integers), compared across ranks (min == max); the world size the process group reports
+    arena = getattr(model, "_arena", None)
+    csum = int(arena.flat.detach().view(torch.int32).to(torch.int64).sum().item()) if arena is not None else 0
+    rccl_world = dist.get_world_size() if dist.is_initialized() else 1
+    backend = dist.get_backend() if dist.is_initialized() else None
+    identical = True
+    if dist.is_initialized():
+        mm = torch.tensor([csum, -csum], dtype=torch.int64, device=dev)
+        dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+        identical = int(mm[0].item()) == csum and int(-mm[1].item()) == csum
     t = torch.tensor([dt, sum(exposed) if exposed else 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # slowest rank's clock and exposed communication
@@ -187,7 +198,13 @@ def main():
                                if dist.is_initialized() else "single replica"),
                            optimizer=type(model.optimizer).__name__, final_loss=round(loss, 4),
                            allreduce_dtype=args.allreduce_dtype or "f32", zero1=bool(args.zero),
-                           exposed_comm_ms_per_step=round(exposed_max, 3)),
+                           bucket_mb=getattr(bucketers[0], "bucket_mb", None) if bucketers else None,
+                           exposed_comm_ms_per_step=round(exposed_max, 3),
+                           forced_collective=os.environ.get("DTF_FORCE_COLLECTIVE", "0") == "1"),
+            "rccl_world": rccl_world,
+            "process_group_backend": backend,
+            "replicas_identical": identical,
+            "weights_checksum": csum,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

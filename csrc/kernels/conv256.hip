@@ -305,6 +305,7 @@ void launch_cfg(GemmArgs& a, int cfg, hipStream_t st) {
   const int bn = cfg == 1 ? 256 : cfg == 2 ? 64 : 128;
   a.tiles_m = cdiv(a.M, BMC);
   a.tiles_n = cdiv(a.N, bn);
+  prep_fin(a);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
   switch (cfg) {
     case 1: hipLaunchKernelGGL((conv256_kernel<AM, BMD, 256, 8, 2>), grid, dim3(512), 0, st, a); break;

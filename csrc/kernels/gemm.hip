@@ -224,6 +224,7 @@ template <int BM, int BN, int WM, int WN, int AM, int BMODE, int PIPE = 2>
 static void launch_t(GemmArgs& a, hipStream_t st) {
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
+  prep_fin(a);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE, 0, PIPE>), grid, dim3(NT), 0, st, a);
 }
@@ -548,11 +549,61 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
 
 // NHWC conv forward: Y[N,P,Q,K] = X[N,H,W,C] * W[K,R,S,C] (+bias, act, BN stats of Y)
 // stats (optional): BN partial rows [tiles_m][2K] (capacity ceil(N*P*Q/64) rows); *stat_rows = tiles_m.
+static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
+                         int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
+                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin);
+
 DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
                          int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
                          int pw, int dh, int dw, int act, int out_f32, int tile, void* stream) {
+  return conv_fwd_impl(X, Wt, Y, bias, stats, stat_rows, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, act,
+                       out_f32, tile, stream, nullptr);
+}
+
+DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float* beta, float* running_mean,
+                            float* running_var, long M, int C, float momentum, float eps, float* scale,
+                            float* shift, float* mean_out, float* invstd_out, void* stream);  // norm.hip
+
+static bool fin_on() {
+  static const bool on = [] {
+    const char* e = getenv("DTF_BN_FIN_FUSED");  // DTF_BN_FIN_FUSED=0: separate reduction + finalize launches
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Conv forward + training BatchNorm statistics AND their finalize: scale/shift/mean/invstd of the output's
+// BatchNorm and the running-statistics update, computed in the conv launch's own tail (BnFin) — or, when that is
+// not possible (split tiling, no ticket slots during a capture), by dtf_bn_finalize right after. stats: partial-row
+// scratch as for dtf_conv_fwd. *fused (optional): 1 when the conv launch finalized.
+DTF_API int dtf_conv_fwd_bn(const void* X, const void* Wt, void* Y, float* stats, int N, int H, int W, int C, int K,
+                            int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int tile,
+                            const float* gamma, const float* beta, float* rmean, float* rvar, float momentum,
+                            float eps, float* scale, float* shift, float* mean, float* invstd, int* fused,
+                            void* stream) {
+  int done = 0, rows = 0;
+  BnFin f{};
+  f.mode = fin_on() ? 1 : 0;
+  f.p0 = gamma; f.p1 = beta; f.p2 = rmean; f.p3 = rvar;
+  f.o0 = scale; f.o1 = shift; f.o2 = mean; f.o3 = invstd;
+  f.momentum = momentum; f.eps = eps;
+  f.count = (long)N * P * Q;
+  f.host_done = &done;
+  int rc = conv_fwd_impl(X, Wt, Y, nullptr, stats, &rows, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0,
+                         tile, stream, &f);
+  if (rc) return rc;
+  if (!done) rc = dtf_bn_finalize(stats, rows, gamma, beta, rmean, rvar, (long)N * P * Q, K, momentum, eps, scale,
+                                  shift, mean, invstd, stream);
+  if (fused) *fused = done;
+  return rc;
+}
+
+static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
+                         int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
+                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin) {
   if ((C & 7) || (K & 3)) return -1;
   GemmArgs a{};
+  if (fin && stats) a.fin = *fin;
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
   a.g_rowrep = rowrep(a.g.R, a.g.S);
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)Wt; a.C = Y; a.bias = bias; a.stats = stats;
@@ -601,7 +652,23 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream);
+                           const void* bsrc2, void* stream, const BnFin* fin = nullptr);
+
+// The BnFin of a data gradient that also finalizes the backward of the BatchNorm whose output it is the gradient
+// of (mode 2): dgamma/dbeta (+= when accumulate) and the apply coefficients coef [3*C] of that BatchNorm (gamma,
+// mean, invstd: its forward's), computed in the dgrad launch's tail. Only a single-launch dgrad can do this.
+static BnFin bwd_fin(const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                     int accumulate, float* coef, long count, int* done) {
+  BnFin f{};
+  f.mode = (coef && invstd && mean && fin_on()) ? 2 : 0;
+  f.p0 = gamma; f.p1 = mean; f.p2 = const_cast<float*>(invstd);
+  f.o0 = dgamma; f.o1 = dbeta; f.o2 = coef;
+  f.accumulate = accumulate;
+  f.count = count;
+  f.host_done = done;
+  if (done) *done = 0;
+  return f;
+}
 
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
@@ -615,6 +682,29 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
 // dtf_conv_dgrad of a stride-1 pointwise conv whose result also adds bsrc2: the compact [N, H/2, W/2, C] data
 // gradient of a stride-2 1x1 projection shortcut of the same input, at the even pixels (the shortcut's full-size
 // gradient, 3/4 zeros, is never written or read). H and W even.
+// dtf_conv_dgrad with the BatchNorm-backward statistics finalized in the launch (see bwd_fin); *fused = 1 when it
+// did (else the caller reduces bnpart itself, as after dtf_conv_dgrad).
+DTF_API int dtf_conv_dgrad_bn(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
+                              int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, float beta,
+                              void* ws, long ws_bf16, const void* bnx, const void* bnmask, const float* bnmean,
+                              float* bnpart, int* bnrows, const void* betamask, const void* bsrc2,
+                              const float* gamma, const float* invstd, float* dgamma, float* dbeta, int accumulate,
+                              float* coef, int* fused, void* stream) {
+  int done = 0;
+  const BnFin f = bwd_fin(gamma, bnmean, invstd, dgamma, dbeta, accumulate, coef, (long)N * H * W, &done);
+  int rc;
+  if (bsrc2) {
+    if ((H & 1) || (W & 1)) return -11;
+    rc = conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, 1, 1, H, W, 1, 1, 0, 0, 1, 1, 0, 1.f, -1, ws, ws_bf16, bnx,
+                         bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, &f);
+  } else {
+    rc = conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, beta, -1, ws, ws_bf16,
+                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, &f);
+  }
+  if (fused) *fused = done;
+  return rc;
+}
+
 DTF_API int dtf_conv_dgrad_addsub2(const void* dY, const void* Wcrsk, void* dX, const void* bsrc2, int N, int H, int W,
                                    int C, int K, int tile, void* ws, long ws_bf16, const void* bnx,
                                    const void* bnmask, const float* bnmean, float* bnpart, int* bnrows,
@@ -628,7 +718,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream) {
+                           const void* bsrc2, void* stream, const BnFin* fin) {
   if ((C & 3) || (K & 7)) return -1;
   if (bnx && (out_f32 || (C & 7) || !bnpart || !bnmean || !bnrows)) return -9;
   if (betamask && (out_f32 || beta == 0.f || (C & 7) || sh > 1 || sw > 1)) return -10;
@@ -661,6 +751,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
     a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
     a.alpha = 1.f; a.beta = beta; a.act = 0; a.out_f32 = out_f32;
     bn_args(a);
+    if (fin && bnx) a.fin = *fin;  // single launch: it may finalize the BatchNorm backward itself
     bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;

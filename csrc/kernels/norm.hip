@@ -1059,6 +1059,17 @@ DTF_API int dtf_bn_bwd_partials(const void* dy, const void* mbits, const void* x
                      coef, (hipStream_t)stream, &sc);
 }
 
+// Backward apply only: the coefficients `coef` (3*C) were already finalized — by the data-gradient GEMM that produced
+// dy (dtf_conv_dgrad_bn's fused finalize). Optional fused projection-shortcut statistics as in dtf_bn_bwd_partials.
+DTF_API int dtf_bn_bwd_apply_coef(const void* dy, const void* mbits, const void* x, long M, int C, void* dx,
+                                  void* dz_out, const float* coef, const void* x2, const float* mean2, float* part2,
+                                  int* rows2, void* stream) {
+  if (C & 7) return -1;
+  const ShortcutStats sc{x2, mean2, part2, rows2};
+  return bn_bwd_tail(dy, nullptr, mbits, x, nullptr, nullptr, nullptr, M, C, dx, dz_out, nullptr, nullptr, 0, nullptr,
+                     0, const_cast<float*>(coef), (hipStream_t)stream, &sc);
+}
+
 // Sum the G partial rows [G][2C] of a BN backward reduction and finalize: dgamma/dbeta and the apply
 // coefficients `coef` (3*C floats). One launch (last-arriver hand-off) when tickets are available.
 static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const float* invstd, const float* gamma,
@@ -1083,7 +1094,7 @@ static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, con
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
                        float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,
                        const ShortcutStats* sc) {
-  bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
+  if (part) bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
   const ColGeo geo = colgeo(C);
   const int grid = ew_grid(M, C);
   const bool fuse_sc = sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&

@@ -26,6 +26,9 @@ _KERNEL_SIGS = {
     "dtf_conv_fwd": [P, P, P, P, P, P] + [I] * 15 + [I, I, I, P],
     "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P, L, P, P, P, P, P, P, P],
     "dtf_conv_dgrad_addsub2": [P, P, P, P, I, I, I, I, I, I, P, L, P, P, P, P, P, P],
+    "dtf_conv_fwd_bn": [P, P, P, P] + [I] * 15 + [I, P, P, P, P, F, F, P, P, P, P, P, P],
+    "dtf_conv_dgrad_bn": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P, P, P, P, I, P, P, P],
+    "dtf_bn_bwd_apply_coef": [P, P, P, L, I, P, P, P, P, P, P, P, P],
     "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P],
     "dtf_conv_wgrad": [P, P, P] + [I] * 15 + [I, I, I, P, L, P],
     "dtf_bn_stats": [P, L, I, P, P, P],

@@ -5,7 +5,8 @@
 
 Every task gets its own process, a free 127.0.0.1 port and a ``TF_CONFIG`` naming the whole
 cluster (chief job ``master``, like the reference). With ``--gpus`` the chief/worker tasks get
-one GPU each through ``DTF_DEVICE_ORDINAL`` (PS tasks too when ``--ps_gpus``), all GPUs staying visible so
+one GPU each through ``DTF_DEVICE_ORDINAL`` (PS tasks too when ``--ps_gpus``), an index into the launcher's own
+visible devices (its ``HIP_VISIBLE_DEVICES`` is inherited unchanged), all of them staying visible so
 the tasks can map each other's HBM (the PS data plane, parallel/ps_shm.py), otherwise
 ``HIP_VISIBLE_DEVICES=''`` (the README runs everything on CPU). Exit code: the first non-zero
 task exit code, else 0. Output lines are prefixed with the task name.
@@ -81,11 +82,10 @@ def launch(cmd, num_ps=1, num_workers=1, num_chief=1, gpus=None, ps_gpus=False, 
         if kv_server is not None:
             e["DTF_KV_ADDR"] = f"127.0.0.1:{kv_server.port}"
         if gpu_list and (t != "ps" or ps_gpus):
-            # every GPU stays visible (a PS shard in one GPU's HBM is mapped by the trainers on the others);
-            # the task's own device is selected by ordinal
+            # every GPU of the launcher's own visible set stays visible (a PS shard in one GPU's HBM is mapped by
+            # the trainers on the others); the task's device is selected by its ordinal WITHIN that set, so
+            # --gpus indexes the caller's HIP_VISIBLE_DEVICES (left untouched), never raw physical ids
             e["DTF_DEVICE_ORDINAL"] = gpu_list[gi % len(gpu_list)]
-            e.pop("HIP_VISIBLE_DEVICES", None)
-            e.pop("CUDA_VISIBLE_DEVICES", None)
             gi += 1
         else:
             e["HIP_VISIBLE_DEVICES"] = ""

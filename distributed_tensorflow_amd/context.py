@@ -25,13 +25,28 @@ def _stack():
     return s
 
 
+def local_ordinal(default=0) -> int:
+    """This process's GPU ordinal among the visible devices: DTF_DEVICE_ORDINAL (set per task by cli.launch, which
+    keeps every GPU visible so PS tasks and trainers can map each other's memory), else LOCAL_RANK (torchrun), else
+    `default`."""
+    return int(os.environ.get("DTF_DEVICE_ORDINAL", os.environ.get("LOCAL_RANK", str(default))))
+
+
 def default_device() -> torch.device:
-    """DTF_DEVICE_ORDINAL (set per task by cli.launch: every GPU stays visible so PS tasks and trainers can map each
-    other's memory), else LOCAL_RANK (torchrun), else GPU 0; the CPU when no GPU is visible."""
+    """The process's own GPU (local_ordinal), or the CPU when no GPU is visible."""
     if torch.cuda.is_available():
-        idx = os.environ.get("DTF_DEVICE_ORDINAL", os.environ.get("LOCAL_RANK", "0"))
-        return torch.device("cuda", int(idx) % max(1, torch.cuda.device_count()))
+        return torch.device("cuda", local_ordinal() % max(1, torch.cuda.device_count()))
     return torch.device("cpu")
+
+
+def bind_device(dev) -> torch.device:
+    """Make `dev` the process's current HIP device. Every kernel wrapper issues on the CURRENT device's stream
+    (ops._util.stream), so a task whose GPU is not ordinal 0 must bind it before its first op — otherwise a copy
+    issued on cuda:k's stream and a kernel issued on cuda:0's stream are unordered."""
+    dev = parse_device(dev)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    return dev
 
 
 def current_device() -> torch.device:

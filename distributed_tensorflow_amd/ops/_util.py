@@ -76,16 +76,40 @@ def fork_side(device, *tensors):
     return torch.cuda.stream(side)
 
 
+_COMM = {}
+_COMM_USED = set()
+
+
+def comm_stream(device):
+    s = _COMM.get(device.index)
+    if s is None:
+        s = _COMM[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
 def comm_stream_ctx(device):
-    """Where to issue a collective over arena gradients: on the side stream (after it has also waited for the
-    main stream) when weight gradients are in flight there — the collective then waits for both without
-    blocking the main stream's dgrad chain — else the current stream."""
+    """Where to issue a collective (or a PS push copy) over arena gradients: a dedicated communication stream
+    that waits on events recorded NOW on the main stream and, when weight gradients are in flight there, on the
+    weight-gradient side stream. Neither compute stream ever waits for the other or for the collective until the
+    step's join (join_comm_stream): the bucket's all-reduce starts the moment both producers have passed this
+    point, while the dgrad chain and the side stream's wgrads keep running (the side stream
+    used to wait for the main stream at every bucket)."""
     import contextlib
-    if device.type != "cuda" or device.index not in _SIDE_USED:
+    if device.type != "cuda":
         return contextlib.nullcontext()
-    side = _SIDE[device.index]
-    side.wait_stream(torch.cuda.current_stream(device))
-    return torch.cuda.stream(side)
+    comm = comm_stream(device)
+    comm.wait_stream(torch.cuda.current_stream(device))  # = record an event on main, make comm wait on it
+    if device.index in _SIDE_USED:
+        comm.wait_stream(_SIDE[device.index])
+    _COMM_USED.add(device.index)
+    return torch.cuda.stream(comm)
+
+
+def join_comm_stream(device):
+    """The current stream waits for everything issued on the communication stream (a no-op when unused)."""
+    if device.type == "cuda" and device.index in _COMM_USED:
+        torch.cuda.current_stream(device).wait_stream(_COMM[device.index])
+        _COMM_USED.discard(device.index)
 
 
 _UPD = {}
@@ -120,8 +144,10 @@ def join_side_streams():
     _SIDE_USED.clear()
 
 
-def stream():
-    return torch.cuda.current_stream().cuda_stream
+def stream(device=None):
+    """Raw handle of the current stream of `device` (default: the current device). Pass the device of the tensors
+    a native call touches when it may differ from the current device."""
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 # ---------------------------------------------------------------- per-step dropout stream

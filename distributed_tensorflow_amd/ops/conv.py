@@ -53,6 +53,19 @@ def conv_fwd_raw(x, w16, g, stats=False, bias=None, act=0):
     return y
 
 
+def conv_fwd_bn_raw(x, w16, g, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean, invstd):
+    """Training ConvBN forward: y plus the output BatchNorm's scale/shift/mean/invstd and running-statistics update,
+    finalized inside the conv launch's tail (gemm_core.h BnFin) — or by the separate reduction + finalize launches
+    when the launch cannot (the native side falls back by itself)."""
+    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
+    y = torch.empty((N, P, Q, K), dtype=BF16, device=x.device)
+    part = torch.empty(((N * P * Q + 63) // 64) * 2 * K, dtype=F32, device=x.device)
+    call("dtf_conv_fwd_bn", ptr(x), ptr(w16), ptr(y), ptr(part), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+         -1, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), float(momentum), float(eps), ptr(scale), ptr(shift),
+         ptr(mean), ptr(invstd), None, stream())
+    return y
+
+
 def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=None):
     """dX (bf16); with `acc` (a bf16 [N,H,W,C] gradient already holding another contribution) the epilogue
     adds into it (beta = 1) and returns it; `acc_mask` (1 bit per element) first zeroes the acc values whose
@@ -70,6 +83,28 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=N
         part = torch.empty(((N * H * W + 63) // 64 + sh * sw) * 2 * C, dtype=F32, device=dy.device)
         rows = IntOut()
     bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
+    if bn is not None and bn.invstd is not None and _FUSE_BN_FIN:
+        # the producing BatchNorm's backward is finalized in this launch's tail: dgamma/dbeta (straight into the
+        # arena gradients when they are direct) and the apply coefficients
+        Kb = C
+        tg, tb = direct_grad(bn.gamma_p), direct_grad(bn.beta_p)
+        direct = tg is not None and tb is not None
+        dgamma = tg if direct else torch.empty(Kb, dtype=F32, device=dy.device)
+        dbeta = tb if direct else torch.empty(Kb, dtype=F32, device=dy.device)
+        coef = torch.empty(3 * Kb, dtype=F32, device=dy.device)
+        fused = IntOut()
+        beta = 1.0 if (acc is not None or acc_sub2 is not None) else 0.0
+        if acc_sub2 is not None:
+            assert acc is None and (R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0)
+        call("dtf_conv_dgrad_bn", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+             beta, ptr(ws), 2 * ws.numel(), *bn_ptrs, ptr(part), rows.addr,
+             ptr(acc_mask) if acc is not None else None, ptr(acc_sub2), ptr(bn.gamma), ptr(bn.invstd),
+             ptr(dgamma), ptr(dbeta), int(direct), ptr(coef), fused.addr, stream())
+        if fused.value:
+            bn.provide_fin(dx, coef, dgamma, dbeta, direct)
+        else:
+            bn.provide(dx, part, rows.value)
+        return dx
     if acc_sub2 is not None:  # + the compact gradient of a stride-2 1x1 shortcut at the even pixels
         assert acc is None and (R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0)
         call("dtf_conv_dgrad_addsub2", ptr(dy), ptr(wc), ptr(dx), ptr(acc_sub2), N, H, W, C, K, -1, ptr(ws),
@@ -195,26 +230,44 @@ class _BNSource:
     gradient) lets the GEMM epilogue write sum(dz), sum(dz*(x-mean)) partial rows; the producing ConvBN's
     backward then skips its reduction pass (bn_bwd_reduce), provided the gradient it receives is exactly the
     tensor that dgrad wrote (same storage: autograd added nothing else to it)."""
-    __slots__ = ("yc", "mbits", "mean", "consumers", "part", "rows", "dptr", "__weakref__")
+    __slots__ = ("yc", "mbits", "mean", "invstd", "gamma", "gamma_p", "beta_p", "consumers", "part", "rows", "dptr",
+                 "fin", "__weakref__")
 
-    def __init__(self, yc, mbits, mean):
+    def __init__(self, yc, mbits, mean, invstd=None, gamma=None, params=(None, None)):
         self.yc, self.mbits, self.mean = yc, mbits, mean
+        # what the consumer's dgrad needs to FINALIZE this BatchNorm's backward too (gemm_core.h BnFin mode 2)
+        self.invstd, self.gamma = invstd, gamma
+        self.gamma_p, self.beta_p = params
         self.consumers = 0
         self.part = self.rows = self.dptr = None
+        self.fin = None
 
     def provide(self, dx, part, rows):
         self.part, self.rows, self.dptr = part, rows, dx.data_ptr()
+        self.fin = None
+
+    def provide_fin(self, dx, coef, dgamma, dbeta, direct):
+        self.part, self.rows, self.dptr = None, None, dx.data_ptr()
+        self.fin = (coef, dgamma, dbeta, direct)
 
     def take(self, dout):
-        """The partial rows for this gradient, or None (then the regular reduction runs)."""
-        part, rows, dptr = self.part, self.rows, self.dptr
-        self.part = self.rows = self.dptr = None
-        if part is None or rows < 1 or dout.data_ptr() != dptr or not dout.is_contiguous():
+        """("partials", part, rows) for this gradient, ("coef", coef, dgamma, dbeta, direct) when the consumer's dgrad
+        already finalized it, or None (then the regular reduction runs)."""
+        part, rows, dptr, fin = self.part, self.rows, self.dptr, self.fin
+        self.part = self.rows = self.dptr = self.fin = None
+        if dptr is None or dout.data_ptr() != dptr or not dout.is_contiguous():
             return None
-        return part, rows
+        if fin is not None:
+            return ("coef",) + fin
+        if part is None or rows < 1:
+            return None
+        return "partials", part, rows
 
 
 _FUSE_BN_BWD = __import__("os").environ.get("DTF_FUSE_BN_BWD", "1") != "0"
+# BatchNorm finalize (forward statistics, backward reductions) in the tail of the producing GEMM launch instead of
+# separate row-reduction + finalize launches (gemm_core.h BnFin); DTF_BN_FIN_FUSED=0 turns it off (native side too)
+_FUSE_BN_FIN = __import__("os").environ.get("DTF_BN_FIN_FUSED", "1") != "0"
 _LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
 _DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
 _COMPACT_PROJ = __import__("os").environ.get("DTF_COMPACT_PROJ", "1") != "0"
@@ -239,9 +292,8 @@ class _ConvBNFn(torch.autograd.Function):
         work = torch.empty(4 * K, dtype=F32, device=dev)  # scale shift mean invstd
         scale, shift, mean, invstd = work[:K], work[K:2 * K], work[2 * K:3 * K], work[3 * K:]
         if training:
-            yc, part, rows = conv_fwd_raw(x, bf16_shadow(w), g, stats=True)
-            call("dtf_bn_finalize", ptr(part), rows, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, K,
-                 float(momentum), float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
+            yc = conv_fwd_bn_raw(x, bf16_shadow(w), g, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean,
+                                 invstd)
         else:
             yc = conv_fwd_raw(x, bf16_shadow(w), g)
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
@@ -274,7 +326,7 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.res_src = res_src if (training and _FUSE_BN_BWD) else None
         ctx.src = None
         if training and _FUSE_BN_BWD and any(ctx.needs_input_grad):
-            src = _BNSource(yc, mbits, mean)
+            src = _BNSource(yc, mbits, mean, invstd, gamma, (gamma, beta))
             out._dtf_bnsrc = src
             ctx.src = src
         return out
@@ -303,10 +355,17 @@ class _ConvBNFn(torch.autograd.Function):
         if rsrc is not None:  # projection shortcut BN: its backward reduction rides on our apply pass
             part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=yc.device), IntOut()
             sc = (ptr(rsrc.yc), ptr(rsrc.mean), ptr(part2), rows2.addr)
-        if fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
+        if fused is not None and fused[0] == "coef":
+            # the consumer's dgrad launch reduced AND finalized this BatchNorm's backward: only the apply is left
+            coef, fg, fb, fdirect = fused[1:]
+            call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(mbits), ptr(yc), M, K, ptr(dyc), ptr(dres), ptr(coef), *sc,
+                 stream())
+            direct_bn = fdirect
+            dgamma, dbeta = fg, fb
+        elif fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
             coef = torch.empty(3 * K, dtype=F32, device=yc.device)
             call("dtf_bn_bwd_partials", ptr(dout), ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
-                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(fused[0]), fused[1], ptr(coef),
+                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(fused[1]), fused[2], ptr(coef),
                  *sc, stream())
         else:
             work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
@@ -395,9 +454,7 @@ class _ConvBNPoolFn(torch.autograd.Function):
         work = torch.empty(4 * K, dtype=F32, device=dev)  # scale shift mean invstd
         scale, shift, mean, invstd = work[:K], work[K:2 * K], work[2 * K:3 * K], work[3 * K:]
         if training:
-            yc, part, rows = conv_fwd_raw(x, w16, g, stats=True)
-            call("dtf_bn_finalize", ptr(part), rows, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), M, K,
-                 float(momentum), float(eps), ptr(scale), ptr(shift), ptr(mean), ptr(invstd), stream())
+            yc = conv_fwd_bn_raw(x, w16, g, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean, invstd)
         else:
             yc = conv_fwd_raw(x, w16, g)
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),

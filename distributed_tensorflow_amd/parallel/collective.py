@@ -79,7 +79,8 @@ class GradientBucketer:
         # exposed-communication timing (bench): events around the wait for the last buckets, per step
         self.timing = False
         self._timed = []
-        cap = int((bucket_mb if bucket_mb is not None else _DEFAULT_BUCKET_MB) * (1 << 20) / 4)
+        self.bucket_mb = float(bucket_mb if bucket_mb is not None else _DEFAULT_BUCKET_MB)
+        cap = int(self.bucket_mb * (1 << 20) / 4)
         nv = len(arena.variables)
         self.buckets = []          # [start, end) element ranges of arena.grad
         self.var_bucket = [0] * nv
@@ -188,6 +189,8 @@ class GradientBucketer:
 
     def finalize(self):
         """Issue buckets whose variables got no gradient (in order), then wait for all of them."""
+        # buckets the post-accumulate hooks launched DURING backward (the overlap actually happened)
+        self.launched_in_backward = self._next
         if self.arena.grad.is_cuda:
             from ..ops._util import join_side_streams
             join_side_streams()
@@ -201,14 +204,18 @@ class GradientBucketer:
         if self._opt is not None:
             # every bucket was updated on the update stream: the step's tail is its last updates
             if self.arena.grad.is_cuda:
-                from ..ops._util import join_update_stream
+                from ..ops._util import join_comm_stream, join_update_stream
                 join_update_stream(self.arena.grad.device)
+                join_comm_stream(self.arena.grad.device)
             self._opt = None
             self.updated = True
         else:
             for w in self._works:
                 if w is not None:
                     w.wait()
+            if self.arena.grad.is_cuda:
+                from ..ops._util import join_comm_stream
+                join_comm_stream(self.arena.grad.device)
             if self.wire == "bf16" and self.collective:
                 for lo, hi in self.buckets:
                     _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])
@@ -311,6 +318,9 @@ class ShardedGradientBucketer(GradientBucketer):
         for w in self._works:
             if w is not None:
                 w.wait()
+        if self.arena.grad.is_cuda:
+            from ..ops._util import join_comm_stream
+            join_comm_stream(self.arena.grad.device)
         for b, r in self._recv.items():
             s, _, _, c = self.shards[b]
             _cast(r, self.sgrad[c:c + s])

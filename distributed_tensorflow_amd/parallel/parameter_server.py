@@ -148,7 +148,7 @@ class ParameterServer:
         self.num_trainers = len(self.r.trainer_tasks())
         host, port = _host_port(self.r.cluster.task_address("ps", self.index))
         self.lib = _native.runtime()
-        self.device = context.parse_device(device) if device is not None else context.default_device()
+        self.device = context.bind_device(device if device is not None else context.default_device())
         kh, kp = kv_address(self.r)
         self.kv = KVClient(kh, kp, timeout_s=kv_timeout_s)
         self._hb = Heartbeat(self.kv, f"ps{self.index}").start()
@@ -210,10 +210,14 @@ class ParameterServer:
                 self.lib.dtfrt_ps_register(self.srv, 2 + k, m.data_ptr(), m.numel() * 4)
         self.kv.set(f"ps/{self.index}/ready", "1")
 
-    def apply_flat(self, t, assign=False):
+    def apply_flat(self, t, assign=False, consumed=None):
         """Apply one request whose payload `t` is in this shard's arena layout (the shm transport's inbox):
-        ASSIGN overwrites the variables and resets the slots, a gradient push runs the fused optimizer."""
+        ASSIGN overwrites the variables and resets the slots, a gradient push runs the fused optimizer.
+        consumed(): called once `t` has been read (copied into the arena's gradient buffer) and before the update
+        is issued — the pusher may then refill `t` while the update runs."""
         if self.arena is None:
+            if consumed is not None:
+                consumed()
             return
         if assign:
             self.arena.flat.copy_(t)
@@ -221,6 +225,12 @@ class ParameterServer:
                 self.arena.slots[nm].fill_(init)
         else:
             self.arena.grad.copy_(t)
+            if consumed is not None:
+                if self.arena.grad.is_cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(self.arena.grad.device))
+                    ev.synchronize()  # only the inbox copy (queued behind the previous update), not the device
+                consumed()
             self.opt.apply_arena(self.arena, zero_grad=True)
             self.applies += 1
 
@@ -294,8 +304,60 @@ def run_parameter_server(resolver=None, device=None):
 
 
 # ---------------------------------------------------------------------------- worker side
+class PSPushBucketer:
+    """Overlaps a trainer's gradient push with its backward pass (shm transport, GPU trainer).
+
+    The arena gradient is cut into buckets in reverse variable order (collective.GradientBucketer's cut, hooks and
+    issue order); the moment a bucket's last gradient lands, its slice is copied into the PS inboxes (peer copies
+    over xGMI for a GPU PS) on the communication stream, which waits on events of the main and the weight-gradient
+    side stream (ops._util.comm_stream_ctx). After backward only the last buckets' copies remain; the PS tasks are
+    told once they landed (ShmPSClient.post_push)."""
+
+    def __init__(self, arena, client, bucket_mb=None):
+        from .collective import GradientBucketer
+        self.client = client
+        bucketer = self
+
+        class _B(GradientBucketer):
+            def _launch(self, b):
+                lo, hi = self.buckets[b]
+                from ..ops._util import comm_stream_ctx
+                with comm_stream_ctx(self.arena.grad.device):
+                    bucketer.client.copy_range(self.arena.grad, lo, hi)
+
+        self.b = _B(arena, bucket_mb=bucket_mb, collective=False).install()
+
+    def begin(self):
+        self.client.wait_pending()  # the inboxes are free again (the previous push was consumed)
+        self.b.enabled = True
+
+    def finalize(self):
+        from ..ops._util import comm_stream, join_comm_stream, join_side_streams
+        b = self.b
+        dev = b.arena.grad.device
+        join_side_streams()
+        while b._next < len(b.buckets):
+            b._launch(b._next)
+            b._next += 1
+        ev = torch.cuda.Event()
+        ev.record(comm_stream(dev))
+        ev.synchronize()  # every inbox copy has landed before the PS tasks are told
+        join_comm_stream(dev)
+        b.reset()
+        b.enabled = False
+
+    def remove(self):
+        self.b.remove()
+
+
 class ParameterServerStrategy(Strategy):
-    def __init__(self, cluster_resolver=None, variable_partitioner="round_robin", device=None, kv_timeout_s=900):
+    def __init__(self, cluster_resolver=None, variable_partitioner="round_robin", device=None, kv_timeout_s=900,
+                 staleness=None, overlap_push=None):
+        """staleness: 0 — a push returns after every PS applied it (TF's synchronous-apply-per-step semantics);
+        1 — it returns once the PS consumed the gradient bytes and the trainer moves on while the update runs
+        (default for GPU trainers on the shm transport; see ps_shm.ShmPSClient). overlap_push: copy gradient buckets
+        into the PS inboxes during backward (default on for GPU trainers on the shm transport; DTF_PS_OVERLAP=0
+        turns it off)."""
         super().__init__()
         self.r = cluster_resolver or TFConfigClusterResolver()
         if self.r.standalone or self.r.cluster.num_tasks("ps") == 0:
@@ -305,7 +367,7 @@ class ParameterServerStrategy(Strategy):
         self.partitioner = variable_partitioner
         self.num_ps = self.r.cluster.num_tasks("ps")
         self.num_trainers = len(self.r.trainer_tasks())
-        self._device = context.parse_device(device) if device is not None else context.default_device()
+        self._device = context.bind_device(device if device is not None else context.default_device())
         kh, kp = kv_address(self.r)
         self._kv_server = None
         if self.r.is_chief and not os.environ.get("DTF_KV_ADDR"):
@@ -319,6 +381,13 @@ class ParameterServerStrategy(Strategy):
         self._assign = {}
         self.kv_timeout_s = kv_timeout_s
         self.transport = negotiate_transport(self.kv, self.r, self._device, kv_timeout_s)
+        gpu_shm = self.transport == "shm" and self._device.type == "cuda"
+        env_st = os.environ.get("DTF_PS_STALENESS")
+        self.staleness = int(staleness if staleness is not None else env_st if env_st else (1 if gpu_shm else 0))
+        self.overlap_push = gpu_shm and (overlap_push if overlap_push is not None
+                                         else os.environ.get("DTF_PS_OVERLAP", "1") != "0")
+        self._push_b = None
+        self._pushed = False
 
     # ---- properties
     @property
@@ -355,7 +424,7 @@ class ParameterServerStrategy(Strategy):
             if self._shm is None:
                 from .ps_shm import ShmPSClient
                 self._shm = ShmPSClient(self.kv, self.num_ps, self.worker_index, self._arena.flat.device,
-                                        self._segments, self.kv_timeout_s)
+                                        self._segments, self.kv_timeout_s, staleness=self.staleness)
             return self._shm
         if self._clients is None:
             self._clients = [PSClient(*_host_port(self.r.cluster.task_address("ps", i))) for i in
@@ -473,9 +542,27 @@ class ParameterServerStrategy(Strategy):
     def _overlap_bucketer(self, arena, optimizer):
         return None  # the parameter servers own the update
 
+    def backward(self, loss, arena, optimizer=None):
+        """Backward with the gradient push overlapped bucket by bucket (PSPushBucketer) when enabled."""
+        if not (self.overlap_push and arena is getattr(self, "_arena", None)) or \
+                torch.cuda.is_current_stream_capturing():
+            loss.backward()
+            return
+        if self._push_b is None:
+            self._push_b = PSPushBucketer(arena, self._connect())
+        self._push_b.begin()
+        loss.backward()
+        self._push_b.finalize()
+        self._pushed = True
+
     def apply_gradients(self, optimizer, arena):
-        """Async step: push this worker's gradients, the PS applies them, pull fresh values."""
-        self._push_all(GRAD)
+        """Async step: push this worker's gradients (already in the inboxes when backward overlapped the copies),
+        the PS applies them, pull fresh values."""
+        if self._pushed:
+            self._pushed = False
+            self._connect().post_push()
+        else:
+            self._push_all(GRAD)
         arena.grad.zero_()
         self._pull_all()
         with torch.no_grad():

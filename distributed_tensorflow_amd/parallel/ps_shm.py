@@ -32,7 +32,7 @@ import torch
 from .. import _native
 from .._runtime_sigs import err
 
-OP_PUSH, OP_ASSIGN, OP_DONE = 1, 2, 3
+OP_PUSH, OP_ASSIGN, OP_DONE, OP_PUSH_ASYNC = 1, 2, 3, 4
 
 
 def _rt():
@@ -73,6 +73,34 @@ class _Region:
             self._shm = None
 
 
+_IPC_MAPS = {}  # (handle hex, local device index) -> [mapped base, open count]
+
+
+def _ipc_open(handle_hex, device):
+    """Map a peer allocation once per process: several exported PS regions (inbox, parameters, slots) can live in
+    ONE caching-allocator segment and so carry the same IPC handle; each distinct handle is opened once and
+    reference-counted (repeated hipIpcOpenMemHandle / close of one handle is driver-dependent)."""
+    key = (handle_hex, device.index)
+    ent = _IPC_MAPS.get(key)
+    if ent is None:
+        base = ctypes.c_void_p()
+        _native.call("dtf_ipc_open", bytes.fromhex(handle_hex), ctypes.addressof(base))
+        ent = _IPC_MAPS[key] = [base.value, 0]
+    ent[1] += 1
+    return ent[0]
+
+
+def _ipc_release(handle_hex, device):
+    key = (handle_hex, device.index)
+    ent = _IPC_MAPS.get(key)
+    if ent is None:
+        return
+    ent[1] -= 1
+    if ent[1] <= 0:
+        _native.call("dtf_ipc_close", ent[0])
+        del _IPC_MAPS[key]
+
+
 class _Remote:
     """A trainer's mapping of one PS region: copy_in / copy_out between a local f32 slice and the region."""
 
@@ -80,13 +108,13 @@ class _Remote:
         self.desc, self.numel = desc, int(desc["numel"])
         self.device = device
         self._shm = None
+        self._mapped = False
         if desc["kind"] == "hip":
             if device.type != "cuda":
                 raise RuntimeError("the PS shard lives in GPU memory but this task has no GPU")
-            base = ctypes.c_void_p()
-            _native.call("dtf_ipc_open", bytes.fromhex(desc["handle"]), ctypes.addressof(base))
-            self._base = base.value
-            self.ptr = base.value + int(desc["offset"])
+            self._base = _ipc_open(desc["handle"], device)
+            self._mapped = True
+            self.ptr = self._base + int(desc["offset"])
             self.tensor = None
         else:
             nbytes = max(4, self.numel * 4)
@@ -104,7 +132,7 @@ class _Remote:
             self.tensor[offset:offset + n].copy_(src.detach().reshape(-1).cpu() if src.is_cuda else src.reshape(-1))
         else:
             from ..ops._util import stream
-            _native.call("dtf_memcpy_async", self.ptr + 4 * offset, src.data_ptr(), 4 * n, stream())
+            _native.call("dtf_memcpy_async", self.ptr + 4 * offset, src.data_ptr(), 4 * n, stream(src.device))
 
     def copy_out(self, dst, offset=0):
         """dst <- region[offset:offset+n]."""
@@ -113,20 +141,23 @@ class _Remote:
             dst.reshape(-1).copy_(self.tensor[offset:offset + n])
         else:
             from ..ops._util import stream
-            _native.call("dtf_memcpy_async", dst.data_ptr(), self.ptr + 4 * offset, 4 * n, stream())
+            _native.call("dtf_memcpy_async", dst.data_ptr(), self.ptr + 4 * offset, 4 * n, stream(dst.device))
 
     def close(self):
         if self._shm is not None:
             _rt().dtfrt_shmem_close(self._shm[0], self._shm[1], None, 0)
             self._shm = None
-        elif self.desc["kind"] == "hip" and getattr(self, "_base", None):
-            _native.call("dtf_ipc_close", self._base)
-            self._base = None
+        elif self._mapped:
+            _ipc_release(self.desc["handle"], self.device)
+            self._mapped = False
 
 
 def _sync(device):
+    """Host waits for the work issued so far on `device`'s current stream (one recorded event, not the device)."""
     if device.type == "cuda":
-        torch.cuda.current_stream(device).synchronize()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        ev.synchronize()
 
 
 # ---------------------------------------------------------------------------------------------- PS side
@@ -178,19 +209,28 @@ class ShmPSServer:
                 if not forever and self.kv.wait_ge("done", self.T, timeout_s=0):
                     break
                 continue
-            t, status = slot.value, 0
+            t, status, acked = slot.value, 0, [False]
+
+            def ack_early(t=t, s=seq.value):
+                # the inbox has been consumed (the gradient copy landed): the trainer may refill it while the update
+                # itself is still running — an OP_PUSH_ASYNC trainer does not wait for the apply (bounded staleness 1)
+                lib.dtfrt_mbox_complete(self.mbox, t, s, 0)
+                acked[0] = True
             try:
                 if op.value == OP_DONE:
                     finished.add(t)
                 elif self.ps.arena is not None:
                     inbox = self.inboxes[t].tensor[:self.ps.arena.numel]
-                    self.ps.apply_flat(inbox, assign=(op.value == OP_ASSIGN))
+                    early = op.value == OP_PUSH_ASYNC
+                    self.ps.apply_flat(inbox, assign=(op.value == OP_ASSIGN), consumed=ack_early if early else None)
                     self._publish(slots=(op.value == OP_ASSIGN or self.ps.applies % self.ps.slot_sync_every == 0))
-                    _sync(self.dev)  # the parameters a trainer pulls next are the updated ones
+                    if not early:
+                        _sync(self.dev)  # OP_PUSH / OP_ASSIGN: the parameters a trainer pulls next are the updated ones
             except Exception as e:  # report to the pushing trainer instead of dying silently
                 print(f"[ps{self.ps.index}] request {op.value} from trainer {t} failed: {e}", flush=True)
                 status = -7
-            lib.dtfrt_mbox_complete(self.mbox, t, seq.value, status)
+            if not acked[0]:
+                lib.dtfrt_mbox_complete(self.mbox, t, seq.value, status)
         self._publish(slots=True)
 
     def close(self):
@@ -216,9 +256,15 @@ class ShmPSClient:
     segments[p]: list of (arena_offset, shard_offset, numel) runs of the trainer's arena that belong to PS p (one
     run when the arena is grouped by PS)."""
 
-    def __init__(self, kv, num_ps, trainer_index, device, segments, timeout_s=900):
+    def __init__(self, kv, num_ps, trainer_index, device, segments, timeout_s=900, staleness=0):
         self.kv, self.P, self.t, self.dev = kv, num_ps, trainer_index, device
         self.segments = segments
+        # staleness 0: a push returns once every PS applied it (the next pull sees this trainer's update, TF's
+        # sess.run(train_op) semantics); 1: a push returns once its bytes are in the inboxes — the PS acknowledges
+        # as soon as it has consumed them, and the trainer only waits for that acknowledgement before it refills the
+        # inbox on its NEXT push (its next pull may miss its own latest update: Hogwild with staleness <= 1)
+        self.staleness = int(staleness)
+        self._pending = []
         self.timeout_ms = int(timeout_s * 1000)
         self.desc = [kv.get_json(f"ps/{p}/shm", timeout_s=timeout_s) for p in range(num_ps)]
         self.inbox = [_Remote(d["inboxes"][trainer_index], device) for d in self.desc]
@@ -232,21 +278,56 @@ class ShmPSClient:
                 raise ConnectionError(err(lib))
             self.mbox.append(h)
 
-    def _post_all(self, op, ps_list):
+    def _wait(self, seqs, op):
         lib = _rt()
-        seqs = [(p, lib.dtfrt_mbox_post(self.mbox[p], self.t, op, 0)) for p in ps_list]
         for p, s in seqs:
             st = lib.dtfrt_mbox_wait(self.mbox[p], self.t, s, self.timeout_ms)
             if st != 0:
                 raise ConnectionError(f"ps{p}: request {op} failed ({st}): {err(lib)}")
 
+    def _post_all(self, op, ps_list, wait=True):
+        lib = _rt()
+        seqs = [(p, lib.dtfrt_mbox_post(self.mbox[p], self.t, op, 0)) for p in ps_list]
+        if wait:
+            self._wait(seqs, op)
+        else:
+            self._pending = seqs
+
+    def wait_pending(self):
+        """Block until the PS tasks consumed this trainer's previous push (its inboxes may be refilled)."""
+        if self._pending:
+            seqs, self._pending = self._pending, []
+            self._wait(seqs, OP_PUSH_ASYNC)
+
+    def _ps_list(self):
+        return [p for p in range(self.P) if self.segments[p]]
+
+    def copy_range(self, src_flat, lo, hi):
+        """Issue the inbox copies of the arena elements [lo, hi) on the current stream (one bucket of a push)."""
+        for p in self._ps_list():
+            for ao, so, n in self.segments[p]:
+                a, b = max(ao, lo), min(ao + n, hi)
+                if a < b:
+                    self.inbox[p].copy_in(src_flat[a:b], so + (a - ao))
+
+    def post_push(self):
+        """Tell every PS that this trainer's gradient is in its inbox (the copies must have landed)."""
+        if self.staleness > 0:
+            self._post_all(OP_PUSH_ASYNC, self._ps_list(), wait=False)
+        else:
+            self._post_all(OP_PUSH, self._ps_list())
+
     def _send(self, src_flat, op):
-        ps_list = [p for p in range(self.P) if self.segments[p]]
+        self.wait_pending()
+        ps_list = self._ps_list()
         for p in ps_list:
             for ao, so, n in self.segments[p]:
                 self.inbox[p].copy_in(src_flat[ao:ao + n], so)
         _sync(self.dev)  # the inbox bytes have landed before the PS is told
-        self._post_all(op, ps_list)
+        if op == OP_PUSH:
+            self.post_push()
+        else:
+            self._post_all(op, ps_list)
 
     def push(self, grad_flat):
         self._send(grad_flat, OP_PUSH)
@@ -255,10 +336,11 @@ class ShmPSClient:
         self._send(flat, OP_ASSIGN)
 
     def pull(self, flat):
+        """flat <- the live PS parameters. GPU PS: peer copies on the current stream (stream-ordered before every
+        later kernel: no host wait); CPU PS: host copies."""
         for p in range(self.P):
             for ao, so, n in self.segments[p]:
                 self.params[p].copy_out(flat[ao:ao + n], so)
-        _sync(self.dev)
 
     def pull_slots(self, nslots, like):
         out = [torch.zeros_like(like) for _ in range(nslots)]
@@ -266,10 +348,10 @@ class ShmPSClient:
             for k in range(nslots):
                 for ao, so, n in self.segments[p]:
                     self.slots[p][k].copy_out(out[k][ao:ao + n], so)
-        _sync(self.dev)
         return out
 
     def done(self):
+        self.wait_pending()
         self._post_all(OP_DONE, list(range(self.P)))
 
     def close(self):

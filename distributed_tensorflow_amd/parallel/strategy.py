@@ -244,8 +244,10 @@ class MultiWorkerMirroredStrategy(Strategy):
             port = int(port)
             self._local_rank = int(os.environ.get("LOCAL_RANK", self._rank if torch.cuda.device_count() > 1 else 0))
         if torch.cuda.is_available():
-            dev = torch.device("cuda", self._local_rank % torch.cuda.device_count())
-            torch.cuda.set_device(dev)
+            # the launcher's per-task ordinal (cli.launch --gpus) wins over the rank-derived one
+            ordinal = context.local_ordinal(self._local_rank) if "DTF_DEVICE_ORDINAL" in os.environ \
+                else self._local_rank
+            dev = context.bind_device(torch.device("cuda", ordinal % torch.cuda.device_count()))
         else:
             dev = torch.device("cpu")
         self._device = dev
@@ -329,10 +331,15 @@ class MultiWorkerMirroredStrategy(Strategy):
             if isinstance(b, collective.ShardedGradientBucketer):
                 b.gather_slots(optimizer)
 
-    def agree(self, flag):
-        """Rank 0's decision (e.g. a time-based checkpoint trigger) on every replica."""
+    def agree(self, flag, every=16):
+        """Rank 0's decision (e.g. a time-based checkpoint trigger) on every replica. The decision is exchanged
+        only on every `every`-th call (all replicas count calls identically, so they consult together); on the
+        other calls it is False without a collective — no per-batch broadcast + host sync."""
         if self._world <= 1 or not self.shard_optimizer:
             return flag
+        self._agree_calls = getattr(self, "_agree_calls", 0) + 1
+        if self._agree_calls % max(1, int(every)):
+            return False
         t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=self._device)
         dist.broadcast(t, src=0)
         return bool(t.item())

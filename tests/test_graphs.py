@@ -119,9 +119,13 @@ def test_overlapped_update_bitwise_equals_single_update(cuda, model, monkeypatch
         torch.cuda.synchronize()
         b = s._bucketers.get(id(m._arena))
         res.append((ls, [w.detach().clone() for w in m.trainable_variables],
-                    0 if b is None else len(b.buckets), [w.name for w in m.trainable_variables]))
+                    0 if b is None else len(b.buckets), [w.name for w in m.trainable_variables],
+                    0 if b is None else b.launched_in_backward))
         s._bucketers.clear()
     assert res[1][2] > 3, "expected several buckets with the overlapped update"
+    # the hooks must fire DURING backward for direct-gradient layers (conv/dense weight gradients accumulated
+    # into the arena and returned as None), the tied GPT-2 embedding included: most buckets update early
+    assert res[1][4] >= res[1][2] // 2, (res[1][4], res[1][2])
     bad = [(n, float((a - b).abs().max()), float(a.abs().max()))
            for n, a, b in zip(res[0][3], res[0][1], res[1][1])
            if not torch.allclose(a, b, rtol=2.5e-7, atol=1e-9)]

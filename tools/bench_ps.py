@@ -12,8 +12,11 @@ copied into per-trainer inboxes in the PS's HBM (HIP IPC, xGMI between GPUs) and
 shared-memory mailbox carries the requests (parallel/ps_shm.py); `--ps_cpu` keeps the shards in host shared memory.
 Training is asynchronous as in the reference: every trainer pushes its gradients to the PS shards after each step
 and continues with the values it pulls.
-Each trainer times its own `--steps` steps after `--warmup`; the chief sums the trainers' images/sec and
-prints one JSON line (metric: images/sec whole node, async PS).
+After `--warmup` steps every trainer waits at a coordination-store barrier, then runs `--steps` steps; each reports
+its wall-clock (start, end) window and the chief prints one JSON line whose value is ALL images processed divided by
+(latest end - earliest start): a whole-node throughput over one common window (summing per-trainer
+rates over non-coincident windows overstated it). With at least as many GPUs as tasks it also checks that every
+task sits on its own GPU and that the trainers reach the PS shards through the HIP-IPC peer path.
 """
 import argparse
 import json
@@ -75,17 +78,30 @@ def task(a):
     for _ in range(a.warmup):
         logs = model.train_step(next(data))
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    # every trainer starts its timed window together (coordination-store barrier)
+    strat.kv.add("bench/ready", 1)
+    strat.kv.wait_ge("bench/ready", strat.num_workers, timeout_s=600)
+    t0 = time.time()
     for _ in range(a.steps):
         logs = model.train_step(next(data))
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    ips = a.batch * a.steps / dt
-    strat.kv.set(f"bench/{strat.worker_index}", json.dumps({"ips": ips, "ms": dt / a.steps * 1e3,
-                                                            "loss": float(logs["loss"])}))
+    t1 = time.time()
+    ips = a.batch * a.steps / (t1 - t0)
+    peer = bool(strat._shm is not None and any(r_.desc.get("kind") == "hip" for r_ in strat._shm.inbox))
+    strat.kv.set(f"bench/{strat.worker_index}", json.dumps({"ips": ips, "ms": (t1 - t0) / a.steps * 1e3,
+                                                            "t0": t0, "t1": t1, "loss": float(logs["loss"]),
+                                                            "ipc_peer": peer}))
     if strat.is_chief:
         res = [json.loads(strat.kv.get(f"bench/{i}").decode()) for i in range(strat.num_workers)]
-        total = sum(x["ips"] for x in res)
+        span = max(x["t1"] for x in res) - min(x["t0"] for x in res)
+        total = a.batch * a.steps * len(res) / span
+        roles = [f"ps{i}" for i in range(r.cluster.num_tasks("ps"))] + [f"{t}{i}" for t, i in r.trainer_tasks()]
+        devs = {ro: json.loads(strat.kv.get(f"task/{ro}/dev").decode())["device"] for ro in roles}
+        own_gpu = len(set(devs.values())) == len(devs) and all(d.startswith("cuda") for d in devs.values())
+        if a.gpus >= len(roles) and not ps_cpu:
+            # the 8-GPU layout must really be one task per GPU over the IPC peer path
+            assert own_gpu, f"tasks share GPUs: {devs}"
+            assert strat.transport == "shm" and all(x["ipc_peer"] for x in res), "PS data plane is not HIP IPC"
         print(json.dumps({
             "metric": f"images/sec (whole node) ResNet-{a.depth} bf16, ParameterServerStrategy (async)",
             "value": round(total, 2), "unit": "images/sec", "n_gpus": a.gpus, "steps": a.steps,
@@ -94,6 +110,11 @@ def task(a):
             "config": {"model": f"ResNet-{a.depth} v1.5", "per_trainer_batch": a.batch,
                        "ps_tasks": r.cluster.num_tasks("ps"), "trainers": strat.num_workers,
                        "ps_device": "cpu" if ps_cpu else "gpu", "transport": strat.transport,
+                       "staleness": strat.staleness, "overlap_push": strat.overlap_push,
+                       "task_devices": devs, "one_task_per_gpu": own_gpu,
+                       "ipc_peer_path": all(x["ipc_peer"] for x in res),
+                       "aggregate": "all images / (latest end - earliest start) after a store barrier",
+                       "window_s": round(span, 3),
                        "per_trainer_images_per_sec": [round(x["ips"], 1) for x in res]}}), flush=True)
     strat.shutdown()
     return 0
