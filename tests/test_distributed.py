@@ -203,14 +203,17 @@ def test_ps_runbook_negotiated_transport(tmp_path, transport):
 
 
 @pytest.mark.slow
-def test_ps_shm_two_ps_six_trainers(tmp_path):
+@pytest.mark.parametrize("staleness", ["0", "1"])
+def test_ps_shm_two_ps_six_trainers(tmp_path, staleness):
     """BASELINE config 4's topology (2 PS + 6 trainers) on the CPU through ONE serve loop per PS: 6 trainers
     (master + 5 workers) push/pull concurrently through the shared-memory mailbox; every update is applied
-    (global_step counts all of them) and the model converges (async SGD, reference trainer/task.py:232-236)."""
+    (global_step counts all of them) and the model converges (async SGD, reference trainer/task.py:232-236).
+    staleness 1: pushes return once the PS consumed the inbox (OP_PUSH_ASYNC), the trainer only waits for that
+    acknowledgement before refilling its inbox on the next push — still every push applied exactly once."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", DTF_PS_STALENESS=staleness)
     env.pop("DTF_PS_TRANSPORT", None)
     env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     cmd = [sys.executable, "-m", "distributed_tensorflow_amd.cli.launch", "--ps", "2", "--workers", "5", "--chief",
@@ -268,3 +271,35 @@ def test_overlapped_bucket_update_matches_single_update(monkeypatch):
         assert nb > 2 and ia == ib == 8
         for u, v in zip(a, b):
             np.testing.assert_allclose(u, v, rtol=1e-6, atol=1e-7)
+
+
+def test_launcher_gpu_ordinals_keep_callers_visible_set():
+    """cli.launch --gpus: every chief/worker task gets DTF_DEVICE_ORDINAL = its entry of --gpus, an index INTO the
+    caller's visible devices, and the caller's HIP_VISIBLE_DEVICES passes through unchanged (popping it
+    turned --gpus indices into physical ids outside the allowed set)."""
+    import io
+    import sys
+    from distributed_tensorflow_amd.cli.launch import launch
+    code = ("import os, json; print(json.dumps({'role': os.environ['DTF_ROLE'], "
+            "'ord': os.environ.get('DTF_DEVICE_ORDINAL'), 'vis': os.environ.get('HIP_VISIBLE_DEVICES')}))")
+    buf = io.StringIO()
+    rc, _ = launch([sys.executable, "-c", code], num_ps=1, num_workers=1, num_chief=1, gpus="1,0",
+                   env={"HIP_VISIBLE_DEVICES": "3,5"}, timeout=60, log=buf)
+    assert rc == 0, buf.getvalue()
+    import json
+    got = {d["role"]: d for d in (json.loads(l.split("] ", 1)[1]) for l in buf.getvalue().splitlines() if "{" in l)}
+    assert got["master0"]["ord"] == "1" and got["worker0"]["ord"] == "0", got
+    assert got["master0"]["vis"] == "3,5" and got["worker0"]["vis"] == "3,5", got
+    assert got["ps0"]["ord"] is None and got["ps0"]["vis"] == "", got  # PS on CPU unless --ps_gpus
+
+
+def test_agree_exchanges_only_every_nth_call(monkeypatch):
+    """ZeRO-1 + a wall-clock checkpoint trigger: rank 0's decision is broadcast only every `every`-th batch, never
+    per batch."""
+    from distributed_tensorflow_amd.parallel import strategy as S
+    s = S.MultiWorkerMirroredStrategy.__new__(S.MultiWorkerMirroredStrategy)
+    s._world, s.shard_optimizer, s._device = 2, True, torch.device("cpu")
+    calls = []
+    monkeypatch.setattr(S.dist, "broadcast", lambda t, src=0: calls.append(int(t.item())))
+    out = [s.agree(True, every=4) for _ in range(8)]
+    assert out == [False, False, False, True] * 2 and len(calls) == 2

@@ -118,3 +118,31 @@ def test_bert_tiny_trains_like_cpu_reference(cuda):
     worst = max((_rel(gw[k], cw[k]), k) for k in cw if cw[k].size > 1 and np.linalg.norm(cw[k]) > 0)
     assert worst[0] < 0.05, worst
 
+
+
+def test_gpt2_tiny_fp8_trains_like_bf16(cuda):
+    """The fp8 configuration of BASELINE.json:11 on a tiny GPT-2: every projection GEMM on the block-scaled fp8 MFMA
+    (e4m3 x e4m3 forward, e5m2 x e4m3 backward, delayed per-tensor scaling) against the same model, initial weights
+    and batches in bf16. 30 AdamW steps over 3 revisited batches: the loss curves must agree within 5% at every step
+    and both must learn (a whole-model fp8 test)."""
+    from distributed_tensorflow_amd.models.transformer import GPT2
+    g = torch.Generator().manual_seed(4)
+    V, S, B = 512, 128, 4
+    batches = [(torch.randint(0, V, (B, S), generator=g), None) for _ in range(3)]
+    batches = [(x, torch.roll(x, -1, 1)) for x, _ in batches] * 10
+
+    def run(fp8):
+        def model_fn():
+            initializers.set_seed(21)
+            return GPT2(vocab=V, ctx=S, hidden=256, layers=2, heads=4, dropout=0.0, fp8=fp8)
+
+        def opt_fn():
+            return optimizers.AdamW(1e-3, weight_decay=0.01)
+        return _train(model_fn, opt_fn, batches, cuda)
+
+    l8, _ = run(True)
+    lb, _ = run(False)
+    assert all(np.isfinite(l8)), l8
+    for a, b in zip(l8, lb):
+        assert abs(a - b) <= 0.05 * abs(b), (l8, lb)
+    assert l8[-1] < 0.8 * l8[0] and lb[-1] < 0.8 * lb[0], (l8, lb)
