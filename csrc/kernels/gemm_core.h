@@ -131,7 +131,53 @@ struct GemmArgs {
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
   BnFin fin;
+  // BatchNorm(+ReLU) of an activation operand that was never materialised (kernels instantiated with XF != 0):
+  // the staged values are the producing conv's raw output z, and v = max(z * xsc[c] + xsh[c], 0) on channel c is
+  // applied in LDS (LDS-DMA loaders: each lane rewrites its own landed 16-B slots) or in registers before the
+  // ds_write (register-staged loaders). Zero-filled slots (padding taps, rows past the operand) stay zero.
+  const float* xsc;
+  const float* xsh;
+  // ReLU mask of the BN-backward statistics (bnx != nullptr) when no bit mask exists: relu'(bnx * bnsc + bnsh)
+  const float* bnsc;
+  const float* bnsh;
 };
+
+// ---- on-the-fly BatchNorm + ReLU of 8 staged bf16 values (channels c .. c+7) ---------------------------------------
+struct Coef8 {
+  float4 s0, s1, h0, h1;
+};
+__device__ __forceinline__ Coef8 load_coef8x(const float* sc, const float* sh, int c) {
+  Coef8 k;
+  k.s0 = *reinterpret_cast<const float4*>(sc + c);
+  k.s1 = *reinterpret_cast<const float4*>(sc + c + 4);
+  k.h0 = *reinterpret_cast<const float4*>(sh + c);
+  k.h1 = *reinterpret_cast<const float4*>(sh + c + 4);
+  return k;
+}
+// (the same f32 formula and bf16 rounding as norm.hip's bn_apply pass: the MFMA sees the bits that pass would store)
+__device__ __forceinline__ uint32_t bnrelu2(uint32_t w, float s0, float s1, float h0, float h1) {
+  return pack2bf(fmaxf(fmaf(__uint_as_float(w << 16), s0, h0), 0.f),
+                 fmaxf(fmaf(__uint_as_float(w & 0xffff0000u), s1, h1), 0.f));
+}
+__device__ __forceinline__ uint4 bnrelu8(uint4 v, const Coef8& k) {
+  return make_uint4(bnrelu2(v.x, k.s0.x, k.s0.y, k.h0.x, k.h0.y), bnrelu2(v.y, k.s0.z, k.s0.w, k.h0.z, k.h0.w),
+                    bnrelu2(v.z, k.s1.x, k.s1.y, k.h1.x, k.h1.y), bnrelu2(v.w, k.s1.z, k.s1.w, k.h1.z, k.h1.w));
+}
+// ReLU mask bits (bit j = channel c + j) of those 8 values: set where the stored bf16 output would be > 0 (the bit
+// norm.hip's bn_apply writes for the backward)
+__device__ __forceinline__ uint32_t bnrelu_bits8(uint4 v, const float* sc, const float* sh) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t bits = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 2 * q + h;
+      const float o = fmaf(__uint_as_float(h ? (w[q] & 0xffff0000u) : (w[q] << 16)), sc[j], sh[j]);
+      bits |= (uint32_t)(o > 0.f && f2bf(o) != 0) << j;
+    }
+  return bits;
+}
 
 __device__ __forceinline__ long out_row(const GemmArgs& a, int m) {
   if (!a.crm) return m;
@@ -163,7 +209,15 @@ __device__ __forceinline__ void stat_acc(const GemmArgs& a, long mrow, int n, co
     const uint2 xr = *reinterpret_cast<const uint2*>(a.bnx + e);
     const float x[4] = {__uint_as_float(xr.x << 16), __uint_as_float(xr.x & 0xffff0000u),
                         __uint_as_float(xr.y << 16), __uint_as_float(xr.y & 0xffff0000u)};
-    const uint32_t bits = a.bnmask ? ((uint32_t)a.bnmask[e >> 3] >> (e & 4)) : 0xFu;  // e % 8 is 0 or 4
+    uint32_t bits = a.bnmask ? ((uint32_t)a.bnmask[e >> 3] >> (e & 4)) : 0xFu;  // e % 8 is 0 or 4
+    if (!a.bnmask && a.bnsc) {
+      bits = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float o = fmaf(x[r], a.bnsc[n + r], a.bnsh[n + r]);
+        bits |= (uint32_t)(o > 0.f && f2bf(o) != 0) << r;
+      }
+    }
     const float4 mu = *reinterpret_cast<const float4*>(a.bnmean + n);
     const float m4[4] = {mu.x, mu.y, mu.z, mu.w};
 #pragma unroll
@@ -219,8 +273,9 @@ __device__ __forceinline__ uint32_t tap_mask(int R, int S, int h0, int h1, int w
 }
 
 // ---- K-contiguous operand: LDS tile [R][64] bf16, 128-B rows ---------------
-template <int R, int MODE>
+template <int R, int MODE, bool XF = false>
 struct KContigLoader {
+  static_assert(!XF, "on-the-fly BatchNorm of a K-contiguous operand needs the LDS-DMA loader");
   static constexpr int L = R / 32;  // 16-B loads per thread per K tile
   const bf16_t* base[L];
   int i0[L], i1[L], i2[L];  // per-row gather state
@@ -377,6 +432,7 @@ struct KContigLoader {
       *reinterpret_cast<uint4*>(lds + row * 128 + pc * 16) = reg[i];
     }
   }
+  __device__ __forceinline__ void xform(char*) const {}
 };
 
 // fragment read from a [R][64] tile: rows rb..rb+15, k-substep kk
@@ -394,7 +450,7 @@ __device__ __forceinline__ int kouter_swz(int k) {
   else return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);               // R == 64: 4 values
 }
 
-template <int R, int MODE>
+template <int R, int MODE, bool XF = false>
 struct KOuterLoader {
   static constexpr int CPR = R / 8;       // 16-B chunks per k-row
   static constexpr int RPP = NT / CPR;    // k-rows per pass
@@ -405,6 +461,8 @@ struct KOuterLoader {
   bool cv;
   int khoff, kwoff, ci;  // OP_WGRADX column decomposition
   uint4 reg[L];
+  Coef8 xk;              // XF: BN coefficients of the thread's (fixed) 8 columns = channels
+  uint32_t okb;          // XF: loads of the staged tile that read data (the rest are zeros and stay zero)
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld_, int r0, int Rtot) {
     const int t = threadIdx.x;
@@ -421,10 +479,14 @@ struct KOuterLoader {
       khoff = (int)kh * a.g.dh - a.g.ph;
       kwoff = (int)kw * a.g.dw - a.g.pw;
     }
+    if constexpr (XF) {
+      if (cv) xk = load_coef8x(a.xsc, a.xsh, MODE == OP_WGRADX ? ci : col);
+    }
   }
 
   __device__ __forceinline__ void load(const GemmArgs& a, int k0, int Kend) {
     const int t = threadIdx.x;
+    uint32_t okbits = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       int kr = t / CPR + RPP * i;
@@ -442,7 +504,9 @@ struct KOuterLoader {
         if (v) reg[i] = *reinterpret_cast<const uint4*>(p + (((long)n * a.g.H + hi) * a.g.W + wi) * a.g.C + ci);
         else reg[i] = make_uint4(0, 0, 0, 0);
       }
+      okbits |= (uint32_t)v << i;
     }
+    if constexpr (XF) okb = okbits;
   }
 
   __device__ __forceinline__ void store(char* lds) {
@@ -451,13 +515,19 @@ struct KOuterLoader {
     for (int i = 0; i < L; ++i) {
       int kr = t / CPR + RPP * i;
       int pc = c ^ (kouter_swz<R>(kr) << 1);
-      *reinterpret_cast<uint4*>(lds + kr * (R * 2) + pc * 16) = reg[i];
+      uint4 v = reg[i];
+      if constexpr (XF) {
+        if ((okb >> i) & 1u) v = bnrelu8(v, xk);
+      }
+      *reinterpret_cast<uint4*>(lds + kr * (R * 2) + pc * 16) = v;
     }
   }
+  __device__ __forceinline__ void xform(char*) const {}
 };
 
-template <int R, int MODE>
+template <int R, int MODE, bool XF = false>
 struct PixelRowLoader {
+  static_assert(!XF, "on-the-fly BatchNorm of a row-mapped operand needs the LDS-DMA loader");
   static constexpr int CPT = R / 32;  // 16-B chunks per thread (4 threads per 64-deep k-row)
   int kr;
   int coff[CPT];                      // byte offset of the chunk's column within a pixel row (+ tap shift)
@@ -538,6 +608,8 @@ struct PixelRowLoader {
     }
   }
 
+  __device__ __forceinline__ void xform(char*) const {}
+
   // Logical 16-B chunk written by thread t in store instruction i. Odd k-rows take their chunks in the
   // other half-order (^4): a ds_write_b128 8-lane group spans two k-rows (4 lanes each), and this puts the
   // two rows' 64-B pieces on different banks (the rows are 256 B apart, i.e. the same bank set).
@@ -566,14 +638,17 @@ __device__ __forceinline__ v8bf frag_kouter(const char* lds, int cb, int kk, int
 // fetches the LOGICAL chunk that belongs at its physical slot (the XOR swizzle is undone on the source side).
 // Rows past the operand, k past Kend and (tap-uniform gathers) out-of-image taps get an out-of-range offset
 // and the range check writes zeros.
-template <int R, int MODE>
+template <int R, int MODE, bool XF = false>
 struct GldsLoader {
   static_assert(MODE == OP_KCONTIG || MODE == OP_IM2COL_T || MODE == OP_DGRAD_T, "K-contiguous modes only");
   static constexpr int L = R / 32;  // wave instructions per thread per K-tile
   __amdgpu_buffer_rsrc_t rsrc;
   int roff[L];        // byte offset of the row (KCONTIG) / of the row's tap-(0,0) pixel (gathers)
   uint32_t tmask[L];  // KCONTIG: ~0 for valid rows; gathers: in-image tap mask
-  int coff[L];        // byte offset of this lane's logical chunk in the 64-wide K-tile
+  int coff[L];        // byte offset of this lane's logical chunk in the 64-wide K-tile (the same for every i:
+                      // rows 32 i + (t >> 3) share (row >> 1) & 7)
+  uint32_t okb;       // XF: slots of the last issued tile that loaded data
+  Coef8 xk;           // XF: BN coefficients of this lane's 8 channels in that tile
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot) {
     const int t = threadIdx.x;
@@ -621,26 +696,46 @@ struct GldsLoader {
   __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int Kend, char* lds) {
     const int wave = threadIdx.x >> 6;
     int toff;
-    uint32_t tap = 0;
+    uint32_t tap = 0, c0 = (uint32_t)k0;
     if constexpr (MODE == OP_KCONTIG) {
       toff = k0 * 2;
     } else {
       const ConvGeom& g = a.g;
-      uint32_t c0, kh, kw;
+      uint32_t kh, kw;
       fdivmod((uint32_t)k0, MODE == OP_IM2COL_T ? g.dC : g.dK, tap, c0);
       fdivmod(tap, g.dS, kh, kw);
       toff = MODE == OP_IM2COL_T ? (((int)kh * g.dh * g.W + (int)kw * g.dw) * g.C + (int)c0) * 2
                                  : ((int)c0 - ((int)kh * g.dh * g.Q + (int)kw * g.dw) * g.Kout) * 2;
     }
+    uint32_t okbits = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       bool ok;
       if constexpr (MODE == OP_KCONTIG) ok = tmask[i] != 0u && k0 + (coff[i] >> 1) < Kend;
       else ok = (tmask[i] >> tap) & 1u;
+      okbits |= (uint32_t)ok << i;
       const uint32_t off = ok ? (uint32_t)(roff[i] + toff + coff[i]) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 +
                                                                                               wave * 1024),
                                                16, off, 0, 0, 0);
+    }
+    if constexpr (XF) {
+      okb = okbits;
+      if (okbits) xk = load_coef8x(a.xsc, a.xsh, (int)c0 + (coff[0] >> 1));  // channel of the lane's chunk
+    }
+  }
+
+  // XF: BatchNorm + ReLU of this lane's own landed slots of the last issued tile, in place (after the issuing
+  // wave's vmcnt wait, before the barrier that publishes the tile)
+  __device__ __forceinline__ void xform(char* lds) const {
+    if constexpr (XF) {
+      const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        if (!((okb >> i) & 1u)) continue;
+        uint4* p = reinterpret_cast<uint4*>(lds + i * 4096 + wave * 1024 + lane * 16);
+        *p = bnrelu8(*p, xk);
+      }
     }
   }
 };
@@ -650,7 +745,7 @@ struct GldsLoader {
 // the XOR swizzle puts at its physical slot. OP_KOUTER_R: plain rows (dY of a weight gradient: row stride
 // = Kout); OP_WGRADX_R: the row is an output pixel whose input pixel is decoded per K-tile, the column a
 // (tap, channel) pair fixed per lane; out-of-image taps / rows past K read zeros via the range check.
-template <int R, int MODE>
+template <int R, int MODE, bool XF = false>
 struct GldsKOuter {
   static_assert(MODE == OP_KOUTER_R || MODE == OP_WGRADX_R || MODE == OP_KOUTER, "K-outer operands only");
   static constexpr int L = R / 32;
@@ -661,6 +756,12 @@ struct GldsKOuter {
   int coff[L];      // byte offset of the lane's column chunk (+ tap shift for OP_WGRADX_R)
   int hoff[L], woff[L];
   bool cv[L];
+  // XF: the lane's column chunk is the same 8 channels in every instruction (k-rows i*4096/ROWB + t*16/ROWB share
+  // the swizzle term of kouter_swz for R <= 128), so ONE set of BN coefficients, loaded once; okb: slots of the last
+  // issued tile that loaded data
+  static_assert(!XF || R <= 128, "XF K-outer images of more than 128 columns change channels per instruction");
+  Coef8 xk;
+  uint32_t okb;
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld, int r0, int Rtot) {
     const int t = threadIdx.x;
@@ -684,8 +785,27 @@ struct GldsKOuter {
         hoff[i] = (int)kh * g.dh - g.ph;
         woff[i] = (int)kw * g.dw - g.pw;
         coff[i] = ((hoff[i] * g.W + woff[i]) * g.C + (int)ci) * 2;
+        if constexpr (XF) {
+          if (i == 0 && cv[0]) xk = load_coef8x(a.xsc, a.xsh, (int)ci);
+        }
       } else {
         coff[i] = col * 2;
+        if constexpr (XF) {
+          if (i == 0 && cv[0]) xk = load_coef8x(a.xsc, a.xsh, col);  // OP_KOUTER: the column IS the channel
+        }
+      }
+    }
+  }
+
+  // XF: BatchNorm + ReLU of this lane's own landed slots of the last issued tile (see GldsLoader::xform)
+  __device__ __forceinline__ void xform(char* lds) const {
+    if constexpr (XF) {
+      const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        if (!((okb >> i) & 1u)) continue;
+        uint4* p = reinterpret_cast<uint4*>(lds + i * 4096 + wave * 1024 + lane * 16);
+        *p = bnrelu8(*p, xk);
       }
     }
   }
@@ -693,6 +813,7 @@ struct GldsKOuter {
   __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int Kend, char* lds) {
     const ConvGeom& g = a.g;
     const int wave = threadIdx.x >> 6;
+    uint32_t okbits = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       const int k = k0 + kr[i];
@@ -713,25 +834,28 @@ struct GldsKOuter {
       } else {
         off = k * ldb + coff[i];
       }
+      okbits |= (uint32_t)ok << i;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 + wave * 1024), 16,
           ok ? (uint32_t)off : 0x80000000u, 0, 0, 0);
     }
+    if constexpr (XF) okb = okbits;
   }
 };
 
-template <int R, int MODE>
+template <int R, int MODE, bool XF = false>
 using LoaderFor = typename std::conditional<
-    (MODE == OP_KOUTER_R || MODE == OP_WGRADX_R), PixelRowLoader<R, MODE>,
-    typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE>,
-                              KContigLoader<R, MODE>>::type>::type;
+    (MODE == OP_KOUTER_R || MODE == OP_WGRADX_R), PixelRowLoader<R, MODE, XF>,
+    typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE, XF>,
+                              KContigLoader<R, MODE, XF>>::type>::type;
 
 constexpr bool glds_kcontig(int m) { return m == OP_KCONTIG || m == OP_IM2COL_T || m == OP_DGRAD_T; }
 constexpr bool glds_kouter(int m) { return m == OP_KOUTER_R || m == OP_WGRADX_R || m == OP_KOUTER; }
 constexpr bool glds_mode(int m) { return glds_kcontig(m) || glds_kouter(m); }
 
-template <int R, int MODE>
-using GldsFor = typename std::conditional<glds_kouter(MODE), GldsKOuter<R, MODE>, GldsLoader<R, MODE>>::type;
+template <int R, int MODE, bool XF = false>
+using GldsFor =
+    typename std::conditional<glds_kouter(MODE), GldsKOuter<R, MODE, XF>, GldsLoader<R, MODE, XF>>::type;
 
 constexpr bool kouter_mode(int m) {
   return m == OP_KOUTER || m == OP_WGRADX || m == OP_KOUTER_R || m == OP_WGRADX_R;
@@ -981,14 +1105,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
     constexpr int C8 = BN / 8;
     static_assert(NTH % C8 == 0, "a thread's channel chunk must stay fixed across the store pass");
     const int c8t = threadIdx.x % C8;  // this thread's 8-channel chunk (constant over the pass)
-    float bs[8], bq[8], bmu[8];
+    float bs[8], bq[8], bmu[8], bsc[8], bsh[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) bs[r] = bq[r] = bmu[r] = 0.f;
+    for (int r = 0; r < 8; ++r) bs[r] = bq[r] = bmu[r] = bsc[r] = bsh[r] = 0.f;
+    const bool mask_coef = bn_bwd && !a.bnmask && a.bnsc;  // ReLU mask recomputed from the BN input
     if (bn_bwd && n0 + c8t * 8 < a.N) {
       const float4 m0v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8);
       const float4 m1v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8 + 4);
       bmu[0] = m0v.x; bmu[1] = m0v.y; bmu[2] = m0v.z; bmu[3] = m0v.w;
       bmu[4] = m1v.x; bmu[5] = m1v.y; bmu[6] = m1v.z; bmu[7] = m1v.w;
+      if (mask_coef) {
+        const Coef8 k = load_coef8x(a.bnsc, a.bnsh, n0 + c8t * 8);
+        bsc[0] = k.s0.x; bsc[1] = k.s0.y; bsc[2] = k.s0.z; bsc[3] = k.s0.w;
+        bsc[4] = k.s1.x; bsc[5] = k.s1.y; bsc[6] = k.s1.z; bsc[7] = k.s1.w;
+        bsh[0] = k.h0.x; bsh[1] = k.h0.y; bsh[2] = k.h0.z; bsh[3] = k.h0.w;
+        bsh[4] = k.h1.x; bsh[5] = k.h1.y; bsh[6] = k.h1.z; bsh[7] = k.h1.w;
+      }
     }
 #pragma unroll 4
     for (int c = threadIdx.x; c < BM * C8; c += NTH) {
@@ -1020,7 +1152,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
       *reinterpret_cast<uint4*>(cp) = val;
       if (bn_bwd) {
         const uint4 xr = *reinterpret_cast<const uint4*>(a.bnx + e);
-        const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3] : 0xFFu;  // e % 8 == 0
+        const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3]  // e % 8 == 0
+                              : mask_coef ? bnrelu_bits8(xr, bsc, bsh) : 0xFFu;
         const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1179,7 +1312,8 @@ __device__ __forceinline__ void xcd_block(int nwg, int& bid, int& z) {
 //  2: register-staged, double-buffered LDS (one barrier per K-tile).
 //  3: LDS-DMA (GldsLoader), one buffer, synchronous per K-tile: no staging VGPRs, occupancy hides latency.
 //  4: LDS-DMA, double-buffered: the next K-tile's DMA runs under this tile's MFMAs.
-template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int PIPE = 2>
+// XF: on-the-fly BatchNorm + ReLU of operand A (1) or B (2) (GemmArgs.xsc/xsh; LDS-DMA or K-outer register loaders)
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int PIPE = 2, int XF = 0>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   constexpr int NBUF = (PIPE == 2 || PIPE == 4) ? 2 : 1;
   constexpr bool GLDS = PIPE >= 3;
@@ -1214,8 +1348,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const bf16_t* Ap = a.A + (long)bz * a.sA;
   const bf16_t* Bp = a.B + (long)bz * a.sB;
 
-  typename std::conditional<GLDS, GldsFor<BM, AM>, LoaderFor<BM, AM>>::type la;
-  typename std::conditional<GLDS, GldsFor<BN, BMODE>, LoaderFor<BN, BMODE>>::type lb;
+  typename std::conditional<GLDS, GldsFor<BM, AM, XF == 1>, LoaderFor<BM, AM, XF == 1>>::type la;
+  typename std::conditional<GLDS, GldsFor<BN, BMODE, XF == 2>, LoaderFor<BN, BMODE, XF == 2>>::type lb;
   la.init(a, Ap, a.lda, m0, a.M);
   lb.init(a, Bp, a.ldb, n0, a.N);
 
@@ -1268,6 +1402,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
       }
       for (int kt = 0; kt < nk; ++kt) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (XF) {  // this lane's own landed slots of tile kt (the last tile issued)
+          la.xform((kt & 1) ? sA1 : sA0);
+          lb.xform((kt & 1) ? sB1 : sB0);
+        }
         __syncthreads();  // tile kt landed for every wave; every wave is done reading tile kt-1's buffer
         if (kt + 1 < nk) {
           la.issue(a, kbeg + (kt + 1) * BK, kend, (kt & 1) ? sA0 : sA1);
@@ -1281,6 +1419,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
         la.issue(a, kbeg + kt * BK, kend, sA0);
         lb.issue(a, kbeg + kt * BK, kend, sB0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (XF) {
+          la.xform(sA0);
+          lb.xform(sB0);
+        }
         __syncthreads();
         compute(sA0, sB0);
       }

@@ -343,8 +343,12 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// dz = dy masked by ReLU: either from the bf16 output (sign/zero test) or from the 1-bit mask
-__device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const uint8_t* mbits, long i8) {
+// dz = dy masked by ReLU: from the 1-bit mask, the bf16 output (sign/zero test), or — for a BatchNorm output that was
+// never materialised (its consumer applied BN + ReLU on the fly) — recomputed from the BN input xv with the forward's
+// scale/shift (msc/msh: this thread's 8 channels), the same test as the bit bn_apply would have stored
+__device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const uint8_t* mbits, long i8,
+                                           const float* xv = nullptr, const float* msc = nullptr,
+                                           const float* msh = nullptr) {
   if (mbits) {
     const uint32_t b = mbits[i8];
 #pragma unroll
@@ -360,18 +364,27 @@ __device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const 
       if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
       if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
     }
+  } else if (msc) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float o = fmaf(xv[j], msc[j], msh[j]);
+      if (!(o > 0.f && f2bf(o) != 0)) d[j] = 0.f;
+    }
   }
 }
 
 // Backward reduce: dz = dy * (y > 0 if relu-mask given); partial rows [gridDim.x][2C]:
 // [0,C) sum dz, [C,2C) sum dz*xhat. No atomics; bn_bwd_finalize sums the rows.
+template <bool MC>  // MC: ReLU mask recomputed from x with msc/msh (a lazy BatchNorm output)
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
                                                             const bf16_t* __restrict__ ymask,
                                                             const uint8_t* __restrict__ mbits,
                                                             const bf16_t* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long M, int C,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part,
+                                                            const float* __restrict__ msc,
+                                                            const float* __restrict__ msh) {
   __shared__ float red[4096];
   ColGeo g = colgeo(C);
   const int t = threadIdx.x;
@@ -380,8 +393,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
     const int cc = cc0 + t % g.TPR;
     float s[8] = {0}, q[8] = {0};
     if (t < g.TPR * g.RPB && cc < g.cols8) {
-      float mu[8];
+      float mu[8], ms[8], mh[8];
       load_coef8(mean + cc * 8, mu);
+      if constexpr (MC) {
+        load_coef8(msc + cc * 8, ms);
+        load_coef8(msh + cc * 8, mh);
+      }
       // sum dz*(x - mean) here; the invstd factor is applied once per channel in bn_bwd_finalize
       const long rstep = (long)gridDim.x * g.RPB;
       long r = (long)blockIdx.x * g.RPB + rsub;
@@ -392,7 +409,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
           const long i8 = (r + u * rstep) * g.cols8 + cc;
           load8(dy + i8 * 8, d[u]);
           load8(x + i8 * 8, xv[u]);
-          relu_mask8(d[u], ymask, mbits, i8);
+          if constexpr (MC) relu_mask8(d[u], nullptr, nullptr, i8, xv[u], ms, mh);
+          else relu_mask8(d[u], ymask, mbits, i8);
         }
 #pragma unroll
         for (int u = 0; u < EU; ++u)
@@ -407,7 +425,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
         const long i8 = r * g.cols8 + cc;
         load8(dy + i8 * 8, d);
         load8(x + i8 * 8, xv);
-        relu_mask8(d, ymask, mbits, i8);
+        if constexpr (MC) relu_mask8(d, nullptr, nullptr, i8, xv, ms, mh);
+        else relu_mask8(d, ymask, mbits, i8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           s[j] += d[j];
@@ -466,7 +485,7 @@ __device__ __forceinline__ void bn_bwd_apply_row(const float* d, const float* xv
 // x2 (mean2): its backward reduction (sum dz, sum dz*(x2 - mean2), over the bf16-rounded dz that is stored) is
 // taken here as one partial row per block into part2 — the shortcut's own reduce pass disappears.
 // (host: C/8 <= 256 and 256 % (C/8) == 0, so every thread owns exactly one channel chunk)
-template <bool SC>
+template <bool SC, bool MC = false>  // MC: ReLU mask recomputed from x with msc/msh (a lazy BatchNorm output)
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ ymask,
                                                            const uint8_t* __restrict__ mbits,
@@ -475,13 +494,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out,
                                                            const bf16_t* __restrict__ x2,
                                                            const float* __restrict__ mean2,
-                                                           float* __restrict__ part2, int rev) {
+                                                           float* __restrict__ part2, int rev,
+                                                           const float* __restrict__ msc,
+                                                           const float* __restrict__ msh) {
   const ColGeo g = colgeo(C);
   const int t = threadIdx.x;
   if (!SC && t >= g.TPR * g.RPB) return;
   const int rsub = t / g.TPR;
   const long rstep = (long)gridDim.x * g.RPB;
-  if (!ymask && !mbits) dz_out = nullptr;
+  if (!ymask && !mbits && !MC) dz_out = nullptr;
   float s2[8] = {0}, q2[8] = {0}, mu2[8];
   auto sc_acc = [&](const float* d, long i8) {
     if constexpr (SC) {
@@ -496,10 +517,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
     }
   };
   for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
-    float ka[8], kb[8], kc[8];
+    float ka[8], kb[8], kc[8], ms[8], mh[8];
     load_coef8(coef + cc * 8, ka);
     load_coef8(coef + C + cc * 8, kb);
     load_coef8(coef + 2 * C + cc * 8, kc);
+    if constexpr (MC) {
+      load_coef8(msc + cc * 8, ms);
+      load_coef8(msh + cc * 8, mh);
+    }
     if constexpr (SC) load_coef8(mean2 + cc * 8, mu2);
     long r = (long)blockIdx.x * g.RPB + rsub;
     for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
@@ -509,7 +534,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
         const long i8 = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
         load8(dy + i8 * 8, d[u]);
         load8(x + i8 * 8, xv[u]);
-        relu_mask8(d[u], ymask, mbits, i8);
+        if constexpr (MC) relu_mask8(d[u], nullptr, nullptr, i8, xv[u], ms, mh);
+        else relu_mask8(d[u], ymask, mbits, i8);
       }
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
@@ -523,7 +549,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
       const long i8 = (rev ? M - 1 - r : r) * g.cols8 + cc;
       load8(dy + i8 * 8, d);
       load8(x + i8 * 8, xv);
-      relu_mask8(d, ymask, mbits, i8);
+      if constexpr (MC) relu_mask8(d, nullptr, nullptr, i8, xv, ms, mh);
+      else relu_mask8(d, ymask, mbits, i8);
       bn_bwd_apply_row(d, xv, ka, kb, kc, dx, dz_out, i8);
       sc_acc(d, i8);
     }
@@ -1026,7 +1053,7 @@ struct ShortcutStats {  // optional fused projection-shortcut BN reduction (bn_b
 static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
                        float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,
-                       const ShortcutStats* sc = nullptr);
+                       const ShortcutStats* sc = nullptr, const float* msc = nullptr, const float* msh = nullptr);
 
 // work: (2*1024 + 3) * C floats (partials + coefficients)
 // ReLU mask from mbits (1 bit/element, preferred) or from the bf16 output ymask; neither = no ReLU
@@ -1034,17 +1061,22 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
                        const float* invstd,
                        const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma, float* dbeta,
                        int accumulate, float* work, const void* x2, const float* mean2, float* part2, int* rows2,
-                       void* stream) {
+                       const float* msc, const float* msh, void* stream) {
   if (C & 7) return -1;
   const ShortcutStats sc{x2, mean2, part2, rows2};
   hipStream_t st = (hipStream_t)stream;
   float* coef = work;
   float* part = work + 3 * C;
   int G = red_grid(M, C);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
-                     (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part);
+  if (msc && !mbits && !ymask)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, nullptr, nullptr,
+                       (const bf16_t*)x, mean, invstd, M, C, part, msc, msh);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(G), dim3(256), 0, st, (const bf16_t*)dy,
+                       (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part,
+                       nullptr, nullptr);
   return bn_bwd_tail(dy, ymask, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, G,
-                     coef, st, &sc);
+                     coef, st, &sc, msc, msh);
 }
 
 // Backward with the reduction already done by the GEMM that produced dy (dtf_conv_dgrad's fused BN-backward
@@ -1052,22 +1084,23 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
 DTF_API int dtf_bn_bwd_partials(const void* dy, const void* mbits, const void* x, const float* mean,
                                 const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out,
                                 float* dgamma, float* dbeta, int accumulate, float* part, int T, float* coef,
-                                const void* x2, const float* mean2, float* part2, int* rows2, void* stream) {
+                                const void* x2, const float* mean2, float* part2, int* rows2, const float* msc,
+                                const float* msh, void* stream) {
   if ((C & 7) || T < 1) return -1;
   const ShortcutStats sc{x2, mean2, part2, rows2};
   return bn_bwd_tail(dy, nullptr, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, T,
-                     coef, (hipStream_t)stream, &sc);
+                     coef, (hipStream_t)stream, &sc, msc, msh);
 }
 
 // Backward apply only: the coefficients `coef` (3*C) were already finalized — by the data-gradient GEMM that produced
 // dy (dtf_conv_dgrad_bn's fused finalize). Optional fused projection-shortcut statistics as in dtf_bn_bwd_partials.
 DTF_API int dtf_bn_bwd_apply_coef(const void* dy, const void* mbits, const void* x, long M, int C, void* dx,
                                   void* dz_out, const float* coef, const void* x2, const float* mean2, float* part2,
-                                  int* rows2, void* stream) {
+                                  int* rows2, const float* msc, const float* msh, void* stream) {
   if (C & 7) return -1;
   const ShortcutStats sc{x2, mean2, part2, rows2};
   return bn_bwd_tail(dy, nullptr, mbits, x, nullptr, nullptr, nullptr, M, C, dx, dz_out, nullptr, nullptr, 0, nullptr,
-                     0, const_cast<float*>(coef), (hipStream_t)stream, &sc);
+                     0, const_cast<float*>(coef), (hipStream_t)stream, &sc, msc, msh);
 }
 
 // Sum the G partial rows [G][2C] of a BN backward reduction and finalize: dgamma/dbeta and the apply
@@ -1093,21 +1126,27 @@ static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const 
 static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
                        float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,
-                       const ShortcutStats* sc) {
+                       const ShortcutStats* sc, const float* msc, const float* msh) {
+  if (mbits || ymask) msc = msh = nullptr;
   if (part) bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
   const ColGeo geo = colgeo(C);
   const int grid = ew_grid(M, C);
-  const bool fuse_sc = sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&
+  const bool fuse_sc = !msc && sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&
                        geo.TPR * geo.RPB == 256;
   if (sc && sc->rows2) *sc->rows2 = fuse_sc ? grid : 0;
-  if (fuse_sc)
+  if (msc) {  // lazy BatchNorm output: no bit mask, no residual branch
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, nullptr,
+                       nullptr, (const bf16_t*)x, coef, M, C, (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr,
+                       ew_reverse(), msc, msh);
+  } else if (fuse_sc) {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                       (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse());
-  else
+                       (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse(), nullptr, nullptr);
+  } else {
     hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
                        (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                       (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse());
+                       (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse(), nullptr, nullptr);
+  }
   return (int)hipGetLastError();
 }
 

@@ -303,10 +303,11 @@ class ConvBN(Layer):
         self.moving_variance = self.add_weight("bn/moving_variance", (self.filters,), "ones", trainable=False)
         self.built = True
 
-    def call(self, x, residual=None, training=None, link=None, role=None, pool=None, s2d=False):
+    def call(self, x, residual=None, training=None, link=None, role=None, pool=None, s2d=False, lazy=False):
         """link/role: residual-gradient join of a block (ops.conv.ResidualGradLink). pool: a MaxPooling2D
         applied to the (ReLU) output, fused with the BatchNorm (ops.conv_bn_maxpool); s2d: x is the
-        space-to-depth image of a 7x7/2 conv's input (ops.image_to_s2d_bf16; the layer must be built)."""
+        space-to-depth image of a 7x7/2 conv's input (ops.image_to_s2d_bf16; the layer must be built).
+        lazy: the caller feeds the output ONLY to another ConvBN (ops.conv_bn lazy outputs)."""
         if self.padding == "same":
             pad = ((self.kernel_size[0] - 1) // 2, (self.kernel_size[1] - 1) // 2)
         else:
@@ -318,9 +319,10 @@ class ConvBN(Layer):
                                        self.moving_variance, stride=self.strides, pad=pad, momentum=self.momentum,
                                        eps=self.epsilon, training=bool(training), pool_size=pool.pool_size,
                                        pool_strides=pool.strides, pool_pad=pool.pads(), s2d=s2d)
+        kw = {"lazy": True} if lazy else {}
         return ops.conv_bn(x, self.kernel, self.gamma, self.beta, self.moving_mean, self.moving_variance,
                            stride=self.strides, pad=pad, relu=self.relu, residual=residual, momentum=self.momentum,
-                           eps=self.epsilon, training=bool(training), link=link, role=role)
+                           eps=self.epsilon, training=bool(training), link=link, role=role, **kw)
 
 
 class MaxPooling2D(Layer):

@@ -14,6 +14,14 @@ BF = torch.bfloat16
 F32 = torch.float32
 
 
+@pytest.fixture(autouse=True)
+def _fin_fused():
+    """The in-launch finalize is opt-in (gemm.hip fin_on): switch it on for these tests only."""
+    call("dtf_set_bn_fin_fused", 1)
+    yield
+    call("dtf_set_bn_fin_fused", 0)
+
+
 def rnd(*shape, dev, scale=1.0):
     return (torch.randn(*shape, device=dev) * scale).to(BF)
 
@@ -52,7 +60,7 @@ def test_conv_fwd_fused_bn_finalize(cuda, case):
             done = IntOut()
             call("dtf_conv_fwd_bn", ptr(x), ptr(w), ptr(y), ptr(part), N, H, W, Cin, K, R, S, P, Q, st, st, pd, pd,
                  1, 1, -1, ptr(gamma), ptr(beta), ptr(rm), ptr(rv), 0.9, 1e-5, ptr(sc), ptr(sh), ptr(mu), ptr(inv),
-                 done.addr, stream())
+                 done.addr, None, None, stream())
             torch.cuda.synchronize()
             assert done.value == 1, "the conv launch did not finalize the BatchNorm"
         else:
@@ -104,7 +112,7 @@ def test_conv_dgrad_fused_bn_backward_finalize(cuda, case, accumulate):
     wc = crsk_shadow(w, K, R * S, Cin)
     call("dtf_conv_dgrad_bn", ptr(dy), ptr(wc), ptr(dx), N, H, W, Cin, K, R, S, P, Q, st, st, pd, pd, 1, 1, 0.0,
          ptr(ws), 2 * ws.numel(), ptr(yc), ptr(bits), ptr(mean), ptr(part), rows.addr, None, None, ptr(gamma),
-         ptr(invstd), ptr(dgamma), ptr(dbeta), accumulate, ptr(coef), done.addr, stream())
+         ptr(invstd), ptr(dgamma), ptr(dbeta), accumulate, ptr(coef), done.addr, None, None, stream())
     torch.cuda.synchronize()
     if st > 1:
         assert done.value == 0 and rows.value >= 1

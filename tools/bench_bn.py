@@ -42,9 +42,9 @@ def main():
         t_res = timeit(lambda: call("dtf_bn_apply", ptr(x), ptr(sc), ptr(sh), ptr(res), ptr(y), M, C, 1, ptr(mb), None, None,
                                     stream()))
         t_bwd = timeit(lambda: call("dtf_bn_bwd", ptr(dy), None, ptr(mb), ptr(x), ptr(mean), ptr(inv), ptr(gm), M, C,
-                                    ptr(dx), None, ptr(dg), ptr(db), 0, ptr(work), None, None, None, None, stream()))
+                                    ptr(dx), None, ptr(dg), ptr(db), 0, ptr(work), None, None, None, None, None, None, stream()))
         t_bwdr = timeit(lambda: call("dtf_bn_bwd", ptr(dy), None, ptr(mb), ptr(x), ptr(mean), ptr(inv), ptr(gm), M,
-                                     C, ptr(dx), ptr(dz), ptr(dg), ptr(db), 0, ptr(work), None, None, None, None, stream()))
+                                     C, ptr(dx), ptr(dz), ptr(dg), ptr(db), 0, ptr(work), None, None, None, None, None, None, stream()))
         gb = lambda b, t: b / t / 1e9  # noqa: E731
         print(f"M={M:8d} C={C:5d} copy {gb(2 * n, t_copy):6.0f} GB/s | apply {t_app * 1e6:7.1f}us "
               f"{gb(2.0625 * n, t_app):6.0f} GB/s | apply+res {t_res * 1e6:7.1f}us {gb(3.0625 * n, t_res):6.0f} | "
