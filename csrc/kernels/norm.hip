@@ -289,6 +289,7 @@ __device__ __forceinline__ void bn_apply_row(const bf16_t* __restrict__ x, const
 
 // rscale/rshift (optional): the residual is itself a BatchNorm input (a projection shortcut's conv output) whose
 // affine normalisation is applied here, so the shortcut's BN output is never materialised.
+template <int NU = EU>  // rows per trip (all loads of a trip issued before the first use)
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
@@ -315,16 +316,16 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
       }
     };
     long r = (long)blockIdx.x * g.RPB + rsub;
-    for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
-      float f[EU][8], rv[EU][8];
+    for (; r + (NU - 1) * rstep < M; r += NU * rstep) {
+      float f[NU][8], rv[NU][8];
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
+      for (int u = 0; u < NU; ++u) {
         const long i8 = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
         load8(x + i8 * 8, f[u]);
         if (res) load8(res + i8 * 8, rv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
+      for (int u = 0; u < NU; ++u) {
         if (res) raff(rv[u]);
         bn_apply_row(x, res, y, mbits, (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc, f[u], rv[u],
                      sc, sh, relu);
@@ -485,7 +486,30 @@ __device__ __forceinline__ void bn_bwd_apply_row(const float* d, const float* xv
 // x2 (mean2): its backward reduction (sum dz, sum dz*(x2 - mean2), over the bf16-rounded dz that is stored) is
 // taken here as one partial row per block into part2 — the shortcut's own reduce pass disappears.
 // (host: C/8 <= 256 and 256 % (C/8) == 0, so every thread owns exactly one channel chunk)
-template <bool SC, bool MC = false>  // MC: ReLU mask recomputed from x with msc/msh (a lazy BatchNorm output)
+// 16-B streaming load/store with the nontemporal hint (the pass reads and writes each byte once)
+__device__ __forceinline__ void load8s(const bf16_t* p, float* f, bool nt) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 v = nt ? __builtin_nontemporal_load(reinterpret_cast<const u4*>(p)) : *reinterpret_cast<const u4*>(p);
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ void store8s(bf16_t* p, const float* f, bool nt) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 v = {pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7])};
+  if (nt) __builtin_nontemporal_store(v, reinterpret_cast<u4*>(p));
+  else *reinterpret_cast<u4*>(p) = v;
+}
+
+// dx = a*dz + b*x + c per channel (coefficients from bn_bwd_finalize); dz_out: the masked dz for the
+// residual branch (only when a ReLU mask is given)
+// SC: the masked dz (dz_out, the residual gradient) also feeds a projection shortcut's BatchNorm whose input is
+// x2 (mean2): its backward reduction (sum dz, sum dz*(x2 - mean2), over the bf16-rounded dz that is stored) is
+// taken here as one partial row per block into part2 — the shortcut's own reduce pass disappears.
+// (host: C/8 <= 256 and 256 % (C/8) == 0, so every thread owns exactly one channel chunk)
+// NU rows per trip, all of their loads (dy, x, mask bytes) issued before the first use; NT: nontemporal hints.
+template <bool SC, bool MC = false, int NU = EU, bool NT = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ ymask,
                                                            const uint8_t* __restrict__ mbits,
@@ -516,6 +540,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
       }
     }
   };
+  auto row_out = [&](const float* d, const float* xv, const float* ka, const float* kb, const float* kc, long i8) {
+    if (dz_out) store8s(dz_out + i8 * 8, d, NT);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(ka[j], d[j], fmaf(kb[j], xv[j], kc[j]));
+    store8s(dx + i8 * 8, o, NT);
+  };
   for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
     float ka[8], kb[8], kc[8], ms[8], mh[8];
     load_coef8(coef + cc * 8, ka);
@@ -527,21 +558,30 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
     }
     if constexpr (SC) load_coef8(mean2 + cc * 8, mu2);
     long r = (long)blockIdx.x * g.RPB + rsub;
-    for (; r + (EU - 1) * rstep < M; r += EU * rstep) {
-      float d[EU][8], xv[EU][8];
+    for (; r + (NU - 1) * rstep < M; r += NU * rstep) {
+      float d[NU][8], xv[NU][8];
+      uint32_t mb[NU];
+      long i8[NU];
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
-        const long i8 = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
-        load8(dy + i8 * 8, d[u]);
-        load8(x + i8 * 8, xv[u]);
-        if constexpr (MC) relu_mask8(d[u], nullptr, nullptr, i8, xv[u], ms, mh);
-        else relu_mask8(d[u], ymask, mbits, i8);
+      for (int u = 0; u < NU; ++u) {
+        i8[u] = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
+        load8s(dy + i8[u] * 8, d[u], NT);
+        load8s(x + i8[u] * 8, xv[u], NT);
+        if (!MC && mbits) mb[u] = mbits[i8[u]];
       }
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
-        const long i8 = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
-        bn_bwd_apply_row(d[u], xv[u], ka, kb, kc, dx, dz_out, i8);
-        sc_acc(d[u], i8);
+      for (int u = 0; u < NU; ++u) {
+        if constexpr (MC) {
+          relu_mask8(d[u], nullptr, nullptr, i8[u], xv[u], ms, mh);
+        } else if (mbits) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (!((mb[u] >> j) & 1u)) d[u][j] = 0.f;
+        } else {
+          relu_mask8(d[u], ymask, nullptr, i8[u]);
+        }
+        row_out(d[u], xv[u], ka, kb, kc, i8[u]);
+        sc_acc(d[u], i8[u]);
       }
     }
     for (; r < M; r += rstep) {
@@ -551,7 +591,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
       load8(x + i8 * 8, xv);
       if constexpr (MC) relu_mask8(d, nullptr, nullptr, i8, xv, ms, mh);
       else relu_mask8(d, ymask, mbits, i8);
-      bn_bwd_apply_row(d, xv, ka, kb, kc, dx, dz_out, i8);
+      row_out(d, xv, ka, kb, kc, i8);
       sc_acc(d, i8);
     }
   }
@@ -980,10 +1020,23 @@ static int ew_reverse() {
   return on;
 }
 
-// elementwise channels-last passes: enough blocks to fill the chip, each with >= EU row trips when possible
-int ew_grid(long M, int C) {
+// Variant of the streaming BN passes (tools/bench_bnb.py sweeps it; dtf_set_ew_variant): 0 = EU rows per trip,
+// 1 = + nontemporal hints, 2 = 8 rows per trip, 3 = 8 rows + nontemporal, 4 = 2 rows per trip
+// Measured (tools/bench_bnb.py, MI355X, ResNet-50 b256 shapes): 2 rows per trip is 3-9% faster than 4 on the
+// tensors that miss the Infinity Cache; nontemporal hints and 8 rows are not faster.
+int g_ew_variant = [] {
+  const char* e = getenv("DTF_EW_VARIANT");
+  return e ? atoi(e) : 4;
+}();
+int g_ew_apply_nu = [] {  // rows per trip of the forward apply pass (2, 4 or 8)
+  const char* e = getenv("DTF_EW_APPLY_NU");
+  return e ? atoi(e) : 2;
+}();
+
+// elementwise channels-last passes: enough blocks to fill the chip, each with >= nu row trips when possible
+int ew_grid(long M, int C, int nu = EU) {
   ColGeo g = colgeo(C);
-  long blocks = (M + (long)g.RPB * EU - 1) / ((long)g.RPB * EU);
+  long blocks = (M + (long)g.RPB * nu - 1) / ((long)g.RPB * nu);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
@@ -1026,6 +1079,15 @@ DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float*
   return (int)hipGetLastError();
 }
 
+DTF_API int dtf_set_ew_variant(int v) {
+  g_ew_variant = v;
+  return 0;
+}
+DTF_API int dtf_set_ew_apply_nu(int nu) {
+  g_ew_apply_nu = nu;
+  return 0;
+}
+
 DTF_API int dtf_bn_infer_coeff(const float* gamma, const float* beta, const float* rmean, const float* rvar, int C,
                                float eps, float* scale, float* shift, void* stream) {
   hipLaunchKernelGGL(bn_infer_coeff_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, gamma, beta,
@@ -1038,7 +1100,9 @@ DTF_API int dtf_bn_infer_coeff(const float* gamma, const float* beta, const floa
 DTF_API int dtf_bn_apply(const void* x, const float* scale, const float* shift, const void* res, void* y, long M,
                          int C, int relu, void* mbits, const float* rscale, const float* rshift, void* stream) {
   if ((C & 7) || ((rscale == nullptr) != (rshift == nullptr))) return -1;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(M, C)), dim3(256), 0, (hipStream_t)stream,
+  const int nu = g_ew_apply_nu;
+  hipLaunchKernelGGL((nu == 2 ? bn_apply_kernel<2> : nu == 8 ? bn_apply_kernel<8> : bn_apply_kernel<4>),
+                     dim3(ew_grid(M, C, nu == 2 || nu == 8 ? nu : 4)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)x, scale, shift, (const bf16_t*)res, (bf16_t*)y, M, C, relu,
                      relu ? (uint8_t*)mbits : nullptr, res ? rscale : nullptr, res ? rshift : nullptr, ew_reverse());
   return (int)hipGetLastError();
@@ -1130,7 +1194,7 @@ static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, con
   if (mbits || ymask) msc = msh = nullptr;
   if (part) bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
   const ColGeo geo = colgeo(C);
-  const int grid = ew_grid(M, C);
+  const int grid = ew_grid(M, C, g_ew_variant == 4 ? 2 : EU);  // (the shortcut-fused launch: one partial row per block)
   const bool fuse_sc = !msc && sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&
                        geo.TPR * geo.RPB == 256;
   if (sc && sc->rows2) *sc->rows2 = fuse_sc ? grid : 0;
@@ -1139,13 +1203,27 @@ static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, con
                        nullptr, (const bf16_t*)x, coef, M, C, (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr,
                        ew_reverse(), msc, msh);
   } else if (fuse_sc) {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                       (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse(), nullptr, nullptr);
+    if (g_ew_variant == 4)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, 2>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
+                         (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
+                         (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse(), nullptr, nullptr);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
+                         (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
+                         (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse(), nullptr, nullptr);
   } else {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                       (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse(), nullptr, nullptr);
+#define DTF_BNB(NU, NT)                                                                                        \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false, NU, NT>), dim3(ew_grid(M, C, NU)), dim3(256), 0, st,     \
+                     (const bf16_t*)dy, (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, \
+                     (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse(), nullptr, nullptr)
+    switch (g_ew_variant) {
+      case 1: DTF_BNB(EU, true); break;
+      case 2: DTF_BNB(8, false); break;
+      case 3: DTF_BNB(8, true); break;
+      case 4: DTF_BNB(2, false); break;
+      default: DTF_BNB(EU, false); break;
+    }
+#undef DTF_BNB
   }
   return (int)hipGetLastError();
 }
