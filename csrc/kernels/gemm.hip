@@ -278,6 +278,14 @@ static void launch_modes(GemmArgs& a, int tile, hipStream_t st) {
         launch_t<128, 128, 2, 2, AM, BMODE, 1>(a, st);
       }
       break;
+    case 15: case 16:  // 64 x 256 LDS-DMA (one block covers 256 output channels: the A rows are read once)
+      if constexpr (glds_mode(AM) && glds_mode(BMODE)) {
+        if (tile == 15) launch_t<64, 256, 1, 4, AM, BMODE, 3>(a, st);
+        else launch_t<64, 256, 1, 4, AM, BMODE, 4>(a, st);
+      } else {
+        launch_t<64, 256, 1, 4, AM, BMODE>(a, st);
+      }
+      break;
     default: launch_t<64, 64, 2, 2, AM, BMODE>(a, st); break;
   }
 }

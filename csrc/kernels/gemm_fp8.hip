@@ -427,10 +427,26 @@ DTF_API int dtf_gemm_fp8_ex(const void* A, const void* B, void* C, void* aux, co
   a.tiles_m = cdiv(M, 128);
   a.tiles_n = cdiv(N, big ? 128 : 64);
   dim3 grid(a.tiles_m * a.tiles_n, 1, 1);
-  if (big && fp8 == 2) hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, OP_KCONTIG, OP_KCONTIG, 2>), grid, dim3(NT), 0, st, a);
-  else if (big) hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT), 0, st, a);
-  else if (fp8 == 2) hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, OP_KCONTIG, OP_KCONTIG, 2>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((gemm_kernel<128, 64, 2, 2, OP_KCONTIG, OP_KCONTIG, 1>), grid, dim3(NT), 0, st, a);
+  // staging of the 128-row tiles (DTF_FP8_PIPE): 2 = register-staged double-buffered LDS, 3 / 4 = LDS-DMA single /
+  // double buffered (both operand rows are 16-B aligned: host-checked above). 3 measured fastest standalone on the
+  // GPT-2-medium projections (tools/bench_fp8_gemms.py: 0.602 vs 0.631 ms per layer for 2, 0.615 for 4) but slower in
+  // the model step (35.89 vs 35.17 ms: the side-stream weight gradients share the CUs), so 2 stays the default
+  static const int pipe = [] {
+    const char* e = getenv("DTF_FP8_PIPE");
+    return e ? atoi(e) : 2;
+  }();
+#define DTF_FP8_L(BN_, F_, P_) hipLaunchKernelGGL((gemm_kernel<128, BN_, 2, 2, OP_KCONTIG, OP_KCONTIG, F_, P_>), grid, \
+                                                  dim3(NT), 0, st, a)
+#define DTF_FP8_P(BN_, F_)                  \
+  if (pipe == 4) DTF_FP8_L(BN_, F_, 4);     \
+  else if (pipe == 3) DTF_FP8_L(BN_, F_, 3); \
+  else DTF_FP8_L(BN_, F_, 2);
+  if (big && fp8 == 2) { DTF_FP8_P(128, 2) }
+  else if (big) { DTF_FP8_P(128, 1) }
+  else if (fp8 == 2) { DTF_FP8_P(64, 2) }
+  else { DTF_FP8_P(64, 1) }
+#undef DTF_FP8_P
+#undef DTF_FP8_L
   return (int)hipGetLastError();
 }
 

@@ -1001,6 +1001,16 @@ int red_grid(long M, int C) {
 // BN statistic reduce + finalize as ONE launch (last-arriver hand-off) or two (group pass, finalize pass):
 // the agent-scope fences of the one-launch form cost more than the second launch boundary, mostly in the backward
 // where the side-stream weight gradients keep the CUs busy. DTF_BN_ONE_LAUNCH=1 selects the one-launch form.
+// leader rows left by the first (grouping) pass of a BN statistics reduction, which the finalize kernel then sums:
+// the grouping pass runs one block per leader row (more rows = more blocks reading the partials in parallel)
+static int bn_group_target() {
+  static const int t = [] {
+    const char* e = getenv("DTF_BN_GROUP_TARGET");
+    return e ? std::max(1, atoi(e)) : 32;
+  }();
+  return t;
+}
+
 static bool bn_one_launch() {
   static const bool on = [] {
     const char* e = getenv("DTF_BN_ONE_LAUNCH");  // two launches measured 1.9 % faster on ResNet-50 (b256)
@@ -1072,7 +1082,7 @@ DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float*
       return (int)hipGetLastError();
     }
   }
-  T = dtf_group_rows_once(part, rs, T, 2L * C, 32, &rs, stream);  // <= 32 leader rows, one launch
+  T = dtf_group_rows_once(part, rs, T, 2L * C, bn_group_target(), &rs, stream);  // <= target leader rows, one launch
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, T, rs, gamma,
                      beta,
                      running_mean, running_var, M, C, momentum, eps, scale, shift, mean_out, invstd_out);
@@ -1182,7 +1192,7 @@ static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const 
                        accumulate, tk);
     return;
   }
-  int T = dtf_group_rows_once(part, rs, G, 2L * C, 32, &rs, (void*)st);
+  int T = dtf_group_rows_once(part, rs, G, 2L * C, bn_group_target(), &rs, (void*)st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, mean, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);
 }

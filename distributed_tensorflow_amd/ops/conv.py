@@ -338,6 +338,9 @@ class _ConvBNFn(torch.autograd.Function):
             yc = conv_fwd_raw(x, bf16_shadow(w), g)
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
                  ptr(shift), stream())
+            if any(ctx.needs_input_grad):  # frozen BN: the backward normalises with the running statistics
+                mean.copy_(rmean)
+                torch.rsqrt(rvar + eps, out=invstd)
         raff = getattr(res, "_dtf_affine", None) if res is not None else None
         # the deferred projection BN (its input + mean): its backward reduction is taken in our apply pass
         res_src = getattr(res, "_dtf_bnsrc", None) if raff is not None else None
@@ -386,6 +389,8 @@ class _ConvBNFn(torch.autograd.Function):
         K = g[4]
         M = yc.numel() // K
         dout = dout.to(BF16).contiguous()
+        if not ctx.training:
+            return _ConvBNFn._backward_frozen(ctx, dout, x, w, gamma, yc, mbits, mean, invstd)
         dyc = torch.empty_like(yc)
         link, role = ctx.link, ctx.role
         # identity shortcut with ReLU: park dout + the ReLU mask instead of writing the masked residual gradient
@@ -464,6 +469,35 @@ class _ConvBNFn(torch.autograd.Function):
         if direct_bn:
             dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None, None
+
+
+    @staticmethod
+    def _backward_frozen(ctx, dout, x, w, gamma, yc, mbits, mean, invstd):
+        """Backward of an inference-mode (frozen) BatchNorm — Keras' BatchNormalization(training=False) under a
+        GradientTape, e.g. fine-tuning with frozen statistics: the BN is the fixed affine gamma*invstd*(z - mean) +
+        beta of the running statistics, so dz = dy * relu' * gamma*invstd, dgamma = sum(dy relu' xhat),
+        dbeta = sum(dy relu'). Rare path: torch ops on the GPU, f32 math."""
+        K = yc.shape[-1]
+        dz = dout.float()
+        if mbits is not None:
+            bits = (mbits.view(-1, 1) >> torch.arange(8, device=mbits.device, dtype=torch.uint8)) & 1
+            dz = dz * bits.view(dz.shape).to(dz.dtype)
+        dzr = dz.reshape(-1, K)
+        xhat = (yc.float().reshape(-1, K) - mean) * invstd
+        dgamma, dbeta = (dzr * xhat).sum(0), dzr.sum(0)
+        gm = gamma if gamma is not None else torch.ones_like(invstd)
+        dyc = (dz * (gm * invstd)).to(BF16).contiguous()
+        dres = None
+        if ctx.has_res:
+            dres = dz.to(BF16) if ctx.relu else dout
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad_raw(x, dyc, ctx.g, xf=ctx.xf)
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad_raw(dyc, w, ctx.g)
+        ctx.xf = ctx.mcoef = ctx.in_src = ctx.src = ctx.res_src = None
+        return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
+                dres, None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 def conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1), relu=True, residual=None,
@@ -628,7 +662,10 @@ def conv_bn_maxpool(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), d
     pk, ps, pp = tuple(pool_size), tuple(pool_strides), tuple(pool_pad)
     if s2d:
         assert tuple(w.shape[1:3]) == (7, 7) and stride == (2, 2) and pad == (3, 3) and dil == (1, 1)
-    if on_gpu(x) and w.shape[0] % 8 == 0 and pk[0] * pk[1] <= 127:
+    frozen_grad = not training and torch.is_grad_enabled() and any(
+        getattr(t, "requires_grad", False) for t in (x, w, gamma, beta))
+    if on_gpu(x) and w.shape[0] % 8 == 0 and pk[0] * pk[1] <= 127 and not frozen_grad:
+        # (inference-mode BN under a tape takes the unfused pair below: conv_bn's frozen-BN backward + max_pool2d)
         return _ConvBNPoolFn.apply(x.to(BF16), w, gamma, beta, rmean, rvar, stride, pad, dil, float(momentum),
                                    float(eps), bool(training), pk, ps, pp, bool(s2d))
     if s2d:

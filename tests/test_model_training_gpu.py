@@ -90,6 +90,58 @@ def test_resnet_trains_like_cpu_reference(cuda, monkeypatch):
         assert ls[-2] < ls[0] and ls[-1] < ls[1], (gl, cl)
 
 
+def _frozen_bn_grads(dev, x, y, ref_weights=None):
+    """Gradients of the cross-entropy through a reduced ResNet with its BatchNorms in inference mode (running
+    statistics from 3 training-mode forwards of the same batch on the CPU, copied into the device model)."""
+    from distributed_tensorflow_amd import context
+    from distributed_tensorflow_amd.models import ResNet
+    with context.device(dev):
+        initializers.set_seed(11)
+        m = ResNet(26, num_classes=10, width=16)
+        with torch.no_grad():
+            if ref_weights is None:
+                for _ in range(3):
+                    m(x.to(dev), training=True)
+            else:
+                m(x.to(dev)[:1], training=False)
+                for w, r in zip(m.weights, ref_weights):
+                    w.data.copy_(r.to(dev))
+        logits = m(x.to(dev), training=False).float()
+        loss = torch.nn.functional.cross_entropy(logits, y.to(dev))
+        grads = torch.autograd.grad(loss, m.trainable_weights)
+        return float(loss), [g.detach().float().cpu() for g in grads], [w.detach().float().cpu() for w in m.weights]
+
+
+def test_resnet_frozen_bn_gradients_match_cpu_reference(cuda, monkeypatch):
+    """Well-conditioned whole-model gradient check. With batch-statistics BN the gradient of a
+    random-init ResNet is chaotic: the f32 CPU reference itself moves by a median 23% per parameter under a 1e-3
+    input perturbation, and bf16 rounding alone by 33-49% (profiles/r3_resnet_grad_calibration.txt), so no bf16
+    implementation can match it per layer. With the BatchNorms frozen (inference mode, running statistics: Keras
+    fine-tuning semantics) the same network is well conditioned (f32: 3.3% at 1e-3), and every parameter's
+    gradient through the HIP path (s2d stem conv, fused ConvBN forward, frozen-BN backward, conv dgrad/wgrad on the
+    MFMA kernels, residual joins, max-pool, global pool, Dense) must match the bf16-emulating CPU reference at a
+    small median relative error, on fixed learnable (teacher) labels."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(8, 3, 64, 64, generator=g)
+    t = torch.randn(3 * 16, 10, generator=torch.Generator().manual_seed(99))
+    y = (torch.nn.functional.adaptive_avg_pool2d(x, 4).flatten(1) @ t).argmax(1)
+    import test_resnet_gpu as emu
+    from distributed_tensorflow_amd import ops
+    from distributed_tensorflow_amd.ops import conv as OC
+    gpu_ops = (ops.conv_bn, OC.conv_bn)
+    monkeypatch.setattr(ops, "conv_bn", emu._emu_conv_bn)
+    monkeypatch.setattr(OC, "conv_bn", emu._emu_conv_bn)
+    cpu = torch.device("cpu")
+    lc, gc, wc = _frozen_bn_grads(cpu, x, y)
+    monkeypatch.setattr(ops, "conv_bn", gpu_ops[0])
+    monkeypatch.setattr(OC, "conv_bn", gpu_ops[1])
+    lg, gg, _ = _frozen_bn_grads(cuda, x, y, ref_weights=wc)
+    assert abs(lg - lc) <= 0.01 * abs(lc), (lg, lc)
+    rel = [float((a - b).norm() / (b.norm() + 1e-12)) for a, b in zip(gg, gc) if b.numel() > 1]
+    med = float(np.median(rel))
+    assert all(np.isfinite(rel)) and med <= 0.05, (med, sorted(rel)[-5:])
+
+
 def test_bert_tiny_trains_like_cpu_reference(cuda):
     from distributed_tensorflow_amd.models.transformer import BertModel
     g = torch.Generator().manual_seed(1)
