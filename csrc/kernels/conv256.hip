@@ -330,6 +330,14 @@ bool conv256_on() {
 // Returns 0 if launched, 1 if not eligible (the caller falls back to gemm_core's kernels).
 int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool force) {
   if ((!conv256_on() && !force) || a.atomic_out) return 1;
+  // pointwise convolutions (K-contiguous x K-contiguous) stay on gemm_core.h's LDS-DMA tiles: measured slower here
+  // on every ResNet-50 1x1 layer it was eligible for (fwd 49.5 vs 43 us stage-3 c1, 96-101 vs 71-73 us stage-4
+  // c1/proj; dgrad 48 vs 41 us stage-3 c3: tools/conv_roofline.py --tiles, r3)
+  static const bool pw256 = [] {  // DTF_CONV256_1X1=1: let pointwise convolutions take this kernel again
+    const char* e = getenv("DTF_CONV256_1X1");
+    return e && e[0] == '1';
+  }();
+  if (!force && !pw256 && amode == OP_KCONTIG && bmode == OP_KCONTIG) return 1;
   if (cfg < 0) {
     static const int env = [] {
       const char* e = getenv("DTF_CONV256_CFG");

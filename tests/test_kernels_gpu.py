@@ -438,7 +438,7 @@ def test_conv_dgrad_fused_bn_backward_stats(cuda, case, beta, tile):
     close(p[Cin:], q_ref, 1e-3)
 
 
-@pytest.mark.parametrize("tile", [0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("tile", [0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("case", [(2, 14, 14, 64, 128, 3, 3, 1, 1), (3, 9, 9, 128, 64, 1, 1, 1, 0),
                                   (2, 15, 15, 64, 64, 3, 3, 2, 1), (5, 13, 11, 128, 192, 3, 3, 1, 1)])
 def test_conv_staging_pipelines_agree(cuda, case, tile):
