@@ -32,7 +32,6 @@ _KERNEL_SIGS = {
     "dtf_bn_bwd_apply_coef": [P, P, P, L, I, P, P, P, P, P, P, P, P, P, P],
     "dtf_set_bn_fin_fused": [I],
     "dtf_set_ew_variant": [I],
-    "dtf_gemm4w": [P, P, P, I, I, I, L, L, L, I, I, I, I, P, P],
     "dtf_set_ew_apply_nu": [I],
     "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P],
     "dtf_conv_wgrad": [P, P, P] + [I] * 15 + [I, I, I, P, L, P],
