@@ -67,7 +67,11 @@ def _compile(cmd, src, obj, deps, verbose):
 
 
 def _link(cmd, objs, out, verbose):
-    if os.path.exists(out) and os.path.getmtime(out) >= _newest(objs):
+    # the object list is part of the staleness check: a removed source must relink too
+    manifest = os.path.join(OBJDIR, os.path.basename(out) + ".objs")
+    listing = "\n".join(sorted(os.path.basename(o) for o in objs))
+    same = os.path.exists(manifest) and open(manifest).read() == listing
+    if same and os.path.exists(out) and os.path.getmtime(out) >= _newest(objs):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     if verbose:
@@ -76,6 +80,8 @@ def _link(cmd, objs, out, verbose):
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {out}\n{r.stdout}\n{r.stderr}")
     os.replace(out + ".tmp", out)
+    with open(manifest, "w") as f:
+        f.write(listing)
     return out
 
 
