@@ -307,7 +307,8 @@ class ConvBN(Layer):
         """link/role: residual-gradient join of a block (ops.conv.ResidualGradLink). pool: a MaxPooling2D
         applied to the (ReLU) output, fused with the BatchNorm (ops.conv_bn_maxpool); s2d: x is the
         space-to-depth image of a 7x7/2 conv's input (ops.image_to_s2d_bf16; the layer must be built).
-        lazy: the caller feeds the output ONLY to another ConvBN (ops.conv_bn lazy outputs)."""
+        lazy: the caller feeds the output ONLY to another ConvBN (ops.conv_bn lazy outputs); "1x1"/"3x3" name
+        the consuming convolution's kind (DTF_LAZY_BN selects which kinds stay lazy)."""
         if self.padding == "same":
             pad = ((self.kernel_size[0] - 1) // 2, (self.kernel_size[1] - 1) // 2)
         else:
@@ -319,7 +320,7 @@ class ConvBN(Layer):
                                        self.moving_variance, stride=self.strides, pad=pad, momentum=self.momentum,
                                        eps=self.epsilon, training=bool(training), pool_size=pool.pool_size,
                                        pool_strides=pool.strides, pool_pad=pool.pads(), s2d=s2d)
-        kw = {"lazy": True} if lazy else {}
+        kw = {"lazy": lazy} if lazy else {}
         return ops.conv_bn(x, self.kernel, self.gamma, self.beta, self.moving_mean, self.moving_variance,
                            stride=self.strides, pad=pad, relu=self.relu, residual=residual, momentum=self.momentum,
                            eps=self.epsilon, training=bool(training), link=link, role=role, **kw)

@@ -297,10 +297,16 @@ _LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
 # its consuming ConvBN applies it to the staged conv output in its forward and weight-gradient operand loaders
 # (gemm_core.h XF) and the ReLU mask is recomputed from the conv output in the backward. Opt-in (DTF_LAZY_BN=1):
 # measured on MI355X (ResNet-50 b256) the in-LDS transform between the DMA wait and the barrier slows the consuming
-# 3x3 convolutions by ~50% (no 256-row pipelined form) and the step went from 22.7 to 24.9 ms.
-_LAZY_BN = __import__("os").environ.get("DTF_LAZY_BN", "0") == "1"
+# 3x3 convolutions by ~50% (no 256-row pipelined form) and the step went from 22.7 to 24.9 ms. DTF_LAZY_BN=1x1: only
+# outputs whose consumer is a pointwise convolution (a bottleneck's c2 -> c3; conv_bn(lazy="1x1")) stay lazy.
+_LAZY_BN = __import__("os").environ.get("DTF_LAZY_BN", "0")
 _DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
 _COMPACT_PROJ = __import__("os").environ.get("DTF_COMPACT_PROJ", "1") != "0"
+
+
+def _lazy_enabled(consumer):
+    """consumer: True / "1x1" / "3x3" — the kind of convolution that reads the lazy output."""
+    return _LAZY_BN == "1" or (_LAZY_BN == "1x1" and consumer == "1x1")
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -346,7 +352,7 @@ class _ConvBNFn(torch.autograd.Function):
         res_src = getattr(res, "_dtf_bnsrc", None) if raff is not None else None
         if res is not None:
             res = res.contiguous()
-        lazy = bool(lazy and _LAZY_BN and training and relu and res is None and role != "proj")
+        lazy = bool(lazy and _lazy_enabled(lazy) and training and relu and res is None and role != "proj")
         mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if (relu and not lazy) else None
         if lazy:
             # the BN+ReLU output is never written: the consumer's loaders apply scale/shift + ReLU to yc, and the
@@ -509,7 +515,7 @@ def conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1
     stride, pad, dil = tuple(stride), tuple(pad), tuple(dil)
     if on_gpu(x):
         return _ConvBNFn.apply(x.to(BF16), w, gamma, beta, residual, rmean, rvar, stride, pad, dil, bool(relu),
-                               float(momentum), float(eps), bool(training), link, role, bool(lazy))
+                               float(momentum), float(eps), bool(training), link, role, lazy or False)
     y = _ref_conv(x, w, None, stride, pad, dil)
     from .norm import batch_norm_ref
     y = batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training)

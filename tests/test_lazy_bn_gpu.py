@@ -135,15 +135,17 @@ def test_lazy_bottlenecks_match_materialised(cuda, monkeypatch):
 
     monkeypatch.setattr(OC, "call", spy)
     runs, applies = {}, {}
-    for lazy in (False, True):  # (lazy outputs are opt-in: DTF_LAZY_BN=1)
-        monkeypatch.setattr(OC, "_LAZY_BN", lazy)
+    for mode in ("0", "1", "1x1"):  # DTF_LAZY_BN: off / every bottleneck c1+c2 / only c2 (pointwise consumer)
+        monkeypatch.setattr(OC, "_LAZY_BN", mode)
         seen.clear()
-        runs[lazy] = _run(_blocks(), x)
+        runs[mode] = _run(_blocks(), x)
         torch.cuda.synchronize()
-        applies[lazy] = seen.count("dtf_bn_apply")
-    assert applies[False] - applies[True] == 4, applies
-    worst = 0.0
-    for a, b in zip(runs[False], runs[True]):
-        s = a.abs().max().item() + 1e-6
-        worst = max(worst, (a - b).abs().max().item() / s)
-    assert worst < 2e-2, worst
+        applies[mode] = seen.count("dtf_bn_apply")
+    assert applies["0"] - applies["1"] == 4, applies
+    assert applies["0"] - applies["1x1"] == 2, applies
+    for mode in ("1", "1x1"):
+        worst = 0.0
+        for a, b in zip(runs["0"], runs[mode]):
+            s = a.abs().max().item() + 1e-6
+            worst = max(worst, (a - b).abs().max().item() / s)
+        assert worst < 2e-2, (mode, worst)
