@@ -258,6 +258,21 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   if (staged) {
     constexpr int CS = BN + 8;  // LDS row stride (elements): conflict-free 8-B fragment writes
     bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
+    // fp8 copies of C (GemmArgs::q8*): the delayed scale, and this thread's running max |value|
+    const bool q8on = a.q8 || a.q8T || a.q8col;
+    const bool q8tp = a.q8T || a.q8col;  // the column pass over the LDS tile
+    const float q8fmax = a.q8fmt ? 57344.f : 448.f;
+    float q8inv = 0.f, q8max = 0.f;
+    if (q8on) {
+      const float ap = a.q8amax_prev ? a.q8amax_prev[0] : 0.f;
+      const float sc = ap > 0.f ? ap / q8fmax : fmaxf(a.q8scale[0], 1e-30f);
+      q8inv = 1.f / sc;
+      if (a.q8used && blockIdx.x == 0 && blockIdx.z == 0 && tid == 0) {
+        a.q8used[0] = sc;
+        if (a.q8used2) a.q8used2[0] = sc;
+      }
+    }
+    auto q8v = [&](float f) { return fminf(fmaxf(f * q8inv, -q8fmax), q8fmax); };
     __syncthreads();  // every wave is done with the operand buffers
     for (int o = 0; o < (a.aux ? 2 : 1); ++o) {
       bf16_t* dst = (o ? a.aux : reinterpret_cast<bf16_t*>(a.C)) + cbase;
@@ -309,10 +324,68 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
               val.z = pack2bf(f[4], f[5]); val.w = pack2bf(f[6], f[7]);
             }
             if (o == 0 && a.dact) val = dact8(val, *reinterpret_cast<const uint4*>(a.dact_src + (long)m * a.ldc + n), a.dact);
-            *reinterpret_cast<uint4*>(dst + (long)m * a.ldc + n) = val;
+            if (o != 0 || !a.no_c) *reinterpret_cast<uint4*>(dst + (long)m * a.ldc + n) = val;
+            if (o == 0 && q8on) {
+              const uint32_t vw[4] = {val.x, val.y, val.z, val.w};
+              float f[8];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                f[2 * q] = __uint_as_float(vw[q] << 16);
+                f[2 * q + 1] = __uint_as_float(vw[q] & 0xffff0000u);
+              }
+#pragma unroll
+              for (int r = 0; r < 8; ++r) q8max = fmaxf(q8max, fabsf(f[r]));
+              if (a.q8)
+                *reinterpret_cast<uint2*>(a.q8 + (long)m * a.N + n) =
+                    make_uint2(q8pack4(a.q8fmt, q8v(f[0]), q8v(f[1]), q8v(f[2]), q8v(f[3])),
+                               q8pack4(a.q8fmt, q8v(f[4]), q8v(f[5]), q8v(f[6]), q8v(f[7])));
+              // the column pass reads the final values from LDS (beta / dact changed them in registers)
+              if (q8tp && (a.dact || a.beta != 0.f)) *reinterpret_cast<uint4*>(ct + row * CS + c8 * 8) = val;
+            }
           }
         }
         __syncthreads();
+        if (o == 0 && q8tp) {
+          // column pass: thread -> one column of this 128-row half (16-row groups: 16 LDS reads, one 16-B store of
+          // the transposed copy each; the column sum in a fixed row order: deterministic)
+          for (int nl = tid; nl < BN; nl += NT2) {
+            const int n = n0 + nl;
+            float cs = 0.f;
+#pragma unroll 2
+            for (int rg = 0; rg < 8; ++rg) {
+              float f[16];
+#pragma unroll
+              for (int i = 0; i < 16; ++i) f[i] = __uint_as_float((uint32_t)ct[(rg * 16 + i) * CS + nl] << 16);
+#pragma unroll
+              for (int i = 0; i < 16; ++i) cs += f[i];
+              if (a.q8T) {
+                uint4 qv;
+                qv.x = q8pack4(a.q8fmt, q8v(f[0]), q8v(f[1]), q8v(f[2]), q8v(f[3]));
+                qv.y = q8pack4(a.q8fmt, q8v(f[4]), q8v(f[5]), q8v(f[6]), q8v(f[7]));
+                qv.z = q8pack4(a.q8fmt, q8v(f[8]), q8v(f[9]), q8v(f[10]), q8v(f[11]));
+                qv.w = q8pack4(a.q8fmt, q8v(f[12]), q8v(f[13]), q8v(f[14]), q8v(f[15]));
+                *reinterpret_cast<uint4*>(a.q8T + (long)n * a.M + m0 + h * 128 + rg * 16) = qv;
+              }
+            }
+            if (a.q8col) a.q8col[(long)((m0 + h * 128) >> 7) * a.N + n] = cs;
+          }
+          __syncthreads();
+        }
+      }
+    }
+    if (q8on && a.q8amax) {  // block max |value| -> the amax slot (relaxed check first: most blocks lose)
+      float mx = q8max;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      float* red = reinterpret_cast<float*>(smem);
+      if (lane == 0) red[w] = mx;
+      __syncthreads();
+      if (tid == 0) {
+#pragma unroll
+        for (int i = 1; i < NT2 / 64; ++i) mx = fmaxf(mx, red[i]);
+        unsigned int* am = reinterpret_cast<unsigned int*>(a.q8amax);
+        const unsigned int cur = __hip_atomic_load(am, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__float_as_uint(mx) > cur) atomicMax(am, __float_as_uint(mx));
       }
     }
     return;

@@ -140,7 +140,35 @@ struct GemmArgs {
   // ReLU mask of the BN-backward statistics (bnx != nullptr) when no bit mask exists: relu'(bnx * bnsc + bnsh)
   const float* bnsc;
   const float* bnsh;
+  // fp8 copies of the (bf16-rounded, post-activation / post-dact) output written by the staged epilogue of
+  // gemm256.hip (host-checked; the bf16 C store is skipped when no_c): q8 [M][N] row-major, q8T [N][M] transposed,
+  // q8col [M/128][N] per-128-row column sums of the values (a bias gradient's partials). Delayed scaling as
+  // gemm_fp8.hip's transposing quantizer: scale = q8amax_prev / fmax when > 0 (else *q8scale), published to
+  // q8used / q8used2 by block 0; max |value| accumulated into q8amax. q8fmt 0 = e4m3, 1 = e5m2.
+  uint8_t* q8;
+  uint8_t* q8T;
+  float* q8col;
+  const float* q8scale;
+  float* q8amax;
+  const float* q8amax_prev;
+  float* q8used;
+  float* q8used2;
+  int q8fmt;
+  int no_c;
 };
+
+// 4 floats -> 4 packed OCP fp8 bytes (fmt 0 e4m3, 1 e5m2), values already scaled and clamped
+__device__ __forceinline__ uint32_t q8pack4(int fmt, float a0, float a1, float a2, float a3) {
+  int r;
+  if (fmt) {
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a0, a1, 0, false);
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a2, a3, r, true);
+  } else {
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
+  }
+  return (uint32_t)r;
+}
 
 // ---- on-the-fly BatchNorm + ReLU of 8 staged bf16 values (channels c .. c+7) ---------------------------------------
 struct Coef8 {

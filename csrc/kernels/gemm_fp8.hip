@@ -481,3 +481,37 @@ DTF_API int dtf_gemm_fp8(const void* A, const void* B, void* C, void* aux, const
                        (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
+
+// fp8 GEMM whose epilogue also writes fp8 copies of its (bf16-rounded) output for the next fp8 layer (GemmArgs::q8*):
+// C[M][N] = (s0*s1) * A_q . B_q^T (+bias, act with the pre-activation to aux; dact_src/dact: the output is the
+// gradient of act(dact_src) — the activation backward applied in the store pass). C may be null (only the fp8
+// copies are written). Runs on the 256-row pipelined kernel only: returns -6 (nothing launched) when that kernel
+// cannot take the shape, and the caller falls back to the bf16 output + a quantize pass.
+DTF_API int dtf_gemm_fp8_q8(const void* A, const void* B, void* C, void* aux, const float* bias, const float* scales,
+                            int M, int N, int K, long lda, long ldb, int act, int fmt_a, const void* dact_src,
+                            int dact, float* zero_slot, void* q8, void* q8T, float* q8col, int q8fmt,
+                            const float* q8scale, float* q8amax, const float* q8amax_prev, float* q8used,
+                            float* q8used2, void* stream) {
+  if ((N & 7) || (K & 127) || (lda & 15) || (ldb & 15) || M <= 0) return -1;
+  if ((M & 255) || !q8scale || (C && ((uintptr_t)C & 15)) || (aux && ((uintptr_t)aux & 15)) ||
+      (dact_src && ((uintptr_t)dact_src & 15)) || (q8T && (M & 15)) || (q8 && ((uintptr_t)q8 & 7)) ||
+      (q8T && ((uintptr_t)q8T & 15)))
+    return -6;
+  int bn = pick256(M, N, 2L * K, 1);
+  if (!bn) bn = (N % 256 == 0) ? 256 : 128;
+  if (N % bn) return -6;
+  GemmArgs a{};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C; a.aux = (bf16_t*)aux;
+  a.bias = bias; a.scales = scales;
+  a.M = M; a.N = N; a.K = K / 2;
+  a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = N;
+  a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
+  a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = 0;
+  a.dact_src = (const bf16_t*)dact_src; a.dact = dact_src ? dact : 0;
+  a.zero_slot = zero_slot;
+  a.q8 = (uint8_t*)q8; a.q8T = (uint8_t*)q8T; a.q8col = q8col; a.q8fmt = q8fmt;
+  a.q8scale = q8scale; a.q8amax = q8amax; a.q8amax_prev = q8amax_prev; a.q8used = q8used; a.q8used2 = q8used2;
+  a.no_c = C ? 0 : 1;
+  if (gemm256_try(a, OP_KCONTIG, OP_KCONTIG, (hipStream_t)stream, fmt_a == 1 ? 2 : 1, bn)) return -6;
+  return (int)hipGetLastError();
+}

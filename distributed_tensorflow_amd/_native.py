@@ -86,6 +86,7 @@ _KERNEL_SIGS = {
     "dtf_fp8_update_scale2": [P, P, P, F, F, P],
     "dtf_reduce_rows": [P, L, I, L, P, I, P],
     "dtf_gemm_fp8_ex": [P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, F, I, P, L, P, P],
+    "dtf_gemm_fp8_q8": [P, P, P, P, P, P, I, I, I, L, L, I, I, P, I, P, P, P, P, I, P, P, P, P, P, P],
     "dtf_quant_fp8_t2": [P, P, I, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P],
     "dtf_group_rows_once": [P, L, I, L, I, P, P],
     "dtf_sum_rows": [P, L, I, L, P, I, P],  # void: the int return value is meaningless

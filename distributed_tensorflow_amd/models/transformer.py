@@ -45,7 +45,7 @@ class _Proj(KL.Layer):
     def call(self, x, training=None, link=None):
         if self.fp8 and x.is_cuda:
             from ..ops.fp8 import dense_fp8
-            return dense_fp8(x, self.kernel, self.bias, self.activation, self)
+            return dense_fp8(x, self.kernel, self.bias, self.activation, self, getattr(self, "_fp8_next", None))
         return ops.dense(x, self.kernel, self.bias, act=self.activation, link=link, tag_act=self.single_consumer)
 
 
@@ -146,6 +146,8 @@ class GPT2Block(KL.Layer):
         self.ln2 = KL.LayerNormalization(epsilon=1e-5)
         self.fc = _Proj(4 * hidden, activation="gelu", fp8=fp8, single_consumer=True)
         self.proj = _Proj(hidden, fp8=fp8)
+        if fp8:  # FFN1's output feeds only FFN2: fp8 operands from FFN1's epilogue (ops.fp8 DTF_FP8_FUSE); untracked
+            object.__setattr__(self.fc, "_fp8_next", self.proj)
         self.dropout = dropout
 
     def call(self, x, training=None):

@@ -25,7 +25,7 @@ import torch
 
 import contextlib
 
-from ._util import BF16, F32, bf16_shadow, call, direct_grad, fork_side, ptr, stream, weights_epoch, workspace
+from ._util import BF16, F32, K, bf16_shadow, call, direct_grad, fork_side, ptr, stream, weights_epoch, workspace
 from .linalg import DENSE_SIDE_ON, colsum, dense_dgrad, dense_wgrad
 
 E4M3_MAX = 448.0
@@ -111,6 +111,10 @@ class _Fp8State:
         self.w_prev = None  # the weight amax slot this step's pass read (cleared by this step's weight gradient)
         self.wq = self.wqT = None
         self.w_key = None
+        # fp8 operands written by the neighbouring layer's GEMM epilogue (gemm256.hip q8 outputs), matched by the
+        # data pointer of the placeholder that stands for the bf16 tensor nobody wrote:
+        self.pending_x = None  # (ptr, xq, xqT, amax slot to clear, producer state, producer pre, producer act)
+        self.pending_g = None  # (ptr, dzq, dzqT, column-sum partials, amax slot to clear)
 
 
 def _state(layer, dev):
@@ -157,21 +161,89 @@ def _fp8_bwd_ok(M, K, N):
     return _FP8_BWD and M % 128 == 0 and K % 128 == 0 and N % 128 == 0
 
 
+# Producer-side quantization (DTF_FP8_FUSE, default on): a GELU projection whose only consumer is another fp8
+# projection (GPT-2's FFN1 -> FFN2, linked by _Proj.fp8_next) writes FFN2's e4m3 input and its transpose from its own
+# GEMM epilogue, and FFN2's data-gradient GEMM writes FFN1's e5m2 gradient (GELU backward applied), its transpose and
+# the bias-gradient column sums from its epilogue: the bf16 GELU output and the bf16 gradient of it are never
+# written, and two quantize passes per layer and step leave the critical stream. Delayed scaling is unchanged (the
+# same amax slots, parities and scale publication as the quantize pass).
+_FUSE = os.environ.get("DTF_FP8_FUSE", "1") != "0"
+
+
+def _placeholder(shape, dev):
+    """A stand-in for a bf16 activation / gradient that only exists in fp8 (its consumer finds the fp8 copies by
+    this tensor's data pointer): one element, expanded (zero strides, no storage of the full size)."""
+    return torch.empty(1, dtype=BF16, device=dev).expand(*shape)
+
+
+def _gemm_q8(a, b, scales, out, *, fmt_a, q8, q8T, q8col, q8fmt, q8buf, q8scale, q8cur, q8prev, q8used2=None,
+             bias=None, act=0, aux=None, dact_src=None, dact=0, zero_slot=None):
+    """gemm_fp8 whose epilogue also writes fp8 copies of its output (dtf_gemm_fp8_q8); False when the pipelined
+    kernel cannot take the shape (nothing was launched)."""
+    M, Kd = a.shape
+    N = b.shape[0]
+    rc = K().dtf_gemm_fp8_q8(ptr(a), ptr(b), ptr(out), ptr(aux), ptr(bias), ptr(scales), M, N, Kd, a.stride(0),
+                             b.stride(0), int(act), int(fmt_a), ptr(dact_src), int(dact), ptr(zero_slot), ptr(q8),
+                             ptr(q8T), ptr(q8col), int(q8fmt), ptr(q8buf[q8scale:q8scale + 1]),
+                             ptr(q8buf[q8cur:q8cur + 1]), ptr(q8buf[q8prev:q8prev + 1]),
+                             ptr(q8buf[q8scale:q8scale + 1]), ptr(q8used2), stream())
+    if rc == -6:
+        return False
+    if rc != 0:
+        raise RuntimeError(f"dtf_gemm_fp8_q8 failed with status {rc}")
+    return True
+
+
 class _DenseFP8(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, st):
+    def forward(ctx, x, w, b, act, st, nxt=None):
         shp = x.shape
-        x2 = x.reshape(-1, shp[-1]).contiguous()
-        M, K = x2.shape
         N = w.shape[0]
         buf = st.buf
+        pend, st.pending_x = st.pending_x, None
+        ctx.src = None
+        if pend is not None and x.data_ptr() == pend[0]:
+            # x exists only in fp8: the producing layer's epilogue wrote it (and its transpose) with our scale
+            xq, xqT, prev = pend[1], pend[2], pend[3]
+            M, K = xq.shape
+            ctx.src = pend[4:]  # (producer state, its pre-activation, its activation): the fused dgrad target
+            y = torch.empty((M, N), dtype=BF16, device=x.device)
+            pre = torch.empty((M, N), dtype=BF16, device=x.device) if act else None
+            wq, wqT = _weight_fp8(st, w, True)
+            gemm_fp8(xq, wq, buf[X_SCALE:X_SCALE + 2], y, bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1])
+            return _DenseFP8._finish_fwd(ctx, True, xqT, w, pre, st, b, act, shp, (M, K, N), y)
+        x2 = x.reshape(-1, shp[-1]).contiguous()
+        M, K = x2.shape
         fbwd = _fp8_bwd_ok(M, K, N)
         if not st.x_ready:  # bootstrap the delayed activation scale once
             buf[X_SCALE:X_SCALE + 1].copy_(x2.abs().amax().float().clamp_min(1e-12) / E4M3_MAX)
             st.x_ready = True
         xs = buf[X_SCALE:X_SCALE + 1]
-        y = torch.empty((M, N), dtype=BF16, device=x.device)
         pre = torch.empty((M, N), dtype=BF16, device=x.device) if act else None
+        nst = _state(nxt, x.device) if nxt is not None else None
+        if (nst is not None and _FUSE and fbwd and act and nst.x_ready and M % 256 == 0
+                and not torch.cuda.is_current_stream_capturing()):
+            # our output feeds only the next fp8 projection: write its e4m3 operand (+ transpose) instead of bf16
+            cur, prev = (X_AMAX, X_AMAX2) if st.tx % 2 == 0 else (X_AMAX2, X_AMAX)
+            ncur, nprev = (X_AMAX, X_AMAX2) if nst.tx % 2 == 0 else (X_AMAX2, X_AMAX)
+            xq, xqT, _ = quantize_t(x2, xs, buf[cur:cur + 1], amax_prev=buf[prev:prev + 1], scale_used=xs,
+                                    scale_used2=buf[X_USED:X_USED + 1])
+            st.tx += 1
+            wq, wqT = _weight_fp8(st, w, True)
+            yq = torch.empty((M, N), dtype=torch.uint8, device=x.device)
+            yqT = torch.empty((N, M), dtype=torch.uint8, device=x.device)
+            nb = nst.buf
+            if _gemm_q8(xq, wq, buf[X_SCALE:X_SCALE + 2], None, fmt_a=0, q8=yq, q8T=yqT, q8col=None, q8fmt=0,
+                        q8buf=nb, q8scale=X_SCALE, q8cur=ncur, q8prev=nprev, q8used2=nb[X_USED:X_USED + 1],
+                        bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1]):
+                nst.tx += 1
+                y = _placeholder((M, N), x.device)
+                nst.pending_x = (y.data_ptr(), yq, yqT, nprev, st, pre, act)
+                return _DenseFP8._finish_fwd(ctx, True, xqT, w, pre, st, b, act, shp, (M, K, N), y)
+            y = torch.empty((M, N), dtype=BF16, device=x.device)  # (shape not taken by the pipelined kernel)
+            gemm_fp8(xq, wq, buf[X_SCALE:X_SCALE + 2], y, bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1])
+            return _DenseFP8._finish_fwd(ctx, True, xqT, w, pre, st, b, act, shp, (M, K, N), y)
+        y = torch.empty((M, N), dtype=BF16, device=x.device)
         if fbwd and not torch.cuda.is_current_stream_capturing():
             # delayed scaling folded into the quantize pass (amax slots double-buffered by step parity)
             cur, prev = (X_AMAX, X_AMAX2) if st.tx % 2 == 0 else (X_AMAX2, X_AMAX)
@@ -191,18 +263,19 @@ class _DenseFP8(torch.autograd.Function):
                  K, K, N, int(act), -1, stream())
             # next step's x scale from this pass's amax; the scale this pass used is kept for the weight gradient
             call("dtf_fp8_update_scale2", ptr(xa), ptr(xs), ptr(buf[X_USED:X_USED + 1]), E4M3_MAX, 0.0, stream())
+        return _DenseFP8._finish_fwd(ctx, fbwd, xqT if fbwd else x2, w, pre, st, b, act, shp, (M, K, N), y)
+
+    @staticmethod
+    def _finish_fwd(ctx, fbwd, xs, w, pre, st, b, act, shp, MKN, y):
         ctx.fbwd = fbwd
-        if fbwd:
-            ctx.save_for_backward(xqT, w, pre)
-        else:
-            ctx.save_for_backward(x2, w, pre)
+        ctx.save_for_backward(xs, w, pre)  # xs: x^T in e4m3 (fp8 backward) or the bf16 x
         ctx.st = st
         ctx.b_param = b
         ctx.act = act
         ctx.has_b = b is not None
         ctx.shp = shp
-        ctx.MKN = (M, K, N)
-        return y.reshape(*shp[:-1], N)
+        ctx.MKN = MKN
+        return y.reshape(*shp[:-1], MKN[2])
 
     @staticmethod
     def backward(ctx, dy):
@@ -211,16 +284,21 @@ class _DenseFP8(torch.autograd.Function):
         xqT, w, pre = ctx.saved_tensors
         st, (M, K, N) = ctx.st, ctx.MKN
         buf = st.buf
-        dy2 = dy.reshape(-1, N).to(BF16).contiguous()
         gs, ga = buf[G_SCALE:G_SCALE + 1], buf[G_AMAX:G_AMAX + 1]
-        if not st.g_ready:  # bootstrap the delayed gradient scale once (GELU' <= 1.13)
-            gs.copy_(dy2.abs().amax().float().clamp_min(1e-30) * (1.2 if ctx.act else 1.0) / E5M2_MAX)
-            st.g_ready = True
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_db = ctx.has_b and ctx.needs_input_grad[2]
+        gpend, st.pending_g = st.pending_g, None
+        fused_in = gpend is not None and dy.data_ptr() == gpend[0] and need_dx
+        if not fused_in:
+            dy2 = dy.reshape(-1, N).to(BF16).contiguous()
+            if not st.g_ready:  # bootstrap the delayed gradient scale once (GELU' <= 1.13)
+                gs.copy_(dy2.abs().amax().float().clamp_min(1e-30) * (1.2 if ctx.act else 1.0) / E5M2_MAX)
+                st.g_ready = True
         folded = need_dx and not torch.cuda.is_current_stream_capturing()
         prev = None
-        if folded:  # delayed gradient scaling folded into the quantize pass (see forward)
+        if fused_in:  # the consumer's data-gradient epilogue quantized our gradient (act backward applied)
+            dzq, dzqT, cp, prev = gpend[1], gpend[2], gpend[3], gpend[4]
+        elif folded:  # delayed gradient scaling folded into the quantize pass (see forward)
             cur, prev = (G_AMAX, G_AMAX2) if st.tg % 2 == 0 else (G_AMAX2, G_AMAX)
             st.tg += 1
             dzq, dzqT, cp = quantize_t(dy2, gs, buf[cur:cur + 1], fmt=1, pre=pre if ctx.act else None, act=ctx.act,
@@ -232,10 +310,29 @@ class _DenseFP8(torch.autograd.Function):
         dx = dw = db = None
         if need_dx:
             _, wqT = _weight_fp8(st, w, True)
-            dx = torch.empty((M, K), dtype=BF16, device=dy.device)
-            gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1,  # scales (s_w, s_g)
-                     zero_slot=buf[prev:prev + 1] if folded else None)
-            dx = dx.reshape(ctx.shp)
+            src, ctx.src = ctx.src, None
+            dx = None
+            if src is not None and folded and src[0].g_ready and src[2] and M % 256 == 0:
+                # our input came from the producer's fp8 epilogue: quantize ITS gradient here (the activation
+                # backward from its saved pre-activation, e5m2 + transpose + bias-gradient column partials)
+                pst, ppre, pact = src
+                pb = pst.buf
+                pcur, pprev = (G_AMAX, G_AMAX2) if pst.tg % 2 == 0 else (G_AMAX2, G_AMAX)
+                gq = torch.empty((M, K), dtype=torch.uint8, device=dy.device)
+                gqT = torch.empty((K, M), dtype=torch.uint8, device=dy.device)
+                gcp = torch.empty((M // 128, K), dtype=F32, device=dy.device)
+                if _gemm_q8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], None, fmt_a=1, q8=gq, q8T=gqT, q8col=gcp, q8fmt=1,
+                            q8buf=pb, q8scale=G_SCALE, q8cur=pcur, q8prev=pprev, dact_src=ppre, dact=pact,
+                            zero_slot=buf[prev:prev + 1]):
+                    pst.tg += 1
+                    dx = _placeholder((M, K), dy.device)
+                    pst.pending_g = (dx.data_ptr(), gq, gqT, gcp, pprev)
+                    dx = dx.reshape(ctx.shp)
+            if dx is None:
+                dx = torch.empty((M, K), dtype=BF16, device=dy.device)
+                gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1,  # scales (s_w, s_g)
+                         zero_slot=buf[prev:prev + 1] if folded else None)
+                dx = dx.reshape(ctx.shp)
         tw = direct_grad(w) if need_dw else None
         tb = direct_grad(ctx.b_param) if need_db else None
         # arena-accumulated weight / bias gradients go to the side stream (off the dgrad critical path)
@@ -258,7 +355,7 @@ class _DenseFP8(torch.autograd.Function):
                 # next step's gradient scale: on the stream of the last reader of this step's scale (the weight
                 # gradient), which was forked after the data gradient was issued
                 call("dtf_fp8_update_scale2", ptr(ga), ptr(gs), None, E5M2_MAX, 0.0, stream())
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
     @staticmethod
     def _backward_bf16(ctx, dy):
@@ -283,11 +380,13 @@ class _DenseFP8(torch.autograd.Function):
                 colsum(dz, out=tb, accumulate=True)
             else:
                 db = colsum(dz)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
-def dense_fp8(x, w, b, activation, layer):
+def dense_fp8(x, w, b, activation, layer, next_layer=None):
+    """next_layer: the fp8 projection that is the ONLY consumer of this one's output (its operands may then be
+    written by this layer's epilogue; see DTF_FP8_FUSE)."""
     from .linalg import act_code
     a = act_code(activation)
     st = _state(layer, x.device)
-    return _DenseFP8.apply(x.to(BF16), w, b, a, st)
+    return _DenseFP8.apply(x if x.dtype == BF16 else x.to(BF16), w, b, a, st, next_layer)
