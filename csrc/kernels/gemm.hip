@@ -230,8 +230,9 @@ static void launch_t(GemmArgs& a, hipStream_t st) {
 }
 
 // Launch with the on-the-fly BatchNorm + ReLU of operand XF (1 = A, 2 = B; GemmArgs.xsc/xsh): the LDS-DMA tiles
-// (7-10) transform each lane's landed slots in place; the register-staged tiles (0, 2, 3, 4) exist only for a
-// K-outer X operand (the 1x1 weight gradient). Returns false when the combination has no XF kernel.
+// (7-10) transform each lane's landed slots in place; the register-staged tiles (0, 2, 3, 4) transform in registers
+// before the ds_write (K-outer X of a 1x1 weight gradient, plain K-contiguous X of a pointwise forward). Returns false
+// when the combination has no XF kernel.
 template <int AM, int BMODE, int XF>
 static bool launch_modes_xf(GemmArgs& a, int tile, hipStream_t st) {
   constexpr int XM = XF == 1 ? AM : BMODE;
@@ -244,7 +245,7 @@ static bool launch_modes_xf(GemmArgs& a, int tile, hipStream_t st) {
       default: break;
     }
   }
-  if constexpr (XM == OP_KOUTER) {  // register-staged K-outer X operand (KOuterLoader transforms before ds_write)
+  if constexpr (XM == OP_KOUTER || XM == OP_KCONTIG) {  // register-staged X operand (transform before ds_write)
     switch (tile) {
       case 0: launch_t<128, 128, 2, 2, AM, BMODE, 1, XF>(a, st); return true;
       case 2: launch_t<128, 64, 2, 2, AM, BMODE, 1, XF>(a, st); return true;
@@ -660,9 +661,17 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
     if (!xsh || (am != OP_KCONTIG && am != OP_IM2COL_T)) return -20;
     a.xsc = xsc;
     a.xsh = xsh;
-    if (tile < 7 || tile > 10) tile = pick_glds_tile(a, am, OP_KCONTIG);
-    const bool ok = tile >= 7 && (am == OP_KCONTIG ? launch_modes_xf<OP_KCONTIG, OP_KCONTIG, 1>(a, tile, (hipStream_t)stream)
-                                                   : launch_modes_xf<OP_IM2COL_T, OP_KCONTIG, 1>(a, tile, (hipStream_t)stream));
+    // pointwise: DTF_XF_TILE >= 0 forces a tile, e.g. a register-staged one (0, 2: transform before the ds_write);
+    // default: the LDS-DMA pick (rewrites the landed slots in LDS). Measured on ResNet-50 b256 with DTF_LAZY_BN=1x1:
+    // 11,661 img/s LDS-DMA vs 11,516 (tile 2) and 11,132 (tile 0); materialised BN outputs 11,768 (profiles/)
+    static const int xf_tile = [] {
+      const char* e = getenv("DTF_XF_TILE");
+      return e ? atoi(e) : -1;
+    }();
+    if (am == OP_KCONTIG && tile < 0 && xf_tile >= 0) tile = xf_tile;
+    if (tile < 0 || (am != OP_KCONTIG && (tile < 7 || tile > 10))) tile = pick_glds_tile(a, am, OP_KCONTIG);
+    const bool ok = am == OP_KCONTIG ? launch_modes_xf<OP_KCONTIG, OP_KCONTIG, 1>(a, tile, (hipStream_t)stream)
+                                     : tile >= 7 && launch_modes_xf<OP_IM2COL_T, OP_KCONTIG, 1>(a, tile, (hipStream_t)stream);
     if (!ok) return -20;
     if (stat_rows) *stat_rows = a.tiles_m;
     return (int)hipGetLastError();

@@ -303,13 +303,19 @@ __device__ __forceinline__ uint32_t tap_mask(int R, int S, int h0, int h1, int w
 // ---- K-contiguous operand: LDS tile [R][64] bf16, 128-B rows ---------------
 template <int R, int MODE, bool XF = false>
 struct KContigLoader {
-  static_assert(!XF, "on-the-fly BatchNorm of a K-contiguous operand needs the LDS-DMA loader");
+  static_assert(!XF || MODE == OP_KCONTIG, "register-staged on-the-fly BatchNorm: plain K-contiguous operands only");
   static constexpr int L = R / 32;  // 16-B loads per thread per K tile
   const bf16_t* base[L];
   int i0[L], i1[L], i2[L];  // per-row gather state
   bool rv[L];
   int chunk;
   uint4 reg[L];
+  // XF: BatchNorm + ReLU of the staged values (channel = k), applied in registers before the ds_write; the 8
+  // channels' coefficients are loaded with the data (this thread's chunk is fixed), zero-filled slots stay zero
+  const float* xsc;
+  const float* xsh;
+  float4 xk[4];
+  bool xv;
   // tap-uniform modes: byte offset of the row's tap-(0,0) pixel and its in-image tap mask
   int roff[L];
   uint32_t tmask[L];
@@ -368,6 +374,10 @@ struct KContigLoader {
       }
       return;
     }
+    if constexpr (XF) {
+      xsc = a.xsc;
+      xsh = a.xsh;
+    }
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       int row = (t >> 3) + 32 * i;
@@ -420,6 +430,15 @@ struct KContigLoader {
         if (rv[i] && kv) reg[i] = *reinterpret_cast<const uint4*>(base[i] + k);
         else reg[i] = make_uint4(0, 0, 0, 0);
       }
+      if constexpr (XF) {
+        xv = kv;
+        if (kv) {
+          xk[0] = *reinterpret_cast<const float4*>(xsc + k);
+          xk[1] = *reinterpret_cast<const float4*>(xsc + k + 4);
+          xk[2] = *reinterpret_cast<const float4*>(xsh + k);
+          xk[3] = *reinterpret_cast<const float4*>(xsh + k + 4);
+        }
+      }
     } else if constexpr (MODE == OP_IM2COL) {
       uint32_t rs, ci, kh, kw;
       fdivmod((uint32_t)k, a.g.dC, rs, ci);
@@ -457,7 +476,16 @@ struct KContigLoader {
     for (int i = 0; i < L; ++i) {
       int row = (t >> 3) + 32 * i;
       int pc = chunk ^ ((row >> 1) & 7);
-      *reinterpret_cast<uint4*>(lds + row * 128 + pc * 16) = reg[i];
+      uint4 v = reg[i];
+      if constexpr (XF) {
+        if (rv[i] && xv) {
+          v.x = bnrelu2(v.x, xk[0].x, xk[0].y, xk[2].x, xk[2].y);
+          v.y = bnrelu2(v.y, xk[0].z, xk[0].w, xk[2].z, xk[2].w);
+          v.z = bnrelu2(v.z, xk[1].x, xk[1].y, xk[3].x, xk[3].y);
+          v.w = bnrelu2(v.w, xk[1].z, xk[1].w, xk[3].z, xk[3].w);
+        }
+      }
+      *reinterpret_cast<uint4*>(lds + row * 128 + pc * 16) = v;
     }
   }
   __device__ __forceinline__ void xform(char*) const {}

@@ -179,8 +179,8 @@ __device__ __forceinline__ uint32_t cvt4(float a0, float a1, float a2, float a3)
 
 // block (x, y) = columns [64x, 64x+64) x rows [QT_ROWS y, QT_ROWS (y+1)), walked as 64-row tiles; thread (wave w,
 // lane l): row 16w + (l & 15) of each tile, the 16 columns 16 (l >> 4) .. +15 (the 16 lanes of a DPP row share
-// the columns: the column sums, kept in registers over the strip, are row16_sum reductions at the end). The next
-// tile's loads are issued before this tile's quantize / transpose.
+// the columns: the column sums, kept in registers over the strip, are row16_sum reductions at the end). All tiles'
+// loads are issued before the first quantize / transpose.
 constexpr int QT_ROWS = 256;
 
 template <int FMT>
@@ -213,19 +213,28 @@ __global__ void __launch_bounds__(256) quant_t_kernel(QtArgs a) {
 #pragma unroll
   for (int j = 0; j < 16; ++j) cs[j] = 0.f;
   float mx = 0.f;
-  uint4 xr[2], pr[2];
-  auto load = [&](int tile) {
-    const long e = (long)(mb + 64 * tile + r) * a.N + n0 + 16 * cc;
-    xr[0] = *reinterpret_cast<const uint4*>(a.x + e);
-    xr[1] = *reinterpret_cast<const uint4*>(a.x + e + 8);
-    if (a.pre) {
-      pr[0] = *reinterpret_cast<const uint4*>(a.pre + e);
-      pr[1] = *reinterpret_cast<const uint4*>(a.pre + e + 8);
+  // every tile's loads are issued before the first use (QT_ROWS / 64 tiles: up to 8 x 16 B per thread in flight;
+  // one tile ahead left the pass latency-bound at ~2.5 TB/s on GPT-2-medium's activations)
+  constexpr int NTL = QT_ROWS / 64;
+  uint4 xa[NTL][2], pa[NTL][2];
+#pragma unroll
+  for (int tile = 0; tile < NTL; ++tile) {
+    if (tile < ntile) {
+      const long e = (long)(mb + 64 * tile + r) * a.N + n0 + 16 * cc;
+      xa[tile][0] = *reinterpret_cast<const uint4*>(a.x + e);
+      xa[tile][1] = *reinterpret_cast<const uint4*>(a.x + e + 8);
+      if (a.pre) {
+        pa[tile][0] = *reinterpret_cast<const uint4*>(a.pre + e);
+        pa[tile][1] = *reinterpret_cast<const uint4*>(a.pre + e + 8);
+      }
     }
-  };
-  load(0);
-  for (int tile = 0; tile < ntile; ++tile) {
+  }
+#pragma unroll
+  for (int tile = 0; tile < NTL; ++tile) {
+    if (tile >= ntile) break;
     const int m0 = mb + 64 * tile;
+    const uint4* xr = xa[tile];
+    const uint4* pr = pa[tile];
     float f[16];
     {
       const uint32_t xw[8] = {xr[0].x, xr[0].y, xr[0].z, xr[0].w, xr[1].x, xr[1].y, xr[1].z, xr[1].w};
@@ -244,7 +253,6 @@ __global__ void __launch_bounds__(256) quant_t_kernel(QtArgs a) {
         }
       }
     }
-    if (tile + 1 < ntile) load(tile + 1);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       mx = fmaxf(mx, fabsf(f[j]));

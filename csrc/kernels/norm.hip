@@ -1208,10 +1208,15 @@ static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, con
   const bool fuse_sc = !msc && sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&
                        geo.TPR * geo.RPB == 256;
   if (sc && sc->rows2) *sc->rows2 = fuse_sc ? grid : 0;
-  if (msc) {  // lazy BatchNorm output: no bit mask, no residual branch
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, nullptr,
-                       nullptr, (const bf16_t*)x, coef, M, C, (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr,
-                       ew_reverse(), msc, msh);
+  if (msc) {  // lazy BatchNorm output: no bit mask, no residual branch (rows per trip as the regular pass)
+    if (g_ew_variant == 4)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true, 2>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
+                         nullptr, nullptr, (const bf16_t*)x, coef, M, C, (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr,
+                         nullptr, ew_reverse(), msc, msh);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, nullptr,
+                         nullptr, (const bf16_t*)x, coef, M, C, (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr,
+                         ew_reverse(), msc, msh);
   } else if (fuse_sc) {
     if (g_ew_variant == 4)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, 2>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
