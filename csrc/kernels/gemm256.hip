@@ -38,8 +38,11 @@ __device__ __forceinline__ int b_row(int r, int h) {
   return (r / S) * (2 * S) + h * S + (r % S);
 }
 
-// K-outer half image [64 k][128 cols]: physical 16-B chunk of logical chunk c in k-row k
-__device__ __forceinline__ int ko_swz(int k) { return (k & 3) << 1; }
+// K-outer half image [64 k][128 cols]: physical 16-B chunk of logical chunk c in k-row k. A transposed fragment read
+// (frag_ko) has its 4 lane groups G on k-rows 8 apart; every 256-B k-row starts on bank 0, so bit 3 of k moves the
+// odd groups' rows to the other 32 banks (without it, groups 0 and 1 hit the same banks: 50% of the LDS cycles of a
+// K-outer x K-outer GEMM were bank-conflict cycles, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/)
+__device__ __forceinline__ int ko_swz(int k) { return ((k & 3) << 1) | (((k >> 3) & 1) << 3); }
 // transposed fragment of a K-outer half: lane (G, i) gets col rb + i, k = 32 kk + 8 G + 0..7
 __device__ __forceinline__ v8bf frag_ko(const char* lds, int rb, int kk, int lane) {
   const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
