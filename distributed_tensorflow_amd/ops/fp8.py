@@ -208,6 +208,7 @@ def _fp8_bwd_ok(M, K, N):
 # written, and two quantize passes per layer and step leave the critical stream. Delayed scaling is unchanged (the
 # same amax slots, parities and scale publication as the quantize pass).
 _FUSE = os.environ.get("DTF_FP8_FUSE", "1") != "0"
+_FUSE_BWD = os.environ.get("DTF_FP8_FUSE_BWD", "1") != "0"  # the gradient half (FFN2's dgrad writes FFN1's e5m2 dZ)
 
 
 def _placeholder(shape, dev):
@@ -352,7 +353,8 @@ class _DenseFP8(torch.autograd.Function):
             _, wqT = _weight_fp8(st, w, True)
             src, ctx.src = ctx.src, None
             dx = None
-            if src is not None and folded and src[0].g_ready and src[2] and M % 256 == 0:
+            if (src is not None and _FUSE_BWD and folded and src[0] is not None and src[0].g_ready and src[2]
+                    and M % 256 == 0):
                 # our input came from the producer's fp8 epilogue: quantize ITS gradient here (the activation
                 # backward from its saved pre-activation, e5m2 + transpose + bias-gradient column partials)
                 pst, ppre, pact = src
