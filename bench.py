@@ -98,6 +98,8 @@ def main():
                     help="1: ZeRO-1 sharded optimizer update (reduce-scatter + 1/N update + all-gather of masters)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture the whole train step in a hipGraph (compile(jit_compile=True))")
+    ap.add_argument("--ar-sweep", type=int, default=1,
+                    help="N>1: after the timed steps, time f32 all-reduces of 1-128 MB and report RCCL bus bandwidth")
     ap.add_argument("--hiprio", type=int, default=0,
                     help="1: issue the train step on a high-priority HIP stream (the weight-gradient side stream "
                          "keeps normal priority, so the dgrad critical path wins block dispatch)")
@@ -171,6 +173,10 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # slowest rank's clock and exposed communication
     dt, exposed_max = float(t[0].item()), float(t[1].item())
+    # after the timed region (it changes nothing that was measured): the collective's own bus bandwidth on this
+    # node at bucket-sized messages, so the bucket cap and wire dtype can be chosen from a measurement on the
+    # hardware the scaling run used (RCCL over xGMI on an 8-GPU node)
+    ar_sweep = _allreduce_sweep(dist, dev, world) if (world > 1 and args.ar_sweep) else None
     ms = dt / args.steps * 1e3
     global_batch = args.batch * world
     per_sample = getattr(args, "tokens_per_sample", 1)
@@ -204,6 +210,7 @@ def main():
                            exposed_comm_ms_per_step=round(exposed_max, 3),
                            forced_collective=os.environ.get("DTF_FORCE_COLLECTIVE", "0") == "1"),
             "rccl_world": rccl_world,
+            "allreduce_busbw_GBps": ar_sweep,
             "process_group_backend": backend,
             "replicas_identical": identical,
             "weights_checksum": csum,
@@ -213,6 +220,29 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _allreduce_sweep(dist, dev, world, sizes_mb=(1, 4, 16, 32, 64, 128), iters=5):
+    """Bus bandwidth (GB/s, the nccl-tests convention: bytes * 2 (n-1) / n / time) of f32 all-reduces on the default
+    process group, slowest rank's time per size."""
+    import torch
+    out = {}
+    for mb in sizes_mb:
+        x = torch.ones(mb * (1 << 20) // 4, dtype=torch.float32, device=dev)
+        sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+        for _ in range(2):
+            dist.all_reduce(x)
+        sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        sync()
+        el = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        out[f"{mb}MB"] = round(mb * (1 << 20) * 2 * (world - 1) / world / float(el.item()) / 1e9, 1)
+        del x
+    return out
 
 
 if __name__ == "__main__":
