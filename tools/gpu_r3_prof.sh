@@ -9,4 +9,4 @@ cd $R
 F=$(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1)
 MK=optim_kernel; [ "$M" = resnet50 ] || MK=softmax_ce_fwd_kernel
 python tools/steady_stats.py $F --marker $MK > $OUT/stats_$TAG.txt 2>&1; head -${HEAD:-60} $OUT/stats_$TAG.txt
-rm -rf $OUT/prof_$TAG
+[ "${KEEP:-0}" = "1" ] || rm -rf $OUT/prof_$TAG
