@@ -155,6 +155,7 @@ struct GemmArgs {
   float* q8used2;
   int q8fmt;
   int no_c;
+  int aux_nt;  // gemm256.hip staged epilogue: nontemporal stores for the aux (pre-activation) output
 };
 
 // 4 floats -> 4 packed OCP fp8 bytes (fmt 0 e4m3, 1 e5m2), values already scaled and clamped
