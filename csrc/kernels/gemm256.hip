@@ -70,7 +70,7 @@ __device__ __forceinline__ void barrier() {
 
 // BN = 256 (each wave 128x64: 8x4 fragments) or 128 (each wave 128x32: 8x2 fragments; 256x128 tiles fill the
 // chip where 256x256 would leave half of it idle, e.g. M = 8192 x N = 1024)
-template <int AM, int BMD, int FP8 = 0, int BN = 256>
+template <int AM, int BMD, int FP8 = 0, int BN = 256, bool AUXD = (FP8 == 0)>
 __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
   constexpr int BUF = buf_bytes<BN>();
   constexpr int JN = BN / 128;           // B fragments per wave per half (and glds instructions per B half)
@@ -279,7 +279,8 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     const bool aux_nt = a.aux_nt & 1;
     // aux_nt bit 1: the pre-activation side output is stored straight from the fragments in the main pass (8-B
     // pieces, merged in L2) instead of a second LDS-staged pass
-    const bool aux_direct = (FP8 == 0 || (a.aux_nt & 4)) && (a.aux_nt & 2) && a.aux;
+    // (fp8 kernels: a separate instantiation, AUXD — its extra live values cost 4 VGPR spills)
+    const bool aux_direct = AUXD && (a.aux_nt & 2) && a.aux;
     __syncthreads();  // every wave is done with the operand buffers
     for (int o = 0; o < ((a.aux && !aux_direct) ? 2 : 1); ++o) {
       bf16_t* dst = (o ? a.aux : reinterpret_cast<bf16_t*>(a.C)) + cbase;
@@ -468,7 +469,10 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
 template <int BN>
 void launch256(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8) {
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
-  if (fp8 == 2) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 2, BN>), grid, dim3(NT2), 0, st, a);
+  const bool auxd = a.aux && (a.aux_nt & 4);
+  if (fp8 == 2 && auxd) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 2, BN, true>), grid, dim3(NT2), 0, st, a);
+  else if (fp8 == 2) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 2, BN>), grid, dim3(NT2), 0, st, a);
+  else if (fp8 && auxd) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 1, BN, true>), grid, dim3(NT2), 0, st, a);
   else if (fp8) hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 1, BN>), grid, dim3(NT2), 0, st, a);
   else if (amode == OP_KCONTIG && bmode == OP_KCONTIG)
     hipLaunchKernelGGL((gemm256_kernel<OP_KCONTIG, OP_KCONTIG, 0, BN>), grid, dim3(NT2), 0, st, a);
@@ -497,10 +501,11 @@ int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int 
   // pre-activation side output (aux, read again only by the backward), DTF_G256_AUX_NT bits: 0 = nontemporal
   // stores (measured +-0); 1 = stored straight from the fragments in the main store pass instead of a second
   // LDS-staged pass (BERT-base +1.5%, GPT-2-medium +1.8%; FFN1 forward 167 -> 141 us / 123 -> 104 us); 2 = also
-  // for the fp8 kernels (GPT-2-medium fp8 +1.3%). Default 6 = bits 1 + 2
+  // for the fp8 kernels (their own instantiation: 4 VGPR spills; GPT-2-medium fp8 erratic with it, 180-233k vs a
+  // steady 231-234k tok/s without: off by default). Default 2 = bit 1
   static const int aux_nt = [] {
     const char* e = getenv("DTF_G256_AUX_NT");
-    return e ? atoi(e) : 6;
+    return e ? atoi(e) : 2;
   }();
   a.aux_nt = aux_nt;
   if (bn == 256) launch256<256>(a, amode, bmode, st, fp8);
