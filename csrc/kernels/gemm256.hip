@@ -281,7 +281,15 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
     // pieces, merged in L2) instead of a second LDS-staged pass
     // (fp8 kernels: a separate instantiation, AUXD — its extra live values cost 4 VGPR spills)
     const bool aux_direct = AUXD && (a.aux_nt & 2) && a.aux;
+    // the tile's bias columns staged in LDS (past the C staging area) once, instead of a global float4 load per
+    // row fragment in the loop below
+    float* sbias = reinterpret_cast<float*>(smem + 128 * CS * 2);
+    static_assert(128 * CS * 2 + BN * 4 <= 2 * BUF, "bias staging must fit past the C tile");
     __syncthreads();  // every wave is done with the operand buffers
+    if (a.bias && tid < BN / 4)
+      reinterpret_cast<float4*>(sbias)[tid] =
+          n0 + 4 * tid < a.N ? *reinterpret_cast<const float4*>(a.bias + n0 + 4 * tid) : make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
     for (int o = 0; o < ((a.aux && !aux_direct) ? 2 : 1); ++o) {
       bf16_t* dst = (o ? a.aux : reinterpret_cast<bf16_t*>(a.C)) + cbase;
       for (int h = 0; h < 2; ++h) {
@@ -294,8 +302,9 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmArgs a) {
               float v[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = alpha * acc[i][j][r];
-              if (a.bias && n0 + nl < a.N) {
-                float4 b = *reinterpret_cast<const float4*>(a.bias + n0 + nl);
+              if (a.bias) {
+                const float4 b = (a.aux_nt & 8) ? *reinterpret_cast<const float4*>(a.bias + n0 + nl)
+                                                : reinterpret_cast<const float4*>(sbias)[nl >> 2];
                 v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
               }
               if (aux_direct) {
