@@ -583,6 +583,16 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
   return (int)hipGetLastError();
 }
 
+DTF_API int dtf_stem_fwd(const void* X, const void* Wt, void* Y, float* part, int* rows, int N, int Hs, int Ws, int C,
+                         int K, int R, int S, int P, int Q, void* stream);  // stem.hip
+static bool stem_kernel_on() {  // DTF_STEM_KERNEL=0: the stem runs on the implicit-GEMM conv (A/B)
+  static const bool on = [] {
+    const char* e = getenv("DTF_STEM_KERNEL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // NHWC conv forward: Y[N,P,Q,K] = X[N,H,W,C] * W[K,R,S,C] (+bias, act, BN stats of Y)
 // stats (optional): BN partial rows [tiles_m][2K] (capacity ceil(N*P*Q/64) rows); *stat_rows = tiles_m.
 static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
@@ -645,6 +655,16 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
                          int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin,
                          const float* xsc, const float* xsh) {
   if ((C & 7) || (K & 3)) return -1;
+  if (stats && !bias && !act && !out_f32 && !xsc && tile < 0 && stem_kernel_on() && sh == 1 && sw == 1 && ph == 0 &&
+      pw == 0 && dh == 1 && dw == 1) {
+    // the space-to-depth ResNet stem (C 16, K 64, 4x4): its own kernel (stem.hip); the finalize runs after
+    int rows = 0;
+    const int rc = dtf_stem_fwd(X, Wt, Y, stats, &rows, N, H, W, C, K, R, S, P, Q, stream);
+    if (rc != -1) {
+      if (stat_rows) *stat_rows = rows;
+      return rc;
+    }
+  }
   GemmArgs a{};
   if (fin && stats) a.fin = *fin;
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
@@ -906,6 +926,9 @@ DTF_API int dtf_conv_wgrad_x(const void* X, const void* dY, float* dW, int N, in
                              void* stream) {
   if ((C & 7) || (K & 7)) return -1;
   if (xsc && !xsh) return -20;
+  // the space-to-depth stem filter (4x4 x 16 channels -> 64): the register-staged 64-row tile beats the swapped
+  // LDS-DMA default (tools/bench_stem.py: 251 vs 289 us at batch 256; round 1: 289 vs 309)
+  if (tile < 0 && !xsc && C == 16 && R == 4 && S == 4 && K == 64) tile = 3;
   hipStream_t st = (hipStream_t)stream;
   GemmArgs a{};
   a.xsc = xsc;

@@ -50,6 +50,7 @@ _KERNEL_SIGS = {
     "dtf_softmax_ce_fwd": [P, I, P, P, P, L, I, F, P],
     "dtf_softmax_ce_bwd": [P, I, P, P, P, P, L, I, F, P],
     "dtf_nchw_to_s2d": [P, P, I, I, I, I, P],
+    "dtf_stem_fwd": [P, P, P, P, P] + [I] * 9 + [P],
     "dtf_bn_relu_maxpool_fwd": [P, P, P, P, P] + [I] * 12 + [P],
     "dtf_maxpool_bn_bwd": [P, P, P, P, P, P] + [I] * 12 + [P, P, P, I, P, P],
     "dtf_gap_fwd": [P, P, I, I, I, I, P],
