@@ -220,41 +220,13 @@ namespace dtf {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int AM, int BMODE, int PIPE = 2, int XF = 0>
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int PIPE = 2>
 static void launch_t(GemmArgs& a, hipStream_t st) {
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
   prep_fin(a);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE, 0, PIPE, XF>), grid, dim3(NT), 0, st, a);
-}
-
-// Launch with the on-the-fly BatchNorm + ReLU of operand XF (1 = A, 2 = B; GemmArgs.xsc/xsh): the LDS-DMA tiles
-// (7-10) transform each lane's landed slots in place; the register-staged tiles (0, 2, 3, 4) transform in registers
-// before the ds_write (K-outer X of a 1x1 weight gradient, plain K-contiguous X of a pointwise forward). Returns false
-// when the combination has no XF kernel.
-template <int AM, int BMODE, int XF>
-static bool launch_modes_xf(GemmArgs& a, int tile, hipStream_t st) {
-  constexpr int XM = XF == 1 ? AM : BMODE;
-  if constexpr (glds_mode(AM) && glds_mode(BMODE)) {
-    switch (tile) {
-      case 7: launch_t<128, 128, 2, 2, AM, BMODE, 3, XF>(a, st); return true;
-      case 8: launch_t<128, 64, 2, 2, AM, BMODE, 3, XF>(a, st); return true;
-      case 9: launch_t<128, 128, 2, 2, AM, BMODE, 4, XF>(a, st); return true;
-      case 10: launch_t<128, 64, 2, 2, AM, BMODE, 4, XF>(a, st); return true;
-      default: break;
-    }
-  }
-  if constexpr (XM == OP_KOUTER || XM == OP_KCONTIG) {  // register-staged X operand (transform before ds_write)
-    switch (tile) {
-      case 0: launch_t<128, 128, 2, 2, AM, BMODE, 1, XF>(a, st); return true;
-      case 2: launch_t<128, 64, 2, 2, AM, BMODE, 1, XF>(a, st); return true;
-      case 4: launch_t<64, 256, 1, 4, AM, BMODE, 2, XF>(a, st); return true;
-      case 3: launch_t<64, 64, 2, 2, AM, BMODE, 2, XF>(a, st); return true;
-      default: break;
-    }
-  }
-  return false;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE, 0, PIPE>), grid, dim3(NT), 0, st, a);
 }
 
 template <int AM, int BMODE>
@@ -597,8 +569,7 @@ static bool stem_kernel_on() {  // DTF_STEM_KERNEL=0: the stem runs on the impli
 // stats (optional): BN partial rows [tiles_m][2K] (capacity ceil(N*P*Q/64) rows); *stat_rows = tiles_m.
 static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
                          int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
-                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin,
-                         const float* xsc = nullptr, const float* xsh = nullptr);
+                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin);
 
 DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
                          int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
@@ -632,7 +603,7 @@ DTF_API int dtf_conv_fwd_bn(const void* X, const void* Wt, void* Y, float* stats
                             int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int tile,
                             const float* gamma, const float* beta, float* rmean, float* rvar, float momentum,
                             float eps, float* scale, float* shift, float* mean, float* invstd, int* fused,
-                            const float* xsc, const float* xsh, void* stream) {
+                            void* stream) {
   int done = 0, rows = 0;
   BnFin f{};
   f.mode = fin_on() ? 1 : 0;
@@ -642,7 +613,7 @@ DTF_API int dtf_conv_fwd_bn(const void* X, const void* Wt, void* Y, float* stats
   f.count = (long)N * P * Q;
   f.host_done = &done;
   int rc = conv_fwd_impl(X, Wt, Y, nullptr, stats, &rows, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0,
-                         tile, stream, &f, xsc, xsh);
+                         tile, stream, &f);
   if (rc) return rc;
   if (!done) rc = dtf_bn_finalize(stats, rows, gamma, beta, rmean, rvar, (long)N * P * Q, K, momentum, eps, scale,
                                   shift, mean, invstd, stream);
@@ -652,10 +623,9 @@ DTF_API int dtf_conv_fwd_bn(const void* X, const void* Wt, void* Y, float* stats
 
 static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
                          int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
-                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin,
-                         const float* xsc, const float* xsh) {
+                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin) {
   if ((C & 7) || (K & 3)) return -1;
-  if (stats && !bias && !act && !out_f32 && !xsc && tile < 0 && stem_kernel_on() && sh == 1 && sw == 1 && ph == 0 &&
+  if (stats && !bias && !act && !out_f32 && tile < 0 && stem_kernel_on() && sh == 1 && sw == 1 && ph == 0 &&
       pw == 0 && dh == 1 && dw == 1) {
     // the space-to-depth ResNet stem (C 16, K 64, 4x4): its own kernel (stem.hip); the finalize runs after
     int rows = 0;
@@ -676,26 +646,6 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
-  if (xsc) {
-    // X is a BatchNorm(+ReLU) output that was never written: the LDS-DMA tiles apply it to the staged input
-    if (!xsh || (am != OP_KCONTIG && am != OP_IM2COL_T)) return -20;
-    a.xsc = xsc;
-    a.xsh = xsh;
-    // pointwise: DTF_XF_TILE >= 0 forces a tile, e.g. a register-staged one (0, 2: transform before the ds_write);
-    // default: the LDS-DMA pick (rewrites the landed slots in LDS). Measured on ResNet-50 b256 with DTF_LAZY_BN=1x1:
-    // 11,661 img/s LDS-DMA vs 11,516 (tile 2) and 11,132 (tile 0); materialised BN outputs 11,768 (profiles/)
-    static const int xf_tile = [] {
-      const char* e = getenv("DTF_XF_TILE");
-      return e ? atoi(e) : -1;
-    }();
-    if (am == OP_KCONTIG && tile < 0 && xf_tile >= 0) tile = xf_tile;
-    if (tile < 0 || (am != OP_KCONTIG && (tile < 7 || tile > 10))) tile = pick_glds_tile(a, am, OP_KCONTIG);
-    const bool ok = am == OP_KCONTIG ? launch_modes_xf<OP_KCONTIG, OP_KCONTIG, 1>(a, tile, (hipStream_t)stream)
-                                     : tile >= 7 && launch_modes_xf<OP_IM2COL_T, OP_KCONTIG, 1>(a, tile, (hipStream_t)stream);
-    if (!ok) return -20;
-    if (stat_rows) *stat_rows = a.tiles_m;
-    return (int)hipGetLastError();
-  }
   if (!try_conv256(a, am, OP_KCONTIG, tile, (hipStream_t)stream)) {
     if (tile < 0) tile = pick_glds_tile(a, am, OP_KCONTIG);
     dispatch(a, am, OP_KCONTIG, tile, (hipStream_t)stream);
@@ -735,8 +685,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream, const BnFin* fin = nullptr,
-                           const float* bnsc = nullptr, const float* bnsh = nullptr);
+                           const void* bsrc2, void* stream, const BnFin* fin = nullptr);
 
 // The BnFin of a data gradient that also finalizes the backward of the BatchNorm whose output it is the gradient
 // of (mode 2): dgamma/dbeta (+= when accumulate) and the apply coefficients coef [3*C] of that BatchNorm (gamma,
@@ -773,17 +722,17 @@ DTF_API int dtf_conv_dgrad_bn(const void* dY, const void* Wcrsk, void* dX, int N
                               void* ws, long ws_bf16, const void* bnx, const void* bnmask, const float* bnmean,
                               float* bnpart, int* bnrows, const void* betamask, const void* bsrc2,
                               const float* gamma, const float* invstd, float* dgamma, float* dbeta, int accumulate,
-                              float* coef, int* fused, const float* bnsc, const float* bnsh, void* stream) {
+                              float* coef, int* fused, void* stream) {
   int done = 0;
   const BnFin f = bwd_fin(gamma, bnmean, invstd, dgamma, dbeta, accumulate, coef, (long)N * H * W, &done);
   int rc;
   if (bsrc2) {
     if ((H & 1) || (W & 1)) return -11;
     rc = conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, 1, 1, H, W, 1, 1, 0, 0, 1, 1, 0, 1.f, -1, ws, ws_bf16, bnx,
-                         bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, &f, bnsc, bnsh);
+                         bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, &f);
   } else {
     rc = conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, beta, -1, ws, ws_bf16,
-                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, &f, bnsc, bnsh);
+                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, &f);
   }
   if (fused) *fused = done;
   return rc;
@@ -791,20 +740,18 @@ DTF_API int dtf_conv_dgrad_bn(const void* dY, const void* Wcrsk, void* dX, int N
 
 // The general bf16 data gradient of the ConvBN path: optional beta accumulate (+ deferred ReLU mask betamask), the
 // compact stride-2 shortcut gradient bsrc2 (pointwise stride-1 convs, H and W even), and the BN-backward statistics
-// of dX (bnx/bnmask/bnmean -> bnpart/bnrows) whose ReLU mask may be recomputed from bnx with bnsc/bnsh (the scale and
-// shift of a BatchNorm whose output was never materialised) when there is no bit mask.
+// of dX (bnx/bnmask/bnmean -> bnpart/bnrows).
 DTF_API int dtf_conv_dgrad_x(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                              int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, float beta, void* ws,
                              long ws_bf16, const void* bnx, const void* bnmask, const float* bnmean, float* bnpart,
-                             int* bnrows, const void* betamask, const void* bsrc2, const float* bnsc,
-                             const float* bnsh, void* stream) {
+                             int* bnrows, const void* betamask, const void* bsrc2, void* stream) {
   if (bsrc2) {
     if ((H & 1) || (W & 1) || R != 1 || S != 1 || sh != 1 || sw != 1 || ph != 0 || pw != 0) return -11;
     return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, 1, 1, H, W, 1, 1, 0, 0, 1, 1, 0, 1.f, -1, ws, ws_bf16, bnx,
-                           bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, nullptr, bnsc, bnsh);
+                           bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, nullptr);
   }
   return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, beta, -1, ws, ws_bf16,
-                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, nullptr, bnsc, bnsh);
+                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, nullptr);
 }
 
 DTF_API int dtf_conv_dgrad_addsub2(const void* dY, const void* Wcrsk, void* dX, const void* bsrc2, int N, int H, int W,
@@ -820,10 +767,8 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream, const BnFin* fin, const float* bnsc,
-                           const float* bnsh) {
+                           const void* bsrc2, void* stream, const BnFin* fin) {
   if ((C & 3) || (K & 7)) return -1;
-  if (bnsc && (!bnsh || !bnx || bnmask)) return -12;
   if (bnx && (out_f32 || (C & 7) || !bnpart || !bnmean || !bnrows)) return -9;
   if (betamask && (out_f32 || beta == 0.f || (C & 7) || sh > 1 || sw > 1)) return -10;
   hipStream_t st = (hipStream_t)stream;
@@ -842,8 +787,6 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
     a.bnx = (const bf16_t*)bnx;
     a.bnmask = (const uint8_t*)bnmask;
     a.bnmean = bnmean;
-    a.bnsc = bnsc;
-    a.bnsh = bnsh;
   };
   const bool phased = (sh > 1 || sw > 1) && dh == 1 && dw == 1 && ws != nullptr &&
                       ws_bf16 >= (long)C * R * S * K && !(C & 7);
@@ -916,23 +859,17 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
   return (int)hipGetLastError();
 }
 
-// NHWC conv weight-gradient: dW[K][R][S][C] (f32, accumulated with atomics over split-K)
+// NHWC conv weight-gradient: dW[K][R][S][C] (f32, accumulated over split-K slabs)
 //   = sum_{n,p,q} dY[n,p,q,k] * X[n, p*sh-ph+r*dh, q*sw-pw+s*dw, c]
-// xsc/xsh (optional): X is a BatchNorm(+ReLU) output that was never materialised (X holds the BN input); the
-// X operand's loader applies it (LDS-DMA spatial tiles, register-staged pointwise tiles); -20 if no XF kernel fits.
-DTF_API int dtf_conv_wgrad_x(const void* X, const void* dY, float* dW, int N, int H, int W, int C, int K, int R,
-                             int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int accumulate,
-                             int splitk, int tile, float* ws, long ws_elems, const float* xsc, const float* xsh,
-                             void* stream) {
+DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int H, int W, int C, int K, int R,
+                           int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int accumulate,
+                           int splitk, int tile, float* ws, long ws_elems, void* stream) {
   if ((C & 7) || (K & 7)) return -1;
-  if (xsc && !xsh) return -20;
   // the space-to-depth stem filter (4x4 x 16 channels -> 64): the register-staged 64-row tile beats the swapped
   // LDS-DMA default (tools/bench_stem.py: 251 vs 289 us at batch 256; round 1: 289 vs 309)
-  if (tile < 0 && !xsc && C == 16 && R == 4 && S == 4 && K == 64) tile = 3;
+  if (tile < 0 && C == 16 && R == 4 && S == 4 && K == 64) tile = 3;
   hipStream_t st = (hipStream_t)stream;
   GemmArgs a{};
-  a.xsc = xsc;
-  a.xsh = xsh;
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
   a.g_rowrep = rowrep(a.g.R, a.g.S);
   a.A = (const bf16_t*)dY; a.B = (const bf16_t*)X;
@@ -967,7 +904,7 @@ DTF_API int dtf_conv_wgrad_x(const void* X, const void* dY, float* dW, int N, in
     return e && e[0] == '1';
   }();
   const bool c256_forced = tile >= 11 && tile <= 14;
-  if (!xsc && small && ws != nullptr && (c256_forced || (tile < 0 && c256w && conv256_on())) &&
+  if (small && ws != nullptr && (c256_forced || (tile < 0 && c256w && conv256_on())) &&
       (pointwise || (C % 8 == 0 && (dh == 1 && dw == 1)))) {
     GemmArgs b = a;
     b.A = (const bf16_t*)X; b.B = (const bf16_t*)dY;
@@ -1012,11 +949,7 @@ DTF_API int dtf_conv_wgrad_x(const void* X, const void* dY, float* dW, int N, in
       b.C = ws;
       b.slab = mnT;
       b.beta = 0.f;
-      if (xsc) {
-        if (!launch_modes_xf<OP_WGRADX_R, OP_KOUTER_R, 1>(b, 8, st)) return -20;
-      } else {
-        dispatch(b, OP_WGRADX_R, OP_KOUTER_R, 8, st);
-      }
+      dispatch(b, OP_WGRADX_R, OP_KOUTER_R, 8, st);
       float* dwt = ws + (long)sk * mnT;
       dtf_sum_rows(ws, mnT, sk, mnT, dwt, 0, st);
       hipLaunchKernelGGL(transpose_acc_kernel, dim3(cdiv(b.N, 32), cdiv(b.M, 32)), dim3(256), 0, st, dwt, dW, b.M,
@@ -1029,34 +962,18 @@ DTF_API int dtf_conv_wgrad_x(const void* X, const void* dY, float* dW, int N, in
     if (a.M <= 64) tile = pointwise && a.N >= 256 ? 4 : 3;  // Kout = 64: no half-empty 128-row tiles
     else if (R * S > 1) tile = 0;                  // spatial filters: 128x128
   }
-  auto run = [&]() -> bool {
-    if (!xsc) {
-      dispatch(a, rowmap ? OP_KOUTER_R : OP_KOUTER, rowmap ? OP_WGRADX_R : pointwise ? OP_KOUTER : OP_WGRADX, tile,
-               st);
-      return true;
-    }
-    if (rowmap) return use_glds && launch_modes_xf<OP_KOUTER_R, OP_WGRADX_R, 2>(a, tile < 0 ? 7 : tile, st);
-    if (!pointwise) return false;
-    int t = tile < 0 ? pick_tile(a.M, a.N, (long)a.batch * a.splitk, a.kchunk) : tile;
-    if (t != 0 && t != 2 && t != 3 && t != 4) t = 0;
-    return launch_modes_xf<OP_KOUTER, OP_KOUTER, 2>(a, t, st);
+  auto run = [&]() {
+    dispatch(a, rowmap ? OP_KOUTER_R : OP_KOUTER, rowmap ? OP_WGRADX_R : pointwise ? OP_KOUTER : OP_WGRADX, tile, st);
   };
   if (splitk == 1) {
     a.C = dW;
     a.beta = accumulate ? 1.f : 0.f;
-    if (!run()) return -20;
+    run();
     return (int)hipGetLastError();
   }
   a.C = ws;
   a.slab = mn;
-  if (!run()) return -20;
+  run();
   dtf_sum_rows(ws, mn, splitk, mn, dW, accumulate, st);
   return (int)hipGetLastError();
-}
-
-DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int H, int W, int C, int K, int R,
-                           int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int accumulate,
-                           int splitk, int tile, float* ws, long ws_elems, void* stream) {
-  return dtf_conv_wgrad_x(X, dY, dW, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, accumulate, splitk, tile, ws,
-                          ws_elems, nullptr, nullptr, stream);
 }

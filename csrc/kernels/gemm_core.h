@@ -62,7 +62,8 @@ struct ConvGeom {
 
 // Fused BatchNorm finalize (mode != 0, on a launch that writes BN partial rows): the launch reduces its own partial
 // rows in its tail and writes the per-channel coefficients — no separate row-reduction / finalize launches on the
-// critical path. Two-level last-arriver hand-off (common.h last_arriver): the last block of each group of `gs`
+// critical path. Two-level last-arriver hand-off (common.h last_arriver: write-through partial rows, a relaxed
+// ticket add per block, sc1 loads by the reducer; no release fences): the last block of each group of `gs`
 // M-tiles (per column tile) sums the group's rows into the group's first row, the last group of a column tile sums
 // the group rows and finalizes its channels; every sum runs in a fixed row order (deterministic).
 //   mode 1 (forward, stats = sum / sum of squares): scale, shift, mean, invstd (o0..o3), running statistics updated
@@ -131,15 +132,6 @@ struct GemmArgs {
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
   BnFin fin;
-  // BatchNorm(+ReLU) of an activation operand that was never materialised (kernels instantiated with XF != 0):
-  // the staged values are the producing conv's raw output z, and v = max(z * xsc[c] + xsh[c], 0) on channel c is
-  // applied in LDS (LDS-DMA loaders: each lane rewrites its own landed 16-B slots) or in registers before the
-  // ds_write (register-staged loaders). Zero-filled slots (padding taps, rows past the operand) stay zero.
-  const float* xsc;
-  const float* xsh;
-  // ReLU mask of the BN-backward statistics (bnx != nullptr) when no bit mask exists: relu'(bnx * bnsc + bnsh)
-  const float* bnsc;
-  const float* bnsh;
   // fp8 copies of the (bf16-rounded, post-activation / post-dact) output written by the staged epilogue of
   // gemm256.hip (host-checked; the bf16 C store is skipped when no_c): q8 [M][N] row-major, q8T [N][M] transposed,
   // q8col [M/128][N] per-128-row column sums of the values (a bias gradient's partials). Delayed scaling as
@@ -169,43 +161,6 @@ __device__ __forceinline__ uint32_t q8pack4(int fmt, float a0, float a1, float a
     r = __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, r, true);
   }
   return (uint32_t)r;
-}
-
-// ---- on-the-fly BatchNorm + ReLU of 8 staged bf16 values (channels c .. c+7) ---------------------------------------
-struct Coef8 {
-  float4 s0, s1, h0, h1;
-};
-__device__ __forceinline__ Coef8 load_coef8x(const float* sc, const float* sh, int c) {
-  Coef8 k;
-  k.s0 = *reinterpret_cast<const float4*>(sc + c);
-  k.s1 = *reinterpret_cast<const float4*>(sc + c + 4);
-  k.h0 = *reinterpret_cast<const float4*>(sh + c);
-  k.h1 = *reinterpret_cast<const float4*>(sh + c + 4);
-  return k;
-}
-// (the same f32 formula and bf16 rounding as norm.hip's bn_apply pass: the MFMA sees the bits that pass would store)
-__device__ __forceinline__ uint32_t bnrelu2(uint32_t w, float s0, float s1, float h0, float h1) {
-  return pack2bf(fmaxf(fmaf(__uint_as_float(w << 16), s0, h0), 0.f),
-                 fmaxf(fmaf(__uint_as_float(w & 0xffff0000u), s1, h1), 0.f));
-}
-__device__ __forceinline__ uint4 bnrelu8(uint4 v, const Coef8& k) {
-  return make_uint4(bnrelu2(v.x, k.s0.x, k.s0.y, k.h0.x, k.h0.y), bnrelu2(v.y, k.s0.z, k.s0.w, k.h0.z, k.h0.w),
-                    bnrelu2(v.z, k.s1.x, k.s1.y, k.h1.x, k.h1.y), bnrelu2(v.w, k.s1.z, k.s1.w, k.h1.z, k.h1.w));
-}
-// ReLU mask bits (bit j = channel c + j) of those 8 values: set where the stored bf16 output would be > 0 (the bit
-// norm.hip's bn_apply writes for the backward)
-__device__ __forceinline__ uint32_t bnrelu_bits8(uint4 v, const float* sc, const float* sh) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t bits = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = 2 * q + h;
-      const float o = fmaf(__uint_as_float(h ? (w[q] & 0xffff0000u) : (w[q] << 16)), sc[j], sh[j]);
-      bits |= (uint32_t)(o > 0.f && f2bf(o) != 0) << j;
-    }
-  return bits;
 }
 
 __device__ __forceinline__ long out_row(const GemmArgs& a, int m) {
@@ -238,15 +193,7 @@ __device__ __forceinline__ void stat_acc(const GemmArgs& a, long mrow, int n, co
     const uint2 xr = *reinterpret_cast<const uint2*>(a.bnx + e);
     const float x[4] = {__uint_as_float(xr.x << 16), __uint_as_float(xr.x & 0xffff0000u),
                         __uint_as_float(xr.y << 16), __uint_as_float(xr.y & 0xffff0000u)};
-    uint32_t bits = a.bnmask ? ((uint32_t)a.bnmask[e >> 3] >> (e & 4)) : 0xFu;  // e % 8 is 0 or 4
-    if (!a.bnmask && a.bnsc) {
-      bits = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float o = fmaf(x[r], a.bnsc[n + r], a.bnsh[n + r]);
-        bits |= (uint32_t)(o > 0.f && f2bf(o) != 0) << r;
-      }
-    }
+    const uint32_t bits = a.bnmask ? ((uint32_t)a.bnmask[e >> 3] >> (e & 4)) : 0xFu;  // e % 8 is 0 or 4
     const float4 mu = *reinterpret_cast<const float4*>(a.bnmean + n);
     const float m4[4] = {mu.x, mu.y, mu.z, mu.w};
 #pragma unroll
@@ -302,21 +249,14 @@ __device__ __forceinline__ uint32_t tap_mask(int R, int S, int h0, int h1, int w
 }
 
 // ---- K-contiguous operand: LDS tile [R][64] bf16, 128-B rows ---------------
-template <int R, int MODE, bool XF = false>
+template <int R, int MODE>
 struct KContigLoader {
-  static_assert(!XF || MODE == OP_KCONTIG, "register-staged on-the-fly BatchNorm: plain K-contiguous operands only");
   static constexpr int L = R / 32;  // 16-B loads per thread per K tile
   const bf16_t* base[L];
   int i0[L], i1[L], i2[L];  // per-row gather state
   bool rv[L];
   int chunk;
   uint4 reg[L];
-  // XF: BatchNorm + ReLU of the staged values (channel = k), applied in registers before the ds_write; the 8
-  // channels' coefficients are loaded with the data (this thread's chunk is fixed), zero-filled slots stay zero
-  const float* xsc;
-  const float* xsh;
-  float4 xk[4];
-  bool xv;
   // tap-uniform modes: byte offset of the row's tap-(0,0) pixel and its in-image tap mask
   int roff[L];
   uint32_t tmask[L];
@@ -375,10 +315,6 @@ struct KContigLoader {
       }
       return;
     }
-    if constexpr (XF) {
-      xsc = a.xsc;
-      xsh = a.xsh;
-    }
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       int row = (t >> 3) + 32 * i;
@@ -431,15 +367,6 @@ struct KContigLoader {
         if (rv[i] && kv) reg[i] = *reinterpret_cast<const uint4*>(base[i] + k);
         else reg[i] = make_uint4(0, 0, 0, 0);
       }
-      if constexpr (XF) {
-        xv = kv;
-        if (kv) {
-          xk[0] = *reinterpret_cast<const float4*>(xsc + k);
-          xk[1] = *reinterpret_cast<const float4*>(xsc + k + 4);
-          xk[2] = *reinterpret_cast<const float4*>(xsh + k);
-          xk[3] = *reinterpret_cast<const float4*>(xsh + k + 4);
-        }
-      }
     } else if constexpr (MODE == OP_IM2COL) {
       uint32_t rs, ci, kh, kw;
       fdivmod((uint32_t)k, a.g.dC, rs, ci);
@@ -477,19 +404,9 @@ struct KContigLoader {
     for (int i = 0; i < L; ++i) {
       int row = (t >> 3) + 32 * i;
       int pc = chunk ^ ((row >> 1) & 7);
-      uint4 v = reg[i];
-      if constexpr (XF) {
-        if (rv[i] && xv) {
-          v.x = bnrelu2(v.x, xk[0].x, xk[0].y, xk[2].x, xk[2].y);
-          v.y = bnrelu2(v.y, xk[0].z, xk[0].w, xk[2].z, xk[2].w);
-          v.z = bnrelu2(v.z, xk[1].x, xk[1].y, xk[3].x, xk[3].y);
-          v.w = bnrelu2(v.w, xk[1].z, xk[1].w, xk[3].z, xk[3].w);
-        }
-      }
-      *reinterpret_cast<uint4*>(lds + row * 128 + pc * 16) = v;
+      *reinterpret_cast<uint4*>(lds + row * 128 + pc * 16) = reg[i];
     }
   }
-  __device__ __forceinline__ void xform(char*) const {}
 };
 
 // fragment read from a [R][64] tile: rows rb..rb+15, k-substep kk
@@ -507,7 +424,7 @@ __device__ __forceinline__ int kouter_swz(int k) {
   else return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);               // R == 64: 4 values
 }
 
-template <int R, int MODE, bool XF = false>
+template <int R, int MODE>
 struct KOuterLoader {
   static constexpr int CPR = R / 8;       // 16-B chunks per k-row
   static constexpr int RPP = NT / CPR;    // k-rows per pass
@@ -518,8 +435,6 @@ struct KOuterLoader {
   bool cv;
   int khoff, kwoff, ci;  // OP_WGRADX column decomposition
   uint4 reg[L];
-  Coef8 xk;              // XF: BN coefficients of the thread's (fixed) 8 columns = channels
-  uint32_t okb;          // XF: loads of the staged tile that read data (the rest are zeros and stay zero)
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld_, int r0, int Rtot) {
     const int t = threadIdx.x;
@@ -536,14 +451,10 @@ struct KOuterLoader {
       khoff = (int)kh * a.g.dh - a.g.ph;
       kwoff = (int)kw * a.g.dw - a.g.pw;
     }
-    if constexpr (XF) {
-      if (cv) xk = load_coef8x(a.xsc, a.xsh, MODE == OP_WGRADX ? ci : col);
-    }
   }
 
   __device__ __forceinline__ void load(const GemmArgs& a, int k0, int Kend) {
     const int t = threadIdx.x;
-    uint32_t okbits = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       int kr = t / CPR + RPP * i;
@@ -561,9 +472,7 @@ struct KOuterLoader {
         if (v) reg[i] = *reinterpret_cast<const uint4*>(p + (((long)n * a.g.H + hi) * a.g.W + wi) * a.g.C + ci);
         else reg[i] = make_uint4(0, 0, 0, 0);
       }
-      okbits |= (uint32_t)v << i;
     }
-    if constexpr (XF) okb = okbits;
   }
 
   __device__ __forceinline__ void store(char* lds) {
@@ -572,19 +481,13 @@ struct KOuterLoader {
     for (int i = 0; i < L; ++i) {
       int kr = t / CPR + RPP * i;
       int pc = c ^ (kouter_swz<R>(kr) << 1);
-      uint4 v = reg[i];
-      if constexpr (XF) {
-        if ((okb >> i) & 1u) v = bnrelu8(v, xk);
-      }
-      *reinterpret_cast<uint4*>(lds + kr * (R * 2) + pc * 16) = v;
+      *reinterpret_cast<uint4*>(lds + kr * (R * 2) + pc * 16) = reg[i];
     }
   }
-  __device__ __forceinline__ void xform(char*) const {}
 };
 
-template <int R, int MODE, bool XF = false>
+template <int R, int MODE>
 struct PixelRowLoader {
-  static_assert(!XF, "on-the-fly BatchNorm of a row-mapped operand needs the LDS-DMA loader");
   static constexpr int CPT = R / 32;  // 16-B chunks per thread (4 threads per 64-deep k-row)
   int kr;
   int coff[CPT];                      // byte offset of the chunk's column within a pixel row (+ tap shift)
@@ -665,8 +568,6 @@ struct PixelRowLoader {
     }
   }
 
-  __device__ __forceinline__ void xform(char*) const {}
-
   // Logical 16-B chunk written by thread t in store instruction i. Odd k-rows take their chunks in the
   // other half-order (^4): a ds_write_b128 8-lane group spans two k-rows (4 lanes each), and this puts the
   // two rows' 64-B pieces on different banks (the rows are 256 B apart, i.e. the same bank set).
@@ -695,7 +596,7 @@ __device__ __forceinline__ v8bf frag_kouter(const char* lds, int cb, int kk, int
 // fetches the LOGICAL chunk that belongs at its physical slot (the XOR swizzle is undone on the source side).
 // Rows past the operand, k past Kend and (tap-uniform gathers) out-of-image taps get an out-of-range offset
 // and the range check writes zeros.
-template <int R, int MODE, bool XF = false>
+template <int R, int MODE>
 struct GldsLoader {
   static_assert(MODE == OP_KCONTIG || MODE == OP_IM2COL_T || MODE == OP_DGRAD_T, "K-contiguous modes only");
   static constexpr int L = R / 32;  // wave instructions per thread per K-tile
@@ -704,8 +605,6 @@ struct GldsLoader {
   uint32_t tmask[L];  // KCONTIG: ~0 for valid rows; gathers: in-image tap mask
   int coff[L];        // byte offset of this lane's logical chunk in the 64-wide K-tile (the same for every i:
                       // rows 32 i + (t >> 3) share (row >> 1) & 7)
-  uint32_t okb;       // XF: slots of the last issued tile that loaded data
-  Coef8 xk;           // XF: BN coefficients of this lane's 8 channels in that tile
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot) {
     const int t = threadIdx.x;
@@ -764,35 +663,15 @@ struct GldsLoader {
       toff = MODE == OP_IM2COL_T ? (((int)kh * g.dh * g.W + (int)kw * g.dw) * g.C + (int)c0) * 2
                                  : ((int)c0 - ((int)kh * g.dh * g.Q + (int)kw * g.dw) * g.Kout) * 2;
     }
-    uint32_t okbits = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       bool ok;
       if constexpr (MODE == OP_KCONTIG) ok = tmask[i] != 0u && k0 + (coff[i] >> 1) < Kend;
       else ok = (tmask[i] >> tap) & 1u;
-      okbits |= (uint32_t)ok << i;
       const uint32_t off = ok ? (uint32_t)(roff[i] + toff + coff[i]) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 +
                                                                                               wave * 1024),
                                                16, off, 0, 0, 0);
-    }
-    if constexpr (XF) {
-      okb = okbits;
-      if (okbits) xk = load_coef8x(a.xsc, a.xsh, (int)c0 + (coff[0] >> 1));  // channel of the lane's chunk
-    }
-  }
-
-  // XF: BatchNorm + ReLU of this lane's own landed slots of the last issued tile, in place (after the issuing
-  // wave's vmcnt wait, before the barrier that publishes the tile)
-  __device__ __forceinline__ void xform(char* lds) const {
-    if constexpr (XF) {
-      const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-      for (int i = 0; i < L; ++i) {
-        if (!((okb >> i) & 1u)) continue;
-        uint4* p = reinterpret_cast<uint4*>(lds + i * 4096 + wave * 1024 + lane * 16);
-        *p = bnrelu8(*p, xk);
-      }
     }
   }
 };
@@ -802,7 +681,7 @@ struct GldsLoader {
 // the XOR swizzle puts at its physical slot. OP_KOUTER_R: plain rows (dY of a weight gradient: row stride
 // = Kout); OP_WGRADX_R: the row is an output pixel whose input pixel is decoded per K-tile, the column a
 // (tap, channel) pair fixed per lane; out-of-image taps / rows past K read zeros via the range check.
-template <int R, int MODE, bool XF = false>
+template <int R, int MODE>
 struct GldsKOuter {
   static_assert(MODE == OP_KOUTER_R || MODE == OP_WGRADX_R || MODE == OP_KOUTER, "K-outer operands only");
   static constexpr int L = R / 32;
@@ -813,12 +692,6 @@ struct GldsKOuter {
   int coff[L];      // byte offset of the lane's column chunk (+ tap shift for OP_WGRADX_R)
   int hoff[L], woff[L];
   bool cv[L];
-  // XF: the lane's column chunk is the same 8 channels in every instruction (k-rows i*4096/ROWB + t*16/ROWB share
-  // the swizzle term of kouter_swz for R <= 128), so ONE set of BN coefficients, loaded once; okb: slots of the last
-  // issued tile that loaded data
-  static_assert(!XF || R <= 128, "XF K-outer images of more than 128 columns change channels per instruction");
-  Coef8 xk;
-  uint32_t okb;
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* ptr, long ld, int r0, int Rtot) {
     const int t = threadIdx.x;
@@ -842,27 +715,8 @@ struct GldsKOuter {
         hoff[i] = (int)kh * g.dh - g.ph;
         woff[i] = (int)kw * g.dw - g.pw;
         coff[i] = ((hoff[i] * g.W + woff[i]) * g.C + (int)ci) * 2;
-        if constexpr (XF) {
-          if (i == 0 && cv[0]) xk = load_coef8x(a.xsc, a.xsh, (int)ci);
-        }
       } else {
         coff[i] = col * 2;
-        if constexpr (XF) {
-          if (i == 0 && cv[0]) xk = load_coef8x(a.xsc, a.xsh, col);  // OP_KOUTER: the column IS the channel
-        }
-      }
-    }
-  }
-
-  // XF: BatchNorm + ReLU of this lane's own landed slots of the last issued tile (see GldsLoader::xform)
-  __device__ __forceinline__ void xform(char* lds) const {
-    if constexpr (XF) {
-      const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-      for (int i = 0; i < L; ++i) {
-        if (!((okb >> i) & 1u)) continue;
-        uint4* p = reinterpret_cast<uint4*>(lds + i * 4096 + wave * 1024 + lane * 16);
-        *p = bnrelu8(*p, xk);
       }
     }
   }
@@ -870,7 +724,6 @@ struct GldsKOuter {
   __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int Kend, char* lds) {
     const ConvGeom& g = a.g;
     const int wave = threadIdx.x >> 6;
-    uint32_t okbits = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       const int k = k0 + kr[i];
@@ -891,28 +744,25 @@ struct GldsKOuter {
       } else {
         off = k * ldb + coff[i];
       }
-      okbits |= (uint32_t)ok << i;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 + wave * 1024), 16,
           ok ? (uint32_t)off : 0x80000000u, 0, 0, 0);
     }
-    if constexpr (XF) okb = okbits;
   }
 };
 
-template <int R, int MODE, bool XF = false>
+template <int R, int MODE>
 using LoaderFor = typename std::conditional<
-    (MODE == OP_KOUTER_R || MODE == OP_WGRADX_R), PixelRowLoader<R, MODE, XF>,
-    typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE, XF>,
-                              KContigLoader<R, MODE, XF>>::type>::type;
+    (MODE == OP_KOUTER_R || MODE == OP_WGRADX_R), PixelRowLoader<R, MODE>,
+    typename std::conditional<(MODE == OP_KOUTER || MODE == OP_WGRADX), KOuterLoader<R, MODE>,
+                              KContigLoader<R, MODE>>::type>::type;
 
 constexpr bool glds_kcontig(int m) { return m == OP_KCONTIG || m == OP_IM2COL_T || m == OP_DGRAD_T; }
 constexpr bool glds_kouter(int m) { return m == OP_KOUTER_R || m == OP_WGRADX_R || m == OP_KOUTER; }
 constexpr bool glds_mode(int m) { return glds_kcontig(m) || glds_kouter(m); }
 
-template <int R, int MODE, bool XF = false>
-using GldsFor =
-    typename std::conditional<glds_kouter(MODE), GldsKOuter<R, MODE, XF>, GldsLoader<R, MODE, XF>>::type;
+template <int R, int MODE>
+using GldsFor = typename std::conditional<glds_kouter(MODE), GldsKOuter<R, MODE>, GldsLoader<R, MODE>>::type;
 
 constexpr bool kouter_mode(int m) {
   return m == OP_KOUTER || m == OP_WGRADX || m == OP_KOUTER_R || m == OP_WGRADX_R;
@@ -969,12 +819,12 @@ __device__ __forceinline__ float4 fin_sum_rows(const GemmArgs& a, const float* b
     for (; r + 3 * TPI < cnt; r += 4 * TPI) {
       float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(p + (long)(r + u * TPI) * stride);
+      for (int u = 0; u < 4; ++u) v[u] = ld_wt4(p + (long)(r + u * TPI) * stride);
 #pragma unroll
       for (int u = 0; u < 4; ++u) { s[u].x += v[u].x; s[u].y += v[u].y; s[u].z += v[u].z; s[u].w += v[u].w; }
     }
     for (int u = 0; r < cnt; r += TPI, ++u) {
-      const float4 v = *reinterpret_cast<const float4*>(p + (long)r * stride);
+      const float4 v = ld_wt4(p + (long)r * stride);
       s[u & 3].x += v.x; s[u & 3].y += v.y; s[u & 3].z += v.z; s[u & 3].w += v.w;
     }
   }
@@ -1042,7 +892,10 @@ __device__ __forceinline__ void bn_fin_tail(const GemmArgs& a, char* smem, int t
   // level 1: the group's rows -> its first row
   const float4 g1 = fin_sum_rows<BN, NTH>(a, a.stats + (long)r0 * rs, rs, r1 - r0, n0, red);
   const int item = threadIdx.x % I4, h = item / (BN / 4), c = n0 + (item % (BN / 4)) * 4;
-  if (threadIdx.x < I4 && c < a.N) *reinterpret_cast<float4*>(a.stats + (long)r0 * rs + (long)h * a.N + c) = g1;
+  if (threadIdx.x < I4 && c < a.N) {
+    float* p = a.stats + (long)r0 * rs + (long)h * a.N + c;
+    st_wt(p, g1.x); st_wt(p + 1, g1.y); st_wt(p + 2, g1.z); st_wt(p + 3, g1.w);
+  }
   if (!last_arriver(f.tickets + ngroups * a.tiles_n + tn, ngroups, flag)) return;
   // level 2: the group rows (stride G rows) -> finalize
   const float4 g2 = fin_sum_rows<BN, NTH>(a, a.stats, (long)G * rs, ngroups, n0, red);
@@ -1162,22 +1015,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
     constexpr int C8 = BN / 8;
     static_assert(NTH % C8 == 0, "a thread's channel chunk must stay fixed across the store pass");
     const int c8t = threadIdx.x % C8;  // this thread's 8-channel chunk (constant over the pass)
-    float bs[8], bq[8], bmu[8], bsc[8], bsh[8];
+    float bs[8], bq[8], bmu[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) bs[r] = bq[r] = bmu[r] = bsc[r] = bsh[r] = 0.f;
-    const bool mask_coef = bn_bwd && !a.bnmask && a.bnsc;  // ReLU mask recomputed from the BN input
+    for (int r = 0; r < 8; ++r) bs[r] = bq[r] = bmu[r] = 0.f;
     if (bn_bwd && n0 + c8t * 8 < a.N) {
       const float4 m0v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8);
       const float4 m1v = *reinterpret_cast<const float4*>(a.bnmean + n0 + c8t * 8 + 4);
       bmu[0] = m0v.x; bmu[1] = m0v.y; bmu[2] = m0v.z; bmu[3] = m0v.w;
       bmu[4] = m1v.x; bmu[5] = m1v.y; bmu[6] = m1v.z; bmu[7] = m1v.w;
-      if (mask_coef) {
-        const Coef8 k = load_coef8x(a.bnsc, a.bnsh, n0 + c8t * 8);
-        bsc[0] = k.s0.x; bsc[1] = k.s0.y; bsc[2] = k.s0.z; bsc[3] = k.s0.w;
-        bsc[4] = k.s1.x; bsc[5] = k.s1.y; bsc[6] = k.s1.z; bsc[7] = k.s1.w;
-        bsh[0] = k.h0.x; bsh[1] = k.h0.y; bsh[2] = k.h0.z; bsh[3] = k.h0.w;
-        bsh[4] = k.h1.x; bsh[5] = k.h1.y; bsh[6] = k.h1.z; bsh[7] = k.h1.w;
-      }
     }
 #pragma unroll 4
     for (int c = threadIdx.x; c < BM * C8; c += NTH) {
@@ -1209,8 +1054,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
       *reinterpret_cast<uint4*>(cp) = val;
       if (bn_bwd) {
         const uint4 xr = *reinterpret_cast<const uint4*>(a.bnx + e);
-        const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3]  // e % 8 == 0
-                              : mask_coef ? bnrelu_bits8(xr, bsc, bsh) : 0xFFu;
+        const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3] : 0xFFu;  // e % 8 == 0
         const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1239,8 +1083,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
         if (n >= a.N) continue;
         float sv = 0.f, qv = 0.f;
         for (int t = nl >> 3; t < NTH; t += C8) { sv += red[t * 16 + (nl & 7)]; qv += red[t * 16 + 8 + (nl & 7)]; }
-        prow[n] = sv;
-        prow[a.N + n] = qv;
+        if (a.fin.mode) {  // read by this launch's last arriver: write-through
+          st_wt(prow + n, sv);
+          st_wt(prow + a.N + n, qv);
+        } else {
+          prow[n] = sv;
+          prow[a.N + n] = qv;
+        }
       }
     } else if (a.stats) {
       __syncthreads();  // the statistics reduction below reuses the LDS
@@ -1343,8 +1192,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
       float s = 0.f, q = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) { s += red[w * BN + nl]; q += red[WM * BN + w * BN + nl]; }
-      prow[n] = s;
-      prow[a.N + n] = q;
+      if (a.fin.mode) {  // read by this launch's last arriver: write-through
+        st_wt(prow + n, s);
+        st_wt(prow + a.N + n, q);
+      } else {
+        prow[n] = s;
+        prow[a.N + n] = q;
+      }
     }
   }
   if (a.stats && a.fin.mode) bn_fin_tail<BN, NTH>(a, smem, tile_m, n0);
@@ -1369,8 +1223,7 @@ __device__ __forceinline__ void xcd_block(int nwg, int& bid, int& z) {
 //  2: register-staged, double-buffered LDS (one barrier per K-tile).
 //  3: LDS-DMA (GldsLoader), one buffer, synchronous per K-tile: no staging VGPRs, occupancy hides latency.
 //  4: LDS-DMA, double-buffered: the next K-tile's DMA runs under this tile's MFMAs.
-// XF: on-the-fly BatchNorm + ReLU of operand A (1) or B (2) (GemmArgs.xsc/xsh; LDS-DMA or K-outer register loaders)
-template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int PIPE = 2, int XF = 0>
+template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int PIPE = 2>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   constexpr int NBUF = (PIPE == 2 || PIPE == 4) ? 2 : 1;
   constexpr bool GLDS = PIPE >= 3;
@@ -1405,8 +1258,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
   const bf16_t* Ap = a.A + (long)bz * a.sA;
   const bf16_t* Bp = a.B + (long)bz * a.sB;
 
-  typename std::conditional<GLDS, GldsFor<BM, AM, XF == 1>, LoaderFor<BM, AM, XF == 1>>::type la;
-  typename std::conditional<GLDS, GldsFor<BN, BMODE, XF == 2>, LoaderFor<BN, BMODE, XF == 2>>::type lb;
+  typename std::conditional<GLDS, GldsFor<BM, AM>, LoaderFor<BM, AM>>::type la;
+  typename std::conditional<GLDS, GldsFor<BN, BMODE>, LoaderFor<BN, BMODE>>::type lb;
   la.init(a, Ap, a.lda, m0, a.M);
   lb.init(a, Bp, a.ldb, n0, a.N);
 
@@ -1459,10 +1312,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
       }
       for (int kt = 0; kt < nk; ++kt) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (XF) {  // this lane's own landed slots of tile kt (the last tile issued)
-          la.xform((kt & 1) ? sA1 : sA0);
-          lb.xform((kt & 1) ? sB1 : sB0);
-        }
         __syncthreads();  // tile kt landed for every wave; every wave is done reading tile kt-1's buffer
         if (kt + 1 < nk) {
           la.issue(a, kbeg + (kt + 1) * BK, kend, (kt & 1) ? sA0 : sA1);
@@ -1476,10 +1325,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
         la.issue(a, kbeg + kt * BK, kend, sA0);
         lb.issue(a, kbeg + kt * BK, kend, sB0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (XF) {
-          la.xform(sA0);
-          lb.xform(sB0);
-        }
         __syncthreads();
         compute(sA0, sB0);
       }

@@ -171,7 +171,8 @@ __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restri
   const long off = (col < 16 ? 0 : C) + c;            // sum half / sum-of-squares half
   const bool cv = c < C;
   // sum rows r0 + lane, r0 + lane + 8, ... < r1 with row stride `stride` (in rows of rs floats)
-  auto sweep = [&](int r0, int r1, long stride) {
+  // wt: the rows were written by other blocks of THIS launch (write-through hand-off, common.h last_arriver): sc1 loads
+  auto sweep = [&](int r0, int r1, long stride, bool wt) {
     float4 acc[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -180,14 +181,18 @@ __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restri
       for (; r + 7 * RF_LANES < r1; r += 8 * RF_LANES) {
         float4 v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(part + (long)(r + u * RF_LANES) * stride * rs + off);
+        for (int u = 0; u < 8; ++u) {
+          const float* p = part + (long)(r + u * RF_LANES) * stride * rs + off;
+          v[u] = wt ? ld_wt4(p) : *reinterpret_cast<const float4*>(p);
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           acc[u & 3].x += v[u].x; acc[u & 3].y += v[u].y; acc[u & 3].z += v[u].z; acc[u & 3].w += v[u].w;
         }
       }
       for (int u = 0; r < r1; r += RF_LANES, ++u) {
-        const float4 v = *reinterpret_cast<const float4*>(part + (long)r * stride * rs + off);
+        const float* p = part + (long)r * stride * rs + off;
+        const float4 v = wt ? ld_wt4(p) : *reinterpret_cast<const float4*>(p);
         acc[u & 3].x += v.x; acc[u & 3].y += v.y; acc[u & 3].z += v.z; acc[u & 3].w += v.w;
       }
     }
@@ -209,10 +214,13 @@ __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restri
     return s;
   };
   const int r0 = blockIdx.y * sg, r1 = min(T, r0 + sg);
-  const float4 grp = sweep(r0, r1, 1);
-  if (lane == 0 && cv) *reinterpret_cast<float4*>(part + (long)r0 * rs + off) = grp;
+  const float4 grp = sweep(r0, r1, 1, false);
+  if (lane == 0 && cv) {
+    float* p = part + (long)r0 * rs + off;
+    st_wt(p, grp.x); st_wt(p + 1, grp.y); st_wt(p + 2, grp.z); st_wt(p + 3, grp.w);
+  }
   if (!last_arriver(tickets + blockIdx.x, gridDim.y, &flag)) return;
-  const float4 tot = sweep(0, gridDim.y, sg);  // the leader rows: row g*sg
+  const float4 tot = sweep(0, gridDim.y, sg, true);  // the leader rows: row g*sg
   __syncthreads();
   if (lane == 0) red[0][col] = tot;
   __syncthreads();
@@ -230,8 +238,7 @@ __global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restri
 }
 
 // groups for bn_reduce_finalize_kernel: about sqrt(T) rows per group and sqrt(T) groups (<= 128), so both the
-// group pass and the leader-row pass are ~sqrt(T)/8 loads per thread (each group's agent-scope release costs
-// an L2 write-back, so the group count stays bounded)
+// group pass and the leader-row pass are ~sqrt(T)/8 loads per thread
 static inline int bn_groups(int T, int* sg) {
   static const int gmax = [] {
     const char* e = getenv("DTF_BN_GROUPS");  // tuning knob: fixed group cap instead of the sqrt rule
@@ -344,12 +351,8 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// dz = dy masked by ReLU: from the 1-bit mask, the bf16 output (sign/zero test), or — for a BatchNorm output that was
-// never materialised (its consumer applied BN + ReLU on the fly) — recomputed from the BN input xv with the forward's
-// scale/shift (msc/msh: this thread's 8 channels), the same test as the bit bn_apply would have stored
-__device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const uint8_t* mbits, long i8,
-                                           const float* xv = nullptr, const float* msc = nullptr,
-                                           const float* msh = nullptr) {
+// dz = dy masked by ReLU: from the 1-bit mask or the bf16 output (sign/zero test)
+__device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const uint8_t* mbits, long i8) {
   if (mbits) {
     const uint32_t b = mbits[i8];
 #pragma unroll
@@ -365,27 +368,18 @@ __device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const 
       if (!(lo != 0 && !(lo & 0x8000u))) d[2 * j] = 0.f;
       if (!(hi != 0 && !(hi & 0x8000u))) d[2 * j + 1] = 0.f;
     }
-  } else if (msc) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float o = fmaf(xv[j], msc[j], msh[j]);
-      if (!(o > 0.f && f2bf(o) != 0)) d[j] = 0.f;
-    }
   }
 }
 
 // Backward reduce: dz = dy * (y > 0 if relu-mask given); partial rows [gridDim.x][2C]:
 // [0,C) sum dz, [C,2C) sum dz*xhat. No atomics; bn_bwd_finalize sums the rows.
-template <bool MC>  // MC: ReLU mask recomputed from x with msc/msh (a lazy BatchNorm output)
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
                                                             const bf16_t* __restrict__ ymask,
                                                             const uint8_t* __restrict__ mbits,
                                                             const bf16_t* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long M, int C,
-                                                            float* __restrict__ part,
-                                                            const float* __restrict__ msc,
-                                                            const float* __restrict__ msh) {
+                                                            float* __restrict__ part) {
   __shared__ float red[4096];
   ColGeo g = colgeo(C);
   const int t = threadIdx.x;
@@ -394,12 +388,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
     const int cc = cc0 + t % g.TPR;
     float s[8] = {0}, q[8] = {0};
     if (t < g.TPR * g.RPB && cc < g.cols8) {
-      float mu[8], ms[8], mh[8];
+      float mu[8];
       load_coef8(mean + cc * 8, mu);
-      if constexpr (MC) {
-        load_coef8(msc + cc * 8, ms);
-        load_coef8(msh + cc * 8, mh);
-      }
       // sum dz*(x - mean) here; the invstd factor is applied once per channel in bn_bwd_finalize
       const long rstep = (long)gridDim.x * g.RPB;
       long r = (long)blockIdx.x * g.RPB + rsub;
@@ -410,8 +400,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
           const long i8 = (r + u * rstep) * g.cols8 + cc;
           load8(dy + i8 * 8, d[u]);
           load8(x + i8 * 8, xv[u]);
-          if constexpr (MC) relu_mask8(d[u], nullptr, nullptr, i8, xv[u], ms, mh);
-          else relu_mask8(d[u], ymask, mbits, i8);
+          relu_mask8(d[u], ymask, mbits, i8);
         }
 #pragma unroll
         for (int u = 0; u < EU; ++u)
@@ -426,8 +415,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
         const long i8 = r * g.cols8 + cc;
         load8(dy + i8 * 8, d);
         load8(x + i8 * 8, xv);
-        if constexpr (MC) relu_mask8(d, nullptr, nullptr, i8, xv, ms, mh);
-        else relu_mask8(d, ymask, mbits, i8);
+        relu_mask8(d, ymask, mbits, i8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           s[j] += d[j];
@@ -509,7 +497,7 @@ __device__ __forceinline__ void store8s(bf16_t* p, const float* f, bool nt) {
 // taken here as one partial row per block into part2 — the shortcut's own reduce pass disappears.
 // (host: C/8 <= 256 and 256 % (C/8) == 0, so every thread owns exactly one channel chunk)
 // NU rows per trip, all of their loads (dy, x, mask bytes) issued before the first use; NT: nontemporal hints.
-template <bool SC, bool MC = false, int NU = EU, bool NT = false>
+template <bool SC, int NU = EU, bool NT = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ ymask,
                                                            const uint8_t* __restrict__ mbits,
@@ -518,15 +506,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ dx, bf16_t* __restrict__ dz_out,
                                                            const bf16_t* __restrict__ x2,
                                                            const float* __restrict__ mean2,
-                                                           float* __restrict__ part2, int rev,
-                                                           const float* __restrict__ msc,
-                                                           const float* __restrict__ msh) {
+                                                           float* __restrict__ part2, int rev) {
   const ColGeo g = colgeo(C);
   const int t = threadIdx.x;
   if (!SC && t >= g.TPR * g.RPB) return;
   const int rsub = t / g.TPR;
   const long rstep = (long)gridDim.x * g.RPB;
-  if (!ymask && !mbits && !MC) dz_out = nullptr;
+  if (!ymask && !mbits) dz_out = nullptr;
   float s2[8] = {0}, q2[8] = {0}, mu2[8];
   auto sc_acc = [&](const float* d, long i8) {
     if constexpr (SC) {
@@ -548,14 +534,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
     store8s(dx + i8 * 8, o, NT);
   };
   for (int cc = t % g.TPR; cc < g.cols8; cc += g.TPR) {
-    float ka[8], kb[8], kc[8], ms[8], mh[8];
+    float ka[8], kb[8], kc[8];
     load_coef8(coef + cc * 8, ka);
     load_coef8(coef + C + cc * 8, kb);
     load_coef8(coef + 2 * C + cc * 8, kc);
-    if constexpr (MC) {
-      load_coef8(msc + cc * 8, ms);
-      load_coef8(msh + cc * 8, mh);
-    }
     if constexpr (SC) load_coef8(mean2 + cc * 8, mu2);
     long r = (long)blockIdx.x * g.RPB + rsub;
     for (; r + (NU - 1) * rstep < M; r += NU * rstep) {
@@ -567,13 +549,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
         i8[u] = (rev ? M - 1 - (r + u * rstep) : r + u * rstep) * g.cols8 + cc;
         load8s(dy + i8[u] * 8, d[u], NT);
         load8s(x + i8[u] * 8, xv[u], NT);
-        if (!MC && mbits) mb[u] = mbits[i8[u]];
+        if (mbits) mb[u] = mbits[i8[u]];
       }
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
-        if constexpr (MC) {
-          relu_mask8(d[u], nullptr, nullptr, i8[u], xv[u], ms, mh);
-        } else if (mbits) {
+        if (mbits) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
             if (!((mb[u] >> j) & 1u)) d[u][j] = 0.f;
@@ -589,8 +569,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
       const long i8 = (rev ? M - 1 - r : r) * g.cols8 + cc;
       load8(dy + i8 * 8, d);
       load8(x + i8 * 8, xv);
-      if constexpr (MC) relu_mask8(d, nullptr, nullptr, i8, xv, ms, mh);
-      else relu_mask8(d, ymask, mbits, i8);
+      relu_mask8(d, ymask, mbits, i8);
       row_out(d, xv, ka, kb, kc, i8);
       sc_acc(d, i8);
     }
@@ -1127,7 +1106,7 @@ struct ShortcutStats {  // optional fused projection-shortcut BN reduction (bn_b
 static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
                        float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,
-                       const ShortcutStats* sc = nullptr, const float* msc = nullptr, const float* msh = nullptr);
+                       const ShortcutStats* sc = nullptr);
 
 // work: (2*1024 + 3) * C floats (partials + coefficients)
 // ReLU mask from mbits (1 bit/element, preferred) or from the bf16 output ymask; neither = no ReLU
@@ -1135,22 +1114,17 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
                        const float* invstd,
                        const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma, float* dbeta,
                        int accumulate, float* work, const void* x2, const float* mean2, float* part2, int* rows2,
-                       const float* msc, const float* msh, void* stream) {
+                       void* stream) {
   if (C & 7) return -1;
   const ShortcutStats sc{x2, mean2, part2, rows2};
   hipStream_t st = (hipStream_t)stream;
   float* coef = work;
   float* part = work + 3 * C;
   int G = red_grid(M, C);
-  if (msc && !mbits && !ymask)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, nullptr, nullptr,
-                       (const bf16_t*)x, mean, invstd, M, C, part, msc, msh);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(G), dim3(256), 0, st, (const bf16_t*)dy,
-                       (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part,
-                       nullptr, nullptr);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
+                     (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part);
   return bn_bwd_tail(dy, ymask, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, G,
-                     coef, st, &sc, msc, msh);
+                     coef, st, &sc);
 }
 
 // Backward with the reduction already done by the GEMM that produced dy (dtf_conv_dgrad's fused BN-backward
@@ -1158,23 +1132,22 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
 DTF_API int dtf_bn_bwd_partials(const void* dy, const void* mbits, const void* x, const float* mean,
                                 const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out,
                                 float* dgamma, float* dbeta, int accumulate, float* part, int T, float* coef,
-                                const void* x2, const float* mean2, float* part2, int* rows2, const float* msc,
-                                const float* msh, void* stream) {
+                                const void* x2, const float* mean2, float* part2, int* rows2, void* stream) {
   if ((C & 7) || T < 1) return -1;
   const ShortcutStats sc{x2, mean2, part2, rows2};
   return bn_bwd_tail(dy, nullptr, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, T,
-                     coef, (hipStream_t)stream, &sc, msc, msh);
+                     coef, (hipStream_t)stream, &sc);
 }
 
 // Backward apply only: the coefficients `coef` (3*C) were already finalized — by the data-gradient GEMM that produced
 // dy (dtf_conv_dgrad_bn's fused finalize). Optional fused projection-shortcut statistics as in dtf_bn_bwd_partials.
 DTF_API int dtf_bn_bwd_apply_coef(const void* dy, const void* mbits, const void* x, long M, int C, void* dx,
                                   void* dz_out, const float* coef, const void* x2, const float* mean2, float* part2,
-                                  int* rows2, const float* msc, const float* msh, void* stream) {
+                                  int* rows2, void* stream) {
   if (C & 7) return -1;
   const ShortcutStats sc{x2, mean2, part2, rows2};
   return bn_bwd_tail(dy, nullptr, mbits, x, nullptr, nullptr, nullptr, M, C, dx, dz_out, nullptr, nullptr, 0, nullptr,
-                     0, const_cast<float*>(coef), (hipStream_t)stream, &sc, msc, msh);
+                     0, const_cast<float*>(coef), (hipStream_t)stream, &sc);
 }
 
 // Sum the G partial rows [G][2C] of a BN backward reduction and finalize: dgamma/dbeta and the apply
@@ -1200,37 +1173,27 @@ static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const 
 static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
                        float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,
-                       const ShortcutStats* sc, const float* msc, const float* msh) {
-  if (mbits || ymask) msc = msh = nullptr;
+                       const ShortcutStats* sc) {
   if (part) bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
   const ColGeo geo = colgeo(C);
   const int grid = ew_grid(M, C, g_ew_variant == 4 ? 2 : EU);  // (the shortcut-fused launch: one partial row per block)
-  const bool fuse_sc = !msc && sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&
+  const bool fuse_sc = sc && sc->x2 && sc->part2 && dz_out && (ymask || mbits) && geo.cols8 <= 256 &&
                        geo.TPR * geo.RPB == 256;
   if (sc && sc->rows2) *sc->rows2 = fuse_sc ? grid : 0;
-  if (msc) {  // lazy BatchNorm output: no bit mask, no residual branch (rows per trip as the regular pass)
+  if (fuse_sc) {
     if (g_ew_variant == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true, 2>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
-                         nullptr, nullptr, (const bf16_t*)x, coef, M, C, (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr,
-                         nullptr, ew_reverse(), msc, msh);
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, nullptr,
-                         nullptr, (const bf16_t*)x, coef, M, C, (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr,
-                         ew_reverse(), msc, msh);
-  } else if (fuse_sc) {
-    if (g_ew_variant == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, 2>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<true, 2>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
                          (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                         (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse(), nullptr, nullptr);
+                         (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse());
     else
       hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
                          (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
-                         (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse(), nullptr, nullptr);
+                         (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse());
   } else {
 #define DTF_BNB(NU, NT)                                                                                        \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false, NU, NT>), dim3(ew_grid(M, C, NU)), dim3(256), 0, st,     \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<false, NU, NT>), dim3(ew_grid(M, C, NU)), dim3(256), 0, st,            \
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, \
-                     (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse(), nullptr, nullptr)
+                     (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse())
     switch (g_ew_variant) {
       case 1: DTF_BNB(EU, true); break;
       case 2: DTF_BNB(8, false); break;

@@ -117,7 +117,10 @@ DTF_API int dtf_stem_fwd(const void* X, const void* Wt, void* Y, float* part, in
     const char* e = getenv("DTF_STEM_GRID");
     return e ? atoi(e) : 512;  // 2 blocks per CU (register-bound: the filter lives in VGPRs)
   }();
-  const int grid = std::min(units, std::max(1, grid_cap));
+  // the callers size `part` for the conv stats contract: ceil(N*P*Q/64) rows — never write more rows than that
+  // (the units loop is persistent, so a smaller grid only means more units per block)
+  const long cap_rows = ((long)N * P * Q + 63) / 64;
+  const int grid = (int)std::min<long>(std::min(units, std::max(1, grid_cap)), std::max<long>(1, cap_rows));
   hipLaunchKernelGGL(stem_fwd_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)X,
                      (const bf16_t*)Wt, (bf16_t*)Y, part, N, Hs, Ws, P, Q);
   if (rows) *rows = grid;

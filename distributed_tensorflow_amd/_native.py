@@ -26,21 +26,20 @@ _KERNEL_SIGS = {
     "dtf_conv_fwd": [P, P, P, P, P, P] + [I] * 15 + [I, I, I, P],
     "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P, L, P, P, P, P, P, P, P],
     "dtf_conv_dgrad_addsub2": [P, P, P, P, I, I, I, I, I, I, P, L, P, P, P, P, P, P],
-    "dtf_conv_fwd_bn": [P, P, P, P] + [I] * 15 + [I, P, P, P, P, F, F, P, P, P, P, P, P, P, P],
-    "dtf_conv_dgrad_bn": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P, P],
-    "dtf_conv_dgrad_x": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P, P, P],
-    "dtf_bn_bwd_apply_coef": [P, P, P, L, I, P, P, P, P, P, P, P, P, P, P],
+    "dtf_conv_fwd_bn": [P, P, P, P] + [I] * 15 + [I, P, P, P, P, F, F, P, P, P, P, P, P],
+    "dtf_conv_dgrad_bn": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P, P, P, P, I, P, P, P],
+    "dtf_conv_dgrad_x": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P],
+    "dtf_bn_bwd_apply_coef": [P, P, P, L, I, P, P, P, P, P, P, P, P],
     "dtf_set_bn_fin_fused": [I],
     "dtf_set_ew_variant": [I],
     "dtf_set_ew_apply_nu": [I],
-    "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P, P, P],
+    "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P],
     "dtf_conv_wgrad": [P, P, P] + [I] * 15 + [I, I, I, P, L, P],
-    "dtf_conv_wgrad_x": [P, P, P] + [I] * 15 + [I, I, I, P, L, P, P, P],
     "dtf_bn_stats": [P, L, I, P, P, P],
     "dtf_bn_finalize": [P, I, P, P, P, P, L, I, F, F, P, P, P, P, P],
     "dtf_bn_infer_coeff": [P, P, P, P, I, F, P, P, P],
     "dtf_bn_apply": [P, P, P, P, P, L, I, I, P, P, P, P],
-    "dtf_bn_bwd": [P, P, P, P, P, P, P, L, I, P, P, P, P, I, P, P, P, P, P, P, P, P],
+    "dtf_bn_bwd": [P, P, P, P, P, P, P, L, I, P, P, P, P, I, P, P, P, P, P, P],
     "dtf_layernorm_fwd": [P, P, P, P, P, P, L, I, F, P],
     "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],
     "dtf_layernorm_bwd2": [P, P, P, P, P, P, P, P, L, L, I, I, P, P],

@@ -149,6 +149,8 @@ class Layer:
         return inputs
 
     def __call__(self, inputs, *args, **kwargs):
+        if _has_symbolic(inputs):
+            return _symbolic_call(self, inputs, args, kwargs)
         if not self.built:
             shape = tuple(inputs.shape) if isinstance(inputs, torch.Tensor) else (
                 [tuple(i.shape) for i in inputs] if isinstance(inputs, (list, tuple)) else None)
@@ -303,12 +305,10 @@ class ConvBN(Layer):
         self.moving_variance = self.add_weight("bn/moving_variance", (self.filters,), "ones", trainable=False)
         self.built = True
 
-    def call(self, x, residual=None, training=None, link=None, role=None, pool=None, s2d=False, lazy=False):
+    def call(self, x, residual=None, training=None, link=None, role=None, pool=None, s2d=False):
         """link/role: residual-gradient join of a block (ops.conv.ResidualGradLink). pool: a MaxPooling2D
         applied to the (ReLU) output, fused with the BatchNorm (ops.conv_bn_maxpool); s2d: x is the
-        space-to-depth image of a 7x7/2 conv's input (ops.image_to_s2d_bf16; the layer must be built).
-        lazy: the caller feeds the output ONLY to another ConvBN (ops.conv_bn lazy outputs); "1x1"/"3x3" name
-        the consuming convolution's kind (DTF_LAZY_BN selects which kinds stay lazy)."""
+        space-to-depth image of a 7x7/2 conv's input (ops.image_to_s2d_bf16; the layer must be built)."""
         if self.padding == "same":
             pad = ((self.kernel_size[0] - 1) // 2, (self.kernel_size[1] - 1) // 2)
         else:
@@ -320,10 +320,9 @@ class ConvBN(Layer):
                                        self.moving_variance, stride=self.strides, pad=pad, momentum=self.momentum,
                                        eps=self.epsilon, training=bool(training), pool_size=pool.pool_size,
                                        pool_strides=pool.strides, pool_pad=pool.pads(), s2d=s2d)
-        kw = {"lazy": lazy} if lazy else {}
         return ops.conv_bn(x, self.kernel, self.gamma, self.beta, self.moving_mean, self.moving_variance,
                            stride=self.strides, pad=pad, relu=self.relu, residual=residual, momentum=self.momentum,
-                           eps=self.epsilon, training=bool(training), link=link, role=role, **kw)
+                           eps=self.epsilon, training=bool(training), link=link, role=role)
 
 
 class MaxPooling2D(Layer):
@@ -452,9 +451,110 @@ class Lambda(Layer):
         return self.fn(x)
 
 
+# ---------------------------------------------------------------------------------------------------------------
+# Functional API: keras.Input returns a symbolic KerasTensor; calling a layer on symbolic inputs records a node
+# (layer, symbolic inputs, call arguments) and returns symbolic outputs, which Model(inputs=..., outputs=...) turns
+# into a graph that it evaluates in topological order. The reference builds its model as a graph of ops
+# (reference trainer/task.py:62-71: placeholders X, keys -> Mul/Add prediction, keys passthrough); this is the Keras
+# form of that construction. Layers are built (their weights created) when the node is recorded, by running the
+# layer once on a batch-1 example of each symbolic input under no_grad.
+_DTYPES = {None: torch.float32, "float32": torch.float32, "float": torch.float32, "float16": torch.float16,
+           "bfloat16": torch.bfloat16, "int32": torch.int32, "int64": torch.int64, "bool": torch.bool}
+
+
+class _Node:
+    """One recorded layer call: the layer, its (nested) symbolic inputs and the extra call arguments."""
+    __slots__ = ("layer", "inputs", "args", "kwargs")
+
+    def __init__(self, layer, inputs, args, kwargs):
+        self.layer, self.inputs, self.args, self.kwargs = layer, inputs, tuple(args), dict(kwargs)
+
+
+class KerasTensor:
+    """Symbolic tensor of a functional model: shape (batch dimension None), dtype and the node that produces it
+    (``node is None``: a model input)."""
+
+    def __init__(self, shape, dtype=torch.float32, node=None, index=None, name=None):
+        self.shape = tuple(shape)
+        self.dtype = dtype
+        self.node = node
+        self.index = index  # path of this output in the layer's (nested) outputs, None for a single output
+        self.name = name or (unique_name("input") if node is None else f"{node.layer.name}/out")
+
+    @property
+    def layer(self):
+        return self.node.layer if self.node is not None else None
+
+    @property
+    def inputs(self):
+        return self.node.inputs if self.node is not None else None
+
+    @property
+    def input_shape(self):  # Sequential([Input(...), ...]) compatibility: the per-sample shape
+        return self.shape[1:]
+
+    def example(self):
+        """A zero batch-1 tensor of this spec on the current device (used to build layers)."""
+        shape = tuple(1 if d is None else d for d in self.shape)
+        return torch.zeros(shape, dtype=self.dtype, device=context.current_device())
+
+    def __repr__(self):
+        src = "input" if self.layer is None else self.layer.name
+        return f"<KerasTensor shape={self.shape} dtype={self.dtype} from={src}>"
+
+
+def _flatten(struct):
+    if isinstance(struct, dict):
+        return [v for k in sorted(struct) for v in _flatten(struct[k])]
+    if isinstance(struct, (list, tuple)):
+        return [v for x in struct for v in _flatten(x)]
+    return [struct]
+
+
+def _map_structure(fn, struct):
+    if isinstance(struct, dict):
+        return {k: _map_structure(fn, v) for k, v in struct.items()}
+    if isinstance(struct, (list, tuple)):
+        return type(struct)(_map_structure(fn, v) for v in struct)
+    return fn(struct)
+
+
+def _has_symbolic(struct):
+    return any(isinstance(t, KerasTensor) for t in _flatten(struct))
+
+
+def _symbolic_call(layer, inputs, args, kwargs):
+    """Record `layer(inputs, *args, **kwargs)` on symbolic inputs; returns symbolic outputs of the same structure
+    as the layer's concrete outputs."""
+    example = _map_structure(lambda t: t.example() if isinstance(t, KerasTensor) else t, inputs)
+    kw = {k: v for k, v in kwargs.items() if k != "training"}
+    with torch.no_grad():
+        out = layer(example, *args, training=False, **kw) if _takes_training(layer) else layer(example, *args, **kw)
+    node = _Node(layer, inputs, args, kw)
+
+    def wrap(o, path):
+        if isinstance(o, dict):
+            return {k: wrap(v, path + (k,)) for k, v in o.items()}
+        if isinstance(o, (list, tuple)):
+            return type(o)(wrap(v, path + (i,)) for i, v in enumerate(o))
+        return KerasTensor((None,) + tuple(o.shape[1:]), o.dtype, node, index=path or None)
+
+    return wrap(out, ())
+
+
+def _takes_training(layer):
+    import inspect
+    try:
+        return "training" in inspect.signature(layer.call).parameters
+    except (TypeError, ValueError):
+        return False
+
+
 def Input(shape=None, batch_size=None, dtype=None, name=None):
-    """Placeholder spec for Sequential/functional models (shape excludes the batch dim)."""
-    return InputLayer(input_shape=tuple(shape) if shape is not None else None, name=name)
+    """A symbolic model input (shape excludes the batch dimension): feed it to layers to build a functional
+    Model(inputs=..., outputs=...), or list it first in a Sequential to declare the input shape."""
+    dt = _DTYPES.get(dtype, dtype) if not isinstance(dtype, torch.dtype) else dtype
+    return KerasTensor((batch_size,) + tuple(shape or ()), dt, name=name)
 
 
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -32,6 +32,7 @@ from . import callbacks as cbs
 from . import losses as L
 from . import metrics as M
 from . import optimizers as O
+from . import layers as KL
 from .layers import InputLayer, Layer
 
 
@@ -109,8 +110,91 @@ class Model(Layer):
         self._initial_epoch = 0
         self.history = None
         self._replicas = {}
+        self._graph = None
         if inputs is not None or outputs is not None:
-            raise NotImplementedError("use Sequential or subclass Model (functional graphs are built by call())")
+            self._init_graph(inputs, outputs)
+
+    # ------------------------------------------------------------ functional graph
+    def _init_graph(self, inputs, outputs):
+        """Model(inputs=..., outputs=...): inputs/outputs are KerasTensors (keras.Input and layer outputs), single
+        or nested in lists/tuples/dicts. The nodes between them are kept in topological order; call() evaluates
+        them, so training, saving and the strategies treat the graph like any other model."""
+        if inputs is None or outputs is None:
+            raise ValueError("a functional Model needs both inputs and outputs")
+        ins = KL._flatten(inputs)
+        if not all(isinstance(t, KL.KerasTensor) and t.layer is None for t in ins):
+            raise ValueError("Model inputs must be keras.Input tensors")
+        order, seen, layers = [], set(), []
+
+        def visit(t):
+            if not isinstance(t, KL.KerasTensor) or id(t) in seen:
+                return
+            seen.add(id(t))
+            if t.layer is None:
+                if all(t is not i for i in ins):
+                    raise ValueError(f"{t} is not reachable from the model inputs")
+                return
+            for u in KL._flatten(t.inputs):
+                visit(u)
+            order.append(t)
+            if t.layer not in layers:
+                layers.append(t.layer)
+
+        for t in KL._flatten(outputs):
+            if not isinstance(t, KL.KerasTensor):
+                raise ValueError("Model outputs must be KerasTensors")
+            visit(t)
+        self._graph = (inputs, outputs, order)
+        for l in layers:
+            if l not in self._layers:
+                self._layers.append(l)
+        self.built = True
+
+    def _run_graph(self, x, training):
+        inputs, outputs, order = self._graph
+        env = {}
+        if isinstance(inputs, KL.KerasTensor):
+            env[id(inputs)] = x
+        elif isinstance(inputs, dict):
+            if not isinstance(x, dict):
+                raise ValueError(f"this model takes a dict of inputs {sorted(inputs)}")
+            for k, t in inputs.items():
+                env[id(t)] = x[k]
+        else:
+            xs = KL._flatten(x) if not isinstance(x, torch.Tensor) else [x]
+            flat = KL._flatten(inputs)
+            if len(xs) != len(flat):
+                raise ValueError(f"expected {len(flat)} inputs, got {len(xs)}")
+            for t, v in zip(flat, xs):
+                env[id(t)] = v
+        done = {}  # one evaluation per node: the outputs of a multi-output layer share their node
+        for t in order:
+            nd = t.node
+            if id(nd) not in done:
+                args = KL._map_structure(lambda u: env[id(u)] if isinstance(u, KL.KerasTensor) else u, nd.inputs)
+                kw = dict(nd.kwargs)
+                if KL._takes_training(nd.layer):
+                    kw["training"] = training
+                done[id(nd)] = nd.layer(args, *nd.args, **kw)
+            out = done[id(nd)]
+            for p in (t.index or ()):
+                out = out[p]
+            env[id(t)] = out
+        return KL._map_structure(lambda t: env[id(t)], outputs)
+
+    def get_layer(self, name=None, index=None):
+        """A direct sublayer by name or position (Keras Model.get_layer)."""
+        if index is not None:
+            return self.layers[index]
+        for l in self.layers:
+            if l.name == name:
+                return l
+        raise ValueError(f"no layer named {name!r} in {self.name}")
+
+    def call(self, inputs, training=None):
+        if self._graph is None:
+            raise NotImplementedError("subclassed models implement call(); functional models pass inputs/outputs")
+        return self._run_graph(inputs, training)
 
     # ------------------------------------------------------------ compile
     def compile(self, optimizer="rmsprop", loss=None, metrics=None, loss_weights=None, steps_per_execution=1,
@@ -453,7 +537,9 @@ class Model(Layer):
         return torch.cat(outs).numpy() if outs else np.zeros((0,))
 
     def __call__(self, inputs, *args, **kwargs):
-        if isinstance(inputs, (np.ndarray, list)) and not isinstance(inputs, torch.Tensor):
+        if self._graph is not None:  # functional: lists / dicts are the model's input structure
+            inputs = KL._map_structure(lambda v: torch.as_tensor(v) if isinstance(v, np.ndarray) else v, inputs)
+        elif isinstance(inputs, (np.ndarray, list)) and not isinstance(inputs, torch.Tensor):
             inputs = torch.as_tensor(np.asarray(inputs))
         return super().__call__(inputs, *args, **kwargs)
 
@@ -494,7 +580,7 @@ class Sequential(Model):
             self.add(l)
 
     def add(self, layer):
-        if isinstance(layer, InputLayer):
+        if isinstance(layer, (InputLayer, KL.KerasTensor)):
             self._input_shape = layer.input_shape
             return
         self._seq.append(layer)

@@ -42,13 +42,12 @@ class Bottleneck(KL.Layer):
         # The projection runs after c1 so that its backward runs before c1's: the shortcut gradient is then
         # parked in `link` and c1's dgrad epilogue adds into it (no separate add of the two gradients of x).
         link = ResidualGradLink() if (training and RES_LINK and torch.is_grad_enabled()) else None
-        # c1's and c2's BN+ReLU outputs feed only the next ConvBN: lazy (never materialised, ops.conv_bn)
-        y = self.c1(x, training=training, link=link, role="acc", lazy="3x3")
+        y = self.c1(x, training=training, link=link, role="acc")
         if self.proj is not None:
             sc = self.proj(x, training=training, link=link, role="proj")
-            y = self.c2(y, training=training, lazy="1x1")
+            y = self.c2(y, training=training)
             return self.c3(y, residual=sc, training=training)
-        y = self.c2(y, training=training, lazy="1x1")
+        y = self.c2(y, training=training)
         return self.c3(y, residual=x, training=training, link=link, role="res")
 
 

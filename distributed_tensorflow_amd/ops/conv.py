@@ -53,27 +53,16 @@ def conv_fwd_raw(x, w16, g, stats=False, bias=None, act=0):
     return y
 
 
-def conv_fwd_bn_raw(x, w16, g, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean, invstd, xf=None):
+def conv_fwd_bn_raw(x, w16, g, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean, invstd):
     """Training ConvBN forward: y plus the output BatchNorm's scale/shift/mean/invstd and running-statistics update,
     finalized inside the conv launch's tail (gemm_core.h BnFin) — or by the separate reduction + finalize launches
-    when the launch cannot (the native side falls back by itself). xf: (scale, shift) when x is a lazy
-    BatchNorm+ReLU output (x holds that BatchNorm's INPUT; the conv's operand loader applies it)."""
+    when the launch cannot (the native side falls back by itself)."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     y = torch.empty((N, P, Q, K), dtype=BF16, device=x.device)
     part = torch.empty(((N * P * Q + 63) // 64) * 2 * K, dtype=F32, device=x.device)
     call("dtf_conv_fwd_bn", ptr(x), ptr(w16), ptr(y), ptr(part), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
          -1, ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), float(momentum), float(eps), ptr(scale), ptr(shift),
-         ptr(mean), ptr(invstd), None, ptr(xf[0]) if xf else None, ptr(xf[1]) if xf else None, stream())
-    return y
-
-
-def materialize_bn(x, xf):
-    """The bf16 BatchNorm+ReLU output that a lazy ConvBN output x stands for (fallback when a kernel has no
-    on-the-fly form for some shape)."""
-    C = x.shape[-1]
-    y = torch.empty_like(x)
-    call("dtf_bn_apply", ptr(x), ptr(xf[0]), ptr(xf[1]), None, ptr(y), x.numel() // C, C, 1, None, None, None,
-         stream())
+         ptr(mean), ptr(invstd), None, stream())
     return y
 
 
@@ -94,8 +83,6 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=N
         part = torch.empty(((N * H * W + 63) // 64 + sh * sw) * 2 * C, dtype=F32, device=dy.device)
         rows = IntOut()
     bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
-    # a lazy BatchNorm output has no bit mask: the epilogue recomputes the ReLU mask from yc with its scale/shift
-    msk = ((ptr(bn.msc), ptr(bn.msh)) if (bn is not None and bn.msc is not None) else (None, None))
     if bn is not None and bn.invstd is not None and _FUSE_BN_FIN:
         # the producing BatchNorm's backward is finalized in this launch's tail: dgamma/dbeta (straight into the
         # arena gradients when they are direct) and the apply coefficients
@@ -112,7 +99,7 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=N
         call("dtf_conv_dgrad_bn", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
              beta, ptr(ws), 2 * ws.numel(), *bn_ptrs, ptr(part), rows.addr,
              ptr(acc_mask) if acc is not None else None, ptr(acc_sub2), ptr(bn.gamma), ptr(bn.invstd),
-             ptr(dgamma), ptr(dbeta), int(direct), ptr(coef), fused.addr, *msk, stream())
+             ptr(dgamma), ptr(dbeta), int(direct), ptr(coef), fused.addr, stream())
         if fused.value:
             bn.provide_fin(dx, coef, dgamma, dbeta, direct)
         else:
@@ -122,27 +109,17 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=N
         assert acc is None and (R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0)
     call("dtf_conv_dgrad_x", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
          1.0 if (acc is not None or acc_sub2 is not None) else 0.0, ptr(ws), 2 * ws.numel(), *bn_ptrs, ptr(part),
-         rows.addr if rows else None, ptr(acc_mask) if acc is not None else None, ptr(acc_sub2), *msk, stream())
+         rows.addr if rows else None, ptr(acc_mask) if acc is not None else None, ptr(acc_sub2), stream())
     if bn is not None:
         bn.provide(dx, part, rows.value)
     return dx
 
 
-def conv_wgrad_raw(x, dy, g, out=None, xf=None):
-    """dW [K,R,S,C] f32; with `out` (an arena gradient view) the result is accumulated into it. xf: (scale, shift)
-    when x is a lazy BatchNorm+ReLU output (see conv_fwd_bn_raw)."""
+def conv_wgrad_raw(x, dy, g, out=None):
+    """dW [K,R,S,C] f32; with `out` (an arena gradient view) the result is accumulated into it."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
     dw_ = torch.empty((K, R, S, C), dtype=F32, device=x.device) if out is None else out
     ws = workspace(x.device)
-    if xf is not None:
-        try:
-            call("dtf_conv_wgrad_x", ptr(x), ptr(dy), ptr(dw_), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
-                 int(out is not None), 0, -1, ptr(ws), ws.numel(), ptr(xf[0]), ptr(xf[1]), stream())
-            return dw_
-        except RuntimeError as e:  # no on-the-fly kernel for this shape (-20): materialise the BN output
-            if "status -20" not in str(e):
-                raise
-            x = materialize_bn(x, xf)
     call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw_), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
          int(out is not None), 0, -1, ptr(ws), ws.numel(), stream())
     return dw_
@@ -251,12 +228,10 @@ class _BNSource:
     backward then skips its reduction pass (bn_bwd_reduce), provided the gradient it receives is exactly the
     tensor that dgrad wrote (same storage: autograd added nothing else to it)."""
     __slots__ = ("yc", "mbits", "mean", "invstd", "gamma", "gamma_p", "beta_p", "consumers", "part", "rows", "dptr",
-                 "fin", "msc", "msh", "__weakref__")
+                 "fin", "__weakref__")
 
-    def __init__(self, yc, mbits, mean, invstd=None, gamma=None, params=(None, None), mcoef=None):
+    def __init__(self, yc, mbits, mean, invstd=None, gamma=None, params=(None, None)):
         self.yc, self.mbits, self.mean = yc, mbits, mean
-        # lazy output (no bit mask): the ReLU mask is recomputed from yc with the forward's scale/shift
-        self.msc, self.msh = mcoef if mcoef is not None else (None, None)
         # what the consumer's dgrad needs to FINALIZE this BatchNorm's backward too (gemm_core.h BnFin mode 2)
         self.invstd, self.gamma = invstd, gamma
         self.gamma_p, self.beta_p = params
@@ -293,20 +268,10 @@ _FUSE_BN_BWD = __import__("os").environ.get("DTF_FUSE_BN_BWD", "1") != "0"
 # step 1.9x slower on MI355X (gemm.hip fin_on)
 _FUSE_BN_FIN = __import__("os").environ.get("DTF_BN_FIN_FUSED", "0") == "1"
 _LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
-# Lazy BatchNorm outputs (conv_bn(lazy=True): a bottleneck's first two ConvBNs): the BN+ReLU output is never written;
-# its consuming ConvBN applies it to the staged conv output in its forward and weight-gradient operand loaders
-# (gemm_core.h XF) and the ReLU mask is recomputed from the conv output in the backward. Opt-in (DTF_LAZY_BN=1):
-# measured on MI355X (ResNet-50 b256) the in-LDS transform between the DMA wait and the barrier slows the consuming
-# 3x3 convolutions by ~50% (no 256-row pipelined form) and the step went from 22.7 to 24.9 ms. DTF_LAZY_BN=1x1: only
-# outputs whose consumer is a pointwise convolution (a bottleneck's c2 -> c3; conv_bn(lazy="1x1")) stay lazy.
-_LAZY_BN = __import__("os").environ.get("DTF_LAZY_BN", "0")
+# (Round 3 also built "lazy" BatchNorm outputs applied by the consuming conv's operand loaders; measured slower than
+# materialising on every configuration — profiles/r3_lazy_bn_modes.txt — and removed in round 4.)
 _DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
 _COMPACT_PROJ = __import__("os").environ.get("DTF_COMPACT_PROJ", "1") != "0"
-
-
-def _lazy_enabled(consumer):
-    """consumer: True / "1x1" / "3x3" — the kind of convolution that reads the lazy output."""
-    return _LAZY_BN == "1" or (_LAZY_BN == "1x1" and consumer == "1x1")
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -314,9 +279,8 @@ class _ConvBNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, res, rmean, rvar, stride, pad, dil, relu, momentum, eps, training,
-                link=None, role=None, lazy=False):
+                link=None, role=None):
         in_src = getattr(x, "_dtf_bnsrc", None)
-        xf = getattr(x, "_dtf_xform", None)  # x is a lazy BN+ReLU output: (scale, shift) of that BatchNorm
         if in_src is not None:
             in_src.consumers += 1
         if res is not None and getattr(res, "_dtf_bnsrc", None) is not None:
@@ -328,18 +292,9 @@ class _ConvBNFn(torch.autograd.Function):
         dev = x.device
         work = torch.empty(4 * K, dtype=F32, device=dev)  # scale shift mean invstd
         scale, shift, mean, invstd = work[:K], work[K:2 * K], work[2 * K:3 * K], work[3 * K:]
-        if xf is not None and not training:
-            x, xf = materialize_bn(x, xf), None
         if training:
-            try:
-                yc = conv_fwd_bn_raw(x, bf16_shadow(w), g, gamma, beta, rmean, rvar, momentum, eps, scale, shift,
-                                     mean, invstd, xf=xf)
-            except RuntimeError as e:  # no on-the-fly kernel for this shape (-20): materialise the BN output
-                if xf is None or "status -20" not in str(e):
-                    raise
-                x, xf = materialize_bn(x, xf), None
-                yc = conv_fwd_bn_raw(x, bf16_shadow(w), g, gamma, beta, rmean, rvar, momentum, eps, scale, shift,
-                                     mean, invstd)
+            yc = conv_fwd_bn_raw(x, bf16_shadow(w), g, gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean,
+                                 invstd)
         else:
             yc = conv_fwd_raw(x, bf16_shadow(w), g)
             call("dtf_bn_infer_coeff", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), K, float(eps), ptr(scale),
@@ -352,14 +307,8 @@ class _ConvBNFn(torch.autograd.Function):
         res_src = getattr(res, "_dtf_bnsrc", None) if raff is not None else None
         if res is not None:
             res = res.contiguous()
-        lazy = bool(lazy and _lazy_enabled(lazy) and training and relu and res is None and role != "proj")
-        mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if (relu and not lazy) else None
-        if lazy:
-            # the BN+ReLU output is never written: the consumer's loaders apply scale/shift + ReLU to yc, and the
-            # backward recomputes the ReLU mask from yc
-            out = yc
-            out._dtf_xform = (scale, shift)
-        elif role == "proj" and not relu and _DEFER_PROJ_BN:
+        mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if relu else None
+        if role == "proj" and not relu and _DEFER_PROJ_BN:
             # projection shortcut: its BN output is consumed only as the residual of the block's last ConvBN,
             # whose apply pass normalises the conv output on the fly (res * scale + shift) — hand autograd the
             # conv output tagged with the affine instead of materialising the BN output
@@ -371,8 +320,6 @@ class _ConvBNFn(torch.autograd.Function):
                  ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, stream())
         # backward needs the conv output and a 1-bit ReLU mask, not the bf16 BN output
         ctx.save_for_backward(x, w, gamma, yc, mbits, mean, invstd)
-        ctx.xf = xf            # the input's lazy BN (the weight gradient applies it to x again)
-        ctx.mcoef = (scale, shift) if lazy else None  # our own lazy output: ReLU mask from yc
         ctx.bn_params = (gamma, beta)
         ctx.g = g
         ctx.relu = relu
@@ -383,7 +330,7 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.res_src = res_src if (training and _FUSE_BN_BWD) else None
         ctx.src = None
         if training and _FUSE_BN_BWD and any(ctx.needs_input_grad):
-            src = _BNSource(yc, mbits, mean, invstd, gamma, (gamma, beta), mcoef=ctx.mcoef)
+            src = _BNSource(yc, mbits, mean, invstd, gamma, (gamma, beta))
             out._dtf_bnsrc = src
             ctx.src = src
         return out
@@ -411,8 +358,6 @@ class _ConvBNFn(torch.autograd.Function):
         fused = ctx.src.take(dout) if ctx.src is not None else None
         rsrc = ctx.res_src if dres is not None else None
         sc = (None, None, None, None)
-        mc = ctx.mcoef  # lazy output: the ReLU mask comes from yc * scale + shift
-        msk = (ptr(mc[0]), ptr(mc[1])) if mc is not None else (None, None)
         if rsrc is not None:  # projection shortcut BN: its backward reduction rides on our apply pass
             part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=yc.device), IntOut()
             sc = (ptr(rsrc.yc), ptr(rsrc.mean), ptr(part2), rows2.addr)
@@ -420,18 +365,18 @@ class _ConvBNFn(torch.autograd.Function):
             # the consumer's dgrad launch reduced AND finalized this BatchNorm's backward: only the apply is left
             coef, fg, fb, fdirect = fused[1:]
             call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(mbits), ptr(yc), M, K, ptr(dyc), ptr(dres), ptr(coef), *sc,
-                 *msk, stream())
+                 stream())
             direct_bn = fdirect
             dgamma, dbeta = fg, fb
         elif fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
             coef = torch.empty(3 * K, dtype=F32, device=yc.device)
             call("dtf_bn_bwd_partials", ptr(dout), ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
                  ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(fused[1]), fused[2], ptr(coef),
-                 *sc, *msk, stream())
+                 *sc, stream())
         else:
             work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
             call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
-                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), *sc, *msk, stream())
+                 ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), *sc, stream())
         if rsrc is not None and rows2.value > 0:
             rsrc.provide(dres, part2, rows2.value)
         ctx.res_src = None
@@ -447,9 +392,9 @@ class _ConvBNFn(torch.autograd.Function):
             tw = direct_grad(w)
             if tw is not None and SIDE_STREAM_ON:
                 with fork_side(x.device, x, dyc):  # off the critical path: overlaps the dgrad chain
-                    conv_wgrad_raw(x, dyc, g, out=tw, xf=ctx.xf)
+                    conv_wgrad_raw(x, dyc, g, out=tw)
             else:
-                dw = conv_wgrad_raw(x, dyc, g, out=tw, xf=ctx.xf)
+                dw = conv_wgrad_raw(x, dyc, g, out=tw)
             if tw is not None:
                 dw = None  # (autograd still runs the parameter's AccumulateGrad node with an undefined
                 #            gradient, so its post-accumulate hooks — gradient bucketing — fire as usual)
@@ -471,10 +416,9 @@ class _ConvBNFn(torch.autograd.Function):
                 if link is not None and role == "proj":
                     dx = link.park(dx)
             ctx.in_src = None
-        ctx.xf = ctx.mcoef = None
         if direct_bn:
             dgamma = dbeta = None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
     @staticmethod
@@ -498,24 +442,21 @@ class _ConvBNFn(torch.autograd.Function):
             dres = dz.to(BF16) if ctx.relu else dout
         dx = dw = None
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad_raw(x, dyc, ctx.g, xf=ctx.xf)
+            dw = conv_wgrad_raw(x, dyc, ctx.g)
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad_raw(dyc, w, ctx.g)
-        ctx.xf = ctx.mcoef = ctx.in_src = ctx.src = ctx.res_src = None
+        ctx.in_src = ctx.src = ctx.res_src = None
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
-                dres, None, None, None, None, None, None, None, None, None, None, None, None)
+                dres, None, None, None, None, None, None, None, None, None, None, None)
 
 
 def conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1), relu=True, residual=None,
-            momentum=0.9, eps=1e-5, training=True, link=None, role=None, lazy=False):
-    """Fused Conv2D -> FusedBatchNorm -> (+residual) -> ReLU, NHWC. `link`/`role`: see ResidualGradLink.
-    lazy: the output is consumed ONLY by another conv_bn (as its x) — in training on the GPU the BN+ReLU output is
-    then not materialised: the returned tensor holds the conv output tagged with the BN scale/shift, which the
-    consumer applies while staging its operands (any other use of a lazy output would read the wrong values)."""
+            momentum=0.9, eps=1e-5, training=True, link=None, role=None):
+    """Fused Conv2D -> FusedBatchNorm -> (+residual) -> ReLU, NHWC. `link`/`role`: see ResidualGradLink."""
     stride, pad, dil = tuple(stride), tuple(pad), tuple(dil)
     if on_gpu(x):
         return _ConvBNFn.apply(x.to(BF16), w, gamma, beta, residual, rmean, rvar, stride, pad, dil, bool(relu),
-                               float(momentum), float(eps), bool(training), link, role, lazy or False)
+                               float(momentum), float(eps), bool(training), link, role)
     y = _ref_conv(x, w, None, stride, pad, dil)
     from .norm import batch_norm_ref
     y = batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training)

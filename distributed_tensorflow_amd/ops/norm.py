@@ -69,7 +69,7 @@ class _BNFn(torch.autograd.Function):
         work = torch.empty((2 * 1024 + 3) * C, dtype=F32, device=x.device)
         call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(x), ptr(mean), ptr(invstd), ptr(gamma), M, C, ptr(dx),
              ptr(dres),
-             ptr(dgamma), ptr(dbeta), 0, ptr(work), None, None, None, None, None, None, stream())
+             ptr(dgamma), ptr(dbeta), 0, ptr(work), None, None, None, None, stream())
         if ctx.has_res and not ctx.relu:
             dres = dout
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None

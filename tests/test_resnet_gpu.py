@@ -25,7 +25,7 @@ class _RoundBF16(torch.autograd.Function):
 
 
 def _emu_conv_bn(x, w, gamma, beta, rmean, rvar, stride=(1, 1), pad=(0, 0), dil=(1, 1), relu=True, residual=None,
-                 momentum=0.9, eps=1e-5, training=True, link=None, role=None, lazy=False):
+                 momentum=0.9, eps=1e-5, training=True, link=None, role=None):
     """f32 conv/BN with bf16 storage of the conv output, the block output and their gradients (GPU layout)."""
     rnd = _RoundBF16.apply
     y = rnd(OC._ref_conv(rnd(x), rnd(w), None, tuple(stride), tuple(pad), tuple(dil)))

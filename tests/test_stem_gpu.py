@@ -46,6 +46,32 @@ def test_stem_fwd_matches_f32_conv(cuda, N, H, W):
     assert torch.allclose(pr[64:], (yf * yf).sum(0), rtol=1e-4)
 
 
+@pytest.mark.parametrize("N,P,Q", [(4, 1, 16), (3, 3, 16), (2, 1, 32)])
+def test_stem_fwd_short_outputs_stay_in_stats_rows(cuda, N, P, Q):
+    """Short outputs: the kernel may write at most ceil(N*P*Q/64) partial rows (the conv stats contract of its
+    callers); the rows behind that must stay untouched, and the rows it wrote still sum to the statistics."""
+    g = torch.Generator().manual_seed(7)
+    Hs, Ws = P + 3, Q + 3
+    x = torch.randn(N, Hs, Ws, 16, generator=g).to(BF).to(cuda)
+    w16 = (torch.randn(64, 4, 4, 16, generator=g) * 0.05).to(BF).to(cuda)
+    y = torch.empty(N, P, Q, 64, dtype=BF, device=cuda)
+    cap = (N * P * Q + 63) // 64
+    part = torch.full(((cap + 64) * 128,), float("nan"), device=cuda)
+    rows = IntOut()
+    rc = K().dtf_stem_fwd(ptr(x), ptr(w16), ptr(y), ptr(part), rows.addr, N, Hs, Ws, 16, 64, 4, 4, P, Q, stream())
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    T = rows.value
+    assert 0 < T <= cap, (T, cap)
+    assert torch.isnan(part[T * 128:]).all(), "stem kernel wrote past its partial-statistics rows"
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w16.float().permute(0, 3, 1, 2))
+    ref = ref.permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() <= 0.01 * ref.abs().max().item()
+    pr = part[:T * 128].view(T, 128).sum(0)
+    yf = y.float().reshape(-1, 64)
+    assert (pr[:64] - yf.sum(0)).abs().max().item() <= 1e-4 * yf.abs().sum(0).max().item()
+
+
 def test_stem_fwd_rejects_other_shapes(cuda):
     x = torch.zeros(1, 53, 53, 16, dtype=BF, device=cuda)  # Q = 50: not a multiple of 16
     w = torch.zeros(64, 4, 4, 16, dtype=BF, device=cuda)
