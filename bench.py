@@ -22,8 +22,6 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# every training stream on its own hardware queue (see distributed_tensorflow_amd/__init__.py; before HIP initialises)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 DEFAULT_BATCH = {"resnet50": 256, "resnet101": 256, "resnet152": 256, "bert_base": 32, "gpt2_medium_fp8": 8,
                  "gpt2_medium": 8}

@@ -41,3 +41,13 @@ DTF_API int dtf_memcpy_async(void* dst, const void* src, long bytes, void* strea
   if (bytes <= 0) return 0;
   return (int)hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
 }
+
+// A non-blocking HIP stream created NOW (not taken from PyTorch's lazily created stream pool): the framework's
+// weight-gradient / collective side stream is created before the process group initialises RCCL, so it takes its
+// own hardware queue ahead of RCCL's streams at HIP's default of 4 queues per process (round 3 measured the side
+// stream landing on the main stream's queue when it was created after RCCL: profiles/r3_hw_queues.txt).
+DTF_API void* dtf_stream_create(int priority) {
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority) != hipSuccess) return nullptr;
+  return (void*)s;
+}

@@ -22,6 +22,7 @@ _rt = None
 P, I, L, F, U = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_ulonglong
 
 _KERNEL_SIGS = {
+    "dtf_stream_create": [I],
     "dtf_gemm": [P, P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, L, L, L, F, F, I, I, I, I, P, L, P],
     "dtf_conv_fwd": [P, P, P, P, P, P] + [I] * 15 + [I, I, I, P],
     "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P, L, P, P, P, P, P, P, P],
@@ -97,6 +98,9 @@ _KERNEL_SIGS = {
 }
 
 
+_RESTYPES = {"dtf_stream_create": P}
+
+
 class NativeMissing(RuntimeError):
     pass
 
@@ -129,7 +133,7 @@ def kernels():
             if fn is None:
                 continue
             fn.argtypes = sig
-            fn.restype = ctypes.c_int
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _kern = lib
         return lib
 

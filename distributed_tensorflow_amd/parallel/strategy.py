@@ -255,6 +255,8 @@ class MultiWorkerMirroredStrategy(Strategy):
         # replica — how the RCCL code path and its hipGraph capture are exercised on a 1-GPU box
         self._force = os.environ.get("DTF_FORCE_COLLECTIVE", "0") == "1"
         if self._world > 1 or self._force:
+            from ..ops._util import reserve_streams
+            reserve_streams(dev)  # the side stream's hardware queue before RCCL's
             collective.init_process_group(self._rank, self._world, addr, port, dev.type)
 
     @property

@@ -38,3 +38,27 @@ def test_allreduce_sweep_gloo_world2():
         assert p.exitcode == 0
     assert set(res[0]) == {"1MB", "2MB"} and res[0] == res[1]
     assert all(v > 0 for v in res[0].values())
+
+
+@pytest.mark.gpu
+def test_bench_multirank_path_on_one_gpu(tmp_path):
+    """bench.py's N>1 path end to end, rehearsed on a 1-GPU box: `--gpus 2` relaunches itself
+    under torch.distributed.run, both ranks share cuda:0 and reduce over gloo (DTF_COLLECTIVE_BACKEND=gloo; RCCL
+    refuses two ranks on one device), and rank 0 prints ONE JSON line with the whole-job value, the world size, the
+    cross-rank weight checksum agreement and the all-reduce sweep."""
+    import json
+    import subprocess
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, DTF_COLLECTIVE_BACKEND="gloo")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "32", "--steps",
+                        "2", "--warmup", "1"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["process_group_backend"] == "gloo"
+    assert out["replicas_identical"] is True
+    assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "dp2"
+    assert isinstance(out["allreduce_busbw_GBps"], dict) and len(out["allreduce_busbw_GBps"]) == 6
+    assert out["value"] > 0 and out["steps"] == 2 and out["warmup"] == 1
