@@ -206,6 +206,9 @@ def main():
                            allreduce_dtype=args.allreduce_dtype or "f32", zero1=bool(args.zero),
                            bucket_mb=getattr(bucketers[0], "bucket_mb", None) if bucketers else None,
                            exposed_comm_ms_per_step=round(exposed_max, 3),
+                           # bucket collectives issued (warmup + timed steps) per path: RCCL, or the one-shot P2P
+                           # all-reduce over IPC-mapped peer arenas for buckets <= DTF_P2P_MAX_KB (parallel/p2p.py)
+                           allreduce_paths=_paths(bucketers),
                            forced_collective=os.environ.get("DTF_FORCE_COLLECTIVE", "0") == "1"),
             "rccl_world": rccl_world,
             "allreduce_busbw_GBps": ar_sweep,
@@ -218,6 +221,14 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _paths(bucketers):
+    out = {}
+    for b in bucketers:
+        for k, v in (getattr(b, "paths", None) or {}).items():
+            out[k] = out.get(k, 0) + v
+    return out or None
 
 
 def _allreduce_sweep(dist, dev, world, sizes_mb=(1, 4, 16, 32, 64, 128), iters=5):

@@ -68,6 +68,7 @@ _KERNEL_SIGS = {
     "dtf_dropout": [P, P, L, F, U, P, P],
     "dtf_rng_advance": [P, P],
     "dtf_gemm256": [P, P, P, I, I, I, L, L, L, I, I, I, I, P, L, P],
+    "dtf_gemm8p": [P, P, P, I, I, I, L, L, L, I, P],
     "dtf_gemm256_bn": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
     "dtf_gemm_dact": [P, P, P, P, I, I, I, I, L, L, L, I, I, P],
     "dtf_quant_fp8_exact": [P, P, L, P, P, P],
@@ -94,6 +95,7 @@ _KERNEL_SIGS = {
     "dtf_ipc_export": [P, P, P],
     "dtf_ipc_open": [P, P],
     "dtf_ipc_close": [P],
+    "dtf_p2p_allreduce_f32": [P, P, P, P, P, L, I, I, I, I, I, P, P],
     "dtf_memcpy_async": [P, P, L, P],
 }
 

@@ -102,6 +102,17 @@ class GradientBucketer:
         self._next = 0
         self._ready = [False] * len(self.buckets)
         self.enabled = True
+        # small buckets (<= p2p.MAX_BYTES) on one node: the one-shot P2P all-reduce over IPC-mapped peer arenas
+        # instead of RCCL (collective setup: every rank constructs its bucketer at the same point)
+        self.p2p = None
+        self.paths = {"rccl": 0, "p2p": 0}
+        if collective and arena.grad.is_cuda and self.wire == "f32" and type(self) is GradientBucketer:
+            from . import p2p
+            if p2p.available(arena.grad, group) and any((hi - lo) * 4 <= p2p.MAX_BYTES for lo, hi in self.buckets):
+                try:
+                    self.p2p = p2p.P2PAllReducer(arena.grad, group)
+                except (RuntimeError, OSError, ValueError) as e:  # e.g. ranks on several nodes: RCCL only
+                    print(f"[dtf] P2P all-reduce unavailable ({e}); RCCL for every bucket", flush=True)
         self.reset()
 
     def _close(self, var_idx):
@@ -144,6 +155,12 @@ class GradientBucketer:
             self._launch(self._next)
             self._next += 1
 
+    def _use_p2p(self, lo, hi):
+        if self.p2p is None:
+            return False
+        from . import p2p
+        return (hi - lo) * 4 <= p2p.MAX_BYTES and not torch.cuda.is_current_stream_capturing()
+
     def begin_step(self, optimizer, grad_scale):
         """Overlap the optimizer with backward: every bucket is updated (masters, slots, bf16 copies, gradient
         zeroing: one fused launch over the bucket's arena range) as soon as its gradients are final — right after
@@ -163,7 +180,11 @@ class GradientBucketer:
             ctx = collective_ctx(t.device)
         work = None
         with ctx:
-            if self.collective:
+            if self.collective and self._use_p2p(lo, hi):
+                self.p2p.all_reduce_(lo, hi)  # one kernel on the side stream: stream-ordered, no Work to wait on
+                self.paths["p2p"] += 1
+            elif self.collective:
+                self.paths["rccl"] += 1
                 if self.wire == "bf16":
                     if self._wirebuf is None:
                         self._wirebuf = torch.empty(self.arena.grad.numel(), dtype=torch.bfloat16, device=t.device)
@@ -212,6 +233,9 @@ class GradientBucketer:
             for w in self._works:
                 if w is not None:
                     w.wait()  # GPU: the main stream waits for the collective's RCCL stream
+            if self.p2p is not None and self.arena.grad.is_cuda:
+                from ..ops._util import join_side_streams
+                join_side_streams()  # P2P buckets were reduced by kernels on the side stream
             if self.wire == "bf16" and self.collective:
                 for lo, hi in self.buckets:
                     _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])

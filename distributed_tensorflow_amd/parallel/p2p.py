@@ -1,0 +1,114 @@
+"""One-shot peer-to-peer all-reduce of small gradient buckets over IPC-mapped HBM (csrc/kernels/p2p_allreduce.hip).
+
+RCCL's ring/tree all-reduce pays a fixed latency per collective; for the small buckets at the tail of a backward
+pass (the ones whose reduction is exposed after the last gradient lands) every rank instead reads the bucket
+straight from each peer's gradient arena over xGMI — all 7 links of an MI355X at once — and sums it in rank order
+in registers ("custom one-shot P2P all-reduce over IPC-mapped HBM for small buckets"). The
+result is bitwise identical on every rank and equal to the ordered f32 sum x0 + x1 + ... + x_{W-1}.
+
+Setup (collective, once per gradient arena): every rank exports its arena gradient, a same-sized f32 scratch and a
+flag array with HIP IPC handles (dtf_ipc_export); the handles travel through the process group
+(all_gather_object: gloo or RCCL) and every rank maps its peers' buffers. Requirements: all ranks on one node
+(same hostname), at most 8 ranks, CUDA tensors. A call launches ONE kernel on the current stream (stream-ordered
+after the kernels that produced the bucket, before the ones that consume it) with a host-side epoch; every rank
+must issue the same calls in the same order (the bucketer's bucket order guarantees it). Not used under hipGraph
+capture (the epoch is a kernel argument).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+
+from .. import _native
+
+MAX_RANKS = 8
+NBLK = int(os.environ.get("DTF_P2P_BLOCKS", "64"))  # blocks per rank and call
+# buckets up to this size (bytes, f32) take the P2P path when it is available (DTF_P2P_MAX_KB; 0 disables)
+MAX_BYTES = int(float(os.environ.get("DTF_P2P_MAX_KB", "4096")) * 1024)
+TIMEOUT_MS = int(os.environ.get("DTF_P2P_TIMEOUT_MS", "60000"))
+
+
+def _export(t):
+    handle = ctypes.create_string_buffer(64)
+    off = ctypes.c_long()
+    _native.call("dtf_ipc_export", t.data_ptr(), handle, ctypes.addressof(off))
+    return handle.raw.hex(), off.value
+
+
+def _open(handle_hex, offset):
+    ptr = ctypes.c_void_p()
+    _native.call("dtf_ipc_open", bytes.fromhex(handle_hex), ctypes.addressof(ptr))
+    return ptr.value, ptr.value + offset
+
+
+class P2PAllReducer:
+    """Bucket all-reduce over IPC-mapped peer gradient arenas (see module docstring)."""
+
+    def __init__(self, grad, group=None):
+        if grad.device.type != "cuda" or grad.dtype != torch.float32:
+            raise ValueError("P2P all-reduce needs an f32 CUDA gradient arena")
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > MAX_RANKS:
+            raise ValueError(f"P2P all-reduce supports at most {MAX_RANKS} ranks")
+        self.grad = grad
+        dev = grad.device
+        self.red = torch.empty_like(grad)
+        self.flags = torch.zeros(2 * NBLK * MAX_RANKS, dtype=torch.int32, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        mine = {"host": socket.gethostname(), "grad": _export(grad), "flags": _export(self.flags)}
+        allv = [None] * self.world
+        dist.all_gather_object(allv, mine, group=group)
+        if len({v["host"] for v in allv}) != 1:
+            raise RuntimeError("P2P all-reduce needs every rank on one node")
+        self._mapped = []
+        self.grad_ptr = [0] * self.world
+        self.flag_ptr = [0] * self.world
+        for p, v in enumerate(allv):
+            if p == self.rank:
+                self.grad_ptr[p], self.flag_ptr[p] = grad.data_ptr(), self.flags.data_ptr()
+                continue
+            base, g = _open(*v["grad"])
+            self._mapped.append(base)
+            fbase, f = _open(*v["flags"])
+            self._mapped.append(fbase)
+            self.grad_ptr[p], self.flag_ptr[p] = g, f
+        self.epoch = 0
+        self.calls = 0
+
+    def all_reduce_(self, lo, hi):
+        """Sum grad[lo:hi] over the ranks in place (on the current stream)."""
+        n = hi - lo
+        if n <= 0:
+            return
+        self.epoch += 1
+        self.calls += 1
+        srcs = (ctypes.c_void_p * self.world)(*[p + 4 * lo for p in self.grad_ptr])
+        flags = (ctypes.c_void_p * self.world)(*self.flag_ptr)
+        nblk = max(1, min(NBLK, -(-n // (256 * 4 * 4))))  # >= 4 float4 per thread
+        from ..ops._util import stream
+        _native.call("dtf_p2p_allreduce_f32", self.grad.data_ptr() + 4 * lo, srcs, self.red.data_ptr() + 4 * lo,
+                     self.flags.data_ptr(), flags, n, self.world, self.rank, self.epoch, nblk, TIMEOUT_MS,
+                     self.err.data_ptr(), stream(self.grad.device))
+
+    def check(self):
+        """Raise if any call timed out waiting for a peer (synchronises the device)."""
+        if int(self.err.item()):
+            raise RuntimeError("P2P all-reduce timed out waiting for a peer rank")
+
+    def close(self):
+        for base in self._mapped:
+            _native.call("dtf_ipc_close", base)
+        self._mapped = []
+
+
+def available(grad, group=None):
+    """Whether the P2P path can be used for this arena (CUDA f32, <= 8 ranks; node locality is checked at setup)."""
+    return (MAX_BYTES > 0 and grad.is_cuda and grad.dtype == torch.float32 and dist.is_initialized()
+            and 1 < dist.get_world_size(group) <= MAX_RANKS and os.environ.get("DTF_P2P", "1") != "0")
