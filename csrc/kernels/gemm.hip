@@ -281,6 +281,29 @@ static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
 }
 
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8 = 0, int bn = 256);  // gemm256.hip
+int gemm8p_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn);  // gemm8p.hip
+
+// The 8-phase 256-row kernel (gemm8p.hip) for a K-contiguous conv / GEMM: forced by tiles 20 (256x256) and 21
+// (256x128); by default (DTF_G8P, 1 = on) when its tiles fill the chip: 256x256 with >= 256 tiles, else 256x128 with
+// >= 256 tiles. True if launched.
+static int g8p_mode() {
+  static const int m = [] {
+    const char* e = getenv("DTF_G8P");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+static bool try_gemm8p(GemmArgs& a, int am, int bm, int& tile, hipStream_t st) {
+  if (tile == 20 || tile == 21) {
+    if (gemm8p_try(a, am, bm, st, tile == 20 ? 256 : 128) == 0) return true;
+    tile = -1;
+    return false;
+  }
+  if (tile >= 0 || !g8p_mode() || a.atomic_out || a.splitk != 1) return false;
+  const long t256 = (long)cdiv(a.M, 256) * cdiv(a.N, 256) * a.batch, t128 = (long)cdiv(a.M, 256) * cdiv(a.N, 128) * a.batch;
+  const int bn = (a.N >= 256 && t256 >= 256) ? 256 : (a.N >= 128 && t128 >= 256) ? 128 : 0;
+  return bn && gemm8p_try(a, am, bm, st, bn) == 0;
+}
 int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool force);  // conv256.hip
 bool conv256_on();
 
@@ -646,7 +669,7 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
-  if (!try_conv256(a, am, OP_KCONTIG, tile, (hipStream_t)stream)) {
+  if (!try_gemm8p(a, am, OP_KCONTIG, tile, (hipStream_t)stream) && !try_conv256(a, am, OP_KCONTIG, tile, (hipStream_t)stream)) {
     if (tile < 0) tile = pick_glds_tile(a, am, OP_KCONTIG);
     dispatch(a, am, OP_KCONTIG, tile, (hipStream_t)stream);
   }
@@ -805,7 +828,8 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
     int t = tile;
-    if (!try_conv256(a, am, OP_KCONTIG, t, st)) dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
+    if (!try_gemm8p(a, am, OP_KCONTIG, t, st) && !try_conv256(a, am, OP_KCONTIG, t, st))
+      dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
     if (bnrows) *bnrows = bnx ? a.tiles_m : 0;
     return (int)hipGetLastError();
   }
@@ -850,7 +874,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
       const int am = pointwise ? OP_KCONTIG
                      : tap_uniform(K, nkh * nkw, (long)N * P * Q * K) ? OP_DGRAD_T : OP_DGRAD;
       int t = tile;
-      if (!try_conv256(a, am, OP_KCONTIG, t, st))
+      if (!try_gemm8p(a, am, OP_KCONTIG, t, st) && !try_conv256(a, am, OP_KCONTIG, t, st))
         dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
       prow += a.tiles_m;
     }

@@ -29,8 +29,21 @@ namespace dtf {
 namespace {
 
 constexpr int T8 = 512;          // threads: 8 waves
-constexpr int HB = 128 * 128;    // bytes of one half-tile image: 128 rows x 64 bf16
-constexpr int STAGE = 4 * HB;    // A0 | A1 | B0 | B1
+constexpr int HA_BYTES = 128 * 128;  // bytes of one A half-tile image: 128 rows x 64 bf16
+
+// Tile geometry by output width BN: 256 -> 8 waves as 2 (M) x 4 (N), 128x64 per wave, 16 MFMA per phase;
+// 128 -> 4 (M) x 2 (N), 64x64 per wave, 8 MFMA per phase (the ResNet-50 stage-2..4 widths: twice the tiles).
+template <int BN>
+struct Geo8 {
+  static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
+  static constexpr int WTM = 256 / WM, WTN = BN / WN;
+  static constexpr int HA = WTM / 2, HBC = WTN / 2;   // rows (A) / columns (B) of one wave in one half image
+  static constexpr int FA = HA / 16, FB = HBC / 16;   // fragments per wave per half
+  static constexpr int HB_BYTES = BN * 64;            // one B half image: BN/2 rows x 64 bf16
+  static constexpr int STAGE = 2 * HA_BYTES + 2 * HB_BYTES;  // A0 | A1 | B0 | B1
+  static constexpr int UA = 2, UB = HB_BYTES / 8192;  // LDS-DMA instructions per thread per half
+  static constexpr int VM_Q3 = 2 * UB + UA;           // halves of tile t+2 in flight at the q3 wait (B0 A0 B1)
+};
 
 __device__ __forceinline__ void barrier8() {
   asm volatile("" ::: "memory");
@@ -38,19 +51,20 @@ __device__ __forceinline__ void barrier8() {
   asm volatile("" ::: "memory");
 }
 
-// image row r of half h -> row of the 256-row block operand (A: wave-row slices of 64; B: wave-col slices of 32)
-__device__ __forceinline__ int a_blk_row(int r, int h) { return (r >> 6) * 128 + h * 64 + (r & 63); }
-__device__ __forceinline__ int b_blk_row(int r, int h) { return (r >> 5) * 64 + h * 32 + (r & 31); }
+// image row r of half h -> row of the block operand: a wave's S rows (A) / columns (B) of one half are contiguous in
+// the image, the two halves of a wave's 2S interleave in the block
+template <int S>
+__device__ __forceinline__ int blk_row(int r, int h) { return (r / S) * (2 * S) + h * S + (r % S); }
 
 // One operand's two half images. Thread t fills, per half and instruction u (0, 1), image row 64u + 8 wave +
 // (lane >> 3), physical 16-B slot lane & 7, i.e. logical chunk (lane & 7) ^ ((row >> 1) & 7) (the same for every u
 // and half: bits 1..3 of the row come from wave and lane only).
-template <int MODE, bool ISA>
+template <int MODE, int S, int U>  // S: rows of a wave per half (blk_row); U: instructions per half (image rows 64U)
 struct HalfLoad {
   static_assert(MODE == OP_KCONTIG || MODE == OP_IM2COL_T || MODE == OP_DGRAD_T, "K-contiguous modes only");
   __amdgpu_buffer_rsrc_t rsrc;
-  int roff[2][2];
-  uint32_t tmask[2][2];
+  int roff[2][U];
+  uint32_t tmask[2][U];
   int coff;
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot) {
@@ -66,9 +80,9 @@ struct HalfLoad {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int ir = 64 * u + rr;
-        const int r = r0 + (ISA ? a_blk_row(ir, h) : b_blk_row(ir, h));
+        const int r = r0 + blk_row<S>(ir, h);
         uint32_t m = 0;
         int off = 0;
         if (r < Rtot) {
@@ -98,7 +112,7 @@ struct HalfLoad {
       }
   }
 
-  // issue half h of the K-tile starting at k0 into its image at `img` (2 LDS-DMA instructions per thread)
+  // issue half h of the K-tile starting at k0 into its image at `img` (U LDS-DMA instructions per thread)
   __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int h, char* img) {
     const int w = threadIdx.x >> 6;
     int toff;
@@ -114,7 +128,7 @@ struct HalfLoad {
                                  : ((int)c0 - ((int)kh * g.dh * g.Q + (int)kw * g.dw) * g.Kout) * 2;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       const bool ok = (tmask[h][u] >> tap) & 1u;
       const uint32_t off = ok ? (uint32_t)(roff[h][u] + toff + coff) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -128,11 +142,13 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int AM>
+template <int AM, int BN>
 __global__ void __launch_bounds__(T8, 1) gemm8p_kernel(GemmArgs a) {
+  using G = Geo8<BN>;
+  constexpr int STAGE = G::STAGE, FA = G::FA, FB = G::FB;
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / G::WN, wc = wave % G::WN;
 
   // block -> tile: XCD-aware bijective remap, then groups of 4 M-tiles x all N-tiles (shared A rows / B columns)
   const int nwg = a.tiles_m * a.tiles_n;
@@ -146,26 +162,29 @@ __global__ void __launch_bounds__(T8, 1) gemm8p_kernel(GemmArgs a) {
   const int in_g = bid - grp * per_group;
   const int tile_m = first_m + in_g % gsize;
   const int tile_n = in_g / gsize;
-  const int m0 = tile_m * 256, n0 = tile_n * 256;
+  const int m0 = tile_m * 256, n0 = tile_n * BN;
   if (a.zero_slot && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) *a.zero_slot = 0.f;
   const int bz = z / a.splitk, sk = z % a.splitk;
   const int kbeg = sk * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
 
-  HalfLoad<AM, true> la;
-  HalfLoad<OP_KCONTIG, false> lb;
+  HalfLoad<AM, G::HA, G::UA> la;
+  HalfLoad<OP_KCONTIG, G::HBC, G::UB> lb;
   la.init(a, a.A + (long)bz * a.sA, a.lda, m0, a.M);
   lb.init(a, a.B + (long)bz * a.sB, a.ldb, n0, a.N);
 
-  v4f acc[8][4];
+  v4f acc[2 * FA][2 * FB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 2 * FA; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-  v8bf fa[4][2], fb0[2][2], fb1[2][2];
+    for (int j = 0; j < 2 * FB; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  v8bf fa[FA][2], fb0[FB][2], fb1[FB][2];
 
-  auto img = [&](int t, int half) { return smem + (t & 1) * STAGE + half * HB; };  // half: 0 A0 1 A1 2 B0 3 B1
+  // half: 0 A0, 1 A1, 2 B0, 3 B1
+  auto img = [&](int t, int half) {
+    return smem + (t & 1) * STAGE + (half < 2 ? half * HA_BYTES : 2 * HA_BYTES + (half - 2) * G::HB_BYTES);
+  };
   auto issue = [&](int t, int half) {
     if (half < 2) la.issue(a, kbeg + t * BK, half, img(t, half));
     else lb.issue(a, kbeg + t * BK, half - 2, img(t, half));
@@ -173,29 +192,29 @@ __global__ void __launch_bounds__(T8, 1) gemm8p_kernel(GemmArgs a) {
   auto read_a = [&](int t, int h) {
     const char* base = img(t, h);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FA; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag_kcontig(base, wr * 64 + i * 16, kk, lane);
+      for (int kk = 0; kk < 2; ++kk) fa[i][kk] = frag_kcontig(base, wr * G::HA + i * 16, kk, lane);
   };
-  auto read_b = [&](v8bf (&fb)[2][2], int t, int h) {
+  auto read_b = [&](v8bf (&fb)[FB][2], int t, int h) {
     const char* base = img(t, 2 + h);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FB; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag_kcontig(base, wc * 32 + j * 16, kk, lane);
+      for (int kk = 0; kk < 2; ++kk) fb[j][kk] = frag_kcontig(base, wc * G::HBC + j * 16, kk, lane);
   };
-  auto mma = [&](const v8bf (&fb)[2][2], int ha, int hb) {
+  auto mma = [&](const v8bf (&fb)[FB][2], int ha, int hb) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FA; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[ha * 4 + i][hb * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk], fa[i][kk], acc[ha * 4 + i][hb * 2 + j], 0, 0, 0);
+        for (int j = 0; j < FB; ++j)
+          acc[ha * FA + i][hb * FB + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk], fa[i][kk], acc[ha * FA + i][hb * FB + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -205,7 +224,7 @@ __global__ void __launch_bounds__(T8, 1) gemm8p_kernel(GemmArgs a) {
   }
   if (nk > 1) {
     issue(1, 2); issue(1, 0); issue(1, 3);
-    vm_wait<6>();
+    vm_wait<G::VM_Q3>();
   } else {
     vm_wait<0>();
   }
@@ -234,21 +253,32 @@ __global__ void __launch_bounds__(T8, 1) gemm8p_kernel(GemmArgs a) {
     barrier8();
     // q3: A1 x B0 from registers (issue B1 of tile t+2); retire every half of tile t+1 before the barrier
     if (n2) issue(t + 2, 3);
-    if (n2) vm_wait<6>();
+    if (n2) vm_wait<G::VM_Q3>();
     else vm_wait<0>();
     barrier8();
     mma(fb0, 1, 0);
     barrier8();
   }
   __syncthreads();  // (no LDS-DMA in flight: the last tiles drained with vmcnt(0)) the epilogue reuses the LDS
-  gemm_epilogue<256, 256, 2, 4, T8, 2 * STAGE>(a, acc, smem, m0, n0, tile_m, z, bz);
+  gemm_epilogue<256, BN, G::WM, G::WN, T8, 2 * STAGE>(a, acc, smem, m0, n0, tile_m, z, bz);
 }
 
 }  // namespace
 
-// Launch C = A . B^T on the 8-phase kernel when eligible (K-contiguous B, K % 64 == 0 per split, 16-B aligned rows,
-// operands < 2 GiB). Returns 0 if launched, 1 if not eligible.
-int gemm8p_try(GemmArgs& a, int amode, int bmode, hipStream_t st) {
+template <int BN>
+void launch8p(GemmArgs& a, int amode, hipStream_t st) {
+  a.tiles_m = cdiv(a.M, 256);
+  a.tiles_n = cdiv(a.N, BN);
+  prep_fin(a);
+  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
+  if (amode == OP_KCONTIG) hipLaunchKernelGGL((gemm8p_kernel<OP_KCONTIG, BN>), grid, dim3(T8), 0, st, a);
+  else if (amode == OP_IM2COL_T) hipLaunchKernelGGL((gemm8p_kernel<OP_IM2COL_T, BN>), grid, dim3(T8), 0, st, a);
+  else hipLaunchKernelGGL((gemm8p_kernel<OP_DGRAD_T, BN>), grid, dim3(T8), 0, st, a);
+}
+
+// Launch C = A . B^T on the 8-phase kernel with tile width bn (256 or 128) when eligible (K-contiguous B,
+// K % 64 == 0 per split, 16-B aligned rows, operands < 2 GiB). Returns 0 if launched, 1 if not eligible.
+int gemm8p_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn) {
   if (bmode != OP_KCONTIG || a.atomic_out) return 1;
   if (amode != OP_KCONTIG && amode != OP_IM2COL_T && amode != OP_DGRAD_T) return 1;
   if (a.kchunk % BK || (a.K % BK) || (a.lda & 7) || (a.ldb & 7)) return 1;
@@ -259,13 +289,9 @@ int gemm8p_try(GemmArgs& a, int amode, int bmode, hipStream_t st) {
   if (amode == OP_IM2COL_T && !fits((long)g.N * g.H * g.W * g.C)) return 1;
   if (amode == OP_DGRAD_T && !fits((long)g.N * g.P * g.Q * g.Kout)) return 1;
   if (!fits((long)a.N * a.ldb)) return 1;
-  a.tiles_m = cdiv(a.M, 256);
-  a.tiles_n = cdiv(a.N, 256);
-  prep_fin(a);
-  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
-  if (amode == OP_KCONTIG) hipLaunchKernelGGL(gemm8p_kernel<OP_KCONTIG>, grid, dim3(T8), 0, st, a);
-  else if (amode == OP_IM2COL_T) hipLaunchKernelGGL(gemm8p_kernel<OP_IM2COL_T>, grid, dim3(T8), 0, st, a);
-  else hipLaunchKernelGGL(gemm8p_kernel<OP_DGRAD_T>, grid, dim3(T8), 0, st, a);
+  if (bn == 256) launch8p<256>(a, amode, st);
+  else if (bn == 128) launch8p<128>(a, amode, st);
+  else return 1;
   return 0;
 }
 
@@ -273,12 +299,12 @@ int gemm8p_try(GemmArgs& a, int amode, int bmode, hipStream_t st) {
 
 // Direct entry for benchmarks/tests: C[M][N] (bf16 or f32) = A[M][K] . B[N][K]^T on the 8-phase kernel.
 DTF_API int dtf_gemm8p(const void* A, const void* B, void* C, int M, int N, int K, long lda, long ldb, long ldc,
-                       int out_f32, void* stream) {
+                       int out_f32, int bn, void* stream) {
   dtf::GemmArgs a{};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = C;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.batch = 1; a.splitk = 1; a.kchunk = K; a.alpha = 1.f; a.beta = 0.f; a.out_f32 = out_f32;
   if ((N & 3) || (K % dtf::BK)) return -1;
-  if (dtf::gemm8p_try(a, dtf::OP_KCONTIG, dtf::OP_KCONTIG, (hipStream_t)stream)) return -2;
+  if (dtf::gemm8p_try(a, dtf::OP_KCONTIG, dtf::OP_KCONTIG, (hipStream_t)stream, bn)) return -2;
   return (int)hipGetLastError();
 }

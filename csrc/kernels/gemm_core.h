@@ -823,9 +823,9 @@ __device__ __forceinline__ float4 fin_sum_rows(const GemmArgs& a, const float* b
 #pragma unroll
       for (int u = 0; u < 4; ++u) { s[u].x += v[u].x; s[u].y += v[u].y; s[u].z += v[u].z; s[u].w += v[u].w; }
     }
-    for (int u = 0; r < cnt; r += TPI, ++u) {
+    for (; r < cnt; r += TPI) {  // (static index: a runtime-indexed s[] would live in scratch)
       const float4 v = ld_wt4(p + (long)r * stride);
-      s[u & 3].x += v.x; s[u & 3].y += v.y; s[u & 3].z += v.z; s[u & 3].w += v.w;
+      s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
     }
   }
   float4 t;
