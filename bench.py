@@ -148,6 +148,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         logs = step()
+    t_issue = time.perf_counter() - t0  # host time to issue the K steps (the GPU may still be running)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -210,6 +211,9 @@ def main():
                            # all-reduce over IPC-mapped peer arenas for buckets <= DTF_P2P_MAX_KB (parallel/p2p.py)
                            allreduce_paths=_paths(bucketers),
                            forced_collective=os.environ.get("DTF_FORCE_COLLECTIVE", "0") == "1"),
+            # host time spent issuing a step (Python + launches); close to ms_per_step = the host, not the GPU, paces
+            # the run (what hipGraph capture, bench.py --graph 1, removes)
+            "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
             "rccl_world": rccl_world,
             "allreduce_busbw_GBps": ar_sweep,
             "process_group_backend": backend,

@@ -560,14 +560,7 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
   }
   if (stats && (a.batch > 1 || a.splitk > 1)) return -7;
   // large K-contiguous problems: the 256x256 glds-pipelined kernel when it fills the chip
-  // GEMMs with a memory-heavy epilogue (pre-activation side output, fused activation derivative): 1 block/CU
-  // 256x256 tiles cannot overlap one tile's store pass with another's main loop, the 2-block/CU 128x128 tiles can
-  static const int epi256 = [] {  // DTF_G256_EPI=0: keep those GEMMs on the 128x128 kernel
-    const char* e = getenv("DTF_G256_EPI");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  const bool heavy_epi = a.aux != nullptr || a.dact != 0;
-  const int bn256 = (tile < 0 && !stats && a.splitk == 1 && (epi256 || !heavy_epi)) ? pick256(M, N, K, a.batch) : 0;
+  const int bn256 = (tile < 0 && !stats && a.splitk == 1) ? pick256(M, N, K, a.batch) : 0;
   if (bn256 && gemm256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream,
                            0, bn256) == 0)
     return (int)hipGetLastError();

@@ -150,106 +150,6 @@ __device__ __forceinline__ void bn_bwd_finalize_channel(int c, int C, float sdz,
   coef[2 * C + c] = k1 * (mean[c] * is * k3 - k2);
 }
 
-// Partial-row reduction and per-channel finalize in ONE launch: block (x, g) sums rows [g*sg, (g+1)*sg) of
-// the 64 channels [64x, 64x+64) (both the [0,C) and [C,2C) halves) into the group's leader row; the last-
-// arriving group of channel block x sums the leader rows in order (deterministic) and finalizes.
-// Thread layout: 32 float4 columns (16 channel quads of each half) x 8 row lanes; every thread keeps up to
-// 8 independent 16-B loads in flight, so a pass over ~sqrt(T) rows is one or two memory latencies.
-constexpr int RF_LANES = 8;
-
-template <bool BWD>
-__global__ void __launch_bounds__(256) bn_reduce_finalize_kernel(float* __restrict__ part, int T, long rs, int sg,
-                                                                 int C, long M, const float* __restrict__ gamma,
-                                                                 const float* __restrict__ beta_or_mean,
-                                                                 float* rm_or_invstd, float* running_var,
-                                                                 float momentum, float eps, float* o0, float* o1,
-                                                                 float* o2, float* o3, int accumulate, int* tickets) {
-  __shared__ float4 red[RF_LANES][32];
-  __shared__ int flag;
-  const int col = threadIdx.x & 31, lane = threadIdx.x >> 5;
-  const int c = blockIdx.x * 64 + (col & 15) * 4;     // first channel of this thread's quad
-  const long off = (col < 16 ? 0 : C) + c;            // sum half / sum-of-squares half
-  const bool cv = c < C;
-  // sum rows r0 + lane, r0 + lane + 8, ... < r1 with row stride `stride` (in rows of rs floats)
-  // wt: the rows were written by other blocks of THIS launch (write-through hand-off, common.h last_arriver): sc1 loads
-  auto sweep = [&](int r0, int r1, long stride, bool wt) {
-    float4 acc[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (cv) {
-      int r = r0 + lane;
-      for (; r + 7 * RF_LANES < r1; r += 8 * RF_LANES) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float* p = part + (long)(r + u * RF_LANES) * stride * rs + off;
-          v[u] = wt ? ld_wt4(p) : *reinterpret_cast<const float4*>(p);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          acc[u & 3].x += v[u].x; acc[u & 3].y += v[u].y; acc[u & 3].z += v[u].z; acc[u & 3].w += v[u].w;
-        }
-      }
-      for (int u = 0; r < r1; r += RF_LANES, ++u) {
-        const float* p = part + (long)r * stride * rs + off;
-        const float4 v = wt ? ld_wt4(p) : *reinterpret_cast<const float4*>(p);
-        acc[u & 3].x += v.x; acc[u & 3].y += v.y; acc[u & 3].z += v.z; acc[u & 3].w += v.w;
-      }
-    }
-    float4 t;
-    t.x = (acc[0].x + acc[1].x) + (acc[2].x + acc[3].x);
-    t.y = (acc[0].y + acc[1].y) + (acc[2].y + acc[3].y);
-    t.z = (acc[0].z + acc[1].z) + (acc[2].z + acc[3].z);
-    t.w = (acc[0].w + acc[1].w) + (acc[2].w + acc[3].w);
-    red[lane][col] = t;
-    __syncthreads();
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lane == 0) {
-#pragma unroll
-      for (int l = 0; l < RF_LANES; ++l) {
-        const float4 q = red[l][col];
-        s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
-      }
-    }
-    return s;
-  };
-  const int r0 = blockIdx.y * sg, r1 = min(T, r0 + sg);
-  const float4 grp = sweep(r0, r1, 1, false);
-  if (lane == 0 && cv) {
-    float* p = part + (long)r0 * rs + off;
-    st_wt(p, grp.x); st_wt(p + 1, grp.y); st_wt(p + 2, grp.z); st_wt(p + 3, grp.w);
-  }
-  if (!last_arriver(tickets + blockIdx.x, gridDim.y, &flag)) return;
-  const float4 tot = sweep(0, gridDim.y, sg, true);  // the leader rows: row g*sg
-  __syncthreads();
-  if (lane == 0) red[0][col] = tot;
-  __syncthreads();
-  if (threadIdx.x >= 16 || !cv) return;
-  const float4 a = red[0][threadIdx.x], b = red[0][threadIdx.x + 16];
-  const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if constexpr (BWD)
-      bn_bwd_finalize_channel(c + j, C, av[j], bv[j], gamma, beta_or_mean, rm_or_invstd, M, o0, o1, accumulate, o2);
-    else
-      bn_finalize_channel(c + j, av[j], bv[j], gamma, beta_or_mean, rm_or_invstd, running_var, M, momentum, eps, o0,
-                          o1, o2, o3);
-  }
-}
-
-// groups for bn_reduce_finalize_kernel: about sqrt(T) rows per group and sqrt(T) groups (<= 128), so both the
-// group pass and the leader-row pass are ~sqrt(T)/8 loads per thread
-static inline int bn_groups(int T, int* sg) {
-  static const int gmax = [] {
-    const char* e = getenv("DTF_BN_GROUPS");  // tuning knob: fixed group cap instead of the sqrt rule
-    return e ? atoi(e) : 0;
-  }();
-  int G = gmax > 0 ? std::min(gmax, (T + 31) / 32) : (int)std::sqrt((double)T);
-  G = std::min(128, std::max(1, G));
-  *sg = (T + G - 1) / G;
-  return (T + *sg - 1) / *sg;
-}
-
 // Inference: scale/shift from running statistics.
 __global__ void bn_infer_coeff_kernel(const float* gamma, const float* beta, const float* rmean,
                                       const float* rvar, int C, float eps, float* scale, float* shift) {
@@ -977,9 +877,6 @@ int red_grid(long M, int C) {
   return (int)blocks;
 }
 
-// BN statistic reduce + finalize as ONE launch (last-arriver hand-off) or two (group pass, finalize pass):
-// the agent-scope fences of the one-launch form cost more than the second launch boundary, mostly in the backward
-// where the side-stream weight gradients keep the CUs busy. DTF_BN_ONE_LAUNCH=1 selects the one-launch form.
 // leader rows left by the first (grouping) pass of a BN statistics reduction, which the finalize kernel then sums:
 // the grouping pass runs one block per leader row (more rows = more blocks reading the partials in parallel)
 static int bn_group_target() {
@@ -988,14 +885,6 @@ static int bn_group_target() {
     return e ? std::max(1, atoi(e)) : 32;
   }();
   return t;
-}
-
-static bool bn_one_launch() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_BN_ONE_LAUNCH");  // two launches measured 1.9 % faster on ResNet-50 (b256)
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 // Elementwise passes that consume a GEMM output sweep the rows last-to-first: the GEMM wrote them first-to-last,
@@ -1050,17 +939,6 @@ DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float*
                             float* running_var, long M, int C, float momentum, float eps, float* scale,
                             float* shift, float* mean_out, float* invstd_out, void* stream) {
   long rs = 2L * C;
-  {
-    int sg = 0;
-    const int G = bn_groups(T, &sg);
-    int* tk = bn_one_launch() ? dtf_tickets(cdiv(C, 64)) : nullptr;
-    if (tk) {
-      hipLaunchKernelGGL((bn_reduce_finalize_kernel<false>), dim3(cdiv(C, 64), G), dim3(256), 0,
-                         (hipStream_t)stream, part, T, rs, sg, C, M, gamma, beta, running_mean, running_var, momentum,
-                         eps, scale, shift, mean_out, invstd_out, 0, tk);
-      return (int)hipGetLastError();
-    }
-  }
   T = dtf_group_rows_once(part, rs, T, 2L * C, bn_group_target(), &rs, stream);  // <= target leader rows, one launch
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, T, rs, gamma,
                      beta,
@@ -1151,20 +1029,11 @@ DTF_API int dtf_bn_bwd_apply_coef(const void* dy, const void* mbits, const void*
 }
 
 // Sum the G partial rows [G][2C] of a BN backward reduction and finalize: dgamma/dbeta and the apply
-// coefficients `coef` (3*C floats). One launch (last-arriver hand-off) when tickets are available.
+// coefficients `coef` (3*C floats): a grouping launch, then the finalize launch.
 static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const float* invstd, const float* gamma,
                                    long M, int C, float* dgamma, float* dbeta, int accumulate, float* coef,
                                    hipStream_t st) {
   long rs = 2L * C;
-  int sg = 0;
-  const int G2 = bn_groups(G, &sg);
-  int* tk = bn_one_launch() ? dtf_tickets(cdiv(C, 64)) : nullptr;
-  if (tk) {
-    hipLaunchKernelGGL((bn_reduce_finalize_kernel<true>), dim3(cdiv(C, 64), G2), dim3(256), 0, st, part, G, rs, sg,
-                       C, M, gamma, mean, const_cast<float*>(invstd), nullptr, 0.f, 0.f, dgamma, dbeta, coef, nullptr,
-                       accumulate, tk);
-    return;
-  }
   int T = dtf_group_rows_once(part, rs, G, 2L * C, bn_group_target(), &rs, (void*)st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, mean, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);

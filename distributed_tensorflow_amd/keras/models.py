@@ -263,10 +263,6 @@ class Model(Layer):
         dev = self._device()
         if dev.type == "cuda":
             advance_rng(dev)  # fresh dropout masks for this step, also under hipGraph replay
-            fl = self._fp8_layers()
-            if fl:  # this step's fp8 weight copies, quantized ahead on their own stream (ops.fp8)
-                from ..ops.fp8 import prequantize_weights
-                prequantize_weights(fl, dev)
         with prof.phase("forward"):
             y_pred = self(x, training=True)
             loss = self.compute_loss(x, y, y_pred, sw)
@@ -282,23 +278,6 @@ class Model(Layer):
         with prof.phase("optimizer"):
             strat.apply_gradients(self.optimizer, arena)
         return self._update_metrics(loss, y, y_pred)
-
-    def _fp8_layers(self):
-        """Built sublayers with fp8 projections (cached once the model is built)."""
-        fl = self.__dict__.get("_fp8_cache")
-        if fl is None:
-            out = []
-
-            def rec(layer):
-                if getattr(layer, "fp8", False) and getattr(layer, "built", False) and hasattr(layer, "kernel"):
-                    out.append(layer)
-                for c in layer._layers:
-                    rec(c)
-            rec(self)
-            fl = out
-            if self._fully_built():
-                object.__setattr__(self, "_fp8_cache", fl)
-        return fl
 
     def make_train_function(self, force=False):
         """The per-batch step fit() drives. With ``compile(jit_compile=True)`` on one GPU rank it is a

@@ -113,7 +113,6 @@ class _Fp8State:
         self.w_key = None
         # fp8 operands written by the neighbouring layer's GEMM epilogue (gemm256.hip q8 outputs), matched by the
         # data pointer of the placeholder that stands for the bf16 tensor nobody wrote:
-        self.w_event = None    # prequantize_weights: the weight copies are ready when this event has completed
         self.pending_x = None  # (ptr, xq, xqT, amax slot to clear, producer state, producer pre, producer act)
         self.pending_g = None  # (ptr, dzq, dzqT, column-sum partials, amax slot to clear)
 
@@ -129,9 +128,6 @@ def _state(layer, dev):
 def _weight_fp8(st, w, need_t):
     key = (weights_epoch(), w._version, need_t)
     if st.wq is not None and st.w_key == key:
-        ev, st.w_event = st.w_event, None
-        if ev is not None:  # quantized ahead on the prequantize stream (prequantize_weights)
-            torch.cuda.current_stream(w.device).wait_event(ev)
         return st.wq, st.wqT
     w16 = bf16_shadow(w)
     N, K = w16.shape
@@ -159,42 +155,6 @@ def _weight_fp8(st, w, need_t):
         st.wqT = None
     st.w_key = key
     return st.wq, st.wqT
-
-
-# Weight quantization ahead of the forward (DTF_FP8_PREQUANT=1, opt-in): at the start of a train step every fp8
-# layer's W / W^T pass (one launch each, the step's weights are final once the previous update ran) is issued on its
-# own stream, so the ~100 weight passes of GPT-2-medium leave the critical stream and overlap the first layers'
-# forward; each layer's forward waits only for its own weight's event. Skipped while capturing a hipGraph and for
-# layers whose scale is not bootstrapped yet (their first forward quantizes inline, as before). Bit-identical to the
-# inline passes, but measured 4% SLOWER on GPT-2-medium fp8 (36.65 vs 35.16 ms/step, profiles/): the 96 passes
-# issued at once compete with the first layers' GEMMs instead of filling gaps.
-_PREQ = os.environ.get("DTF_FP8_PREQUANT", "0") == "1"
-_PREQ_STREAMS = {}
-
-
-def prequantize_weights(layers, device):
-    if not _PREQ or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
-        return 0
-    todo = [lay for lay in layers if getattr(lay, "_fp8", None) is not None and lay._fp8.w_ready
-            and getattr(lay, "built", False)]
-    if not todo:
-        return 0
-    main = torch.cuda.current_stream(device)
-    s = _PREQ_STREAMS.get(device.index)
-    if s is None:
-        s = _PREQ_STREAMS[device.index] = torch.cuda.Stream(device=device)
-    s.wait_stream(main)
-    with torch.cuda.stream(s):
-        for lay in todo:
-            st = lay._fp8
-            wq, wqT = _weight_fp8(st, lay.kernel, True)
-            for t in (wq, wqT):
-                if t is not None:
-                    t.record_stream(main)
-            ev = torch.cuda.Event()
-            ev.record(s)
-            st.w_event = ev
-    return len(todo)
 
 
 def _fp8_bwd_ok(M, K, N):
