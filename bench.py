@@ -155,6 +155,16 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     exposed = [b.exposed_ms() for b in bucketers if hasattr(b, "exposed_ms")]
+    # after the timed region: the host time to issue ONE step into an idle GPU queue (min of 3). In the timed loop
+    # the host is throttled by the queue once it runs ahead, so its issue time there equals the GPU time either way;
+    # this one says whether Python + launches alone would keep up with the GPU.
+    single = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        logs = step()
+        single.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
     exposed = [e for e in exposed if e is not None]
     loss = float(logs["loss"])
     # proof that the N replicas trained in lock step: an exact checksum of every trainable f32 master (the bit
@@ -214,6 +224,7 @@ def main():
             # host time spent issuing a step (Python + launches); close to ms_per_step = the host, not the GPU, paces
             # the run (what hipGraph capture, bench.py --graph 1, removes)
             "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
+            "host_issue_ms_single_step": round(min(single) * 1e3, 3),
             "rccl_world": rccl_world,
             "allreduce_busbw_GBps": ar_sweep,
             "process_group_backend": backend,

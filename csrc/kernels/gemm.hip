@@ -306,6 +306,8 @@ static bool try_gemm8p(GemmArgs& a, int am, int bm, int& tile, hipStream_t st) {
 }
 int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool force);  // conv256.hip
 bool conv256_on();
+int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int C, int K, hipStream_t st);  // pwconv.hip
+bool pwconv_on();
 
 // The 256-row pipelined LDS-DMA kernel (conv256.hip) for a convolution GEMM: forced by tiles 11-14 (variant
 // tile - 11, see conv256.hip launch_cfg); by default whenever it is eligible and fills the chip. True if launched.
@@ -651,6 +653,16 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
       return rc;
     }
   }
+  const bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  if (pointwise && stats && !bias && !act && !out_f32 && (tile < 0 || tile == 30) && pwconv_on()) {
+    // channel-expanding 1x1 layers: the persistent register-resident-filter kernel (pwconv.hip); the BN finalize
+    // then runs as its own launch over its <= 256 partial rows
+    const int rows = pwconv_try(X, Wt, Y, stats, (long)N * P * Q, C, K, (hipStream_t)stream);
+    if (rows > 0) {
+      if (stat_rows) *stat_rows = rows;
+      return (int)hipGetLastError();
+    }
+  }
   GemmArgs a{};
   if (fin && stats) a.fin = *fin;
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
@@ -660,7 +672,6 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
   a.lda = C; a.ldb = (long)R * S * C; a.ldc = K;
   a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
-  bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
   const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
   if (!try_gemm8p(a, am, OP_KCONTIG, tile, (hipStream_t)stream) && !try_conv256(a, am, OP_KCONTIG, tile, (hipStream_t)stream)) {
     if (tile < 0) tile = pick_glds_tile(a, am, OP_KCONTIG);

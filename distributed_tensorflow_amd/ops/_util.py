@@ -1,6 +1,8 @@
 """Small helpers shared by the op wrappers."""
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from .. import _native
@@ -81,16 +83,55 @@ def reserve_streams(device):
         side_stream(device)
 
 
+# Gradients parked on a ResidualGradLink are overwritten IN PLACE later in the same backward (the first conv / dense
+# of the branch accumulates its data gradient into them). A side-stream weight gradient that reads such a tensor
+# (GPT-2: the FFN2 / attention-output projection's dW and bias reduce read the block-output gradient) must have run
+# before that overwrite: fork_side records an event after those side kernels and ResidualGradLink.take makes the
+# overwriting stream wait on it (before_overwrite). Without it the overwrite raced the side reads whenever the side
+# stream ran late (P2P bucket kernels waiting on a peer rank there; hipGraph replay).
+_PARKED = set()      # storage pointers of parked gradients
+_SIDE_READS = {}     # storage pointer -> event on the side stream after the kernels that read it
+
+
+def _sptr(t):
+    return t.untyped_storage().data_ptr()
+
+
+def mark_parked(t):
+    if t is not None and t.is_cuda:
+        _PARKED.add(_sptr(t))
+
+
+def before_overwrite(t):
+    """The current stream waits for the side-stream kernels that read `t` (fork_side) before t is overwritten."""
+    if t is None or not t.is_cuda:
+        return
+    p = _sptr(t)
+    _PARKED.discard(p)
+    ev = _SIDE_READS.pop(p, None)
+    if ev is not None:
+        torch.cuda.current_stream(t.device).wait_event(ev)
+
+
+@contextlib.contextmanager
 def fork_side(device, *tensors):
-    """Make the side stream wait for the main stream's work so far; the tensors it reads stay allocated until
-    the side stream is done with them. Returns the stream context to issue side work in."""
+    """Issue side-stream work: the side stream first waits for the main stream's work so far; the tensors it reads
+    stay allocated until the side stream is done with them, and parked gradients among them are protected from
+    their in-place overwrite (before_overwrite)."""
     side = side_stream(device)
     side.wait_stream(torch.cuda.current_stream(device))
     for t in tensors:
         if t is not None:
             t.record_stream(side)
     _SIDE_USED.add(device.index)
-    return torch.cuda.stream(side)
+    with torch.cuda.stream(side):
+        yield side
+    watch = [t for t in tensors if t is not None and _PARKED and _sptr(t) in _PARKED]
+    if watch:
+        ev = torch.cuda.Event()
+        ev.record(side)
+        for t in watch:
+            _SIDE_READS[_sptr(t)] = ev
 
 
 def collective_ctx(device):
@@ -169,6 +210,8 @@ def join_update_stream(device):
 
 def join_side_streams():
     """Main stream waits for every side-stream weight gradient issued so far."""
+    _SIDE_READS.clear()
+    _PARKED.clear()
     if not _SIDE_USED:
         return
     for idx in list(_SIDE_USED):

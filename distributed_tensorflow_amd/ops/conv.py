@@ -11,8 +11,8 @@ from __future__ import annotations
 
 import torch
 
-from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, bf16_shadow, call, crsk_shadow, direct_grad, fork_side,
-                    on_gpu, ptr, stream, workspace)
+from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, before_overwrite, bf16_shadow, call, crsk_shadow, direct_grad,
+                    fork_side, mark_parked, on_gpu, ptr, stream, workspace)
 
 
 def out_size(h, k, s, p, d=1):
@@ -205,6 +205,7 @@ class ResidualGradLink:
             assert not compact, "a compact gradient can only be parked on an open link"
             return g
         self.buf, self.mask, self.compact = g, mask, compact
+        mark_parked(g)
         return None
 
     def take(self):
@@ -215,6 +216,8 @@ class ResidualGradLink:
         self.compact = False
         if buf is None:
             self.closed = True
+        else:
+            before_overwrite(buf)  # side-stream readers of the parked gradient finish first
         return buf, mask, compact
 
 

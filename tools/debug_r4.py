@@ -34,19 +34,33 @@ def capture(variant):
     torch.manual_seed(0)
     xs = [torch.randn(8, 3, 64, 64, device=cuda) for _ in range(6)]
     ys = [torch.randint(0, 16, (8,), device=cuda) for _ in range(6)]
-    outs = []
+    outs, snaps = [], []
     for jit in (False, True):
         model = _small_resnet(7)
         o = optimizers.SGD(0.05, momentum=0.9)
         model.compile(optimizer=o, loss=losses.SparseCategoricalCrossentropy(from_logits=True), jit_compile=jit)
         fn = model.make_train_function(force=True)
-        ls = [float(fn((x, y))["loss"]) for x, y in zip(xs, ys)]
-        torch.cuda.synchronize()
+        ls, sn = [], []
+        for x, y in zip(xs, ys):
+            ls.append(float(fn((x, y))["loss"]))
+            torch.cuda.synchronize()
+            sn.append([(w.name, w.detach().float().cpu().clone()) for w in model.weights])
         outs.append(ls)
+        snaps.append(sn)
         S.get_strategy()._bucketers.clear()
     print(variant, "eager", [round(v, 4) for v in outs[0]], flush=True)
     print(variant, "graph", [round(v, 4) for v in outs[1]], flush=True)
     print(variant, "MATCH" if all(abs(a - b) < 1e-3 for a, b in zip(*outs)) else "DIFF", flush=True)
+    for step, (a, b) in enumerate(zip(*snaps)):
+        bad = []
+        for (n, wa), (_, wb) in zip(a, b):
+            d = float((wa - wb).abs().max())
+            if d > 1e-6 + 1e-3 * float(wa.abs().max()):
+                bad.append((d, n))
+        bad.sort(reverse=True)
+        print(f"  after step {step + 1}: {len(bad)}/{len(a)} tensors differ; first in model order: "
+              f"{[n for _, n in sorted(bad, key=lambda t: [w[0] for w in a].index(t[1]))[:4]]} worst {bad[:3]}",
+              flush=True)
 
 
 def _port():

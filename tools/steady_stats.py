@@ -21,6 +21,15 @@ import csv
 
 def load(path):
     rows = []
+    if path.endswith(".db"):  # rocprofv3's default rocpd (SQLite) output
+        import sqlite3
+        c = sqlite3.connect(path)
+        q = ("select d.start, d.end, s.display_name, d.stream_id, d.queue_id from rocpd_kernel_dispatch d "
+             "join rocpd_info_kernel_symbol s on d.kernel_id = s.id")
+        for st, en, name, sid, qid in c.execute(q):
+            rows.append((int(st), int(en), name, str(sid if sid is not None else qid)))
+        rows.sort()
+        return rows
     for r in csv.DictReader(open(path)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                      r.get("Stream_Id") or r.get("Queue_Id") or "0"))
