@@ -203,7 +203,13 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
   if (tiles_n != 1 && tiles_n != 2 && tiles_n != 4 && tiles_n != 8) return 0;
   if (M * C * 2 >= (1l << 31) || M * K * 2 >= (1l << 31)) return 0;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 15)) return 0;
-  const int wmw = C == 256 ? 1 : 2;  // C 256: the 128-VGPR filter slice leaves room for one wave per SIMD
+  // C 256: the 128-VGPR filter slice leaves room for one wave per SIMD; C 64 / 128: two row waves per block, or
+  // (DTF_PW_BPC = 2 or 3, C 64 only) several one-row-wave blocks per CU
+  static const int bpc = [] {
+    const char* e = getenv("DTF_PW_BPC");
+    return e ? std::max(1, std::min(3, atoi(e))) : 1;
+  }();
+  const int wmw = (C == 256 || (C == 64 && bpc > 1)) ? 1 : 2;
   const int bm = 64 * wmw;
   PwArgs a{};
   a.X = (const bf16_t*)X; a.W = (const bf16_t*)W; a.Y = (bf16_t*)Y; a.stats = stats;
@@ -211,12 +217,14 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
   a.tiles_m = (int)((M + bm - 1) / bm);
   a.tiles_n = tiles_n;
   if (a.tiles_m < 8) return 0;
-  // one block per CU; fewer when there are fewer tiles (grid stays a multiple of 8 * tiles_n, and the partial rows
-  // (one per row slot) never outnumber the M-tiles: the caller's scratch holds ceil(M/64) rows)
-  int grid = 256;
+  // one block per CU (or bpc); fewer when there are fewer tiles (grid stays a multiple of 8 * tiles_n, and the
+  // partial rows (one per row slot) never outnumber the M-tiles: the caller's scratch holds ceil(M/64) rows)
+  int grid = 256 * (wmw == 1 && C == 64 ? bpc : 1);
   while (grid > 8 * tiles_n && grid / tiles_n > a.tiles_m) grid /= 2;
   a.nslots = grid / tiles_n;
-  if (C == 64) launch_pw<64, 2>(a, grid, st);
+  if (a.nslots > a.tiles_m && a.nslots > 8) return 0;
+  if (C == 64 && wmw == 1) launch_pw<64, 1>(a, grid, st);
+  else if (C == 64) launch_pw<64, 2>(a, grid, st);
   else if (C == 128) launch_pw<128, 2>(a, grid, st);
   else launch_pw<256, 1>(a, grid, st);
   return hipGetLastError() == hipSuccess ? a.nslots : 0;
@@ -224,7 +232,7 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
 
 }  // namespace dtf
 
-// Test / tuning entry: the pointwise forward on its own (stats: [nslots][2K] floats, nslots <= 256).
+// Test / tuning entry: the pointwise forward on its own (stats: [nslots][2K] floats, nslots <= ceil(M/64)).
 DTF_API int dtf_pwconv_fwd(const void* X, const void* W, void* Y, float* stats, int* rows, long M, int C, int K,
                            void* stream) {
   const int r = dtf::pwconv_try(X, W, Y, stats, M, C, K, (hipStream_t)stream);

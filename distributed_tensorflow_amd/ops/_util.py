@@ -113,25 +113,43 @@ def before_overwrite(t):
         torch.cuda.current_stream(t.device).wait_event(ev)
 
 
+# Tensors read by side-stream work stay REFERENCED until that work has run. Autograd sums the gradients of a
+# tensor with several consumers IN PLACE into the first-arrived gradient when it holds the only reference to its
+# storage (torch InputBuffer::accumulate): e.g. a residual add's backward hands the same dy to the branch (whose
+# weight gradient reads it on the side stream) and to the shortcut, where the other branch's gradient is then added
+# into dy on the main stream. With a second reference held here autograd adds out of place instead. Entries are
+# dropped once their event completed (eager; polled at every fork) or when the main stream joins the side stream.
+_SIDE_HOLD = []      # (event recorded after the side work, tensors it reads)
+
+
+def _release_side_holds():
+    if not _SIDE_HOLD or torch.cuda.is_current_stream_capturing():
+        return
+    keep = [h for h in _SIDE_HOLD if not h[0].query()]
+    _SIDE_HOLD[:] = keep
+
+
 @contextlib.contextmanager
 def fork_side(device, *tensors):
     """Issue side-stream work: the side stream first waits for the main stream's work so far; the tensors it reads
-    stay allocated until the side stream is done with them, and parked gradients among them are protected from
-    their in-place overwrite (before_overwrite)."""
+    stay allocated AND referenced until the side stream is done with them (see _SIDE_HOLD), and parked gradients
+    among them are protected from their in-place overwrite (before_overwrite)."""
+    _release_side_holds()
     side = side_stream(device)
     side.wait_stream(torch.cuda.current_stream(device))
-    for t in tensors:
-        if t is not None:
-            t.record_stream(side)
+    held = [t for t in tensors if t is not None]
+    for t in held:
+        t.record_stream(side)
     _SIDE_USED.add(device.index)
     with torch.cuda.stream(side):
         yield side
-    watch = [t for t in tensors if t is not None and _PARKED and _sptr(t) in _PARKED]
-    if watch:
-        ev = torch.cuda.Event()
-        ev.record(side)
-        for t in watch:
-            _SIDE_READS[_sptr(t)] = ev
+    ev = torch.cuda.Event()
+    ev.record(side)
+    _SIDE_HOLD.append((ev, held))
+    if _PARKED:
+        for t in held:
+            if _sptr(t) in _PARKED:
+                _SIDE_READS[_sptr(t)] = ev
 
 
 def collective_ctx(device):
@@ -213,10 +231,12 @@ def join_side_streams():
     _SIDE_READS.clear()
     _PARKED.clear()
     if not _SIDE_USED:
+        _SIDE_HOLD.clear()
         return
     for idx in list(_SIDE_USED):
         torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
     _SIDE_USED.clear()
+    _SIDE_HOLD.clear()  # the main stream is ordered after every side read now
 
 
 def stream(device=None):

@@ -30,6 +30,16 @@ def capture(variant):
     S._OVERLAP_CAPTURE = True
     if variant == "upd_main":
         _util.update_stream_ctx = lambda device, extra_wait=None: contextlib.nullcontext()
+    if variant == "defer":  # every bucket update after backward (finalize), none during it
+        from distributed_tensorflow_amd.parallel import collective
+        collective.GradientBucketer._launch_ready = lambda self: None
+    if variant == "sync_upd":  # the update stream also waits for EVERYTHING on main before each bucket update
+        real = _util.update_stream_ctx
+
+        def ctx(device, extra_wait=None):
+            torch.cuda.current_stream(device).wait_stream(_util.side_stream(device))
+            return real(device, extra_wait)
+        _util.update_stream_ctx = ctx
     cuda = torch.device("cuda:0")
     torch.manual_seed(0)
     xs = [torch.randn(8, 3, 64, 64, device=cuda) for _ in range(6)]
@@ -97,15 +107,25 @@ def _worker(rank, world, port, mode, q):
         import torch.distributed as dist
         from distributed_tensorflow_amd import parallel
         from distributed_tensorflow_amd.parallel import p2p
-        if mode == "p2p_sync":
-            orig = p2p.P2PAllReducer.all_reduce_
+        orig = p2p.P2PAllReducer.all_reduce_
+        from distributed_tensorflow_amd.ops import _util
 
-            def synced(self, lo, hi):
+        def wrapped(self, lo, hi):
+            if mode in ("p2p_sync", "p2p_before"):
                 torch.cuda.synchronize()
+            if mode in ("p2p_sync", "p2p_barrier"):
                 dist.barrier()
-                orig(self, lo, hi)
+            orig(self, lo, hi)
+            if mode == "p2p_sync":
                 torch.cuda.synchronize()
-            p2p.P2PAllReducer.all_reduce_ = synced
+            if mode == "p2p_mainwait":
+                torch.cuda.default_stream().wait_stream(torch.cuda.current_stream())
+        p2p.P2PAllReducer.all_reduce_ = wrapped
+        if mode == "p2p_main":  # issue on the main stream after it joined the side stream
+            def ctx_main(device):
+                torch.cuda.current_stream(device).wait_stream(_util.side_stream(device))
+                return contextlib.nullcontext()
+            _util.collective_ctx = ctx_main
         s = parallel.MultiWorkerMirroredStrategy(bucket_mb=0.25)
         with s.scope():
             m = _gpt2(100 + rank)
@@ -118,7 +138,7 @@ def _worker(rank, world, port, mode, q):
             b = s._bucketers[id(m._arena)]
         torch.cuda.synchronize()
         q.put((rank, [w.detach().float().cpu().numpy() for w in m.trainable_variables],
-               [w.name for w in m.trainable_variables], dict(b.paths), b.buckets))
+               [w.name for w in m.trainable_variables], dict(b.paths), (b.buckets, list(m._arena.offsets))))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:
@@ -152,15 +172,18 @@ def p2p_main():
     torch.cuda.synchronize()
     ref = [w.detach().float().cpu().numpy() for w in m.trainable_variables]
     names = [w.name for w in m.trainable_variables]
-    for mode in ("gloo", "p2p", "p2p_sync"):
+    for mode in sys.argv[2:] or ("gloo", "p2p", "p2p_sync"):
         res = run_ranks(mode)
         same = all((a == b).all() for a, b in zip(res[0][1], res[1][1]))
-        print(f"{mode}: paths={res[0][3]} replicas_identical={same} nbuckets={len(res[0][4])}", flush=True)
-        for n, a, r in zip(names, res[0][1], ref):
+        buckets, offs = res[0][4]
+        print(f"{mode}: paths={res[0][3]} replicas_identical={same} buckets={buckets}", flush=True)
+        for n, a, r, o in zip(names, res[0][1], ref, offs):
             d = np.abs(a - r)
             bad = (d > 2e-4 + 2e-3 * np.abs(r)).mean()
             if bad > 0:
-                print(f"   {n:40s} shape={a.shape} maxdiff={d.max():.3e} frac_bad={bad:.3f}", flush=True)
+                bi = [i for i, (lo, hi) in enumerate(buckets) if lo <= o < hi]
+                print(f"   {n:40s} shape={a.shape} off={o} bucket={bi} maxdiff={d.max():.3e} frac_bad={bad:.3f}",
+                      flush=True)
 
 
 if __name__ == "__main__":
