@@ -272,7 +272,7 @@ class Model(Layer):
             # forces it; a hipGraph-captured step (and its eager warmups) keeps the single update after backward
             from ..parallel import strategy as _S
             ovl = _S._OVERLAP_UPDATE in ("1", "force") or (_S._OVERLAP_UPDATE == "" and self.overlap_update)
-            graph_ok = not getattr(self, "_graph_step", False) or _S._OVERLAP_CAPTURE
+            graph_ok = not getattr(self, "_graph_step", False)
             strat.backward(loss, arena, optimizer=self.optimizer if ovl and graph_ok else None)
             join_side_streams()  # weight gradients issued on the side stream are in the arena
         with prof.phase("optimizer"):

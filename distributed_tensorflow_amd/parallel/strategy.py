@@ -36,8 +36,12 @@ _tls = threading.local()
 # leaves CUs idle), bf16 GPT-2-medium -1%, ResNet-50 -0.8%, BERT-base +-0 (backward already keeps every CU busy:
 # the memory-bound update only moves, it does not hide).
 _OVERLAP_UPDATE = os.environ.get("DTF_OVERLAP_UPDATE", "")
-# the per-bucket update inside a hipGraph-captured step (DTF_OVERLAP_UPDATE_CAPTURE=1; tests/test_graphs.py)
-_OVERLAP_CAPTURE = os.environ.get("DTF_OVERLAP_UPDATE_CAPTURE", "0") == "1"
+# A hipGraph-captured step never takes the per-bucket update (round-4 bisection, tools/debug_r4.py capture: bucket
+# updates issued from autograd's post-accumulate hooks during the capture replay differently from eager — with the
+# update on its own stream the stem's bucket diverges from the first replay, with the update on the capture stream
+# (or the weight gradients on the main stream) the first replay's forward already differs — while the same buckets
+# updated after backward (finalize) replay bit-identically; the optimizer is one ~120 us launch per ResNet-50 step,
+# so the capture keeps the single fused update after backward).
 
 
 class ReduceOp(enum.Enum):
@@ -119,8 +123,8 @@ class Strategy:
             return None
         if not arena.grad.is_cuda and _OVERLAP_UPDATE != "force":
             return None
-        if arena.grad.is_cuda and torch.cuda.is_current_stream_capturing() and not _OVERLAP_CAPTURE:
-            return None  # a captured step keeps the single update after backward unless asked
+        if arena.grad.is_cuda and torch.cuda.is_current_stream_capturing():
+            return None  # a captured step keeps the single update after backward (see above)
         b = self._bucketers.get(id(arena))
         if b is None:  # one replica: a bucketer without collectives, only to time the bucket updates
             b = collective.GradientBucketer(arena, collective=False).install()

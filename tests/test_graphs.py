@@ -68,15 +68,15 @@ def test_captured_step_matches_eager(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("opt", ["adam", "sgdm"])
-def test_captured_overlapped_update_matches_eager(cuda, monkeypatch, opt):
-    """The per-bucket optimizer update during backward (GradientBucketer.begin_step: one fused update per bucket on
-    the update stream as soon as the bucket's gradients are final) inside a hipGraph-captured step must train like
-    the same overlapped update run eagerly: same per-step losses, weights and BN statistics after 6 steps (VERDICT r3
-    weak #7: round 3 disabled it under capture after 'replays diverged' without a reproducer)."""
+def test_overlap_update_request_under_capture_trains_like_eager(cuda, monkeypatch, opt):
+    """DTF_OVERLAP_UPDATE=1 (per-bucket optimizer update during backward) with a hipGraph-captured step: the captured
+    step keeps the single fused update after backward (strategy.py: bucket updates issued from autograd hooks
+    inside a capture replayed differently from eager, tools/debug_r4.py), so it must train like the eager run
+    that does update bucket by bucket: same per-step losses, weights and BN statistics after 6 steps (the two
+    update forms are bit-identical in loss, test_overlapped_update_bitwise_equals_single_update)."""
     from distributed_tensorflow_amd.graphs import CapturedStep
     from distributed_tensorflow_amd.parallel import strategy as S
     monkeypatch.setattr(S, "_OVERLAP_UPDATE", "1")
-    monkeypatch.setattr(S, "_OVERLAP_CAPTURE", True)
     torch.manual_seed(0)
     xs = [torch.randn(8, 3, 64, 64, device=cuda) for _ in range(6)]
     ys = [torch.randint(0, 16, (8,), device=cuda) for _ in range(6)]
@@ -90,9 +90,10 @@ def test_captured_overlapped_update_matches_eager(cuda, monkeypatch, opt):
         losses_seen = [float(fn((x, y))["loss"]) for x, y in zip(xs, ys)]
         torch.cuda.synchronize()
         b = model.distribute_strategy._bucketers.get(id(model._arena))
-        assert b is not None  # the overlapped update path really ran
+        assert (b is not None) == (not jit)  # eager: the bucket-by-bucket update really ran
         outs.append((losses_seen, [w.detach().float().cpu().clone() for w in model.weights],
                      model.optimizer.host_iterations(), int(model.optimizer.iterations.item())))
+        model.distribute_strategy._bucketers.clear()
     (l0, w0, h0, i0), (l1, w1, h1, i1) = outs
     assert h0 == h1 == i0 == i1 == 6
     for a, b in zip(l0, l1):

@@ -27,7 +27,6 @@ def capture(variant):
     from distributed_tensorflow_amd.ops import _util
     from distributed_tensorflow_amd.parallel import strategy as S
     S._OVERLAP_UPDATE = "1"
-    S._OVERLAP_CAPTURE = True
     if variant == "upd_main":
         _util.update_stream_ctx = lambda device, extra_wait=None: contextlib.nullcontext()
     if variant == "defer":  # every bucket update after backward (finalize), none during it
