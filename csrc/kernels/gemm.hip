@@ -308,9 +308,6 @@ int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool
 bool conv256_on();
 int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int C, int K, hipStream_t st);  // pwconv.hip
 bool pwconv_on();
-int conv3p_try(const void* X, const void* W, void* Y, float* stats, int N, int H, int Wd, int C, int K, int R, int S,
-               int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, hipStream_t st);  // conv3p.hip
-bool conv3p_on();
 
 // The 256-row pipelined LDS-DMA kernel (conv256.hip) for a convolution GEMM: forced by tiles 11-14 (variant
 // tile - 11, see conv256.hip launch_cfg); by default whenever it is eligible and fills the chip. True if launched.
@@ -661,15 +658,6 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
     // channel-expanding 1x1 layers: the persistent register-resident-filter kernel (pwconv.hip); the BN finalize
     // then runs as its own launch over its <= 256 partial rows
     const int rows = pwconv_try(X, Wt, Y, stats, (long)N * P * Q, C, K, (hipStream_t)stream);
-    if (rows > 0) {
-      if (stat_rows) *stat_rows = rows;
-      return (int)hipGetLastError();
-    }
-  }
-  if (stats && !bias && !act && !out_f32 && (tile < 0 || tile == 31) && conv3p_on()) {
-    // 3x3 64 -> 64 channels: the persistent register-resident-filter kernel (conv3p.hip)
-    const int rows = conv3p_try(X, Wt, Y, stats, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
-                                (hipStream_t)stream);
     if (rows > 0) {
       if (stat_rows) *stat_rows = rows;
       return (int)hipGetLastError();

@@ -8,10 +8,9 @@
 //  * the grid is one 256-wide column tile per block, persistent over M-tiles (one block per CU, XCD-aware: the
 //    blocks that share A rows for the N/256 column tiles sit on one XCD), so the block's whole weight slice
 //    (64 columns x C_in per wave, <= 128 VGPRs) is loaded into REGISTERS once and never staged again;
-//  * only A (the activation tile, BM x C_in) streams through LDS, by LDS-DMA into a 4-deep ring: three tiles are
-//    landed or in flight while one is multiplied and stored, and each tile's stores get two iterations to drain
-//    before the in-order vmcnt reaches them (waits counted exactly: stores are issued unconditionally — rows past
-//    M go to an out-of-range buffer offset);
+//  * only A (the activation tile, BM x C_in) streams through LDS, by LDS-DMA into a 3-deep ring: the next two
+//    tiles are in flight while this one is multiplied and stored, counted vmcnt waits (stores are issued
+//    unconditionally — rows past M go to an out-of-range buffer offset — so the count is exact);
 //  * the epilogue stores bf16 straight from the accumulators and keeps the BN sum / sum-of-squares of the
 //    stored (bf16) values in registers across ALL of the block's tiles: one partial row per block (<= 256 rows).
 // Reference op: the Conv2D + FusedBatchNorm pair of the model trainer/task.py:62-71 builds.
@@ -41,23 +40,9 @@ struct PwGeo {
   static constexpr int LD = NKT * L;           // DMA instructions per thread per tile
   static constexpr int SUB = BM * 128;         // bytes of one [BM][64] sub-image
   static constexpr int IMG = NKT * SUB;        // bytes of one A tile
-  static constexpr int NBUF = 4;  // A tiles it, it+1, it+2 landed or in flight while tile it+3 is issued
+  static constexpr int NBUF = 3;
   static constexpr int ST = 16;                // stores per thread per tile (4 row frags x 4 column frags)
 };
-
-// s_waitcnt vmcnt(nd * LD + ns * ST) for nd, ns in 0..2 (the immediate must be a constant)
-template <int LD, int ST>
-__device__ __forceinline__ void vm_wait(int nd, int ns) {
-#define DTF_VMW(D, S)                                                                     \
-  if (nd == D && ns == S) {                                                               \
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * LD + S * ST) : "memory");                \
-    return;                                                                               \
-  }
-  DTF_VMW(0, 0) DTF_VMW(1, 0) DTF_VMW(2, 0) DTF_VMW(0, 1) DTF_VMW(1, 1) DTF_VMW(2, 1)
-  DTF_VMW(0, 2) DTF_VMW(1, 2) DTF_VMW(2, 2)
-#undef DTF_VMW
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 template <int C, int WMW>
 __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
@@ -103,10 +88,8 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
 
   const int first = slot, step = a.nslots;
   const int n_mine = first < a.tiles_m ? (a.tiles_m - first + step - 1) / step : 0;
-  // issue order: D0 D1 D2 | S0 D3 | S1 D4 | ... (S = a tile's stores, D = a tile's DMA): a tile's stores get two
-  // iterations to drain before the in-order vmcnt needs them, a tile's DMA three
-  for (int p = 0; p < 3; ++p)
-    if (p < n_mine) issue(first + p * step, p);
+  if (n_mine > 0) issue(first, 0);
+  if (n_mine > 1) issue(first + step, 1);
 
   float cs[4][4], cq[4][4];
 #pragma unroll
@@ -115,12 +98,16 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
     for (int r = 0; r < 4; ++r) cs[j][r] = cq[j][r] = 0.f;
 
   for (int it = 0; it < n_mine; ++it) {
-    // tile `it` landed: the ops this thread issued after D(it) are S(it-2), D(it+1), S(it-1), D(it+2), those that exist
-    {
-      const int nd = (it + 1 < n_mine) + (it + 2 < n_mine), ns = it >= 2 ? 2 : it;
-      vm_wait<G::LD, G::ST>(nd, ns);
+    // tile `it` landed: the ops this thread issued after it are tile it+1's DMA (if any) and tile it-1's stores
+    if (it + 1 < n_mine) {
+      if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD + G::ST) : "memory");
+    } else {
+      if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::ST) : "memory");
     }
-    __syncthreads();  // every wave's DMA share landed; every wave is done with the buffer tile it+3 will reuse
+    __syncthreads();  // every wave's DMA share landed; every wave is done with the buffer tile it+2 reuses
+    if (it + 2 < n_mine) issue(first + (it + 2) * step, (it + 2) % G::NBUF);
     const char* img = smem + (it % G::NBUF) * G::IMG;
 
     v4f acc[4][4];
@@ -165,7 +152,6 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
         cs[j][3] += v3; cq[j][3] = fmaf(v3, v3, cq[j][3]);
       }
     }
-    if (it + 3 < n_mine) issue(first + (it + 3) * step, (it + 3) % G::NBUF);
   }
 
   // ---- one partial row per block: the 16 row lanes by DPP, the WMW row waves through LDS (fixed order)

@@ -48,29 +48,3 @@ def test_conv_fwd_routes_pointwise_to_pwconv(cuda):
     R = _run(cuda, 40000, 64, 256, via_conv=True)
     assert R <= 3 * 256
 
-
-@pytest.mark.parametrize("N,H,pad", [(2, 56, 1), (3, 17, 1), (4, 9, 0)])
-def test_conv3p_matches_fp32_reference(cuda, N, H, pad):
-    """The persistent 3x3 64 -> 64 conv (csrc/kernels/conv3p.hip) through dtf_conv_fwd's routing: output against
-    an fp32 F.conv2d, BN statistics against the stored bf16 output (image borders: masked taps read zeros)."""
-    g = torch.Generator(device="cpu").manual_seed(N * H + pad)
-    x = (torch.rand(N, H, H, 64, generator=g) * 2 - 1).to(BF).to(cuda)
-    w = ((torch.rand(64, 3, 3, 64, generator=g) * 2 - 1) * 0.1).to(BF).to(cuda)
-    P = H + 2 * pad - 2
-    M = N * P * P
-    y = torch.full((N, P, P, 64), float("nan"), dtype=BF, device=cuda)
-    part = torch.full((((M + 63) // 64) * 2 * 64,), float("nan"), dtype=torch.float32, device=cuda)
-    rows = IntOut()
-    call("dtf_conv_fwd", ptr(x), ptr(w), ptr(y), None, ptr(part), rows.addr, N, H, H, 64, 64, 3, 3, P, P, 1, 1, pad,
-         pad, 1, 1, 0, 0, -1, stream())
-    torch.cuda.synchronize()
-    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=pad)
-    ref = ref.permute(0, 2, 3, 1)
-    assert torch.isfinite(y.float()).all()
-    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-2)
-    R = rows.value
-    assert 0 < R <= (M + 63) // 64
-    st = part[:R * 128].view(R, 128).double().sum(0)
-    yd = y.double().reshape(-1, 64)
-    torch.testing.assert_close(st[:64], yd.sum(0), rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(st[64:], (yd * yd).sum(0), rtol=1e-4, atol=1e-3)
