@@ -111,6 +111,8 @@ def before_overwrite(t):
     ev = _SIDE_READS.pop(p, None)
     if ev is not None:
         torch.cuda.current_stream(t.device).wait_event(ev)
+        if torch.cuda.is_current_stream_capturing():
+            _CAPTURE_KEEP.append(ev)
 
 
 # Tensors read by side-stream work stay REFERENCED until that work has run. Autograd sums the gradients of a
@@ -120,6 +122,19 @@ def before_overwrite(t):
 # into dy on the main stream. With a second reference held here autograd adds out of place instead. Entries are
 # dropped once their event completed (eager; polled at every fork) or when the main stream joins the side stream.
 _SIDE_HOLD = []      # (event recorded after the side work, tensors it reads)
+
+
+_CAPTURE_KEEP = []   # events recorded during a hipGraph capture: destroyed only after the capture ended
+
+
+def _drop_holds():
+    """Forget the held side reads (the main stream is ordered after them now). Inside a capture the events stay
+    alive until the capture is over: destroying an event a captured node records crashes the graph's capture end."""
+    if torch.cuda.is_current_stream_capturing():
+        _CAPTURE_KEEP.extend(h[0] for h in _SIDE_HOLD)
+    elif _CAPTURE_KEEP:
+        _CAPTURE_KEEP.clear()
+    _SIDE_HOLD.clear()
 
 
 def _release_side_holds():
@@ -228,15 +243,17 @@ def join_update_stream(device):
 
 def join_side_streams():
     """Main stream waits for every side-stream weight gradient issued so far."""
+    if _SIDE_READS and torch.cuda.is_current_stream_capturing():
+        _CAPTURE_KEEP.extend(_SIDE_READS.values())
     _SIDE_READS.clear()
     _PARKED.clear()
     if not _SIDE_USED:
-        _SIDE_HOLD.clear()
+        _drop_holds()
         return
     for idx in list(_SIDE_USED):
         torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
     _SIDE_USED.clear()
-    _SIDE_HOLD.clear()  # the main stream is ordered after every side read now
+    _drop_holds()  # the main stream is ordered after every side read now
 
 
 def stream(device=None):

@@ -236,6 +236,7 @@ class GradientBucketer:
             if self.p2p is not None and self.arena.grad.is_cuda:
                 from ..ops._util import join_side_streams
                 join_side_streams()  # P2P buckets were reduced by kernels on the side stream
+                self.p2p.poll()
             if self.wire == "bf16" and self.collective:
                 for lo, hi in self.buckets:
                     _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])

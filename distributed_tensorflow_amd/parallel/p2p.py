@@ -29,7 +29,9 @@ MAX_RANKS = 8
 NBLK = int(os.environ.get("DTF_P2P_BLOCKS", "64"))  # blocks per rank and call
 # buckets up to this size (bytes, f32) take the P2P path when it is available (DTF_P2P_MAX_KB; 0 disables)
 MAX_BYTES = int(float(os.environ.get("DTF_P2P_MAX_KB", "4096")) * 1024)
-TIMEOUT_MS = int(os.environ.get("DTF_P2P_TIMEOUT_MS", "60000"))
+# a spinning block gives up after this long (a peer rank far behind, e.g. writing a checkpoint, is waited for)
+TIMEOUT_MS = int(os.environ.get("DTF_P2P_TIMEOUT_MS", "300000"))
+PROBE = 4096 + 3  # floats of the set-up self-test (exercises the float4 body and the scalar tail)
 
 
 def _export(t):
@@ -81,6 +83,64 @@ class P2PAllReducer:
             self.grad_ptr[p], self.flag_ptr[p] = g, f
         self.epoch = 0
         self.calls = 0
+        self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._err_ev = None
+        if not self._selftest(allv):
+            self.close()
+            raise RuntimeError("P2P all-reduce self-test failed (peer memory not reachable or wrong sums)")
+
+    def _selftest(self, allv):
+        """One call over a small probe buffer of every rank (value rank + 1) with a short timeout: every rank must
+        hold the exact sum. All ranks agree on the outcome (a failure anywhere disables the path everywhere)."""
+        dev = self.grad.device
+        probe = torch.full((PROBE,), float(self.rank + 1), dtype=torch.float32, device=dev)
+        pred = torch.empty_like(probe)
+        torch.cuda.synchronize(dev)
+        mine = _export(probe)
+        allp = [None] * self.world
+        dist.all_gather_object(allp, mine, group=self.group)
+        ptrs, opened = [], []
+        ok = True
+        try:
+            for p, v in enumerate(allp):
+                if p == self.rank:
+                    ptrs.append(probe.data_ptr())
+                    continue
+                base, q = _open(*v)
+                opened.append(base)
+                ptrs.append(q)
+            self.epoch += 1
+            srcs = (ctypes.c_void_p * self.world)(*ptrs)
+            flags = (ctypes.c_void_p * self.world)(*self.flag_ptr)
+            from ..ops._util import stream
+            _native.call("dtf_p2p_allreduce_f32", probe.data_ptr(), srcs, pred.data_ptr(), self.flags.data_ptr(),
+                         flags, PROBE, self.world, self.rank, self.epoch, 1, 5000, self.err.data_ptr(), stream(dev))
+            torch.cuda.synchronize(dev)
+            want = float(self.world * (self.world + 1) // 2)
+            ok = int(self.err.item()) == 0 and bool((probe == want).all().item())
+        except (RuntimeError, OSError):
+            ok = False
+        finally:
+            torch.cuda.synchronize(dev)
+            dist.barrier(group=self.group)  # no peer reads this rank's probe any more
+            for base in opened:
+                _native.call("dtf_ipc_close", base)
+        self.err.zero_()
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev if dist.get_backend(self.group) == "nccl"
+                            else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
+
+    def poll(self):
+        """Raise if a spin of an EARLIER step timed out (read back asynchronously: no device sync)."""
+        if self._err_ev is not None and self._err_ev.query():
+            if int(self._err_host.item()):
+                raise RuntimeError("P2P all-reduce timed out waiting for a peer rank (the step's sums are wrong)")
+            self._err_ev = None
+        if self._err_ev is None and not torch.cuda.is_current_stream_capturing():
+            self._err_host.copy_(self.err, non_blocking=True)
+            self._err_ev = torch.cuda.Event()
+            self._err_ev.record()
 
     def all_reduce_(self, lo, hi):
         """Sum grad[lo:hi] over the ranks in place (on the current stream)."""
