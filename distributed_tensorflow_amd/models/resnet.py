@@ -28,6 +28,7 @@ FUSE_STEM = os.environ.get("DTF_FUSE_STEM", "1") != "0"  # stem BN + ReLU + MaxP
 S2D_STEM = os.environ.get("DTF_S2D_STEM", "1") != "0"  # stem conv over the 2x2 space-to-depth image
 STAGES = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3), 26: (2, 2, 2, 2)}
 
+
 class Bottleneck(KL.Layer):
     def __init__(self, width, stride=1, project=False, bn_momentum=0.9, **kw):
         super().__init__(**kw)

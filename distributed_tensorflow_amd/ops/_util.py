@@ -130,9 +130,9 @@ _CAPTURE_KEEP = []   # events recorded during a hipGraph capture: destroyed only
 def _drop_holds():
     """Forget the held side reads (the main stream is ordered after them now). Inside a capture the events stay
     alive until the capture is over: destroying an event a captured node records crashes the graph's capture end."""
-    if torch.cuda.is_current_stream_capturing():
+    if _SIDE_HOLD and torch.cuda.is_current_stream_capturing():
         _CAPTURE_KEEP.extend(h[0] for h in _SIDE_HOLD)
-    elif _CAPTURE_KEEP:
+    elif _CAPTURE_KEEP and not torch.cuda.is_current_stream_capturing():
         _CAPTURE_KEEP.clear()
     _SIDE_HOLD.clear()
 
