@@ -82,6 +82,9 @@ def build(args, strategy, dev, rank):
 
 
 def main():
+    if os.environ.get("DTF_BENCH_WATCHDOG"):  # debugging: dump every thread's stack (and exit) after N seconds
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DTF_BENCH_WATCHDOG"]), exit=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)

@@ -134,7 +134,11 @@ class TorchrunClusterResolver:
 
     @staticmethod
     def active():
-        return int(os.environ.get("WORLD_SIZE", "1")) > 1 and "RANK" in os.environ
+        """A torchrun-style launch: several ranks, or ONE rank whose launcher also published the rendezvous address
+        (torchrun --nproc-per-node 1: the worker must meet torchrun's agent store at MASTER_PORT, not a default)."""
+        if "RANK" not in os.environ:
+            return False
+        return int(os.environ.get("WORLD_SIZE", "1")) > 1 or "MASTER_PORT" in os.environ
 
 
 class SimpleClusterResolver(TFConfigClusterResolver):

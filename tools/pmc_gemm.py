@@ -50,6 +50,8 @@ def summary(paths):
                     print(f"   {c + ' / WAVE_CYCLES':42s} {m[c] / wc:6.3f}")
         if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE", 0) > 0:
             print(f"   LDS bank-conflict share of LDS cycles      {m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:6.3f}")
+        if m.get("TCC_HIT_sum", 0) + m.get("TCC_MISS_sum", 0) > 0:
+            print(f"   L2 hit rate                                {m['TCC_HIT_sum'] / (m['TCC_HIT_sum'] + m['TCC_MISS_sum']):6.3f}")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("GRBM_GUI_ACTIVE", 0) > 0:
             # MFMA busy cycles summed over SIMDs vs (GPU-active cycles per XCD x 256 CUs x 4 SIMDs)
             per = m["GRBM_GUI_ACTIVE"] / 8
