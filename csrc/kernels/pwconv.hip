@@ -20,6 +20,7 @@ namespace dtf {
 namespace {
 
 typedef int v2i __attribute__((ext_vector_type(2)));
+typedef int v4i __attribute__((ext_vector_type(4)));
 
 struct PwArgs {
   const bf16_t* X;  // [M][C] activations
@@ -30,7 +31,7 @@ struct PwArgs {
   int tiles_m, tiles_n, nslots;
 };
 
-template <int C, int WMW>
+template <int C, int WMW, bool STG = false>
 struct PwGeo {
   static constexpr int NTH = 256 * WMW;        // 4 column waves x WMW row waves
   static constexpr int BM = 64 * WMW;          // rows per tile (64 per row wave)
@@ -41,13 +42,17 @@ struct PwGeo {
   static constexpr int SUB = BM * 128;         // bytes of one [BM][64] sub-image
   static constexpr int IMG = NKT * SUB;        // bytes of one A tile
   static constexpr int NBUF = 3;
-  static constexpr int ST = 16;                // stores per thread per tile (4 row frags x 4 column frags)
+  // stores per thread per tile: 4 row frags x 4 column frags of 8 B, or (STG: the tile staged through LDS) 16-B
+  // row-contiguous chunks, BM rows x 32 chunks over NTH threads
+  static constexpr int ST = STG ? BM * 32 / NTH : 16;
+  static constexpr int SROW = 256 + 8;         // staged row (bf16 elements): 16-B pad
+  static constexpr int SMEM = NBUF * IMG + (STG ? BM * SROW * 2 : 0);
 };
 
-template <int C, int WMW>
+template <int C, int WMW, bool STG>
 __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
-  using G = PwGeo<C, WMW>;
-  __shared__ __attribute__((aligned(16))) char smem[G::NBUF * G::IMG];
+  using G = PwGeo<C, WMW, STG>;
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wn = wave & 3, wm = wave >> 2;
   // block -> (column tile, row slot): the blocks of one row slot (all column tiles) are on one XCD
@@ -129,9 +134,11 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][2 * kt + kk], fa[i], acc[i][j], 0, 0, 0);
       }
 
-    // ---- epilogue: bf16 stores straight from the accumulators (lane: row (lane&15), 4 consecutive columns);
-    // rows past M store to an out-of-range offset (dropped by the range check) so every thread issues ST stores
+    // ---- epilogue: bf16 stores straight from the accumulators (lane: row (lane&15), 4 consecutive columns), or
+    // (STG) through an LDS stage as 16-B row-contiguous chunks; rows past M store to an out-of-range offset (dropped
+    // by the range check) so every thread issues ST stores
     const int mt = first + it * step;
+    char* stg = smem + G::NBUF * G::IMG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = mt * G::BM + wm * 64 + 16 * i + (lane & 15);
@@ -141,8 +148,13 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
         uint2 o;
         o.x = pack2bf(acc[i][j][0], acc[i][j][1]);
         o.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-        const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)n) * 2u : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, o), yr, off, 0, 0);
+        if constexpr (STG) {
+          const int ml = wm * 64 + 16 * i + (lane & 15), nl = wn * 64 + 16 * j + 4 * (lane >> 4);
+          *reinterpret_cast<uint2*>(stg + (ml * G::SROW + nl) * 2) = o;
+        } else {
+          const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)n) * 2u : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, o), yr, off, 0, 0);
+        }
         // statistics of the stored values (rows past M hold exact zeros: they add nothing)
         const float v0 = __uint_as_float(o.x << 16), v1 = __uint_as_float(o.x & 0xffff0000u);
         const float v2 = __uint_as_float(o.y << 16), v3 = __uint_as_float(o.y & 0xffff0000u);
@@ -150,6 +162,18 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
         cs[j][1] += v1; cq[j][1] = fmaf(v1, v1, cq[j][1]);
         cs[j][2] += v2; cq[j][2] = fmaf(v2, v2, cq[j][2]);
         cs[j][3] += v3; cq[j][3] = fmaf(v3, v3, cq[j][3]);
+      }
+    }
+    if constexpr (STG) {
+      __syncthreads();  // the tile is staged (the next tile's staging writes come after the next top barrier)
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) {
+        const int c = t + k * G::NTH, row = c >> 5, ch = c & 31;
+        const int m = mt * G::BM + row;
+        const uint4 v = *reinterpret_cast<const uint4*>(stg + (row * G::SROW + ch * 8) * 2);
+        const uint32_t off =
+            m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)(tile_n * 256 + ch * 8)) * 2u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), yr, off, 0, 0);
       }
     }
   }
@@ -179,9 +203,9 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
   }
 }
 
-template <int C, int WMW>
+template <int C, int WMW, bool STG = false>
 void launch_pw(const PwArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((pw_conv_kernel<C, WMW>), dim3(grid), dim3(256 * WMW), 0, st, a);
+  hipLaunchKernelGGL((pw_conv_kernel<C, WMW, STG>), dim3(grid), dim3(256 * WMW), 0, st, a);
 }
 
 }  // namespace
@@ -223,9 +247,16 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
   while (grid > 8 * tiles_n && grid / tiles_n > a.tiles_m) grid /= 2;
   a.nslots = grid / tiles_n;
   if (a.nslots > a.tiles_m && a.nslots > 8) return 0;
+  // DTF_PW_STAGE (default 1): the C_in 64 / 256 tiles store through an LDS stage as row-contiguous 16-B chunks
+  static const bool stage = [] {
+    const char* e = getenv("DTF_PW_STAGE");
+    return !(e && e[0] == '0');
+  }();
   if (C == 64 && wmw == 1) launch_pw<64, 1>(a, grid, st);
+  else if (C == 64 && stage) launch_pw<64, 2, true>(a, grid, st);
   else if (C == 64) launch_pw<64, 2>(a, grid, st);
   else if (C == 128) launch_pw<128, 2>(a, grid, st);
+  else if (stage) launch_pw<256, 1, true>(a, grid, st);
   else launch_pw<256, 1>(a, grid, st);
   return hipGetLastError() == hipSuccess ? a.nslots : 0;
 }
