@@ -11,8 +11,8 @@ from __future__ import annotations
 
 import torch
 
-from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, before_overwrite, bf16_shadow, call, crsk_shadow, direct_grad,
-                    fork_side, mark_parked, on_gpu, ptr, stream, workspace)
+from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, K as K_, before_overwrite, bf16_shadow, call, crsk_shadow,
+                    direct_grad, fork_side, mark_parked, on_gpu, ptr, stream, workspace)
 
 
 def out_size(h, k, s, p, d=1):
@@ -275,6 +275,10 @@ _LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
 # materialising on every configuration — profiles/r3_lazy_bn_modes.txt — and removed in round 4.)
 _DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
 _COMPACT_PROJ = __import__("os").environ.get("DTF_COMPACT_PROJ", "1") != "0"
+# BN apply of a channel-expanding 1x1 ConvBN by recomputing the product from its input (pwconv.hip pw_apply_kernel);
+# needs the pointwise forward kernel for the statistics pass (identical MFMA order: bit-identical y)
+_PW_APPLY = (__import__("os").environ.get("DTF_PW_APPLY", "1") != "0"
+             and __import__("os").environ.get("DTF_PWCONV", "1") != "0")
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -319,8 +323,16 @@ class _ConvBNFn(torch.autograd.Function):
             out._dtf_affine = (scale, shift)
         else:
             out = torch.empty_like(yc)
-            call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
-                 ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, stream())
+            done = False
+            if (_PW_APPLY and training and g[5:7] == (1, 1) and g[9:15] == (1, 1, 0, 0, 1, 1) and C in (64, 128, 256)
+                    and K % 256 == 0):
+                # channel-expanding 1x1 conv: recompute X W^T instead of re-reading its 4x larger output (pwconv.hip)
+                done = K_().dtf_pwconv_apply(ptr(x), ptr(bf16_shadow(w)), ptr(scale), ptr(shift), ptr(res),
+                                             ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, ptr(out),
+                                             ptr(mbits), M, C, K, int(relu), stream()) == 0
+            if not done:
+                call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
+                     ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, stream())
         # backward needs the conv output and a 1-bit ReLU mask, not the bf16 BN output
         ctx.save_for_backward(x, w, gamma, yc, mbits, mean, invstd)
         ctx.bn_params = (gamma, beta)
