@@ -232,7 +232,8 @@ __device__ __forceinline__ void pa_wait(int nd, int nr, int ns) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * LD + R * RL + S * ST) : "memory");     \
     return;                                                                             \
   }
-  DTF_PAW(0, 0, 0) DTF_PAW(1, 0, 0) DTF_PAW(0, 1, 1) DTF_PAW(1, 1, 1) DTF_PAW(0, 1, 2) DTF_PAW(1, 1, 2)
+  DTF_PAW(0, 0, 0) DTF_PAW(1, 0, 0) DTF_PAW(2, 0, 0) DTF_PAW(0, 1, 0) DTF_PAW(1, 1, 0) DTF_PAW(0, 1, 1)
+  DTF_PAW(1, 1, 1) DTF_PAW(0, 1, 2) DTF_PAW(1, 1, 2) DTF_PAW(2, 1, 1) DTF_PAW(2, 1, 0) DTF_PAW(0, 0, 1)
 #undef DTF_PAW
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -299,20 +300,31 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_apply_kernel(PwApplyArgs a) {
 
   const int first = slot, step = a.nslots;
   const int n_mine = first < a.tiles_m ? (a.tiles_m - first + step - 1) / step : 0;
-  if (n_mine > 0) issue(first, 0);
-  if (n_mine > 1) issue(first + step, 1);
   char* stg = smem + G::NBUF * G::IMG;
-
-  for (int it = 0; it < n_mine; ++it) {
-    // after D(it): [S(it-2)] [R(it-1)] [D(it+1)] [S(it-1)] — the issue order is R(it), D(it+2), S(it) per iteration
-    pa_wait<G::LD, CH, STA>(it + 1 < n_mine ? 1 : 0, it >= 1 ? 1 : 0, it >= 2 ? 2 : it);
-    __syncthreads();
-    const int mt = first + it * step;
-    uint4 rv[CH];
+  // issue order: R0 D0 D1 | per iteration it: R(it+1) D(it+2) ... S(it)  (R = a tile's residual chunks into
+  // registers, one tile ahead; D = its activation DMA; S = its stores + mask bytes)
+  uint4 rv[2][CH];
+  auto load_res = [&](int tl, uint4 (&dst)[CH]) {
 #pragma unroll
     for (int k = 0; k < CH; ++k)
-      rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rr, a.res ? chunk_off(mt, k) : 0x80000000u,
-                                                                            0, 0));
+      dst[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rr, a.res ? chunk_off(first + tl * step, k) : 0x80000000u, 0, 0));
+  };
+  if (n_mine > 0) load_res(0, rv[0]);
+  if (n_mine > 0) issue(first, 0);
+  if (n_mine > 1) issue(first + step, 1);
+
+  for (int it = 0; it < n_mine; ++it) {
+    // after D(it): it 0: [D1]; it 1: R1 [D2] S0; it >= 2: S(it-2) R(it) [D(it+1)] S(it-1)
+    {
+      const int d1 = it + 1 < n_mine ? 1 : 0;
+      if (it == 0) pa_wait<G::LD, CH, STA>(d1, 0, 0);
+      else if (it == 1) pa_wait<G::LD, CH, STA>(d1, 1, 1);
+      else pa_wait<G::LD, CH, STA>(d1, 1, 2);
+    }
+    __syncthreads();
+    const int mt = first + it * step;
+    if (it + 1 < n_mine) load_res(it + 1, rv[(it + 1) & 1]);
     if (it + 2 < n_mine) issue(first + (it + 2) * step, (it + 2) % G::NBUF);
     const char* img = smem + (it % G::NBUF) * G::IMG;
     v4f acc[4][4];
@@ -343,14 +355,17 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_apply_kernel(PwApplyArgs a) {
         o.y = pack2bf(acc[i][j][2], acc[i][j][3]);
         *reinterpret_cast<uint2*>(stg + (ml * G::SROW + nl) * 2) = o;
       }
-    pa_wait<G::LD, CH, STA>(it + 2 < n_mine ? 1 : 0, 0, 0);  // R(it) landed (only D(it+2) may be in flight)
+    // R(it) landed: after it come D(it+1) (issued an iteration ago), S(it-1), R(it+1), D(it+2) — those that exist
+    pa_wait<G::LD, CH, STA>((it + 1 < n_mine ? 1 : 0) + (it + 2 < n_mine ? 1 : 0), it + 1 < n_mine ? 1 : 0,
+                            it >= 1 ? 1 : 0);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const int row = (t + k * G::NTH) >> 5;
       float f[8], r[8], o[8];
       load8(reinterpret_cast<const bf16_t*>(stg) + row * G::SROW + ch * 8, f);
-      const uint32_t rw[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+      const uint4 rk = rv[it & 1][k];
+      const uint32_t rw[4] = {rk.x, rk.y, rk.z, rk.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         r[2 * q] = __uint_as_float(rw[q] << 16);
@@ -406,7 +421,13 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
     const char* e = getenv("DTF_PW_BPC");
     return e ? std::max(1, std::min(3, atoi(e))) : 1;
   }();
-  const int wmw = (C == 256 || (C == 64 && bpc > 1)) ? 1 : 2;
+  // DTF_PW_STAGE (default 1): the tile is stored through an LDS stage as row-contiguous 16-B chunks (C_in 128 then
+  // takes one row wave per block: the 3-deep ring plus the stage of a 128-row tile would exceed the LDS)
+  static const bool stage = [] {
+    const char* e = getenv("DTF_PW_STAGE");
+    return !(e && e[0] == '0');
+  }();
+  const int wmw = (C == 256 || (C == 64 && bpc > 1) || (C == 128 && stage)) ? 1 : 2;
   const int bm = 64 * wmw;
   PwArgs a{};
   a.X = (const bf16_t*)X; a.W = (const bf16_t*)W; a.Y = (bf16_t*)Y; a.stats = stats;
@@ -420,14 +441,10 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
   while (grid > 8 * tiles_n && grid / tiles_n > a.tiles_m) grid /= 2;
   a.nslots = grid / tiles_n;
   if (a.nslots > a.tiles_m && a.nslots > 8) return 0;
-  // DTF_PW_STAGE (default 1): the C_in 64 / 256 tiles store through an LDS stage as row-contiguous 16-B chunks
-  static const bool stage = [] {
-    const char* e = getenv("DTF_PW_STAGE");
-    return !(e && e[0] == '0');
-  }();
   if (C == 64 && wmw == 1) launch_pw<64, 1>(a, grid, st);
   else if (C == 64 && stage) launch_pw<64, 2, true>(a, grid, st);
   else if (C == 64) launch_pw<64, 2>(a, grid, st);
+  else if (C == 128 && stage) launch_pw<128, 1, true>(a, grid, st);
   else if (C == 128) launch_pw<128, 2>(a, grid, st);
   else if (stage) launch_pw<256, 1, true>(a, grid, st);
   else launch_pw<256, 1>(a, grid, st);
