@@ -79,26 +79,43 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const bf16_t* __restrict_
 // Per-channel: sum T partial rows, mean/var, scale = gamma*invstd, shift = beta - mean*scale.
 // Running stats follow Keras BatchNormalization: r = r*momentum + batch*(1-momentum),
 // with the unbiased variance, as TF's FusedBatchNormV3 does.
-// grid: ceil(C/64) blocks of 256 threads (4 row-groups x 64 channels).
-__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int T, long rs,
+// grid: ceil(C/64) blocks of FIN_NT threads (FIN_G row-groups x 64 channels): up to ~256 partial rows are summed
+// here directly (16 rows per thread, 4 loads in flight), so the row-grouping launch only runs for larger T.
+constexpr int FIN_G = 16, FIN_NT = 64 * FIN_G;
+
+// this thread's strided share of the T partial rows of channel c (sum half and sum-of-squares / x-weighted half),
+// combined over the FIN_G row groups in a fixed order (deterministic)
+__device__ __forceinline__ void fin_rows(const float* __restrict__ part, int T, long rs, int C, int c, bool cv,
+                                         float (&red)[2][FIN_G][64], float& A, float& B) {
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  float a = 0.f, b = 0.f;
+  if (cv) {
+#pragma unroll 4
+    for (int r = grp; r < T; r += FIN_G) { a += part[(long)r * rs + c]; b += part[(long)r * rs + C + c]; }
+  }
+  red[0][grp][cl] = a;
+  red[1][grp][cl] = b;
+  __syncthreads();
+  A = B = 0.f;
+  if (grp == 0) {
+#pragma unroll
+    for (int g = 0; g < FIN_G; ++g) { A += red[0][g][cl]; B += red[1][g][cl]; }
+  }
+}
+
+__global__ void __launch_bounds__(FIN_NT) bn_finalize_kernel(const float* __restrict__ part, int T, long rs,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
                                                           float* running_var, long M, int C, float momentum,
                                                           float eps, float* __restrict__ scale,
                                                           float* __restrict__ shift, float* __restrict__ mean_out,
                                                           float* __restrict__ invstd_out) {
-  __shared__ float red[2][4][64];
+  __shared__ float red[2][FIN_G][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  float a = 0.f, b = 0.f;
-  if (c < C)
-    for (int r = grp; r < T; r += 4) { a += part[(long)r * rs + c]; b += part[(long)r * rs + C + c]; }
-  red[0][grp][cl] = a;
-  red[1][grp][cl] = b;
-  __syncthreads();
+  float a, b;
+  fin_rows(part, T, rs, C, c, c < C, red, a, b);
   if (grp != 0 || c >= C) return;
-  a = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-  b = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
   float mean = a / (float)M;
   float var = fmaxf(b / (float)M - mean * mean, 0.f);
   float inv = rsqrtf(var + eps);
@@ -330,25 +347,21 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
 // Sum T partial rows; dgamma = sum dz*xhat, dbeta = sum dz; coefficients for the apply pass:
 //   dx = k1 * (dz - k2 - xhat * k3)   with k1 = gamma*invstd, k2 = sum_dz/M, k3 = sum_dzxhat/M
 // folded into dx = a*dz + b*x + c (a = k1, b = -k1*k3*invstd, c = k1*(mean*invstd*k3 - k2)).
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int T, long rs,
+__global__ void __launch_bounds__(FIN_NT) bn_bwd_finalize_kernel(const float* __restrict__ part, int T, long rs,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, long M, int C,
                                                               float* dgamma, float* dbeta, int accumulate,
                                                               float* __restrict__ coef) {
-  __shared__ float red[2][4][64];
+  __shared__ float red[2][FIN_G][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  float a = 0.f, b = 0.f;
-  if (c < C)
-    for (int r = grp; r < T; r += 4) { a += part[(long)r * rs + c]; b += part[(long)r * rs + C + c]; }
-  red[0][grp][cl] = a;
-  red[1][grp][cl] = b;
-  __syncthreads();
+  float sa, sb;
+  fin_rows(part, T, rs, C, c, c < C, red, sa, sb);
   if (grp != 0 || c >= C) return;
-  const float sdz = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  const float sdz = sa;
   const float is = invstd[c];
-  const float sdx = (red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl]) * is;
+  const float sdx = sb * is;
   if (dgamma) dgamma[c] = (accumulate ? dgamma[c] : 0.f) + sdx;
   if (dbeta) dbeta[c] = (accumulate ? dbeta[c] : 0.f) + sdz;
   const float gm = gamma ? gamma[c] : 1.f;
@@ -881,8 +894,8 @@ int red_grid(long M, int C) {
 // the grouping pass runs one block per leader row (more rows = more blocks reading the partials in parallel)
 static int bn_group_target() {
   static const int t = [] {
-    const char* e = getenv("DTF_BN_GROUP_TARGET");
-    return e ? std::max(1, atoi(e)) : 32;
+    const char* e = getenv("DTF_BN_GROUP_TARGET");  // (the finalize kernels sum up to ~256 rows themselves)
+    return e ? std::max(1, atoi(e)) : 256;
   }();
   return t;
 }
@@ -940,7 +953,7 @@ DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float*
                             float* shift, float* mean_out, float* invstd_out, void* stream) {
   long rs = 2L * C;
   T = dtf_group_rows_once(part, rs, T, 2L * C, bn_group_target(), &rs, stream);  // <= target leader rows, one launch
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream, part, T, rs, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_NT), 0, (hipStream_t)stream, part, T, rs, gamma,
                      beta,
                      running_mean, running_var, M, C, momentum, eps, scale, shift, mean_out, invstd_out);
   return (int)hipGetLastError();
@@ -1035,7 +1048,7 @@ static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const 
                                    hipStream_t st) {
   long rs = 2L * C;
   int T = dtf_group_rows_once(part, rs, G, 2L * C, bn_group_target(), &rs, (void*)st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, st, part, T, rs, gamma, mean, invstd, M, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(FIN_NT), 0, st, part, T, rs, gamma, mean, invstd, M, C,
                      dgamma, dbeta, accumulate, coef);
 }
 
