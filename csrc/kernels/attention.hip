@@ -47,6 +47,8 @@ struct AttnArgs {
   const unsigned long long* seedctr;  // optional device step counter (per-step masks under hipGraph replay)
   int nkq;          // (Sk + 3) / 4 hash blocks per query row
   int causal;
+  bf16_t* ds;       // optional dS^T scratch [B*H][Sk][dsld] (the dS backward path)
+  int dsld;         // its row stride: Sq rounded up to 64
 };
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
@@ -374,7 +376,7 @@ __global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
 
 // dK, dV: block = 4 waves x (16 KT) keys, loop over 64-query tiles; grid (cdiv(Sk, 64 KT), B*H).
 // Query subtiles are processed in pairs (one 32-query MFMA k-step) so only 2 x KT score tiles are live.
-template <int KT>
+template <int KT, bool DS>
 __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk, char* sq, char* sdo, float* slse,
                                                float* sdv) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
@@ -489,6 +491,16 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
       for (int kt = 0; kt < KT; ++kt) {
         pf[kt] = pack_slots(P[0][kt], P[1][kt]);
         sf[kt] = pack_slots(dS[0][kt], dS[1][kt]);
+        if constexpr (DS) {
+          // dS^T for the dQ GEMM (attn_dq_ds_kernel): the lane's key row, queries 32 kq + 4 G .. + 3 and + 16
+          const int key = k0w + 16 * kt + i;
+          if (key < a.Sk) {
+            const uint4 u = __builtin_bit_cast(uint4, sf[kt]);
+            bf16_t* row = a.ds + ((long)bh * a.Sk + key) * a.dsld + q0 + 32 * kq + 4 * G;
+            *reinterpret_cast<uint2*>(row) = make_uint2(u.x, u.y);
+            *reinterpret_cast<uint2*>(row + 16) = make_uint2(u.z, u.w);
+          }
+        }
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -518,7 +530,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
 }
 
 // key block kblk walks the query tiles from its diagonal on (causal): heavy = small kblk
-template <int KT>
+template <int KT, bool DS>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a, int nblk) {
   __shared__ __attribute__((aligned(16))) char sq[64 * 128];
   __shared__ __attribute__((aligned(16))) char sdo[64 * 128];
@@ -528,7 +540,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a, int n
     if (blk < 0) break;
     blk = nblk - 1 - blk;  // (pair_block orders by descending index; here the heavy blocks are the low ones)
     if (pass) __syncthreads();
-    attn_dkdv_body<KT>(a, blk, sq, sdo, slse, sdv);
+    attn_dkdv_body<KT, DS>(a, blk, sq, sdo, slse, sdv);
   }
 }
 
@@ -670,6 +682,55 @@ __global__ void __launch_bounds__(256, MINW) attn_bwd_dq_kernel(AttnArgs a, int 
   }
 }
 
+// dQ = scale * dS K from the dS^T scratch the dK/dV kernel wrote (a memory-bound GEMM: no score recompute, no
+// exponentials, no dropout hashes). Block: 4 waves x 16 queries over 64-key tiles (register-staged, two LDS
+// buffers, one barrier per tile); causal: only the key tiles up to the diagonal (exactly the tiles written).
+__global__ void __launch_bounds__(256) attn_dq_ds_kernel(AttnArgs a, int nqt) {
+  __shared__ __attribute__((aligned(16))) char sd[2][64 * 128];
+  __shared__ __attribute__((aligned(16))) char sk[2][64 * 128];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qt = nqt - 1 - (int)blockIdx.x;  // heavy (late) query tiles first under causal masking
+  const int q0 = qt * 64;
+  const int off = a.Sk - a.Sq;
+  int kend = a.Sk;
+  if (a.causal) kend = min(a.Sk, q0 + 64 + off);
+  const int ntiles = kend > 0 ? (kend + 63) / 64 : 0;
+  const bf16_t* D = a.ds + (long)bh * a.Sk * a.dsld + q0;
+  const bf16_t* K = a.k + b * a.ksb + h * a.ksh;
+  TileRegs td, tk;
+  v4f acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) acc[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (ntiles > 0) {
+    tile_load(td, D, a.dsld, 0, a.Sk);
+    tile_load(tk, K, a.kss, 0, a.Sk);
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    char* cd = sd[t & 1];
+    char* ck = sk[t & 1];
+    tile_store(td, cd);
+    tile_store(tk, ck);
+    __syncthreads();  // (the buffer written here was last read two tiles ago, before the previous barrier)
+    if (t + 1 < ntiles) {
+      tile_load(td, D, a.dsld, (t + 1) * 64, a.Sk);
+      tile_load(tk, K, a.kss, (t + 1) * 64, a.Sk);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v8bf sf = frag_tr(cd, 32 * kk, 16 * w, lane);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(frag_tr(ck, 32 * kk, 16 * dt, lane), sf, acc[dt]);
+    }
+  }
+  const int qi = q0 + 16 * w + i;
+  if (qi < a.Sq) {
+    bf16_t* dQ = a.dq + b * a.qsb + h * a.qsh + (long)qi * a.qss;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store4(dQ + 16 * dt + 4 * G, acc[dt], a.scale);
+  }
+}
+
 AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr, const long* kstr, const void* o,
                    const void* dout, const long* ostr, int B, int H, int Sq, int Sk, float scale, float dropout,
                    unsigned long long seed, int causal, const float* kmask,
@@ -756,7 +817,41 @@ DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 2>), dim3(pair_grid(causal, nqb), (unsigned)(B * H)), dim3(256), 0, st,
                        a, nqb);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0, st, a,
-                     nkb);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, false>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0,
+                     st, a, nkb);
+  return (int)hipGetLastError();
+}
+
+// dtf_attn_bwd through a dS^T scratch (ds: bf16, >= B*H*Sk*round_up(Sq, 64) elements): D = rowsum(dO * O) by a
+// small pass, the dK/dV kernel also stores dS^T (the values its dK MFMAs use), and dQ = scale * dS K is a
+// memory-bound GEMM over the stored tiles instead of a second kernel that recomputes the scores, the
+// probabilities and dP (3 of the 5 backward MFMA products). Same results as dtf_attn_bwd up to the f32 order of
+// the dQ sums.
+DTF_API int dtf_attn_bwd_ds(const void* q, const void* k, const void* v, const long* qstr, const long* kstr,
+                            const void* o, const void* dout, const long* ostr, const float* lse, float* dvec, void* dq,
+                            void* dk, void* dv, const float* kmask, int B, int H, int Sq, int Sk, int D, float scale,
+                            float dropout, unsigned long long seed, int causal, const void* seedctr, void* ds,
+                            void* stream) {
+  if (D != HD || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(dout) ||
+      !aligned16(dq) || !aligned16(dk) || !aligned16(dv) || !aligned16(ds))
+    return -1;
+  if ((qstr[0] | qstr[1] | qstr[2] | kstr[0] | kstr[1] | kstr[2] | ostr[0] | ostr[1] | ostr[2]) & 7) return -1;
+  if (dropout < 0.f || dropout >= 1.f) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  AttnArgs a = make_args(q, k, v, qstr, kstr, o, dout, ostr, B, H, Sq, Sk, scale, dropout, seed, causal, kmask,
+                         (const unsigned long long*)seedctr);
+  a.lse = const_cast<float*>(lse);
+  a.dvec = dvec;
+  a.dq = (bf16_t*)dq;
+  a.dk = (bf16_t*)dk;
+  a.dv = (bf16_t*)dv;
+  a.ds = (bf16_t*)ds;
+  a.dsld = (Sq + 63) / 64 * 64;
+  const long rows = (long)B * H * Sq;
+  hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)((rows + 255) / 256 < 4096 ? (rows + 255) / 256 : 4096)), dim3(256), 0, st, a);
+  const int nkb = (Sk + 127) / 128, nqt = (Sq + 63) / 64;
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, true>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0,
+                     st, a, nkb);
+  hipLaunchKernelGGL(attn_dq_ds_kernel, dim3((unsigned)nqt, (unsigned)(B * H)), dim3(256), 0, st, a, nqt);
   return (int)hipGetLastError();
 }

@@ -76,6 +76,7 @@ _KERNEL_SIGS = {
     "dtf_quant_fp8_exact": [P, P, L, P, P, P],
     "dtf_attn_fwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],
     "dtf_attn_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P],
+    "dtf_attn_bwd_ds": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, F, U, I, P, P, P],
     "dtf_colsum": [P, L, I, P, I, P, L, P],
     "dtf_embed_fwd": [P, P, P, P, P, P, P, L, I, I, P],
     "dtf_embed_bwd_sorted": [P, P, P, P, L, I, P],

@@ -277,7 +277,7 @@ _DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
 _COMPACT_PROJ = __import__("os").environ.get("DTF_COMPACT_PROJ", "1") != "0"
 # BN apply of a channel-expanding 1x1 ConvBN by recomputing the product from its input (pwconv.hip pw_apply_kernel);
 # needs the pointwise forward kernel for the statistics pass (identical MFMA order: bit-identical y)
-_PW_APPLY = (__import__("os").environ.get("DTF_PW_APPLY", "1") != "0"
+_PW_APPLY = (__import__("os").environ.get("DTF_PW_APPLY", "0") == "1"
              and __import__("os").environ.get("DTF_PWCONV", "1") != "0")
 
 

@@ -20,6 +20,19 @@ from .nn import softmax
 
 _seed_counter = [0]
 
+# Backward through a dS^T scratch (dtf_attn_bwd_ds: the dK/dV kernel stores dS, dQ is a memory-bound GEMM over it)
+# instead of a dQ kernel that recomputes the scores, probabilities and dP. DTF_ATTN_DS=1: on.
+_ATTN_DS = __import__("os").environ.get("DTF_ATTN_DS", "0") == "1"
+
+
+def _bwd(args_before_ds, B, H, Sq, Sk, dev):
+    """Run the attention backward (args: the dtf_attn_bwd argument list)."""
+    if _ATTN_DS:
+        ds = torch.empty(B * H * Sk * (-(-Sq // 64) * 64), dtype=BF16, device=dev)
+        call("dtf_attn_bwd_ds", *args_before_ds[:-1], ptr(ds), args_before_ds[-1])
+    else:
+        call("dtf_attn_bwd", *args_before_ds)
+
 
 def _next_seed(seed, device):
     """(host seed, device step-counter pointer or None): see ops.nn._auto_seed."""
@@ -65,9 +78,9 @@ class _FlashPackedFn(torch.autograd.Function):
         qs, qsp = _strides3(S * T, T, D)
         os_, osp = _strides3(S * HD, HD, D)
         base, gb = qkv.data_ptr(), dqkv.data_ptr()
-        call("dtf_attn_bwd", base, base + 2 * HD, base + 4 * HD, qsp, qsp, ptr(o), ptr(do), osp, ptr(lse), ptr(dvec),
-             gb, gb + 2 * HD, gb + 4 * HD, ptr(kmask), B, heads, S, S, D, float(scale), float(dropout), seed,
-             int(causal), ctr, stream())
+        _bwd((base, base + 2 * HD, base + 4 * HD, qsp, qsp, ptr(o), ptr(do), osp, ptr(lse), ptr(dvec),
+              gb, gb + 2 * HD, gb + 4 * HD, ptr(kmask), B, heads, S, S, D, float(scale), float(dropout), seed,
+              int(causal), ctr, stream()), B, heads, S, S, qkv.device)
         return dqkv, None, None, None, None, None, None, None
 
 
@@ -100,9 +113,9 @@ class _FlashFn(torch.autograd.Function):
         dvec = torch.empty(B * H, Sq, dtype=F32, device=q.device)
         qs, qsp = _strides3(H * Sq * D, D, Sq * D)
         ks, ksp = _strides3(H * Sk * D, D, Sk * D)
-        call("dtf_attn_bwd", ptr(q), ptr(k), ptr(v), qsp, ksp, ptr(o), ptr(do), qsp, ptr(lse), ptr(dvec), ptr(dq),
-             ptr(dk), ptr(dv), ptr(kmask), B, H, Sq, Sk, D, float(scale), float(dropout), seed, int(causal),
-             ctr, stream())
+        _bwd((ptr(q), ptr(k), ptr(v), qsp, ksp, ptr(o), ptr(do), qsp, ptr(lse), ptr(dvec), ptr(dq),
+              ptr(dk), ptr(dv), ptr(kmask), B, H, Sq, Sk, D, float(scale), float(dropout), seed, int(causal),
+              ctr, stream()), B, H, Sq, Sk, q.device)
         return dq, dk, dv, None, None, None, None, None, None
 
 

@@ -124,3 +124,40 @@ def test_flash_attention_packed(cuda):
     r.backward(do)
     o.backward(do.to(BF))
     close(qkv.grad, qr.grad, 3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,Sq,Sk,causal,masked,dropout", [
+    (2, 3, 128, 128, False, False, 0.0),
+    (2, 2, 200, 200, False, True, 0.0),
+    (1, 4, 256, 256, True, False, 0.0),
+    (2, 2, 100, 164, True, False, 0.0),
+    (3, 2, 64, 512, False, True, 0.0),
+    (2, 2, 128, 192, False, True, 0.1),
+    (1, 2, 256, 256, True, False, 0.2),
+])
+def test_flash_attention_ds_backward(cuda, monkeypatch, B, H, Sq, Sk, causal, masked, dropout):
+    """The dS^T-scratch backward (dtf_attn_bwd_ds: dK/dV kernel stores dS, dQ is a GEMM over it) against the f32
+    reference, on the shapes of the recompute backward's tests (ragged lengths, causal with Sk > Sq, dropout)."""
+    monkeypatch.setattr(A, "_ATTN_DS", True)
+    _run(cuda, B, H, Sq, Sk, causal, masked, dropout=dropout, seed=99 if dropout else 7)
+
+
+@pytest.mark.gpu
+def test_flash_attention_ds_packed_matches_recompute(cuda, monkeypatch):
+    """Packed QKV with causal masking and dropout: the dS^T path and the recompute path agree up to f32 summation
+    order (D = rowsum(dO * O) is summed by another kernel, dQ by a GEMM over the bf16 dS both paths use)."""
+    B, S, H = 2, 320, 4
+    torch.manual_seed(1)
+    qkv = (torch.randn(B, S, 3 * H * 64, device=cuda) * 0.5).to(BF)
+    do = torch.randn(B, S, H * 64, device=cuda).to(BF)
+    grads = []
+    for ds in (False, True):
+        monkeypatch.setattr(A, "_ATTN_DS", ds)
+        x = qkv.clone().requires_grad_(True)
+        o = ops.attention_packed(x, H, causal=True, dropout=0.1, training=True, seed=5)
+        (g,) = torch.autograd.grad(o, [x], do)
+        grads.append(g.float().reshape(B, S, 3, H * 64))
+    a, b = grads
+    for j in range(3):
+        assert (a[:, :, j] - b[:, :, j]).abs().max().item() <= 1e-2 * a[:, :, j].abs().max().item(), j
