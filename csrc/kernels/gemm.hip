@@ -251,14 +251,6 @@ static void launch_modes(GemmArgs& a, int tile, hipStream_t st) {
         launch_t<128, 128, 2, 2, AM, BMODE, 1>(a, st);
       }
       break;
-    case 17: case 18:  // LDS-DMA 3-deep ring (PIPE 5): 128x64 / 128x128
-      if constexpr (glds_mode(AM) && glds_mode(BMODE)) {
-        if (tile == 17) launch_t<128, 64, 2, 2, AM, BMODE, 5>(a, st);
-        else launch_t<128, 128, 2, 2, AM, BMODE, 5>(a, st);
-      } else {
-        launch_t<128, 128, 2, 2, AM, BMODE, 1>(a, st);
-      }
-      break;
     case 15: case 16:  // 64 x 256 LDS-DMA (one block covers 256 output channels: the A rows are read once)
       if constexpr (glds_mode(AM) && glds_mode(BMODE)) {
         if (tile == 15) launch_t<64, 256, 1, 4, AM, BMODE, 3>(a, st);
@@ -379,14 +371,6 @@ static bool dense_glds_on() {
   }();
   return on;
 }
-// DTF_GLDS_RING=1: the LDS-DMA tiles with the 3-deep ring (PIPE 5) instead of the synchronous / double-buffered forms
-static bool glds_ring() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_GLDS_RING");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 static int pick_glds_tile(const GemmArgs& a, int amode, int bmode) {
   if (!glds_on() || !glds_mode(amode) || !glds_mode(bmode) || a.atomic_out) return -1;
   if (amode == OP_KCONTIG && (long)a.M * a.lda * 2 >= (1l << 31)) return -1;
@@ -394,8 +378,7 @@ static int pick_glds_tile(const GemmArgs& a, int amode, int bmode) {
   if (amode == OP_KOUTER && ((long)a.K * a.lda * 2 >= (1l << 31) || (a.M & 7))) return -1;
   if (bmode == OP_KOUTER && ((long)a.K * a.ldb * 2 >= (1l << 31) || (a.N & 7))) return -1;
   const long blocks = (long)cdiv(a.M, 128) * cdiv(a.N, 64) * a.batch * a.splitk;
-  const int t = (blocks <= 1600 && a.kchunk >= 1024) ? 9 : 8;
-  return glds_ring() ? (t == 9 ? 18 : 17) : t;
+  return (blocks <= 1600 && a.kchunk >= 1024) ? 9 : 8;
 }
 
 static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st) {
@@ -994,7 +977,7 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
       b.C = ws;
       b.slab = mnT;
       b.beta = 0.f;
-      dispatch(b, OP_WGRADX_R, OP_KOUTER_R, glds_ring() ? 17 : 8, st);
+      dispatch(b, OP_WGRADX_R, OP_KOUTER_R, 8, st);
       float* dwt = ws + (long)sk * mnT;
       dtf_sum_rows(ws, mnT, sk, mnT, dwt, 0, st);
       hipLaunchKernelGGL(transpose_acc_kernel, dim3(cdiv(b.N, 32), cdiv(b.M, 32)), dim3(256), 0, st, dwt, dW, b.M,
@@ -1002,7 +985,7 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
       return (int)hipGetLastError();
     }
   }
-  if (tile < 0 && use_glds) tile = glds_ring() ? 18 : 7;
+  if (tile < 0 && use_glds) tile = 7;
   if (tile < 0) {  // measured on ResNet-50's filters (tools/conv_roofline.py --only wgrad --tiles)
     if (a.M <= 64) tile = pointwise && a.N >= 256 ? 4 : 3;  // Kout = 64: no half-empty 128-row tiles
     else if (R * S > 1) tile = 0;                  // spatial filters: 128x128

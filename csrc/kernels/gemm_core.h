@@ -1223,12 +1223,9 @@ __device__ __forceinline__ void xcd_block(int nwg, int& bid, int& z) {
 //  2: register-staged, double-buffered LDS (one barrier per K-tile).
 //  3: LDS-DMA (GldsLoader), one buffer, synchronous per K-tile: no staging VGPRs, occupancy hides latency.
 //  4: LDS-DMA, double-buffered: the next K-tile's DMA runs under this tile's MFMAs.
-//  5: LDS-DMA, 3-deep ring: K-tiles kt+1 and kt+2 are in flight under tile kt's MFMAs; the waits count the
-//     loaders' fixed number of DMA instructions per K-tile (issued unconditionally: out-of-range lanes get an
-//     out-of-range offset), so vmcnt(OPS) means "tile kt has landed".
 template <int BM, int BN, int WM, int WN, int AM, int BMODE, int FP8 = 0, int PIPE = 2>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
-  constexpr int NBUF = (PIPE == 2 || PIPE == 4) ? 2 : PIPE == 5 ? 3 : 1;
+  constexpr int NBUF = (PIPE == 2 || PIPE == 4) ? 2 : 1;
   constexpr bool GLDS = PIPE >= 3;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1308,31 +1305,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
   if constexpr (GLDS) {
     // (the loaders issue only LDS-DMA loads: no ordinary global load is waited for inside the loop)
-    if constexpr (NBUF == 3) {
-      constexpr int OPS = BM / 32 + BN / 32;  // DMA wave instructions per thread and K-tile (both loaders)
-      constexpr int SB = A_BYTES + B_BYTES;
-      if (nk > 0) {
-        la.issue(a, kbeg, kend, smem);
-        lb.issue(a, kbeg, kend, smem + A_BYTES);
-      }
-      if (nk > 1) {
-        la.issue(a, kbeg + BK, kend, smem + SB);
-        lb.issue(a, kbeg + BK, kend, smem + SB + A_BYTES);
-      }
-      int cur = 0;
-      for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // tile kt landed for every wave; every wave is done reading tile kt-1's slot
-        if (kt + 2 < nk) {
-          const int nb = cur == 0 ? 2 : cur - 1;  // (kt + 2) % 3 == (kt - 1) % 3
-          la.issue(a, kbeg + (kt + 2) * BK, kend, smem + nb * SB);
-          lb.issue(a, kbeg + (kt + 2) * BK, kend, smem + nb * SB + A_BYTES);
-        }
-        compute(smem + cur * SB, smem + cur * SB + A_BYTES);
-        cur = cur == 2 ? 0 : cur + 1;
-      }
-    } else if constexpr (NBUF == 2) {
+    if constexpr (NBUF == 2) {
       if (nk > 0) {
         la.issue(a, kbeg, kend, sA0);
         lb.issue(a, kbeg, kend, sB0);

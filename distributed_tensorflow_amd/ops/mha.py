@@ -21,13 +21,17 @@ from .nn import softmax
 _seed_counter = [0]
 
 # Backward through a dS^T scratch (dtf_attn_bwd_ds: the dK/dV kernel stores dS, dQ is a memory-bound GEMM over it)
-# instead of a dQ kernel that recomputes the scores, probabilities and dP. DTF_ATTN_DS=1: on.
-_ATTN_DS = __import__("os").environ.get("DTF_ATTN_DS", "0") == "1"
+# instead of a dQ kernel that recomputes the scores, probabilities and dP. DTF_ATTN_DS: 1 always, 0 never, default
+# causal only — measured (tools/bench_attention.py, profiles/r4_attention_bench.txt): GPT-2-medium causal S=1024
+# 178 -> 158 us (213 -> 183 with dropout); BERT-base S=512 203 -> 227 us (the dS round trip costs more than the
+# recompute saves when no tiles are skipped)
+_ATTN_DS = {"1": True, "0": False}.get(__import__("os").environ.get("DTF_ATTN_DS", ""), None)
 
 
 def _bwd(args_before_ds, B, H, Sq, Sk, dev):
-    """Run the attention backward (args: the dtf_attn_bwd argument list)."""
-    if _ATTN_DS:
+    """Run the attention backward (args: the dtf_attn_bwd argument list, causal flag at [-3])."""
+    causal = bool(args_before_ds[-3])
+    if _ATTN_DS or (_ATTN_DS is None and causal):
         ds = torch.empty(B * H * Sk * (-(-Sq // 64) * 64), dtype=BF16, device=dev)
         call("dtf_attn_bwd_ds", *args_before_ds[:-1], ptr(ds), args_before_ds[-1])
     else:
