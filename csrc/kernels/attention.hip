@@ -47,8 +47,8 @@ struct AttnArgs {
   const unsigned long long* seedctr;  // optional device step counter (per-step masks under hipGraph replay)
   int nkq;          // (Sk + 3) / 4 hash blocks per query row
   int causal;
-  bf16_t* ds;       // optional dS^T scratch [B*H][Sk][dsld] (the dS backward path)
-  int dsld;         // its row stride: Sq rounded up to 64
+  bf16_t* ds;       // optional dS^T scratch [B*H][dsld / 64 query tiles][Sk][64] (the dS backward path)
+  int dsld;         // Sq rounded up to 64
 };
 
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
@@ -353,32 +353,51 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a, int nblk) 
 }
 
 // ------------------------------------------------------------------------------------------------ backward
-// D[q] = sum_d dO[q][d] * O[q][d]; one thread per (bh, q) row
+// D[q] = sum_d dO[q][d] * O[q][d]: 8 lanes per (bh, q) row, 16 B each, rows visited in memory order (heads
+// innermost for the packed [B, S, H, 64] layout) so a wave reads 8 consecutive 128-B rows
 __global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
   const long n = (long)a.B * a.H * a.Sq;
-  for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(r % a.Sq);
-    const long bh = r / a.Sq;
-    const int b = (int)(bh / a.H), h = (int)(bh % a.H);
-    const long base = b * a.osb + h * a.osh + (long)q * a.oss;
+  const int sub = threadIdx.x & 7;
+  const bool hfast = a.osh == HD;
+  const long step = ((long)gridDim.x * blockDim.x) >> 3;
+  for (long r = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 3; r < n; r += step) {
+    int b, h, q;
+    if (hfast) {
+      h = (int)(r % a.H);
+      const long t = r / a.H;
+      q = (int)(t % a.Sq);
+      b = (int)(t / a.Sq);
+    } else {
+      q = (int)(r % a.Sq);
+      const long t = r / a.Sq;
+      h = (int)(t % a.H);
+      b = (int)(t / a.H);
+    }
+    const long base = b * a.osb + h * a.osh + (long)q * a.oss + sub * 8;
+    float x[8], y[8];
+    load8(a.o + base, x);
+    load8(a.dout + base, y);
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < HD / 8; ++c) {
-      float x[8], y[8];
-      load8(a.o + base + c * 8, x);
-      load8(a.dout + base + c * 8, y);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += x[j] * y[j];
-    }
-    a.dvec[r] = s;
+    for (int j = 0; j < 8; ++j) s = fmaf(x[j], y[j], s);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (sub == 0) a.dvec[((long)b * a.H + h) * a.Sq + q] = s;
   }
 }
 
 // dK, dV: block = 4 waves x (16 KT) keys, loop over 64-query tiles; grid (cdiv(Sk, 64 KT), B*H).
 // Query subtiles are processed in pairs (one 32-query MFMA k-step) so only 2 x KT score tiles are live.
-template <int KT, bool DS>
+// DS: 0 = no dS^T output, 1 = stored from the registers (8-B pieces), 2 = staged through LDS (sds, [64 KT keys]
+// [64 queries] swizzled) and stored as whole 128-B rows after each query tile
+// GL: the query tiles (Q, dO and their lse / D values) are staged by LDS-DMA through a 3-stage ring (ring, DKR_STG
+// bytes per stage) with counted vmcnt waits — two tiles in flight under the MFMAs — instead of register-staged
+// one-tile-ahead loads
+constexpr int DKR_STG = 2 * 64 * 128 + 2 * 64 * 4;
+template <int KT, int DS, bool GL>
 __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk, char* sq, char* sdo, float* slse,
-                                               float* sdv) {
+                                               float* sdv, char* sds, char* ring) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int BN = 64 * KT;
@@ -426,25 +445,87 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
       dreg = qi < a.Sq ? a.dvec[(long)bh * a.Sq + qi] : 0.f;
     }
   };
-  if (ntiles > 0) {
+  // LDS-DMA ring (GL): a wave instruction fills 1 KiB (8 rows) of a tile lane-linearly, each lane fetching the logical
+  // chunk the swz() swizzle puts at its slot; every wave also fills the tile's 64 lse and D values (identical data),
+  // so each wave issues exactly 6 instructions per tile. Rows past Sq read zeros (their lse 0 instead of +inf is
+  // harmless: zero Q / dO rows give zero dS, dK and dV contributions).
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, (int)(((long)(a.Sq - 1) * a.qss + 64) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro =
+      __builtin_amdgcn_make_buffer_rsrc((void*)dO, (short)0, (int)(((long)(a.Sq - 1) * a.oss + 64) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.lse + (long)bh * a.Sq), (short)0, a.Sq * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.dvec + (long)bh * a.Sq), (short)0, a.Sq * 4, 0x00020000);
+  int rrow[2] = {0, 0}, lch[2] = {0, 0};
+  auto issue = [&](int q0, int slot) {
+    char* cq = ring + slot * DKR_STG;
+    char* cd = cq + 8192;
+    char* cl = cd + 8192;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = q0 + rrow[u];
+      const bool ok = q < a.Sq;
+      const uint32_t oq = ok ? (uint32_t)(((long)q * a.qss + lch[u] * 8) * 2) : 0x80000000u;
+      const uint32_t oo = ok ? (uint32_t)(((long)q * a.oss + lch[u] * 8) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (__attribute__((address_space(3))) void*)(cq + u * 4096 + w * 1024),
+                                               16, oq, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (__attribute__((address_space(3))) void*)(cd + u * 4096 + w * 1024),
+                                               16, oo, 0, 0, 0);
+    }
+    const uint32_t ov = q0 + lane < a.Sq ? (uint32_t)((q0 + lane) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (__attribute__((address_space(3))) void*)cl, 4, ov, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(cl + 256), 4, ov, 0, 0, 0);
+  };
+  int slot = 0;
+  if constexpr (GL) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      rrow[u] = 32 * u + 8 * w + (lane >> 3);
+      lch[u] = (lane & 7) ^ ((rrow[u] >> 1) & 7);
+    }
+    if (ntiles > 0) {
+      issue(qstart, 0);
+      issue(qstart + 64, 1);  // (past the end: zeros, or rows never used)
+    }
+  } else if (ntiles > 0) {
     tile_load(tq, Q, a.qss, qstart, a.Sq);
     tile_load(td, dO, a.oss, qstart, a.Sq);
     load_vec(qstart);
   }
   for (int t = 0; t < ntiles; ++t) {
     const int q0 = qstart + t * 64;
-    __syncthreads();
-    tile_store(tq, sq);
-    tile_store(td, sdo);
-    if (threadIdx.x < 64) {
-      slse[threadIdx.x] = lreg;
-      sdv[threadIdx.x] = dreg;
-    }
-    __syncthreads();
-    if (t + 1 < ntiles) {
-      tile_load(tq, Q, a.qss, q0 + 64, a.Sq);
-      tile_load(td, dO, a.oss, q0 + 64, a.Sq);
-      load_vec(q0 + 64);
+    char* cq_;
+    char* cdo_;
+    float* cl_;
+    float* cv_;
+    if constexpr (GL) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile t landed (tile t + 1's 6 instructions may not have)
+      __syncthreads();  // ... for every wave; every wave is done with tile t - 1's stage
+      issue(q0 + 128, slot == 0 ? 2 : slot - 1);
+      cq_ = ring + slot * DKR_STG;
+      cdo_ = cq_ + 8192;
+      cl_ = reinterpret_cast<float*>(cdo_ + 8192);
+      cv_ = cl_ + 64;
+      slot = slot == 2 ? 0 : slot + 1;
+    } else {
+      __syncthreads();
+      tile_store(tq, sq);
+      tile_store(td, sdo);
+      if (threadIdx.x < 64) {
+        slse[threadIdx.x] = lreg;
+        sdv[threadIdx.x] = dreg;
+      }
+      __syncthreads();
+      if (t + 1 < ntiles) {
+        tile_load(tq, Q, a.qss, q0 + 64, a.Sq);
+        tile_load(td, dO, a.oss, q0 + 64, a.Sq);
+        load_vec(q0 + 64);
+      }
+      cq_ = sq;
+      cdo_ = sdo;
+      cl_ = slse;
+      cv_ = sdv;
     }
     const bool diag = a.causal && (k0w + 16 * KT - 1 > q0 + off);  // wave-uniform
 #pragma unroll
@@ -453,8 +534,8 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int qs = 2 * kq + hh;
-        const v8bf q0f = frag_row(sq, 16 * qs, 0, lane), q1f = frag_row(sq, 16 * qs, 1, lane);
-        const v8bf d0f = frag_row(sdo, 16 * qs, 0, lane), d1f = frag_row(sdo, 16 * qs, 1, lane);
+        const v8bf q0f = frag_row(cq_, 16 * qs, 0, lane), q1f = frag_row(cq_, 16 * qs, 1, lane);
+        const v8bf d0f = frag_row(cdo_, 16 * qs, 0, lane), d1f = frag_row(cdo_, 16 * qs, 1, lane);
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
           v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
@@ -470,7 +551,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
             const int ql = 16 * qs + 4 * G + r, qi = q0 + ql;
             float x = fmaf(s[r], c, km[kt]);
             if (diag && key > qi + off) x = -INFINITY;
-            const float p = ex2(x - slse[ql]);
+            const float p = ex2(x - cl_[ql]);
             float pd = p, dpv = dp[r];
             if (drop) {
               // bits of row r live in the quad lane whose field index is r
@@ -482,7 +563,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
               dpv = z ? dpv * a.inv_keep : 0.f;
             }
             P[hh][kt][r] = pd;
-            dS[hh][kt][r] = p * (dpv - sdv[ql]);
+            dS[hh][kt][r] = p * (dpv - cv_[ql]);
           }
         }
       }
@@ -491,12 +572,20 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
       for (int kt = 0; kt < KT; ++kt) {
         pf[kt] = pack_slots(P[0][kt], P[1][kt]);
         sf[kt] = pack_slots(dS[0][kt], dS[1][kt]);
-        if constexpr (DS) {
+        if constexpr (DS == 2) {
+          // queries 32 kq + 4 G (+16): 16-B chunks 4 kq + G / 2 (+2), 8-B half G & 1, chunk XOR-swizzled by the row
+          const uint4 u = __builtin_bit_cast(uint4, sf[kt]);
+          const int kl = w * 16 * KT + 16 * kt + i, c0 = 4 * kq + (G >> 1), hf = (G & 1) * 8;
+          *reinterpret_cast<uint2*>(sds + kl * 128 + ((c0 ^ (kl & 7)) << 4) + hf) = make_uint2(u.x, u.y);
+          *reinterpret_cast<uint2*>(sds + kl * 128 + (((c0 + 2) ^ (kl & 7)) << 4) + hf) = make_uint2(u.z, u.w);
+        }
+        if constexpr (DS == 1) {
           // dS^T for the dQ GEMM (attn_dq_ds_kernel): the lane's key row, queries 32 kq + 4 G .. + 3 and + 16
           const int key = k0w + 16 * kt + i;
           if (key < a.Sk) {
             const uint4 u = __builtin_bit_cast(uint4, sf[kt]);
-            bf16_t* row = a.ds + ((long)bh * a.Sk + key) * a.dsld + q0 + 32 * kq + 4 * G;
+            // (query-tile-major: the 64 queries of tile q0 / 64 for every key are one contiguous 128-B row)
+            bf16_t* row = a.ds + (((long)bh * (a.dsld >> 6) + (q0 >> 6)) * a.Sk + key) * 64 + 32 * kq + 4 * G;
             *reinterpret_cast<uint2*>(row) = make_uint2(u.x, u.y);
             *reinterpret_cast<uint2*>(row + 16) = make_uint2(u.z, u.w);
           }
@@ -504,8 +593,8 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const v8bf dof = frag_tr(sdo, 32 * kq, 16 * dt, lane);
-        const v8bf qtf = frag_tr(sq, 32 * kq, 16 * dt, lane);
+        const v8bf dof = frag_tr(cdo_, 32 * kq, 16 * dt, lane);
+        const v8bf qtf = frag_tr(cq_, 32 * kq, 16 * dt, lane);
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
           dv[dt][kt] = mfma(dof, pf[kt], dv[dt][kt]);
@@ -513,7 +602,19 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
         }
       }
     }
+    if constexpr (DS == 2) {
+      __syncthreads();  // the tile's dS^T is staged (the next tile writes sds only after its first barrier)
+#pragma unroll
+      for (int u = 0; u < KT * 2; ++u) {
+        const int c = threadIdx.x + 256 * u, kl = c >> 3, ch = c & 7, key = kblk * BN + kl;
+        if (key < a.Sk) {
+          const uint4 v = *reinterpret_cast<const uint4*>(sds + kl * 128 + ((ch ^ (kl & 7)) << 4));
+          *reinterpret_cast<uint4*>(a.ds + (((long)bh * (a.dsld >> 6) + (q0 >> 6)) * a.Sk + key) * 64 + ch * 8) = v;
+        }
+      }
+    }
   }
+  if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outstanding at exit
   bf16_t* dK = a.dk + kb;
   bf16_t* dV = a.dv + kb;
 #pragma unroll
@@ -530,17 +631,19 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
 }
 
 // key block kblk walks the query tiles from its diagonal on (causal): heavy = small kblk
-template <int KT, bool DS>
+template <int KT, int DS, bool GL>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a, int nblk) {
-  __shared__ __attribute__((aligned(16))) char sq[64 * 128];
-  __shared__ __attribute__((aligned(16))) char sdo[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sq[GL ? 16 : 64 * 128];
+  __shared__ __attribute__((aligned(16))) char sdo[GL ? 16 : 64 * 128];
+  __shared__ __attribute__((aligned(16))) char sds[DS == 2 ? 64 * KT * 128 : 16];
+  __shared__ __attribute__((aligned(16))) char ring[GL ? 3 * DKR_STG : 16];
   __shared__ float slse[64], sdv[64];
   for (int pass = 0; pass < 2; ++pass) {
     int blk = pair_block(a.causal, nblk, pass);
     if (blk < 0) break;
     blk = nblk - 1 - blk;  // (pair_block orders by descending index; here the heavy blocks are the low ones)
     if (pass) __syncthreads();
-    attn_dkdv_body<KT, DS>(a, blk, sq, sdo, slse, sdv);
+    attn_dkdv_body<KT, DS, GL>(a, blk, sq, sdo, slse, sdv, sds, ring);
   }
 }
 
@@ -683,11 +786,13 @@ __global__ void __launch_bounds__(256, MINW) attn_bwd_dq_kernel(AttnArgs a, int 
 }
 
 // dQ = scale * dS K from the dS^T scratch the dK/dV kernel wrote (a memory-bound GEMM: no score recompute, no
-// exponentials, no dropout hashes). Block: 4 waves x 16 queries over 64-key tiles (register-staged, two LDS
-// buffers, one barrier per tile); causal: only the key tiles up to the diagonal (exactly the tiles written).
+// exponentials, no dropout hashes). Block: 4 waves x 16 queries of one query tile over 64-key tiles; the tile's dS^T
+// strip is contiguous (64 keys x 128 B per K-tile). LDS-DMA staged through a 3-stage ring (two tiles in flight under
+// the MFMAs, counted vmcnt waits: register-staged loads made the compiler drain the queue every tile), one barrier
+// per tile; causal: only the key tiles up to the diagonal (exactly the tiles the dK/dV kernel wrote).
 __global__ void __launch_bounds__(256) attn_dq_ds_kernel(AttnArgs a, int nqt) {
-  __shared__ __attribute__((aligned(16))) char sd[2][64 * 128];
-  __shared__ __attribute__((aligned(16))) char sk[2][64 * 128];
+  constexpr int NS = 3, TB = 64 * 128;  // ring stages; bytes of one [64][64] bf16 tile
+  __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qt = nqt - 1 - (int)blockIdx.x;  // heavy (late) query tiles first under causal masking
@@ -696,33 +801,64 @@ __global__ void __launch_bounds__(256) attn_dq_ds_kernel(AttnArgs a, int nqt) {
   int kend = a.Sk;
   if (a.causal) kend = min(a.Sk, q0 + 64 + off);
   const int ntiles = kend > 0 ? (kend + 63) / 64 : 0;
-  const bf16_t* D = a.ds + (long)bh * a.Sk * a.dsld + q0;
+  const bf16_t* D = a.ds + ((long)bh * (a.dsld >> 6) + qt) * a.Sk * 64;
   const bf16_t* K = a.k + b * a.ksb + h * a.ksh;
-  TileRegs td, tk;
+  // LDS-DMA: a wave instruction fills 1 KiB = 8 rows of a tile lane-linearly; each lane fetches the logical 16-B
+  // chunk that the swz() XOR swizzle puts at its physical slot; rows past Sk read zeros (range check)
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)D, (short)0, (int)((long)a.Sk * 128), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)K, (short)0, (int)(((long)(a.Sk - 1) * a.kss + 64) * 2), 0x00020000);
+  int rrow[2], lch[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = 32 * u + 8 * w + (lane >> 3);  // physical byte offset (4 u + w) KiB + 16 lane
+    rrow[u] = row;
+    lch[u] = (lane & 7) ^ ((row >> 1) & 7);
+  }
+  auto issue = [&](int t, int slot) {
+    char* sd = smem + slot * 2 * TB;
+    char* sk = sd + TB;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int key = t * 64 + rrow[u];
+      const bool ok = key < a.Sk;
+      const uint32_t od = ok ? (uint32_t)((key * 64 + lch[u] * 8) * 2) : 0x80000000u;
+      const uint32_t okk = ok ? (uint32_t)(((long)key * a.kss + lch[u] * 8) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (__attribute__((address_space(3))) void*)(sd + u * 4096 + w * 1024),
+                                               16, od, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)(sk + u * 4096 + w * 1024),
+                                               16, okk, 0, 0, 0);
+    }
+  };
   v4f acc[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) acc[dt] = v4f{0.f, 0.f, 0.f, 0.f};
-  if (ntiles > 0) {
-    tile_load(td, D, a.dsld, 0, a.Sk);
-    tile_load(tk, K, a.kss, 0, a.Sk);
-  }
+  // every step issues exactly one tile (4 DMA instructions per thread, past the end: zeros), so vmcnt(4) after the
+  // issue of tile t + 1 means tile t has landed
+  issue(0, 0);
+  issue(1, 1);
+  int slot = 0;
   for (int t = 0; t < ntiles; ++t) {
-    char* cd = sd[t & 1];
-    char* ck = sk[t & 1];
-    tile_store(td, cd);
-    tile_store(tk, ck);
-    __syncthreads();  // (the buffer written here was last read two tiles ago, before the previous barrier)
-    if (t + 1 < ntiles) {
-      tile_load(td, D, a.dsld, (t + 1) * 64, a.Sk);
-      tile_load(tk, K, a.kss, (t + 1) * 64, a.Sk);
-    }
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __syncthreads();  // tile t landed for every wave; every wave is done with the slot of tile t - 1
+    issue(t + 2, slot == 0 ? 2 : slot - 1);
+    const char* cd = smem + slot * 2 * TB;
+    const char* ck = cd + TB;
+    v8bf sf[2], kf[2][4];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const v8bf sf = frag_tr(cd, 32 * kk, 16 * w, lane);
+      sf[kk] = frag_tr(cd, 32 * kk, 16 * w, lane);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(frag_tr(ck, 32 * kk, 16 * dt, lane), sf, acc[dt]);
+      for (int dt = 0; dt < 4; ++dt) kf[kk][dt] = frag_tr(ck, 32 * kk, 16 * dt, lane);
     }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(kf[kk][dt], sf[kk], acc[dt]);
+    slot = slot == 2 ? 0 : slot + 1;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA into LDS outstanding when the block retires
   const int qi = q0 + 16 * w + i;
   if (qi < a.Sq) {
     bf16_t* dQ = a.dq + b * a.qsb + h * a.qsh + (long)qi * a.qss;
@@ -768,6 +904,15 @@ AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// DTF_ATTN_GLDS=1: the dK/dV kernel stages its query tiles through the LDS-DMA ring (attn_dkdv_body GL)
+bool attn_glds() {
+  static const bool on = [] {
+    const char* e = getenv("DTF_ATTN_GLDS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 }  // namespace
 
@@ -817,12 +962,16 @@ DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 2>), dim3(pair_grid(causal, nqb), (unsigned)(B * H)), dim3(256), 0, st,
                        a, nqb);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, false>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0,
-                     st, a, nkb);
+  if (attn_glds())
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 0, true>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256),
+                       0, st, a, nkb);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 0, false>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256),
+                       0, st, a, nkb);
   return (int)hipGetLastError();
 }
 
-// dtf_attn_bwd through a dS^T scratch (ds: bf16, >= B*H*Sk*round_up(Sq, 64) elements): D = rowsum(dO * O) by a
+// dtf_attn_bwd through a dS^T scratch (ds: bf16, >= B*H*round_up(Sq, 64)*Sk elements): D = rowsum(dO * O) by a
 // small pass, the dK/dV kernel also stores dS^T (the values its dK MFMAs use), and dQ = scale * dS K is a
 // memory-bound GEMM over the stored tiles instead of a second kernel that recomputes the scores, the
 // probabilities and dP (3 of the 5 backward MFMA products). Same results as dtf_attn_bwd up to the f32 order of
@@ -847,11 +996,18 @@ DTF_API int dtf_attn_bwd_ds(const void* q, const void* k, const void* v, const l
   a.dv = (bf16_t*)dv;
   a.ds = (bf16_t*)ds;
   a.dsld = (Sq + 63) / 64 * 64;
-  const long rows = (long)B * H * Sq;
-  hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)((rows + 255) / 256 < 4096 ? (rows + 255) / 256 : 4096)), dim3(256), 0, st, a);
+  const long blocks = ((long)B * H * Sq + 31) / 32;  // 32 rows per block
+  hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, st, a);
   const int nkb = (Sk + 127) / 128, nqt = (Sq + 63) / 64;
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, true>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0,
-                     st, a, nkb);
+  static const int stage = [] {  // DTF_ATTN_DS_STAGE=1: dS^T staged through LDS and stored as whole rows
+    const char* e = getenv("DTF_ATTN_DS_STAGE");
+    return e && e[0] == '1';
+  }();
+  const dim3 gk(pair_grid(causal, nkb), (unsigned)(B * H));
+  if (stage && attn_glds()) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 2, true>), gk, dim3(256), 0, st, a, nkb);
+  else if (stage) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 2, false>), gk, dim3(256), 0, st, a, nkb);
+  else if (attn_glds()) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 1, true>), gk, dim3(256), 0, st, a, nkb);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 1, false>), gk, dim3(256), 0, st, a, nkb);
   hipLaunchKernelGGL(attn_dq_ds_kernel, dim3((unsigned)nqt, (unsigned)(B * H)), dim3(256), 0, st, a, nqt);
   return (int)hipGetLastError();
 }
