@@ -51,6 +51,19 @@ struct AttnArgs {
   int dsld;         // Sq rounded up to 64
 };
 
+// XCD-aware block order: the hardware deals workgroups to the 8 XCDs round-robin by linear id, so the few blocks
+// of one (batch, head) — which all read the same K/V (or Q/dO, or K) tiles — would land on different XCDs and each
+// fetch those tiles into its own L2. The linear id is remapped bijectively so that every XCD owns one contiguous range
+// of (head, block) pairs: a head's blocks share one L2 and its operand tiles leave HBM once.
+__device__ __forceinline__ int xcd_linear() {
+  const int total = (int)(gridDim.x * gridDim.y);
+  const int L = (int)(blockIdx.x + gridDim.x * blockIdx.y);
+  const int xcd = L & 7, qq = total >> 3, rr = total & 7;
+  return (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (L >> 3);
+}
+__device__ __forceinline__ int attn_bx() { return xcd_linear() % (int)gridDim.x; }
+__device__ __forceinline__ int attn_by() { return xcd_linear() / (int)gridDim.x; }
+
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -162,7 +175,7 @@ __device__ __forceinline__ void stage_mask(float* smask, float mreg) {
 template <int QT, bool DROP>
 __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a, const int qblk, char* sk, char* sv, float* smask) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int bh = attn_by(), b = bh / a.H, h = bh % a.H;
   const int BM = 64 * QT;
   const int q0 = qblk * BM + w * 16 * QT;
   const bf16_t* Q = a.q + b * a.qsb + h * a.qsh;
@@ -330,7 +343,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a, const int qblk,
 // Causal launches pair the logical block x with nblk - 1 - x in one workgroup (heavy block first), so every
 // workgroup walks the same number of tiles; otherwise block x is logical block nblk - 1 - x.
 __device__ __forceinline__ int pair_block(int causal, int nblk, int pass) {
-  const int x = blockIdx.x;
+  const int x = attn_bx();
   if (!causal) return pass == 0 ? nblk - 1 - x : -1;
   const int heavy = nblk - 1 - x, light = x;
   return pass == 0 ? heavy : (light < heavy ? light : -1);
@@ -389,17 +402,12 @@ __global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
 
 // dK, dV: block = 4 waves x (16 KT) keys, loop over 64-query tiles; grid (cdiv(Sk, 64 KT), B*H).
 // Query subtiles are processed in pairs (one 32-query MFMA k-step) so only 2 x KT score tiles are live.
-// DS: 0 = no dS^T output, 1 = stored from the registers (8-B pieces), 2 = staged through LDS (sds, [64 KT keys]
-// [64 queries] swizzled) and stored as whole 128-B rows after each query tile
-// GL: the query tiles (Q, dO and their lse / D values) are staged by LDS-DMA through a 3-stage ring (ring, DKR_STG
-// bytes per stage) with counted vmcnt waits — two tiles in flight under the MFMAs — instead of register-staged
-// one-tile-ahead loads
-constexpr int DKR_STG = 2 * 64 * 128 + 2 * 64 * 4;
-template <int KT, int DS, bool GL>
+// DS: also store dS^T (the values the dK MFMAs use) for the dQ GEMM of the dS backward path
+template <int KT, bool DS>
 __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk, char* sq, char* sdo, float* slse,
-                                               float* sdv, char* sds, char* ring) {
+                                               float* sdv) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int bh = attn_by(), b = bh / a.H, h = bh % a.H;
   const int BN = 64 * KT;
   const int k0w = kblk * BN + w * 16 * KT;
   const long hb = b * a.qsb + h * a.qsh, kb = b * a.ksb + h * a.ksh, ob = b * a.osb + h * a.osh;
@@ -445,87 +453,25 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
       dreg = qi < a.Sq ? a.dvec[(long)bh * a.Sq + qi] : 0.f;
     }
   };
-  // LDS-DMA ring (GL): a wave instruction fills 1 KiB (8 rows) of a tile lane-linearly, each lane fetching the logical
-  // chunk the swz() swizzle puts at its slot; every wave also fills the tile's 64 lse and D values (identical data),
-  // so each wave issues exactly 6 instructions per tile. Rows past Sq read zeros (their lse 0 instead of +inf is
-  // harmless: zero Q / dO rows give zero dS, dK and dV contributions).
-  const __amdgpu_buffer_rsrc_t rq =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Q, (short)0, (int)(((long)(a.Sq - 1) * a.qss + 64) * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ro =
-      __builtin_amdgcn_make_buffer_rsrc((void*)dO, (short)0, (int)(((long)(a.Sq - 1) * a.oss + 64) * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rl =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.lse + (long)bh * a.Sq), (short)0, a.Sq * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.dvec + (long)bh * a.Sq), (short)0, a.Sq * 4, 0x00020000);
-  int rrow[2] = {0, 0}, lch[2] = {0, 0};
-  auto issue = [&](int q0, int slot) {
-    char* cq = ring + slot * DKR_STG;
-    char* cd = cq + 8192;
-    char* cl = cd + 8192;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = q0 + rrow[u];
-      const bool ok = q < a.Sq;
-      const uint32_t oq = ok ? (uint32_t)(((long)q * a.qss + lch[u] * 8) * 2) : 0x80000000u;
-      const uint32_t oo = ok ? (uint32_t)(((long)q * a.oss + lch[u] * 8) * 2) : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (__attribute__((address_space(3))) void*)(cq + u * 4096 + w * 1024),
-                                               16, oq, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (__attribute__((address_space(3))) void*)(cd + u * 4096 + w * 1024),
-                                               16, oo, 0, 0, 0);
-    }
-    const uint32_t ov = q0 + lane < a.Sq ? (uint32_t)((q0 + lane) * 4) : 0x80000000u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (__attribute__((address_space(3))) void*)cl, 4, ov, 0, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(cl + 256), 4, ov, 0, 0, 0);
-  };
-  int slot = 0;
-  if constexpr (GL) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      rrow[u] = 32 * u + 8 * w + (lane >> 3);
-      lch[u] = (lane & 7) ^ ((rrow[u] >> 1) & 7);
-    }
-    if (ntiles > 0) {
-      issue(qstart, 0);
-      issue(qstart + 64, 1);  // (past the end: zeros, or rows never used)
-    }
-  } else if (ntiles > 0) {
+  if (ntiles > 0) {
     tile_load(tq, Q, a.qss, qstart, a.Sq);
     tile_load(td, dO, a.oss, qstart, a.Sq);
     load_vec(qstart);
   }
   for (int t = 0; t < ntiles; ++t) {
     const int q0 = qstart + t * 64;
-    char* cq_;
-    char* cdo_;
-    float* cl_;
-    float* cv_;
-    if constexpr (GL) {
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // tile t landed (tile t + 1's 6 instructions may not have)
-      __syncthreads();  // ... for every wave; every wave is done with tile t - 1's stage
-      issue(q0 + 128, slot == 0 ? 2 : slot - 1);
-      cq_ = ring + slot * DKR_STG;
-      cdo_ = cq_ + 8192;
-      cl_ = reinterpret_cast<float*>(cdo_ + 8192);
-      cv_ = cl_ + 64;
-      slot = slot == 2 ? 0 : slot + 1;
-    } else {
-      __syncthreads();
-      tile_store(tq, sq);
-      tile_store(td, sdo);
-      if (threadIdx.x < 64) {
-        slse[threadIdx.x] = lreg;
-        sdv[threadIdx.x] = dreg;
-      }
-      __syncthreads();
-      if (t + 1 < ntiles) {
-        tile_load(tq, Q, a.qss, q0 + 64, a.Sq);
-        tile_load(td, dO, a.oss, q0 + 64, a.Sq);
-        load_vec(q0 + 64);
-      }
-      cq_ = sq;
-      cdo_ = sdo;
-      cl_ = slse;
-      cv_ = sdv;
+    __syncthreads();
+    tile_store(tq, sq);
+    tile_store(td, sdo);
+    if (threadIdx.x < 64) {
+      slse[threadIdx.x] = lreg;
+      sdv[threadIdx.x] = dreg;
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) {
+      tile_load(tq, Q, a.qss, q0 + 64, a.Sq);
+      tile_load(td, dO, a.oss, q0 + 64, a.Sq);
+      load_vec(q0 + 64);
     }
     const bool diag = a.causal && (k0w + 16 * KT - 1 > q0 + off);  // wave-uniform
 #pragma unroll
@@ -534,8 +480,8 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int qs = 2 * kq + hh;
-        const v8bf q0f = frag_row(cq_, 16 * qs, 0, lane), q1f = frag_row(cq_, 16 * qs, 1, lane);
-        const v8bf d0f = frag_row(cdo_, 16 * qs, 0, lane), d1f = frag_row(cdo_, 16 * qs, 1, lane);
+        const v8bf q0f = frag_row(sq, 16 * qs, 0, lane), q1f = frag_row(sq, 16 * qs, 1, lane);
+        const v8bf d0f = frag_row(sdo, 16 * qs, 0, lane), d1f = frag_row(sdo, 16 * qs, 1, lane);
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
           v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
@@ -551,7 +497,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
             const int ql = 16 * qs + 4 * G + r, qi = q0 + ql;
             float x = fmaf(s[r], c, km[kt]);
             if (diag && key > qi + off) x = -INFINITY;
-            const float p = ex2(x - cl_[ql]);
+            const float p = ex2(x - slse[ql]);
             float pd = p, dpv = dp[r];
             if (drop) {
               // bits of row r live in the quad lane whose field index is r
@@ -563,7 +509,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
               dpv = z ? dpv * a.inv_keep : 0.f;
             }
             P[hh][kt][r] = pd;
-            dS[hh][kt][r] = p * (dpv - cv_[ql]);
+            dS[hh][kt][r] = p * (dpv - sdv[ql]);
           }
         }
       }
@@ -572,14 +518,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
       for (int kt = 0; kt < KT; ++kt) {
         pf[kt] = pack_slots(P[0][kt], P[1][kt]);
         sf[kt] = pack_slots(dS[0][kt], dS[1][kt]);
-        if constexpr (DS == 2) {
-          // queries 32 kq + 4 G (+16): 16-B chunks 4 kq + G / 2 (+2), 8-B half G & 1, chunk XOR-swizzled by the row
-          const uint4 u = __builtin_bit_cast(uint4, sf[kt]);
-          const int kl = w * 16 * KT + 16 * kt + i, c0 = 4 * kq + (G >> 1), hf = (G & 1) * 8;
-          *reinterpret_cast<uint2*>(sds + kl * 128 + ((c0 ^ (kl & 7)) << 4) + hf) = make_uint2(u.x, u.y);
-          *reinterpret_cast<uint2*>(sds + kl * 128 + (((c0 + 2) ^ (kl & 7)) << 4) + hf) = make_uint2(u.z, u.w);
-        }
-        if constexpr (DS == 1) {
+        if constexpr (DS) {
           // dS^T for the dQ GEMM (attn_dq_ds_kernel): the lane's key row, queries 32 kq + 4 G .. + 3 and + 16
           const int key = k0w + 16 * kt + i;
           if (key < a.Sk) {
@@ -593,8 +532,8 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const v8bf dof = frag_tr(cdo_, 32 * kq, 16 * dt, lane);
-        const v8bf qtf = frag_tr(cq_, 32 * kq, 16 * dt, lane);
+        const v8bf dof = frag_tr(sdo, 32 * kq, 16 * dt, lane);
+        const v8bf qtf = frag_tr(sq, 32 * kq, 16 * dt, lane);
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
           dv[dt][kt] = mfma(dof, pf[kt], dv[dt][kt]);
@@ -602,19 +541,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
         }
       }
     }
-    if constexpr (DS == 2) {
-      __syncthreads();  // the tile's dS^T is staged (the next tile writes sds only after its first barrier)
-#pragma unroll
-      for (int u = 0; u < KT * 2; ++u) {
-        const int c = threadIdx.x + 256 * u, kl = c >> 3, ch = c & 7, key = kblk * BN + kl;
-        if (key < a.Sk) {
-          const uint4 v = *reinterpret_cast<const uint4*>(sds + kl * 128 + ((ch ^ (kl & 7)) << 4));
-          *reinterpret_cast<uint4*>(a.ds + (((long)bh * (a.dsld >> 6) + (q0 >> 6)) * a.Sk + key) * 64 + ch * 8) = v;
-        }
-      }
-    }
   }
-  if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outstanding at exit
   bf16_t* dK = a.dk + kb;
   bf16_t* dV = a.dv + kb;
 #pragma unroll
@@ -631,19 +558,17 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
 }
 
 // key block kblk walks the query tiles from its diagonal on (causal): heavy = small kblk
-template <int KT, int DS, bool GL>
+template <int KT, bool DS>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a, int nblk) {
-  __shared__ __attribute__((aligned(16))) char sq[GL ? 16 : 64 * 128];
-  __shared__ __attribute__((aligned(16))) char sdo[GL ? 16 : 64 * 128];
-  __shared__ __attribute__((aligned(16))) char sds[DS == 2 ? 64 * KT * 128 : 16];
-  __shared__ __attribute__((aligned(16))) char ring[GL ? 3 * DKR_STG : 16];
+  __shared__ __attribute__((aligned(16))) char sq[64 * 128];
+  __shared__ __attribute__((aligned(16))) char sdo[64 * 128];
   __shared__ float slse[64], sdv[64];
   for (int pass = 0; pass < 2; ++pass) {
     int blk = pair_block(a.causal, nblk, pass);
     if (blk < 0) break;
     blk = nblk - 1 - blk;  // (pair_block orders by descending index; here the heavy blocks are the low ones)
     if (pass) __syncthreads();
-    attn_dkdv_body<KT, DS, GL>(a, blk, sq, sdo, slse, sdv, sds, ring);
+    attn_dkdv_body<KT, DS>(a, blk, sq, sdo, slse, sdv);
   }
 }
 
@@ -651,7 +576,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a, int n
 template <int QT>
 __device__ __forceinline__ void attn_dq_body(const AttnArgs& a, const int qblk, char* sk, char* sv, float* smask) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int bh = attn_by(), b = bh / a.H, h = bh % a.H;
   const int BM = 64 * QT;
   const int q0 = qblk * BM + w * 16 * QT;
   const long hb = b * a.qsb + h * a.qsh, kb = b * a.ksb + h * a.ksh, ob = b * a.osb + h * a.osh;
@@ -794,8 +719,8 @@ __global__ void __launch_bounds__(256) attn_dq_ds_kernel(AttnArgs a, int nqt) {
   constexpr int NS = 3, TB = 64 * 128;  // ring stages; bytes of one [64][64] bf16 tile
   __shared__ __attribute__((aligned(16))) char smem[NS * 2 * TB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qt = nqt - 1 - (int)blockIdx.x;  // heavy (late) query tiles first under causal masking
+  const int bh = attn_by(), b = bh / a.H, h = bh % a.H;
+  const int qt = nqt - 1 - attn_bx();  // heavy (late) query tiles first under causal masking
   const int q0 = qt * 64;
   const int off = a.Sk - a.Sq;
   int kend = a.Sk;
@@ -905,14 +830,7 @@ AttnArgs make_args(const void* q, const void* k, const void* v, const long* qstr
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// DTF_ATTN_GLDS=1: the dK/dV kernel stages its query tiles through the LDS-DMA ring (attn_dkdv_body GL)
-bool attn_glds() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_ATTN_GLDS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+
 
 }  // namespace
 
@@ -962,12 +880,8 @@ DTF_API int dtf_attn_bwd(const void* q, const void* k, const void* v, const long
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<2, 2>), dim3(pair_grid(causal, nqb), (unsigned)(B * H)), dim3(256), 0, st,
                        a, nqb);
-  if (attn_glds())
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 0, true>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256),
-                       0, st, a, nkb);
-  else
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 0, false>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256),
-                       0, st, a, nkb);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, false>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0,
+                     st, a, nkb);
   return (int)hipGetLastError();
 }
 
@@ -999,15 +913,8 @@ DTF_API int dtf_attn_bwd_ds(const void* q, const void* k, const void* v, const l
   const long blocks = ((long)B * H * Sq + 31) / 32;  // 32 rows per block
   hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, st, a);
   const int nkb = (Sk + 127) / 128, nqt = (Sq + 63) / 64;
-  static const int stage = [] {  // DTF_ATTN_DS_STAGE=1: dS^T staged through LDS and stored as whole rows
-    const char* e = getenv("DTF_ATTN_DS_STAGE");
-    return e && e[0] == '1';
-  }();
-  const dim3 gk(pair_grid(causal, nkb), (unsigned)(B * H));
-  if (stage && attn_glds()) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 2, true>), gk, dim3(256), 0, st, a, nkb);
-  else if (stage) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 2, false>), gk, dim3(256), 0, st, a, nkb);
-  else if (attn_glds()) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 1, true>), gk, dim3(256), 0, st, a, nkb);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, 1, false>), gk, dim3(256), 0, st, a, nkb);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<2, true>), dim3(pair_grid(causal, nkb), (unsigned)(B * H)), dim3(256), 0,
+                     st, a, nkb);
   hipLaunchKernelGGL(attn_dq_ds_kernel, dim3((unsigned)nqt, (unsigned)(B * H)), dim3(256), 0, st, a, nqt);
   return (int)hipGetLastError();
 }
