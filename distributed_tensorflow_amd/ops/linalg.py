@@ -125,14 +125,25 @@ def colsum(x2d, out=None, accumulate=False):
     return out
 
 
-# Every GEMM runs on the hand-written MFMA kernels by default. DTF_PLAIN_BLAS=1 sends the plain (epilogue-free)
-# backward GEMMs to hipBLASLt (torch.mm) instead: standalone it is faster on the data-gradient shapes
-# (tools/bench_blas_plain.py), but with the weight gradients overlapped on the side stream the end-to-end numbers
-# are BERT-base 789k (ours) vs 777k tok/s (hipBLASLt), GPT-2-medium 219k vs 225k, fp8 226k vs 228k.
-_PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "0") == "1"
+# The plain (epilogue-free) backward GEMMs of the dense layers go to hipBLASLt (torch.mm / addmm into the f32 arena):
+# plain library GEMMs, faster than ours on these shapes (tools/bench_blas_plain.py). Round 2 measured them a loss end
+# to end (BERT-base 789k vs 777k tok/s); with round 4's hipBLASLt forward projections and attention changes they win
+# (interleaved A/B, one box): GPT-2-medium 254.1k / 252.7k vs 235.7k / 233.9k tok/s, BERT-base 908.2k / 908.6k vs
+# 887.9k / 885.4k. Fused-epilogue backward GEMMs (activation backward, residual-link accumulation, fp8) stay on
+# ours. DTF_PLAIN_BLAS=0: every backward GEMM on ours.
+_PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "1") != "0"
+# DTF_PLAIN_DACT=1: keep the consumer-fused activation backward (our GEMM) for FFN2's data gradient under _PLAIN_BLAS
+_PLAIN_DACT = __import__("os").environ.get("DTF_PLAIN_DACT", "0") == "1"
 # Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream
 DENSE_SIDE_ON = SIDE_STREAM_ON and __import__("os").environ.get("DTF_DENSE_WGRAD_STREAM", "1") != "0"
 _BLAS_WGRAD_MIN = 4 << 20
+# Activation-free forward projections of at least DTF_BLAS_FWD_MIN multiply-adds (a plain GEMM + bias: GPT-2 / BERT
+# QKV and FFN2, the LM head) on hipBLASLt (F.linear with the bf16 bias shadow); the fused-epilogue GEMMs (GELU with
+# its pre-activation side output, residual/ReLU links) and the small projections stay on ours. Measured end to end
+# (round 4, interleaved A/B on one box): GPT-2-medium 234.1k / 235.2k vs 224.1k / 224.7k tok/s, BERT-base
+# 885.6k / 878.9k vs 856.2k / 856.6k. DTF_BLAS_FWD=0: every forward GEMM on ours.
+_BLAS_FWD = __import__("os").environ.get("DTF_BLAS_FWD", "1") != "0"
+_BLAS_FWD_MIN = float(__import__("os").environ.get("DTF_BLAS_FWD_MIN", str(4 * 2 ** 30)))  # (16G: -1%)
 _SPLIT_DGRAD_K = int(__import__("os").environ.get("DTF_SPLIT_DGRAD_K", "8192"))  # 0 disables the split route
 
 
@@ -210,7 +221,11 @@ class _DenseFn(torch.autograd.Function):
             x2 = x2.contiguous()
         w16 = bf16_shadow(w)
         pre = torch.empty((x2.shape[0], w.shape[0]), dtype=BF16, device=x.device) if act else None
-        y = gemm(x2, w16, bias=b, act=act, aux=pre)
+        if (_BLAS_FWD and not act and x2.is_cuda
+                and float(x2.shape[0]) * w.shape[0] * x2.shape[1] >= _BLAS_FWD_MIN):
+            y = torch.nn.functional.linear(x2, w16, bf16_shadow(b) if b is not None else None)
+        else:
+            y = gemm(x2, w16, bias=b, act=act, aux=pre)
         ctx.save_for_backward(x2, w, pre)
         ctx.act = act
         ctx.has_b = b is not None
@@ -243,7 +258,7 @@ class _DenseFn(torch.autograd.Function):
             acc = ctx.link.take()[0] if ctx.link is not None else None
             isrc = ctx.in_src
             ctx.in_src = None
-            if (acc is None and isrc is not None and isrc.consumers == 1 and not _PLAIN_BLAS
+            if (acc is None and isrc is not None and isrc.consumers == 1 and (_PLAIN_DACT or not _PLAIN_BLAS)
                     and isrc.pre.shape == (dz.shape[0], w.shape[1])):
                 # the producer's activation backward in this GEMM's epilogue
                 dx = torch.empty((dz.shape[0], w.shape[1]), dtype=BF16, device=dz.device)
