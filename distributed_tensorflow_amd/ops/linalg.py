@@ -132,8 +132,8 @@ def colsum(x2d, out=None, accumulate=False):
 # 887.9k / 885.4k. Fused-epilogue backward GEMMs (activation backward, residual-link accumulation, fp8) stay on
 # ours. DTF_PLAIN_BLAS=0: every backward GEMM on ours.
 _PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "1") != "0"
-# DTF_PLAIN_DACT=1: keep the consumer-fused activation backward (our GEMM) for FFN2's data gradient under _PLAIN_BLAS
-_PLAIN_DACT = __import__("os").environ.get("DTF_PLAIN_DACT", "0") == "1"
+# (keeping the consumer-fused activation backward on our GEMM for FFN2's data gradient under _PLAIN_BLAS measured
+# 255.3-255.6k vs 257.2-257.6k tok/s: the library GEMM + the activation pass win)
 # Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream
 DENSE_SIDE_ON = SIDE_STREAM_ON and __import__("os").environ.get("DTF_DENSE_WGRAD_STREAM", "1") != "0"
 _BLAS_WGRAD_MIN = 4 << 20
@@ -258,7 +258,7 @@ class _DenseFn(torch.autograd.Function):
             acc = ctx.link.take()[0] if ctx.link is not None else None
             isrc = ctx.in_src
             ctx.in_src = None
-            if (acc is None and isrc is not None and isrc.consumers == 1 and (_PLAIN_DACT or not _PLAIN_BLAS)
+            if (acc is None and isrc is not None and isrc.consumers == 1 and not _PLAIN_BLAS
                     and isrc.pre.shape == (dz.shape[0], w.shape[1])):
                 # the producer's activation backward in this GEMM's epilogue
                 dx = torch.empty((dz.shape[0], w.shape[1]), dtype=BF16, device=dz.device)
