@@ -256,9 +256,23 @@ def join_side_streams():
     _drop_holds()  # the main stream is ordered after every side read now
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_GET_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream(device=None):
     """Raw handle of the current stream of `device` (default: the current device). Pass the device of the tensors
-    a native call touches when it may differ from the current device."""
+    a native call touches when it may differ from the current device. (Every kernel launch asks for it: the raw
+    accessor skips building a torch.cuda.Stream object — a few microseconds of host time per launch, which adds up
+    to milliseconds per training step of a launch-heavy model.)"""
+    if _RAW_STREAM is not None and _GET_DEVICE is not None:
+        if device is None:
+            idx = _GET_DEVICE()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = device.index if device.index is not None else _GET_DEVICE()
+        return _RAW_STREAM(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

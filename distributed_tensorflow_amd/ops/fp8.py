@@ -128,10 +128,27 @@ def _wgrad_splits(M, N, K, ws_elems):
     return s
 
 
+class _Views:
+    """The state buffer with its slices cached: every projection call takes ~10 one-element views of it, and building
+    a tensor view costs microseconds of host time (a launch-heavy fp8 step is host-bound on a slow CPU)."""
+    __slots__ = ("t", "c")
+
+    def __init__(self, t):
+        self.t, self.c = t, {}
+
+    def __getitem__(self, k):
+        key = (k.start, k.stop) if isinstance(k, slice) else k
+        v = self.c.get(key)
+        if v is None:
+            v = self.c[key] = self.t[k]
+        return v
+
+
 class _Fp8State:
     def __init__(self, dev):
         self.buf = torch.zeros(10, dtype=F32, device=dev)
         self.buf[W_SCALE] = 1.0
+        self.bv = _Views(self.buf)
         self.x_ready = False
         self.g_ready = False
         self.tx = 0  # forward / backward / weight step counters: parity of the double-buffered amax slots
@@ -161,7 +178,7 @@ def _weight_fp8(st, w, need_t):
         return st.wq, st.wqT
     w16 = bf16_shadow(w)
     N, K = w16.shape
-    buf = st.buf
+    buf = st.bv
     if need_t and _W_DELAYED and not torch.cuda.is_current_stream_capturing():
         cur, prev = (W_AMAX, W_AMAX2) if st.tw % 2 == 0 else (W_AMAX2, W_AMAX)
         st.tw += 1
@@ -175,12 +192,12 @@ def _weight_fp8(st, w, need_t):
             st.w_prev = prev
     elif need_t:
         # exact per-tensor scale (amax/448) computed on the device; W and W^T from one transposing pass
-        st.wq, st.wqT, _ = quantize_t(w16, exact_out=st.buf[W_SCALE:W_SCALE + 1])
+        st.wq, st.wqT, _ = quantize_t(w16, exact_out=st.bv[W_SCALE:W_SCALE + 1])
     else:
         if st.wq is None or st.wq.shape != w16.shape:
             st.wq = torch.empty(w16.shape, dtype=torch.uint8, device=w16.device)
         ws = workspace(w16.device)
-        call("dtf_quant_fp8_exact", ptr(w16), ptr(st.wq), w16.numel(), ptr(st.buf[W_SCALE:W_SCALE + 1]), ptr(ws),
+        call("dtf_quant_fp8_exact", ptr(w16), ptr(st.wq), w16.numel(), ptr(st.bv[W_SCALE:W_SCALE + 1]), ptr(ws),
              stream())
         st.wqT = None
     st.w_key = key
@@ -230,7 +247,7 @@ class _DenseFP8(torch.autograd.Function):
     def forward(ctx, x, w, b, act, st, nxt=None):
         shp = x.shape
         N = w.shape[0]
-        buf = st.buf
+        buf = st.bv
         pend, st.pending_x = st.pending_x, None
         ctx.src = None
         if pend is not None and x.data_ptr() == pend[0]:
@@ -268,7 +285,7 @@ class _DenseFP8(torch.autograd.Function):
             wq, wqT = _weight_fp8(st, w, True)
             yq = torch.empty((M, N), dtype=torch.uint8, device=x.device)
             yqT = torch.empty((N, M), dtype=torch.uint8, device=x.device)
-            nb = nst.buf
+            nb = nst.bv
             if _gemm_q8(xq, wq, buf[X_SCALE:X_SCALE + 2], None, fmt_a=0, q8=yq, q8T=yqT, q8col=None, q8fmt=0,
                         q8buf=nb, q8scale=X_SCALE, q8cur=ncur, q8prev=nprev, q8used2=nb[X_USED:X_USED + 1],
                         bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1]):
@@ -325,7 +342,7 @@ class _DenseFP8(torch.autograd.Function):
             return _DenseFP8._backward_bf16(ctx, dy)
         xqT, w, pre = ctx.saved_tensors
         st, (M, K, N) = ctx.st, ctx.MKN
-        buf = st.buf
+        buf = st.bv
         gs, ga = buf[G_SCALE:G_SCALE + 1], buf[G_AMAX:G_AMAX + 1]
         need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         need_db = ctx.has_b and ctx.needs_input_grad[2]
@@ -359,7 +376,7 @@ class _DenseFP8(torch.autograd.Function):
                 # our input came from the producer's fp8 epilogue: quantize ITS gradient here (the activation
                 # backward from its saved pre-activation, e5m2 + transpose + bias-gradient column partials)
                 pst, ppre, pact = src
-                pb = pst.buf
+                pb = pst.bv
                 pcur, pprev = (G_AMAX, G_AMAX2) if pst.tg % 2 == 0 else (G_AMAX2, G_AMAX)
                 gq = torch.empty((M, K), dtype=torch.uint8, device=dy.device)
                 gqT = torch.empty((K, M), dtype=torch.uint8, device=dy.device)
@@ -386,7 +403,7 @@ class _DenseFP8(torch.autograd.Function):
         tw = direct_grad(w) if need_dw else None
         tb = direct_grad(ctx.b_param) if need_db else None
         # arena-accumulated weight / bias gradients go to the side stream (off the dgrad critical path)
-        side = (fork_side(dy.device, dzqT, xqT, cp, buf) if (tw is not None and DENSE_SIDE_ON)
+        side = (fork_side(dy.device, dzqT, xqT, cp, st.buf) if (tw is not None and DENSE_SIDE_ON)
                 else contextlib.nullcontext())
         with side:
             if need_dw:  # dW[N, K] (+)= dZ^T X over the M tokens; inside Model.train_step straight into the arena
