@@ -97,7 +97,8 @@ _blaslt_ok = [True]
 
 
 def _use_blaslt(M, N, K, role, force=False):
-    return bool(_BLASLT & role) and _blaslt_ok[0] and (force or float(M) * N * K >= _BLASLT_MIN_MNK)
+    return (bool(_BLASLT & role) and _blaslt_ok[0] and (force or float(M) * N * K >= _BLASLT_MIN_MNK)
+            and not torch.cuda.is_current_stream_capturing())  # (see linalg._lib_ok)
 
 
 def _gemm_blaslt(a, b, sa, sb, *, fmt_a=0, out_dtype=BF16, bias=None):

@@ -147,11 +147,18 @@ _BLAS_FWD_MIN = float(__import__("os").environ.get("DTF_BLAS_FWD_MIN", str(4 * 2
 _SPLIT_DGRAD_K = int(__import__("os").environ.get("DTF_SPLIT_DGRAD_K", "8192"))  # 0 disables the split route
 
 
+def _lib_ok(t):
+    """hipBLASLt routes only outside a hipGraph capture: under capture a library call that needs a fresh workspace or
+    heuristic query fails (HIPBLAS_STATUS_INTERNAL_ERROR) and torch's rocBLAS fallback is not capturable; captured
+    steps keep every GEMM on our kernels."""
+    return t.is_cuda and not torch.cuda.is_current_stream_capturing()
+
+
 def dense_dgrad(dz, w16, acc=None):
     """dX[T, in] = dZ[T, out] W[out, in] (bf16); with `acc` (another gradient of the same input, [T, in], parked on
     a ResidualGradLink: no other reader) the GEMM adds it in its store pass and returns it — no separate add pass,
     the same values as the GEMM followed by an elementwise add."""
-    if _PLAIN_BLAS:
+    if _PLAIN_BLAS and _lib_ok(dz):
         return torch.mm(dz, w16) if acc is None else torch.addmm(acc, dz, w16)
     M, K, N = dz.shape[0], dz.shape[1], w16.shape[1]
     if acc is None and _SPLIT_DGRAD_K and K >= _SPLIT_DGRAD_K and -(-M // 128) * -(-N // 128) < 256 and dz.is_cuda:
@@ -169,7 +176,7 @@ def dense_dgrad(dz, w16, acc=None):
 def dense_wgrad(dz, x2, out=None):
     """dW[out, in] = dZ^T X in f32; accumulated into `out` (an arena gradient view) when given."""
     o, i = dz.shape[1], x2.shape[1]
-    if _PLAIN_BLAS and o * i >= _BLAS_WGRAD_MIN:
+    if _PLAIN_BLAS and o * i >= _BLAS_WGRAD_MIN and _lib_ok(dz):
         if out is not None and out.is_contiguous():
             return torch.ops.aten.addmm.dtype_out(out, dz.t(), x2, F32, beta=1, alpha=1, out=out)
         r = torch.mm(dz.t(), x2, out_dtype=F32)
@@ -221,8 +228,8 @@ class _DenseFn(torch.autograd.Function):
             x2 = x2.contiguous()
         w16 = bf16_shadow(w)
         pre = torch.empty((x2.shape[0], w.shape[0]), dtype=BF16, device=x.device) if act else None
-        if (_BLAS_FWD and not act and x2.is_cuda
-                and float(x2.shape[0]) * w.shape[0] * x2.shape[1] >= _BLAS_FWD_MIN):
+        if (_BLAS_FWD and not act and float(x2.shape[0]) * w.shape[0] * x2.shape[1] >= _BLAS_FWD_MIN
+                and _lib_ok(x2)):
             y = torch.nn.functional.linear(x2, w16, bf16_shadow(b) if b is not None else None)
         else:
             y = gemm(x2, w16, bias=b, act=act, aux=pre)
@@ -258,7 +265,7 @@ class _DenseFn(torch.autograd.Function):
             acc = ctx.link.take()[0] if ctx.link is not None else None
             isrc = ctx.in_src
             ctx.in_src = None
-            if (acc is None and isrc is not None and isrc.consumers == 1 and not _PLAIN_BLAS
+            if (acc is None and isrc is not None and isrc.consumers == 1 and not (_PLAIN_BLAS and _lib_ok(dz))
                     and isrc.pre.shape == (dz.shape[0], w.shape[1])):
                 # the producer's activation backward in this GEMM's epilogue
                 dx = torch.empty((dz.shape[0], w.shape[1]), dtype=BF16, device=dz.device)
