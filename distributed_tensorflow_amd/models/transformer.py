@@ -163,9 +163,10 @@ class GPT2(Model):
     def __init__(self, vocab=50257, ctx=1024, hidden=1024, layers=24, heads=16, dropout=0.1, fp8=False,
                  name="gpt2", **kw):
         super().__init__(name=name, **kw)
-        # fp8: the quantize passes and fp8 GEMMs leave CUs idle along the data-gradient chain, which the
-        # per-bucket optimizer update fills (+2% measured; bf16 -1%)
-        self.overlap_update = bool(fp8)
+        # per-bucket optimizer update during backward (parallel.strategy): round 4, with the plain GEMMs on hipBLASLt,
+        # it pays for bf16 (256.0k / 255.6k vs 251.2k / 251.3k tok/s) and no longer for fp8 (248.6k / 258.2k vs
+        # 256.9k / 256.5k, with 3-6 ms more host issue time); round 3 had measured the opposite (fp8 +2%, bf16 -1%)
+        self.overlap_update = not fp8
         self.cfg = dict(vocab=vocab, ctx=ctx, hidden=hidden, layers=layers, heads=heads, fp8=fp8)
         from ..keras.initializers import TruncatedNormal
         # vocab padded to a multiple of 64 for the MFMA tiles (padded logits are masked out of the loss)
