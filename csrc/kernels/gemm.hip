@@ -281,6 +281,13 @@ static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
 }
 
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8 = 0, int bn = 256);  // gemm256.hip
+int gemm_w4_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn);  // gemm_w4.hip
+// 256-row tiles: the 4-wave kernel (gemm_w4.hip: 1.0-1.25x gemm256 on every transformer shape, profiles/
+// r5_gemm_vs_hipblaslt.txt) when its epilogue covers the call, else the 8-wave gemm256 kernel.
+static int tile256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn = 256) {
+  if (gemm_w4_try(a, amode, bmode, st, bn) == 0) return 0;
+  return gemm256_try(a, amode, bmode, st, 0, bn);
+}
 int gemm8p_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn);  // gemm8p.hip
 
 // The 8-phase 256-row kernel (gemm8p.hip) for a K-contiguous conv / GEMM: forced by tiles 20 (256x256) and 21
@@ -344,6 +351,22 @@ int pick256(long M, long N, long K, long batch) {
   return 0;
 }
 bool prefer256(long M, long N, long K, long batch) { return pick256(M, N, K, batch) == 256; }
+
+// Tile rule of the bf16 GEMMs: the 4-wave kernels (gemm_w4.hip) with 256x256 or 256x128 tiles, or the 128x128 kernel
+// (2 blocks/CU), by the wave-quantisation efficiency of each tiling on 256 CUs times its per-tile speed (256x128: 0.8
+// of the 256x256 FLOP rate, 128x128: 0.6 — tools/bench_gemm_w4.py, profiles/r5_gemm_vs_hipblaslt.txt; e.g. M=8192
+// N=1024: 128 tiles of 256x256 (half the chip) 523 TF vs 256 tiles of 256x128 761 TF). Returns 256, 128 or 0.
+static int pick_w4(long M, long N, long batch) {
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch, t2x1 = (long)cdiv(M, 256) * cdiv(N, 128) * batch,
+             t128 = (long)cdiv(M, 128) * cdiv(N, 128) * batch;
+  auto eff = [](long t, long slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
+  const double s256 = N > 128 ? eff(t256, 256) : 0.0;
+  const double s2x1 = 0.8 * eff(t2x1, 256);
+  const double s128 = 0.6 * eff(t128, 512);
+  if (s256 >= s2x1 && s256 >= s128) return 256;
+  if (s2x1 >= s128) return 128;
+  return 0;
+}
 
 // LDS-DMA staged tiles for K-contiguous operands (both operand images filled by buffer_load ... lds):
 // 128x64 synchronous (occupancy hides the DMA) almost everywhere, 128x128 double-buffered when there are
@@ -448,6 +471,29 @@ static bool rowmap_ok() {
   return on;
 }
 
+// Split-K plan of an f32-output GEMM (a weight gradient: few output tiles over a long token K) on the 4-wave
+// kernels: per tile width (256x256 at speed 1, 256x128 at 0.8, see pick_w4) the split count s (<= K/1024, <= 16)
+// that maximises speed x the wave-quantisation efficiency of tiles x s blocks on 256 CUs, less 3% per extra split
+// (the f32 slab round trip and its reduction). Returns s (1 = no split) and the tile width in bn; bn = 0 when K is
+// too short to consider splitting (the caller's usual rule then applies).
+static int plan_w4_split(long M, long N, long K, long batch, int& bn) {
+  bn = 0;
+  if (K < 2048) return 0;
+  auto eff = [](long t, long slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
+  double best = -1.0;
+  int best_s = 1;
+  for (int w : {256, 128}) {
+    if (w == 256 && N <= 128) continue;
+    const long t = (long)cdiv(M, 256) * cdiv(N, w) * batch;
+    const double speed = w == 256 ? 1.0 : 0.8;
+    for (long sp = 1; sp <= std::min<long>(16, K / 1024); ++sp) {
+      const double sc = speed * eff(t * sp, 256) - 0.03 * (double)(sp - 1);
+      if (sc > best) { best = sc; best_s = (int)sp; bn = w; }
+    }
+  }
+  return best_s;
+}
+
 static int choose_splitk(long M, long N, long K, int tile_m, int tile_n, long batch) {
   long tiles = (long)cdiv(M, tile_m) * cdiv(N, tile_n) * batch;
   static const long target = [] {
@@ -513,8 +559,10 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
   a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.sA = sA; a.sB = sB; a.sC = sC;
   a.M = M; a.N = N; a.K = K; a.batch = batch < 1 ? 1 : batch;
   a.alpha = alpha; a.beta = beta; a.act = act; a.out_f32 = out_f32;
-  if (splitk <= 0) splitk = out_f32 && (beta == 0.f || beta == 1.f) && !bias && !act && !aux && !stats
-                                ? choose_splitk(M, N, K, 128, 128, a.batch) : 1;
+  const bool split_ok = out_f32 && (beta == 0.f || beta == 1.f) && !bias && !act && !aux && !stats && !dact;
+  int w4bn = 0;  // the 4-wave kernel's tile width for a split-K plan made for it (f32 outputs: weight gradients)
+  if (splitk <= 0 && split_ok && tile < 0 && K % BK == 0) splitk = plan_w4_split(M, N, K, a.batch, w4bn);
+  if (splitk <= 0) splitk = split_ok ? choose_splitk(M, N, K, 128, 128, a.batch) : 1;
   a.splitk = splitk;
   a.kchunk = ((K + splitk - 1) / splitk + BK - 1) / BK * BK;
   if (splitk > 1) {
@@ -532,7 +580,13 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
       a.slab = (long)M * N;  // z = batch*splitk + split -> slab index
       a.beta = 0.f;
       bool big = false;
-      if (tile < 0 && M >= 256 && N >= 256) {  // 256x256 tiles: re-split for them (>= ~1 block per CU)
+      if (w4bn) {  // the split chosen for the 4-wave kernel
+        GemmArgs b = a;
+        if (tile256_try(b, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream,
+                        w4bn) == 0)
+          big = true;
+      }
+      if (!big && tile < 0 && M >= 256 && N >= 256) {  // 256x256 tiles: re-split for them (>= ~1 block per CU)
         GemmArgs b = a;
         const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * a.batch;
         // one round of 1-block/CU tiles: splits so that tiles x splits <= 256 CUs, >= 1024 of K per split
@@ -540,7 +594,7 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
         if (t256 * s2 >= 200 && (long)s2 * mn <= ws_elems) {
           b.splitk = s2;
           b.kchunk = ((K + s2 - 1) / s2 + BK - 1) / BK * BK;
-          if (gemm256_try(b, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG,
+          if (tile256_try(b, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG,
                           (hipStream_t)stream) == 0) {
             big = true;
             splitk = s2;
@@ -562,9 +616,9 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
   }
   if (stats && (a.batch > 1 || a.splitk > 1)) return -7;
   // large K-contiguous problems: the 256x256 glds-pipelined kernel when it fills the chip
-  const int bn256 = (tile < 0 && !stats && a.splitk == 1) ? pick256(M, N, K, a.batch) : 0;
-  if (bn256 && gemm256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream,
-                           0, bn256) == 0)
+  const int bn256 = (tile < 0 && !stats && a.splitk == 1) ? pick_w4(M, N, a.batch) : 0;
+  if (bn256 && tile256_try(a, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream,
+                           bn256) == 0)
     return (int)hipGetLastError();
   const int am = a_kouter ? OP_KOUTER : OP_KCONTIG, bm = b_kouter ? OP_KOUTER : OP_KCONTIG;
   if (tile < 0 && dense_glds_on() && a.batch == 1) tile = pick_glds_tile(a, am, bm);

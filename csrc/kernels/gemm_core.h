@@ -649,6 +649,17 @@ struct GldsLoader {
     }
   }
 
+  // instruction i of issue() alone, plain K-contiguous rows only (kernels that interleave the DMA with MFMAs)
+  __device__ __forceinline__ void issue1(int k0, int Kend, char* lds, int i) {
+    static_assert(MODE == OP_KCONTIG, "issue1: plain rows only");
+    const int wave = threadIdx.x >> 6;
+    const bool ok = tmask[i] != 0u && k0 + (coff[i] >> 1) < Kend;
+    const uint32_t off = ok ? (uint32_t)(roff[i] + k0 * 2 + coff[i]) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 +
+                                                                                            wave * 1024),
+                                             16, off, 0, 0, 0);
+  }
+
   __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int Kend, char* lds) {
     const int wave = threadIdx.x >> 6;
     int toff;
@@ -719,6 +730,17 @@ struct GldsKOuter {
         coff[i] = col * 2;
       }
     }
+  }
+
+  // instruction i of issue() alone, plain K-outer rows only (kernels that interleave the DMA with MFMAs)
+  __device__ __forceinline__ void issue1(int k0, int Kend, char* lds, int i) {
+    static_assert(MODE == OP_KOUTER, "issue1: plain rows only");
+    const int wave = threadIdx.x >> 6;
+    const int k = k0 + kr[i];
+    const bool ok = cv[i] && k < Kend;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 + wave * 1024), 16,
+        ok ? (uint32_t)(k * ldb + coff[i]) : 0x80000000u, 0, 0, 0);
   }
 
   __device__ __forceinline__ void issue(const GemmArgs& a, int k0, int Kend, char* lds) {

@@ -82,37 +82,6 @@ def gemm_fp8(a, b, scales, out, *, fmt_a=0, out_f32=False, beta=0.0, splitk=1, b
     return out
 
 
-# Plain fp8 GEMMs (no activation epilogue, no fp8 output copies) on hipBLASLt through torch._scaled_mm.
-# Standalone (tools/probe_scaled_mm.py, GPT-2-medium shapes, us, hipBLASLt vs ours): forward QKV 34 vs 54, FFN2 38 vs
-# 51; data gradient QKV 33 vs 43, FFN1 38 vs 51; weight gradient QKV 41 vs 65, out 23 vs 58, FFN1 41 vs 93, FFN2 42
-# vs 93 (the out-projection's forward / data gradient are faster on ours; the fused-epilogue GEMMs have no library
-# equivalent). End to end only the weight gradients pay (they run on the side stream): GPT-2-medium fp8 247.4k /
-# 246.1k tok/s with them vs 243.3k / 242.6k without, while also moving the forward + data gradients LOSES (233.6k /
-# 228.5k; all three: 206k) — the library kernels on the critical stream overlap worse with the side stream.
-# DTF_FP8_BLASLT: bit mask of the roles sent to hipBLASLt (1 forward, 2 data gradient, 4 weight gradient; default 4)
-_BLASLT = (int(os.environ.get("DTF_FP8_BLASLT", "4")) if hasattr(torch, "_scaled_mm") and hasattr(torch, "float8_e5m2")
-           else 0)
-_BLASLT_MIN_MNK = float(os.environ.get("DTF_FP8_BLASLT_MIN", str(16 * 2 ** 30)))
-_blaslt_ok = [True]
-
-
-def _use_blaslt(M, N, K, role, force=False):
-    return (bool(_BLASLT & role) and _blaslt_ok[0] and (force or float(M) * N * K >= _BLASLT_MIN_MNK)
-            and not torch.cuda.is_current_stream_capturing())  # (see linalg._lib_ok)
-
-
-def _gemm_blaslt(a, b, sa, sb, *, fmt_a=0, out_dtype=BF16, bias=None):
-    """out[M,N] = sa*sb * a[M,K] . b[N,K]^T on hipBLASLt (a e4m3 / e5m2 when fmt_a 1, b e4m3; sa, sb 0-dim f32 device
-    scales); None when the library call is refused (then the caller runs ours, and later calls skip the library)."""
-    try:
-        av = a.view(torch.float8_e5m2 if fmt_a == 1 else torch.float8_e4m3fn)
-        bv = b.view(torch.float8_e4m3fn)
-        return torch._scaled_mm(av, bv.t(), scale_a=sa, scale_b=sb, bias=bias, out_dtype=out_dtype)
-    except (RuntimeError, TypeError):
-        _blaslt_ok[0] = False
-        return None
-
-
 _WGRAD_SPLIT_MAX = int(os.environ.get("DTF_FP8_WGRAD_SPLITS", "1"))
 
 
@@ -258,13 +227,8 @@ class _DenseFP8(torch.autograd.Function):
             ctx.src = pend[4:]  # (producer state, its pre-activation, its activation): the fused dgrad target
             pre = torch.empty((M, N), dtype=BF16, device=x.device) if act else None
             wq, wqT = _weight_fp8(st, w, True)
-            y = (_gemm_blaslt(xq, wq, buf[X_SCALE], buf[W_SCALE], bias=bf16_shadow(b) if b is not None else None)
-                 if not act and _use_blaslt(M, N, K, 1) else None)
-            if y is not None:
-                buf[prev:prev + 1].zero_()  # (our GEMM clears the consumed amax slot itself)
-            else:
-                y = torch.empty((M, N), dtype=BF16, device=x.device)
-                gemm_fp8(xq, wq, buf[X_SCALE:X_SCALE + 2], y, bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1])
+            y = torch.empty((M, N), dtype=BF16, device=x.device)
+            gemm_fp8(xq, wq, buf[X_SCALE:X_SCALE + 2], y, bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1])
             return _DenseFP8._finish_fwd(ctx, True, xqT, w, pre, st, b, act, shp, (M, K, N), y)
         x2 = x.reshape(-1, shp[-1]).contiguous()
         M, K = x2.shape
@@ -305,13 +269,7 @@ class _DenseFP8(torch.autograd.Function):
             xq, xqT, _ = quantize_t(x2, xs, buf[cur:cur + 1], amax_prev=buf[prev:prev + 1], scale_used=xs,
                                     scale_used2=buf[X_USED:X_USED + 1])
             wq, wqT = _weight_fp8(st, w, True)
-            yl = (_gemm_blaslt(xq, wq, buf[X_SCALE], buf[W_SCALE], bias=bf16_shadow(b) if b is not None else None)
-                  if not act and _use_blaslt(M, N, K, 1) else None)
-            if yl is not None:
-                y = yl
-                buf[prev:prev + 1].zero_()  # (our GEMM clears the consumed amax slot itself)
-            else:
-                gemm_fp8(xq, wq, buf[X_SCALE:X_SCALE + 2], y, bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1])
+            gemm_fp8(xq, wq, buf[X_SCALE:X_SCALE + 2], y, bias=b, act=act, aux=pre, zero_slot=buf[prev:prev + 1])
         else:
             xa = buf[X_AMAX:X_AMAX + 1]
             if fbwd:
@@ -390,16 +348,9 @@ class _DenseFP8(torch.autograd.Function):
                     pst.pending_g = (dx.data_ptr(), gq, gqT, gcp, pprev)
                     dx = dx.reshape(ctx.shp)
             if dx is None:
-                dxl = (_gemm_blaslt(dzq, wqT, buf[G_SCALE], buf[W_SCALE], fmt_a=1) if _use_blaslt(M, K, N, 2)
-                       else None)
-                if dxl is not None:
-                    dx = dxl
-                    if folded:
-                        buf[prev:prev + 1].zero_()
-                else:
-                    dx = torch.empty((M, K), dtype=BF16, device=dy.device)
-                    gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1,  # scales (s_w, s_g)
-                             zero_slot=buf[prev:prev + 1] if folded else None)
+                dx = torch.empty((M, K), dtype=BF16, device=dy.device)
+                gemm_fp8(dzq, wqT, buf[W_SCALE:W_SCALE + 2], dx, fmt_a=1,  # scales (s_w, s_g)
+                         zero_slot=buf[prev:prev + 1] if folded else None)
                 dx = dx.reshape(ctx.shp)
         tw = direct_grad(w) if need_dw else None
         tb = direct_grad(ctx.b_param) if need_db else None
@@ -409,21 +360,12 @@ class _DenseFP8(torch.autograd.Function):
         with side:
             if need_dw:  # dW[N, K] (+)= dZ^T X over the M tokens; inside Model.train_step straight into the arena
                 wprev, st.w_prev = st.w_prev, None
-                dwl = (_gemm_blaslt(dzqT, xqT, buf[G_SCALE], buf[X_USED], fmt_a=1, out_dtype=F32)
-                       if _use_blaslt(N, K, M, 4, force=True) else None)
-                if dwl is not None:  # (the library has no accumulate: one f32 add into the arena slice)
-                    if tw is not None:
-                        tw.add_(dwl)
-                    dw = None if tw is not None else dwl
-                    if wprev is not None:
-                        buf[wprev:wprev + 1].zero_()
-                else:
-                    out = tw if tw is not None else torch.empty((N, K), dtype=F32, device=dy.device)
-                    sk = _wgrad_splits(N, K, M, workspace(dy.device).numel())
-                    gemm_fp8(dzqT, xqT, buf[G_SCALE:G_SCALE + 2], out, fmt_a=1, out_f32=True,
-                             beta=1.0 if tw is not None else 0.0, splitk=sk,  # scales (s_g, s_x used)
-                             zero_slot=None if wprev is None else buf[wprev:wprev + 1])
-                    dw = None if tw is not None else out
+                out = tw if tw is not None else torch.empty((N, K), dtype=F32, device=dy.device)
+                sk = _wgrad_splits(N, K, M, workspace(dy.device).numel())
+                gemm_fp8(dzqT, xqT, buf[G_SCALE:G_SCALE + 2], out, fmt_a=1, out_f32=True,
+                         beta=1.0 if tw is not None else 0.0, splitk=sk,  # scales (s_g, s_x used)
+                         zero_slot=None if wprev is None else buf[wprev:wprev + 1])
+                dw = None if tw is not None else out
             if need_db:
                 out = tb if tb is not None else torch.empty(N, dtype=F32, device=dy.device)
                 call("dtf_reduce_rows", ptr(cp), N, cp.shape[0], N, ptr(out), int(tb is not None), stream())

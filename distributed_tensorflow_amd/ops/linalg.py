@@ -125,41 +125,17 @@ def colsum(x2d, out=None, accumulate=False):
     return out
 
 
-# The plain (epilogue-free) backward GEMMs of the dense layers go to hipBLASLt (torch.mm / addmm into the f32 arena):
-# plain library GEMMs, faster than ours on these shapes (tools/bench_blas_plain.py). Round 2 measured them a loss end
-# to end (BERT-base 789k vs 777k tok/s); with round 4's hipBLASLt forward projections and attention changes they win
-# (interleaved A/B, one box): GPT-2-medium 254.1k / 252.7k vs 235.7k / 233.9k tok/s, BERT-base 908.2k / 908.6k vs
-# 887.9k / 885.4k. Fused-epilogue backward GEMMs (activation backward, residual-link accumulation, fp8) stay on
-# ours. DTF_PLAIN_BLAS=0: every backward GEMM on ours.
-_PLAIN_BLAS = __import__("os").environ.get("DTF_PLAIN_BLAS", "1") != "0"
-# (keeping the consumer-fused activation backward on our GEMM for FFN2's data gradient under _PLAIN_BLAS measured
-# 255.3-255.6k vs 257.2-257.6k tok/s: the library GEMM + the activation pass win)
-# Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream
+# Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream.
+# Every dense GEMM runs on the hand-written kernels (gemm.hip -> gemm_w4.hip for the 256-row tiles); the round-4
+# hipBLASLt routes for the plain projections were removed in round 5.
 DENSE_SIDE_ON = SIDE_STREAM_ON and __import__("os").environ.get("DTF_DENSE_WGRAD_STREAM", "1") != "0"
-_BLAS_WGRAD_MIN = 4 << 20
-# Activation-free forward projections of at least DTF_BLAS_FWD_MIN multiply-adds (a plain GEMM + bias: GPT-2 / BERT
-# QKV and FFN2, the LM head) on hipBLASLt (F.linear with the bf16 bias shadow); the fused-epilogue GEMMs (GELU with
-# its pre-activation side output, residual/ReLU links) and the small projections stay on ours. Measured end to end
-# (round 4, interleaved A/B on one box): GPT-2-medium 234.1k / 235.2k vs 224.1k / 224.7k tok/s, BERT-base
-# 885.6k / 878.9k vs 856.2k / 856.6k. DTF_BLAS_FWD=0: every forward GEMM on ours.
-_BLAS_FWD = __import__("os").environ.get("DTF_BLAS_FWD", "1") != "0"
-_BLAS_FWD_MIN = float(__import__("os").environ.get("DTF_BLAS_FWD_MIN", str(4 * 2 ** 30)))  # (16G: -1%)
 _SPLIT_DGRAD_K = int(__import__("os").environ.get("DTF_SPLIT_DGRAD_K", "8192"))  # 0 disables the split route
-
-
-def _lib_ok(t):
-    """hipBLASLt routes only outside a hipGraph capture: under capture a library call that needs a fresh workspace or
-    heuristic query fails (HIPBLAS_STATUS_INTERNAL_ERROR) and torch's rocBLAS fallback is not capturable; captured
-    steps keep every GEMM on our kernels."""
-    return t.is_cuda and not torch.cuda.is_current_stream_capturing()
 
 
 def dense_dgrad(dz, w16, acc=None):
     """dX[T, in] = dZ[T, out] W[out, in] (bf16); with `acc` (another gradient of the same input, [T, in], parked on
     a ResidualGradLink: no other reader) the GEMM adds it in its store pass and returns it — no separate add pass,
     the same values as the GEMM followed by an elementwise add."""
-    if _PLAIN_BLAS and _lib_ok(dz):
-        return torch.mm(dz, w16) if acc is None else torch.addmm(acc, dz, w16)
     M, K, N = dz.shape[0], dz.shape[1], w16.shape[1]
     if acc is None and _SPLIT_DGRAD_K and K >= _SPLIT_DGRAD_K and -(-M // 128) * -(-N // 128) < 256 and dz.is_cuda:
         # few output tiles over a long K (BERT's MLM decoder: 2432 x 768 over the 30k vocabulary): split-K f32 slabs
@@ -175,12 +151,6 @@ def dense_dgrad(dz, w16, acc=None):
 
 def dense_wgrad(dz, x2, out=None):
     """dW[out, in] = dZ^T X in f32; accumulated into `out` (an arena gradient view) when given."""
-    o, i = dz.shape[1], x2.shape[1]
-    if _PLAIN_BLAS and o * i >= _BLAS_WGRAD_MIN and _lib_ok(dz):
-        if out is not None and out.is_contiguous():
-            return torch.ops.aten.addmm.dtype_out(out, dz.t(), x2, F32, beta=1, alpha=1, out=out)
-        r = torch.mm(dz.t(), x2, out_dtype=F32)
-        return r if out is None else out.add_(r)
     if out is not None:
         return gemm(dz, x2, a_kouter=True, b_kouter=True, out=out, beta=1.0)
     return gemm(dz, x2, a_kouter=True, b_kouter=True, out_dtype=F32)
@@ -228,11 +198,7 @@ class _DenseFn(torch.autograd.Function):
             x2 = x2.contiguous()
         w16 = bf16_shadow(w)
         pre = torch.empty((x2.shape[0], w.shape[0]), dtype=BF16, device=x.device) if act else None
-        if (_BLAS_FWD and not act and float(x2.shape[0]) * w.shape[0] * x2.shape[1] >= _BLAS_FWD_MIN
-                and _lib_ok(x2)):
-            y = torch.nn.functional.linear(x2, w16, bf16_shadow(b) if b is not None else None)
-        else:
-            y = gemm(x2, w16, bias=b, act=act, aux=pre)
+        y = gemm(x2, w16, bias=b, act=act, aux=pre)
         ctx.save_for_backward(x2, w, pre)
         ctx.act = act
         ctx.has_b = b is not None
@@ -265,7 +231,7 @@ class _DenseFn(torch.autograd.Function):
             acc = ctx.link.take()[0] if ctx.link is not None else None
             isrc = ctx.in_src
             ctx.in_src = None
-            if (acc is None and isrc is not None and isrc.consumers == 1 and not (_PLAIN_BLAS and _lib_ok(dz))
+            if (acc is None and isrc is not None and isrc.consumers == 1
                     and isrc.pre.shape == (dz.shape[0], w.shape[1])):
                 # the producer's activation backward in this GEMM's epilogue
                 dx = torch.empty((dz.shape[0], w.shape[1]), dtype=BF16, device=dz.device)

@@ -26,12 +26,26 @@ _seed_counter = [0]
 # 178 -> 158 us (213 -> 183 with dropout); BERT-base S=512 203 -> 227 us (the dS round trip costs more than the
 # recompute saves when no tiles are skipped)
 _ATTN_DS = {"1": True, "0": False}.get(__import__("os").environ.get("DTF_ATTN_DS", ""), None)
+# The dS^T scratch is O(B*H*S^2) (GPT-2-medium S=1024 B=8: 268 MB per call); above this many bytes the backward takes
+# the O(S) recompute kernel instead, so a long-context run keeps flash attention's memory bound.
+DS_SCRATCH_MAX_BYTES = 1 << 30
+
+
+def ds_scratch_bytes(B, H, Sq, Sk):
+    return 2 * B * H * Sk * (-(-Sq // 64) * 64)
+
+
+def uses_ds_path(causal, B, H, Sq, Sk):
+    """True when the attention backward goes through the dS^T scratch (dtf_attn_bwd_ds)."""
+    if not (_ATTN_DS or (_ATTN_DS is None and causal)):
+        return False
+    return ds_scratch_bytes(B, H, Sq, Sk) <= DS_SCRATCH_MAX_BYTES
 
 
 def _bwd(args_before_ds, B, H, Sq, Sk, dev):
     """Run the attention backward (args: the dtf_attn_bwd argument list, causal flag at [-3])."""
     causal = bool(args_before_ds[-3])
-    if _ATTN_DS or (_ATTN_DS is None and causal):
+    if uses_ds_path(causal, B, H, Sq, Sk):
         ds = torch.empty(B * H * Sk * (-(-Sq // 64) * 64), dtype=BF16, device=dev)
         call("dtf_attn_bwd_ds", *args_before_ds[:-1], ptr(ds), args_before_ds[-1])
     else:

@@ -53,6 +53,16 @@ def keep_mask(seed, B, H, Sq, Sk, keep):
     return torch.from_numpy(m), thr / 65536.0
 
 
+def test_ds_scratch_route_is_capped():
+    """The causal backward's dS^T scratch is O(S^2): GPT-2-medium S=1024 keeps it, a long context takes the O(S)
+    recompute kernel (an unbounded scratch could OOM a long-context run)."""
+    if A._ATTN_DS is False:
+        pytest.skip("DTF_ATTN_DS=0")
+    assert A.uses_ds_path(True, 8, 16, 1024, 1024)
+    assert A.ds_scratch_bytes(8, 16, 8192, 8192) > A.DS_SCRATCH_MAX_BYTES
+    assert not A.uses_ds_path(True, 8, 16, 8192, 8192)
+
+
 def test_cpu_reference_paths():
     q, k, v = (torch.randn(2, 3, 16, 8) for _ in range(3))
     o = ops.attention(q, k, v, causal=True)
