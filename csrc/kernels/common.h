@@ -174,3 +174,19 @@ __device__ __forceinline__ bool last_arriver(int* ticket, int expected, int* lds
 // a ring (each launch leaves its slots at zero again). nullptr if they cannot be provided (caller falls back
 // to two launches). Must first be called outside stream capture (it allocates once per device).
 DTF_API int* dtf_tickets(int n);
+
+// Host-side launch counters: which GEMM kernel a call reached (read by the tests through dtf_launch_counts, so a
+// test named for a kernel fails when a dispatch change routes its call elsewhere). Incremented at launch sites on
+// the host only; no device code touches them.
+enum LaunchCounter : int {
+  LC_W4_256 = 0,      // gemm_w4.hip, 256x256 tiles
+  LC_W4_128 = 1,      // gemm_w4.hip, 256x128 tiles
+  LC_GEMM256 = 2,     // gemm256.hip (8-wave)
+  LC_GEMM_TILE = 3,   // gemm_core.h gemm_kernel (128/64-row tiles)
+  LC_GEMM_DACT = 4,   // dtf_gemm_dact (activation backward in the data-gradient epilogue)
+  LC_BETA_BF16 = 5,   // bf16 GEMM accumulating into C (beta != 0)
+  LC_SPLITK = 6,      // split-K GEMM (f32 slabs + ordered reduction)
+  LC_COUNT = 16
+};
+DTF_API long* dtf_launch_counters();
+inline void count_launch(int c) { dtf_launch_counters()[c]++; }

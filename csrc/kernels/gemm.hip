@@ -136,6 +136,16 @@ DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int
 
 #include <mutex>
 
+DTF_API long* dtf_launch_counters() {
+  static long c[LC_COUNT] = {};
+  return c;
+}
+// copies the first n counters into out (tests: ops._util.launch_counts)
+DTF_API int dtf_launch_counts(long* out, int n) {
+  for (int i = 0; i < n && i < LC_COUNT; ++i) out[i] = dtf_launch_counters()[i];
+  return 0;
+}
+
 DTF_API int* dtf_tickets(int n) {
   constexpr int RING = 1 << 16;
   static std::mutex mu;
@@ -405,6 +415,7 @@ static int pick_glds_tile(const GemmArgs& a, int amode, int bmode) {
 }
 
 static void dispatch(GemmArgs& a, int amode, int bmode, int tile, hipStream_t st) {
+  count_launch(LC_GEMM_TILE);
   if (tile < 0) tile = pick_tile(a.M, a.N, (long)a.batch * a.splitk, a.kchunk);
   if (amode == OP_KCONTIG && bmode == OP_KCONTIG) launch_modes<OP_KCONTIG, OP_KCONTIG>(a, tile, st);
   else if (amode == OP_KCONTIG && bmode == OP_KOUTER) launch_modes<OP_KCONTIG, OP_KOUTER>(a, tile, st);
@@ -551,6 +562,8 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
   if (a_kouter && (M & 7)) return -2;
   if (b_kouter && (N & 7)) return -3;
   if (dact && (out_f32 || beta != 0.f || act || aux || splitk > 1 || batch > 1)) return -8;
+  if (dact) count_launch(LC_GEMM_DACT);
+  if (beta != 0.f && !out_f32) count_launch(LC_BETA_BF16);
   GemmArgs a{};
   a.dact_src = (const bf16_t*)dact_src;
   a.dact = dact;
@@ -607,6 +620,7 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
         if (t < 0 && dense_glds_on() && a.batch == 1) t = pick_glds_tile(a, am, bm);
         dispatch(a, am, bm, t, (hipStream_t)stream);
       }
+      count_launch(LC_SPLITK);
       // slabs are [batch][splitk][M*N]: reduce each batch separately
       for (int b = 0; b < a.batch; ++b)
         dtf_sum_rows(ws + (long)b * splitk * M * N, (long)M * N, splitk, (long)M * N, (float*)C + (long)b * M * N,

@@ -517,6 +517,7 @@ int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int 
     return e ? atoi(e) : 2;
   }();
   a.aux_nt = aux_nt;
+  count_launch(LC_GEMM256);
   if (bn == 256) launch256<256>(a, amode, bmode, st, fp8);
   else launch256<128>(a, amode, bmode, st, fp8);
   return 0;

@@ -435,6 +435,7 @@ bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode) {
 // Launch on the 4-wave kernel with tile width bn (256 or 128). Returns 0 if launched, 1 if not eligible.
 int gemm_w4_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn) {
   if (!gemm_w4_ok(a, amode, bmode)) return 1;
+  count_launch(bn == 128 ? LC_W4_128 : LC_W4_256);
   if (bn == 128) w4_launch<128>(a, amode, bmode, st);
   else w4_launch<256>(a, amode, bmode, st);
   return 0;

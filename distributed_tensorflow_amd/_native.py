@@ -73,6 +73,7 @@ _KERNEL_SIGS = {
     "dtf_gemm8p": [P, P, P, I, I, I, L, L, L, I, I, P],
     "dtf_gemm_w4": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
     "dtf_gemm_w4_var": [P, P, P, I, I, I, I, I, P],
+    "dtf_launch_counts": [P, I],
     "dtf_gemm256_bn": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
     "dtf_gemm_dact": [P, P, P, P, I, I, I, I, L, L, L, I, I, P],
     "dtf_quant_fp8_exact": [P, P, L, P, P, P],

@@ -232,6 +232,8 @@ def update_stream_ctx(device, extra_wait=None):
     u.wait_stream(torch.cuda.current_stream(device))
     if device.index in _SIDE_USED:
         u.wait_stream(_SIDE[device.index])
+    if device.index in _COMM_USED:  # a bucket reduced on the communication stream (P2P all-reduce)
+        u.wait_stream(_COMM[device.index])
     return torch.cuda.stream(u)
 
 
@@ -316,11 +318,47 @@ def K():
     return _native.kernels()
 
 
+_CALL_LOG = []  # active call_log() counters (tests: which native entry points an op reached)
+
+
 def call(name, *args):
     fn = getattr(K(), name)
     rc = fn(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with status {rc}")
+    if _CALL_LOG:
+        for c in _CALL_LOG:
+            c[name] += 1
+
+
+@contextlib.contextmanager
+def call_log():
+    """Counts the native entry points called inside the block (collections.Counter by name)."""
+    import collections
+    c = collections.Counter()
+    _CALL_LOG.append(c)
+    try:
+        yield c
+    finally:
+        _CALL_LOG.remove(c)
+
+
+LAUNCH_COUNTERS = ("w4_256", "w4_128", "gemm256", "gemm_tile", "gemm_dact", "beta_bf16", "splitk")
+
+
+def launch_counts():
+    """Host-side launch counters of the GEMM dispatch (csrc/kernels/common.h LaunchCounter): which kernel a GEMM
+    reached. Take two snapshots and subtract."""
+    import ctypes
+    n = len(LAUNCH_COUNTERS)
+    buf = (ctypes.c_long * n)()
+    K().dtf_launch_counts(ctypes.addressof(buf), n)
+    return dict(zip(LAUNCH_COUNTERS, list(buf)))
+
+
+def launch_delta(before):
+    after = launch_counts()
+    return {k: after[k] - before[k] for k in after}
 
 
 def contig(t):

@@ -108,9 +108,10 @@ class GradientBucketer:
         self.paths = {"rccl": 0, "p2p": 0}
         if collective and arena.grad.is_cuda and self.wire == "f32" and type(self) is GradientBucketer:
             from . import p2p
-            if p2p.available(arena.grad, group) and any((hi - lo) * 4 <= p2p.MAX_BYTES for lo, hi in self.buckets):
+            spans = [(lo, hi) for lo, hi in self.buckets if (hi - lo) * 4 <= p2p.MAX_BYTES]
+            if p2p.available(arena.grad, group) and spans:
                 try:
-                    self.p2p = p2p.P2PAllReducer(arena.grad, group)
+                    self.p2p = p2p.P2PAllReducer(arena.grad, group, spans=spans)
                 except (RuntimeError, OSError, ValueError) as e:  # e.g. ranks on several nodes: RCCL only
                     print(f"[dtf] P2P all-reduce unavailable ({e}); RCCL for every bucket", flush=True)
         self.reset()
@@ -174,16 +175,20 @@ class GradientBucketer:
         lo, hi = self.buckets[b]
         t = self.arena.grad[lo:hi]
         import contextlib
-        ctx = contextlib.nullcontext()
-        if t.is_cuda:  # the bucket's weight gradients may still be in flight on the side stream
-            from ..ops._util import collective_ctx
-            ctx = collective_ctx(t.device)
         work = None
-        with ctx:
-            if self.collective and self._use_p2p(lo, hi):
-                self.p2p.all_reduce_(lo, hi)  # one kernel on the side stream: stream-ordered, no Work to wait on
-                self.paths["p2p"] += 1
-            elif self.collective:
+        if self.collective and self._use_p2p(lo, hi):
+            # one kernel on the communication stream (it waits for the main and weight-gradient streams as they are
+            # now): stream-ordered, no Work to wait on, and a spin on a late peer stalls no weight-gradient GEMM
+            from ..ops._util import comm_stream_ctx
+            with comm_stream_ctx(t.device):
+                self.p2p.all_reduce_(lo, hi)
+            self.paths["p2p"] += 1
+        elif self.collective:
+            ctx = contextlib.nullcontext()
+            if t.is_cuda:  # the bucket's weight gradients may still be in flight on the side stream
+                from ..ops._util import collective_ctx
+                ctx = collective_ctx(t.device)
+            with ctx:
                 self.paths["rccl"] += 1
                 if self.wire == "bf16":
                     if self._wirebuf is None:
@@ -234,8 +239,8 @@ class GradientBucketer:
                 if w is not None:
                     w.wait()  # GPU: the main stream waits for the collective's RCCL stream
             if self.p2p is not None and self.arena.grad.is_cuda:
-                from ..ops._util import join_side_streams
-                join_side_streams()  # P2P buckets were reduced by kernels on the side stream
+                from ..ops._util import join_comm_stream
+                join_comm_stream(self.arena.grad.device)  # P2P buckets were reduced by kernels on the comm stream
                 self.p2p.poll()
             if self.wire == "bf16" and self.collective:
                 for lo, hi in self.buckets:

@@ -12,7 +12,9 @@ flag array with HIP IPC handles (dtf_ipc_export); the handles travel through the
 (same hostname), at most 8 ranks, CUDA tensors. A call launches ONE kernel on the current stream (stream-ordered
 after the kernels that produced the bucket, before the ones that consume it) with a host-side epoch; every rank
 must issue the same calls in the same order (the bucketer's bucket order guarantees it). Not used under hipGraph
-capture (the epoch is a kernel argument).
+capture (the epoch is a kernel argument). The bucketer issues the kernel on the communication stream (which waits for
+the main and weight-gradient streams), so a spin waiting for a slow peer holds no weight-gradient GEMM behind it.
+Opt-in: DTF_P2P=1 (see available()).
 """
 from __future__ import annotations
 
@@ -50,7 +52,9 @@ def _open(handle_hex, offset):
 class P2PAllReducer:
     """Bucket all-reduce over IPC-mapped peer gradient arenas (see module docstring)."""
 
-    def __init__(self, grad, group=None):
+    def __init__(self, grad, group=None, spans=None):
+        """spans: the [lo, hi) arena ranges that will be reduced here (the P2P-eligible buckets); the kernel's f32
+        scratch covers only those (default: the whole arena)."""
         if grad.device.type != "cuda" or grad.dtype != torch.float32:
             raise ValueError("P2P all-reduce needs an f32 CUDA gradient arena")
         self.group = group
@@ -60,7 +64,13 @@ class P2PAllReducer:
             raise ValueError(f"P2P all-reduce supports at most {MAX_RANKS} ranks")
         self.grad = grad
         dev = grad.device
-        self.red = torch.empty_like(grad)
+        spans = [(0, grad.numel())] if spans is None else sorted(spans)
+        self._soff = {}
+        tot = 0
+        for lo, hi in spans:
+            self._soff[(lo, hi)] = tot
+            tot += -(-(hi - lo) // 4) * 4  # 16-B aligned slices
+        self.red = torch.empty(max(tot, 4), dtype=torch.float32, device=dev)
         self.flags = torch.zeros(2 * NBLK * MAX_RANKS, dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         torch.cuda.synchronize(dev)
@@ -142,20 +152,28 @@ class P2PAllReducer:
             self._err_ev = torch.cuda.Event()
             self._err_ev.record()
 
-    def all_reduce_(self, lo, hi):
-        """Sum grad[lo:hi] over the ranks in place (on the current stream)."""
+    def all_reduce_(self, lo, hi, timeout_ms=None):
+        """Sum grad[lo:hi] over the ranks in place (on the current stream). [lo, hi) must be one of the spans given
+        at construction, or lie inside the whole-arena default span."""
         n = hi - lo
         if n <= 0:
             return
+        soff = self._soff.get((lo, hi))
+        if soff is None:
+            whole = self._soff.get((0, self.grad.numel()))
+            if whole is None:
+                raise ValueError(f"P2P all-reduce of [{lo}, {hi}): not a span given at construction")
+            soff = lo
         self.epoch += 1
         self.calls += 1
         srcs = (ctypes.c_void_p * self.world)(*[p + 4 * lo for p in self.grad_ptr])
         flags = (ctypes.c_void_p * self.world)(*self.flag_ptr)
         nblk = max(1, min(NBLK, -(-n // (256 * 4 * 4))))  # >= 4 float4 per thread
         from ..ops._util import stream
-        _native.call("dtf_p2p_allreduce_f32", self.grad.data_ptr() + 4 * lo, srcs, self.red.data_ptr() + 4 * lo,
-                     self.flags.data_ptr(), flags, n, self.world, self.rank, self.epoch, nblk, TIMEOUT_MS,
-                     self.err.data_ptr(), stream(self.grad.device))
+        _native.call("dtf_p2p_allreduce_f32", self.grad.data_ptr() + 4 * lo, srcs, self.red.data_ptr() + 4 * soff,
+                     self.flags.data_ptr(), flags, n, self.world, self.rank, self.epoch, nblk,
+                     TIMEOUT_MS if timeout_ms is None else int(timeout_ms), self.err.data_ptr(),
+                     stream(self.grad.device))
 
     def check(self):
         """Raise if any call timed out waiting for a peer (synchronises the device)."""
@@ -169,6 +187,8 @@ class P2PAllReducer:
 
 
 def available(grad, group=None):
-    """Whether the P2P path can be used for this arena (CUDA f32, <= 8 ranks; node locality is checked at setup)."""
+    """Whether the P2P path can be used for this arena (CUDA f32, <= 8 ranks; node locality is checked at setup).
+    Opt-in (DTF_P2P=1) until a cross-GPU run has validated it: every test so far shares one GPU between the ranks
+    (ADVICE r4)."""
     return (MAX_BYTES > 0 and grad.is_cuda and grad.dtype == torch.float32 and dist.is_initialized()
-            and 1 < dist.get_world_size(group) <= MAX_RANKS and os.environ.get("DTF_P2P", "1") != "0")
+            and 1 < dist.get_world_size(group) <= MAX_RANKS and os.environ.get("DTF_P2P", "0") == "1")

@@ -63,9 +63,9 @@ def _batches(kind, dev, steps=3):
     return out
 
 
-def _worker(rank, world, port, kind, q):
+def _worker(rank, world, port, kind, q, p2p="0"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port), DTF_COLLECTIVE_BACKEND="gloo")
+                      MASTER_PORT=str(port), DTF_COLLECTIVE_BACKEND="gloo", DTF_P2P=p2p)
     try:
         import torch.distributed as dist
         from distributed_tensorflow_amd import parallel
@@ -81,18 +81,19 @@ def _worker(rank, world, port, kind, q):
         torch.cuda.synchronize()
         b = s._bucketers[id(m._arena)]
         # numpy, not torch CPU tensors: those travel as shared-memory fds that vanish when the worker exits
-        q.put((rank, [w.detach().float().cpu().numpy() for w in m.trainable_variables], losses, len(b.buckets)))
+        q.put((rank, [w.detach().float().cpu().numpy() for w in m.trainable_variables], losses, len(b.buckets),
+               dict(b.paths)))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:
         q.put((rank, None, traceback.format_exc(), 0))
 
 
-def _run_ranks(kind, world=2):
+def _run_ranks(kind, world=2, p2p="0"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kind, q, p2p)) for r in range(world)]
     [p.start() for p in ps]
     try:
         res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda t: t[0])
@@ -117,6 +118,20 @@ def test_two_rank_gpt2_equals_single_process(cuda):
     torch.cuda.synchronize()
     for a, w in zip(res[0][1], m.trainable_variables):
         torch.testing.assert_close(torch.from_numpy(a), w.detach().float().cpu(), rtol=2e-3, atol=2e-4)
+
+
+def test_two_rank_bucketer_p2p_equals_collective(cuda):
+    """The gradient bucketer with the one-shot P2P all-reduce (DTF_P2P=1: small buckets on the communication stream,
+    the rest on the process group, per-bucket hooks during backward) trains bitwise like the process-group-only run
+    (end-to-end coverage of the bucketer integration). Two ranks share GPU 0."""
+    a = _run_ranks("gpt2", p2p="1")
+    b = _run_ranks("gpt2", p2p="0")
+    assert a[0][4]["p2p"] > 0, a[0][4]
+    assert b[0][4]["p2p"] == 0, b[0][4]
+    for x, y in zip(a[0][1], b[0][1]):
+        assert (x == y).all(), "P2P buckets changed the training result"
+    for x, y in zip(a[0][1], a[1][1]):
+        assert (x == y).all(), "replicas diverged"
 
 
 def test_two_rank_resnet_replicas_stay_identical(cuda):

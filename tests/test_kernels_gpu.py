@@ -296,7 +296,10 @@ def test_dense_fwd_bwd(cuda):
     x = rnd(256, 768, dev=cuda).requires_grad_(True)
     w = (torch.randn(3072, 768, device=cuda) * 0.02).requires_grad_(True)
     b = torch.randn(3072, device=cuda).requires_grad_(True)
-    y = ops.dense(x, w, b, act="gelu")
+    from distributed_tensorflow_amd.ops._util import call_log
+    with call_log() as calls:
+        y = ops.dense(x, w, b, act="gelu")
+    assert calls["dtf_gemm"] == 1, calls  # the forward product on our GEMM (no library route)
     xr = x.detach().float().requires_grad_(True)
     wr = w.detach().to(BF).float().requires_grad_(True)
     br = b.detach().clone().requires_grad_(True)
@@ -304,7 +307,9 @@ def test_dense_fwd_bwd(cuda):
     close(y, yr, 2e-2)
     dy = torch.randn_like(yr)
     yr.backward(dy)
-    y.backward(dy.to(BF))
+    with call_log() as calls:
+        y.backward(dy.to(BF))
+    assert calls["dtf_gemm"] == 2, calls  # data gradient and weight gradient on our GEMM
     close(x.grad, xr.grad, 3e-2)
     close(w.grad, wr.grad, 3e-2)
     close(b.grad, br.grad, 3e-2)
@@ -530,8 +535,10 @@ def test_bert_layer_residual_grad_link(cuda, monkeypatch):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(2, 64, 128, generator=g).to(cuda).to(BF)
     dy = torch.randn(2, 64, 128, generator=g).to(cuda)
+    from distributed_tensorflow_amd.ops._util import launch_counts, launch_delta
     res = {}
     for link in (False, True):
+        before = launch_counts()
         monkeypatch.setattr(T, "RES_LINK", link)
         from distributed_tensorflow_amd.ops import mha as _mha, nn as _nn
         _nn._seed_counter[0], _mha._seed_counter[0] = 0x5EED, 0  # same dropout masks in both runs
@@ -541,6 +548,9 @@ def test_bert_layer_residual_grad_link(cuda, monkeypatch):
         y = layer(xx, training=True)
         grads = torch.autograd.grad((y.float() * dy).sum(), [xx] + list(layer.trainable_weights))
         res[link] = [t.float().cpu() for t in grads]
+        # with the link, the branch projections' data-gradient GEMMs add the parked residual gradient (bf16 beta = 1)
+        beta = launch_delta(before)["beta_bf16"]
+        assert (beta >= 2) if link else (beta == 0), (link, beta)
     for a, b in zip(res[False], res[True]):
         assert (a - b).abs().max().item() <= 2e-2 * a.abs().max().item() + 1e-6
 
@@ -688,12 +698,16 @@ def test_dense_pair_fused_activation_backward(cuda, act):
     b1 = torch.zeros(1024, device=cuda, requires_grad=True)
     w2 = (torch.randn(256, 1024, device=cuda) * 0.05).requires_grad_(True)
     g = rnd(512, 256, dev=cuda)
+    from distributed_tensorflow_amd.ops._util import launch_counts, launch_delta
     res = []
     for fuse in (False, True):
+        before = launch_counts()
         x = x0.clone().requires_grad_(True)
         h = LA.dense(x, w1, b1, act=act, tag_act=fuse)
         y = LA.dense(h, w2, None)
         y.backward(g)
+        # the fused run reaches dtf_gemm_dact (activation backward in FFN2's data-gradient epilogue), the other not
+        assert launch_delta(before)["gemm_dact"] == (1 if fuse else 0)
         res.append((x.grad.clone(), w1.grad.clone(), b1.grad.clone(), w2.grad.clone()))
         for t in (w1, b1, w2):
             t.grad = None
