@@ -373,26 +373,65 @@ class MultiWorkerMirroredStrategy(Strategy):
             dist.barrier()
 
 
-class MirroredStrategy(MultiWorkerMirroredStrategy):
-    """Single-node synchronous data parallelism.
+_MIRRORED_CHILD = "DTF_MIRRORED_CHILD"
 
-    devices=None under a multi-process launch: one replica per process (RCCL).
-    devices=[...] in one process: in-process replicas over those devices (host devices, e.g. the reference's
-    CPU:0 / CPU:1 plumbing config). Several GPUs in ONE process are rejected: on MI355X every GPU gets its own
-    process (its own HIP runtime queues, RCCL rank and Python interpreter), launched by
-    ``python -m distributed_tensorflow_amd.cli.launch --gpus N ...`` or ``torchrun --nproc-per-node N``; the
-    same ``MirroredStrategy()`` then finds its replica through the launcher's environment."""
+
+def _spawn_replicas(devices):
+    """The parent side of MirroredStrategy(devices=[GPU...]): run this same program once per device, each copy a
+    replica of a multi-process MirroredStrategy (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* for the process group,
+    DTF_DEVICE_ORDINAL for its GPU), wait for them and exit with the worst status. The parent touches no GPU: the
+    children are started as plain subprocesses (no exec of the running program)."""
+    import socket
+    import subprocess
+    import sys
+    argv = list(getattr(sys, "orig_argv", []))[1:] or list(sys.argv)
+    if not argv or argv[0] == "-c":
+        raise ValueError("MirroredStrategy over several GPUs re-runs the program once per GPU: it needs a script or "
+                         "module (python script.py / python -m module), not python -c")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r, d in enumerate(devices):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(len(devices)), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DTF_DEVICE_ORDINAL=str(d.index or 0))
+        env[_MIRRORED_CHILD] = "1"
+        procs.append(subprocess.Popen([sys.executable] + argv, env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    raise SystemExit(rc)
+
+
+class MirroredStrategy(MultiWorkerMirroredStrategy):
+    """Single-node synchronous data parallelism (TF's ``MirroredStrategy(devices)``).
+
+    devices=[GPU, GPU, ...]: one replica per listed GPU. On MI355X every GPU gets its own process (its own HIP
+    runtime queues, RCCL rank and Python interpreter), so the constructor, called in the parent, re-runs the program
+    once per device and exits with their status (``_spawn_replicas``); in each child the same constructor call
+    finds its replica through the environment and returns a multi-process strategy bound to its device. Construct
+    the strategy before the program touches a GPU (the parent must not initialise HIP). A device may be listed
+    twice (two replicas sharing one GPU: the 1-GPU rehearsal of the path, with DTF_COLLECTIVE_BACKEND=gloo).
+    devices=None under a multi-process launch (cli.launch --gpus N, torchrun): one replica per process.
+    devices=[host devices] in one process: in-process replicas (the reference's CPU:0 / CPU:1 plumbing config)."""
 
     def __init__(self, devices=None, cross_device_ops=None, bucket_mb=None, communication_options=None,
                  shard_optimizer=None):
         self._devices = [context.parse_device(d) for d in devices] if devices else None
         self.wire_dtype = getattr(communication_options, "wire_dtype", None)
-        gpus = {d for d in (self._devices or []) if d.type == "cuda"}
-        if len(gpus) > 1 and not TorchrunClusterResolver.active():
-            raise ValueError(
-                f"MirroredStrategy over {len(gpus)} GPUs in one process is not supported: run one process per GPU "
-                "(python -m distributed_tensorflow_amd.cli.launch --gpus N <script>, or torchrun --nproc-per-node N) "
-                "and construct MirroredStrategy() without devices in each process")
+        ngpu = sum(1 for d in (self._devices or []) if d.type == "cuda")
+        if ngpu > 1 and not TorchrunClusterResolver.active():
+            if ngpu != len(self._devices):
+                raise ValueError("MirroredStrategy: mixing GPU and host devices is not supported")
+            _spawn_replicas(self._devices)  # (does not return in the parent)
+        if ngpu > 1 and os.environ.get(_MIRRORED_CHILD) == "1":
+            # a child of _spawn_replicas: the listed device of this rank (DTF_DEVICE_ORDINAL) via the launcher path
+            self._inproc = False
+            self._devices = None
+            super().__init__(TorchrunClusterResolver(), communication_options, bucket_mb=bucket_mb,
+                             shard_optimizer=shard_optimizer)
+            return
         if self._devices and len(self._devices) > 1 and not TorchrunClusterResolver.active():
             Strategy.__init__(self)
             self.bucket_mb = bucket_mb

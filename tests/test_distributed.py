@@ -235,12 +235,32 @@ def test_ps_shm_two_ps_six_trainers(tmp_path, staleness):
     assert 1.5 < w < 2.5 and 9.5 < b < 10.5, (w, b)
 
 
-def test_mirrored_rejects_several_gpus_in_one_process():
-    """Several GPUs in ONE process are rejected with a pointer to the one-process-per-GPU launch."""
+def test_mirrored_over_gpu_list_runs_one_process_per_device(tmp_path):
+    """MirroredStrategy(["GPU:0", "GPU:1"]) re-runs the program once per listed device (the parent exits with the
+    children's status); each child is one rank of the multi-process strategy and reduces with the others (gloo here:
+    no GPU in this container; tests/test_dp_gpu.py trains through it on a GPU). Mixed GPU/host lists are rejected."""
+    import subprocess
+    import sys
     import pytest
     from distributed_tensorflow_amd import parallel
-    with pytest.raises(ValueError, match="one process per GPU"):
-        parallel.MirroredStrategy(["GPU:0", "GPU:1"])
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "m.py"
+    script.write_text(
+        "import sys, os\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "import torch\n"
+        "from distributed_tensorflow_amd import parallel\n"
+        "s = parallel.MirroredStrategy(['GPU:0', 'GPU:1'])\n"
+        "t = s.reduce('sum', torch.tensor(float(s.worker_index + 1)))\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'r%d' % s.worker_index), 'w').write("
+        "'%d %d %g' % (s.worker_index, s.num_replicas_in_sync, float(t)))\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(script)], env=env, timeout=240)
+    assert r.returncode == 0
+    for k in range(2):
+        assert (tmp_path / f"r{k}").read_text() == f"{k} 2 3"
+    with pytest.raises(ValueError, match="mixing"):
+        parallel.MirroredStrategy(["GPU:0", "GPU:1", "CPU:0"])
 
 
 def test_overlapped_bucket_update_matches_single_update(monkeypatch):
