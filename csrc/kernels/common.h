@@ -139,41 +139,7 @@ __global__ void __launch_bounds__(256) dtf_group_rows_kernel(float* __restrict__
 // the rows are used as scratch. Defined in gemm.hip.
 DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* out, int accumulate, void* stream);
 
-// ---------------------------------------------------------------------------------------------------------
-// In-launch "last arriver" hand-off (cdna_hip_programming.md §6 Guideline 16, MI355X_MICROARCH.md "Valid forms",
-// first row of the sc1 hand-off table): every block of a group writes its partial result with WRITE-THROUGH
-// (sc1, agent-scope relaxed) stores, every storing wave drains them (s_waitcnt vmcnt(0)), the block joins a
-// barrier and ONE lane adds to the group's ticket; the block whose add returns expected-1 combines the partials
-// IN A FIXED ORDER (deterministic) reading them with sc1 loads only (st_wt / ld_wt), then resets the ticket so the
-// next stream-ordered launch finds it at zero. No agent-scope release / acquire fence: a release writes back the
-// whole XCD L2 (~1.7-6.5 us per block behind a conv epilogue's dirty output), which made every block of the
-// producing GEMM pay it (round 3: ResNet-50 step 22.7 -> 42.9 ms). Replaces separate reduction launches.
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float4 ld_wt4(const float* p) {
-  return make_float4(ld_wt(p), ld_wt(p + 1), ld_wt(p + 2), ld_wt(p + 3));
-}
-__device__ __forceinline__ bool last_arriver(int* ticket, int expected, int* lds_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == expected - 1;
-    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *lds_flag = last;
-  }
-  __syncthreads();  // the other waves load only after this barrier, which the adding wave joins after its add
-  return *lds_flag != 0;
-}
 
-// Zero-initialised ticket counters for last_arriver launches on the current device: `n` consecutive slots from
-// a ring (each launch leaves its slots at zero again). nullptr if they cannot be provided (caller falls back
-// to two launches). Must first be called outside stream capture (it allocates once per device).
-DTF_API int* dtf_tickets(int n);
 
 // Host-side launch counters: which GEMM kernel a call reached (read by the tests through dtf_launch_counts, so a
 // test named for a kernel fails when a dispatch change routes its call elsewhere). Incremented at launch sites on

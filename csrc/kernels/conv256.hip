@@ -298,14 +298,13 @@ __global__ void __launch_bounds__(NW * 64, 1) conv256_kernel(GemmArgs a) {
   gemm_epilogue<BMC, BN, WM, WN, NTH, NS * STAGE_B>(a, acc, smem, m0, n0, tile_m, z, bz);
 }
 
-// Variants (DTF_CONV256_CFG or the tile codes of gemm.hip): 0 = BN 128, 4 waves (128x64 wave tiles), 3 stages;
+// Variants (the tile codes 11-14 of gemm.hip): 0 = BN 128, 4 waves (128x64 wave tiles), 3 stages;
 // 1 = BN 256, 8 waves (128x64), 2 stages; 2 = BN 64, 4 waves (64x64), 3 stages; 3 = BN 128, 8 waves (64x64), 3 stages.
 template <int AM, int BMD>
 void launch_cfg(GemmArgs& a, int cfg, hipStream_t st) {
   const int bn = cfg == 1 ? 256 : cfg == 2 ? 64 : 128;
   a.tiles_m = cdiv(a.M, BMC);
   a.tiles_n = cdiv(a.N, bn);
-  prep_fin(a);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
   switch (cfg) {
     case 1: hipLaunchKernelGGL((conv256_kernel<AM, BMD, 256, 8, 2>), grid, dim3(512), 0, st, a); break;
@@ -317,13 +316,7 @@ void launch_cfg(GemmArgs& a, int cfg, hipStream_t st) {
 
 }  // namespace
 
-bool conv256_on() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_CONV256");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+bool conv256_on() { return true; }
 
 // Launch C = A . B^T on the 256-row pipelined kernel when the operand modes are supported and the problem is
 // large enough to fill the chip with 1-block/CU tiles (at least ~256 blocks). bn: 64 or 128 (0: by N).
@@ -333,21 +326,12 @@ int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool
   // pointwise convolutions (K-contiguous x K-contiguous) stay on gemm_core.h's LDS-DMA tiles: measured slower here
   // on every ResNet-50 1x1 layer it was eligible for (fwd 49.5 vs 43 us stage-3 c1, 96-101 vs 71-73 us stage-4
   // c1/proj; dgrad 48 vs 41 us stage-3 c3: tools/conv_roofline.py --tiles, r3)
-  static const bool pw256 = [] {  // DTF_CONV256_1X1=1: let pointwise convolutions take this kernel again
-    const char* e = getenv("DTF_CONV256_1X1");
-    return e && e[0] == '1';
-  }();
-  if (!force && !pw256 && amode == OP_KCONTIG && bmode == OP_KCONTIG) return 1;
+  if (!force && amode == OP_KCONTIG && bmode == OP_KCONTIG) return 1;
   if (cfg < 0) {
-    static const int env = [] {
-      const char* e = getenv("DTF_CONV256_CFG");
-      return e ? atoi(e) : -1;
-    }();
     // measured per ResNet-50 layer (profiles/r2_conv256_variants.txt): only the 256x256 8-wave form wins, and
     // only with a long K (>= 16 K-tiles: the 2-stage pipeline needs a main loop to amortise its 1-block/CU
     // prologue and epilogue) and N >= 256 (no half-empty column tiles); everything else stays on gemm_core.h
-    if (env >= 0) cfg = env;
-    else if (!force && a.N >= 256 && a.K >= 1024) cfg = 1;
+    if (!force && a.N >= 256 && a.K >= 1024) cfg = 1;
     else if (!force) return 1;
     else cfg = a.N <= 64 ? 2 : a.N >= 256 ? 1 : 0;
   }
@@ -370,17 +354,17 @@ int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool
     if (mode == OP_WGRADX_R && !fits((long)g.N * g.H * g.W * g.C)) return 1;
   }
   if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return 1;
-#define DTF_C256(AMODE, BMODE)           \
+#define C256_LAUNCH(AMODE, BMODE)           \
   if (amode == AMODE && bmode == BMODE) { \
     launch_cfg<AMODE, BMODE>(a, cfg, st); \
     return 0;                             \
   }
-  DTF_C256(OP_KCONTIG, OP_KCONTIG)
-  DTF_C256(OP_IM2COL_T, OP_KCONTIG)
-  DTF_C256(OP_DGRAD_T, OP_KCONTIG)
-  DTF_C256(OP_WGRADX_R, OP_KOUTER_R)
-  DTF_C256(OP_KOUTER, OP_KOUTER_R)
-#undef DTF_C256
+  C256_LAUNCH(OP_KCONTIG, OP_KCONTIG)
+  C256_LAUNCH(OP_IM2COL_T, OP_KCONTIG)
+  C256_LAUNCH(OP_DGRAD_T, OP_KCONTIG)
+  C256_LAUNCH(OP_WGRADX_R, OP_KOUTER_R)
+  C256_LAUNCH(OP_KOUTER, OP_KOUTER_R)
+#undef C256_LAUNCH
   return 1;
 }
 

@@ -108,11 +108,7 @@ __global__ void __launch_bounds__(256) dtf_group_rows_narrow_kernel(const float*
 }
 
 static bool narrow_rows_ok(const float* rows, long stride, long W) {
-  static const bool on = [] {
-    const char* e = getenv("DTF_NARROW_ROWS");
-    return !(e && e[0] == '0');
-  }();
-  return on && !(W & 3) && W <= 1024 && !(stride & 3) && !((uintptr_t)rows & 15);
+  return !(W & 3) && W <= 1024 && !(stride & 3) && !((uintptr_t)rows & 15);
 }
 
 // One launch: sum groups of rows into leader rows so that <= target leaders remain; returns their count
@@ -134,7 +130,6 @@ DTF_API int dtf_group_rows_once(float* rows, long stride, int nrows, long W, int
   return groups;
 }
 
-#include <mutex>
 
 DTF_API long* dtf_launch_counters() {
   static long c[LC_COUNT] = {};
@@ -144,30 +139,6 @@ DTF_API long* dtf_launch_counters() {
 DTF_API int dtf_launch_counts(long* out, int n) {
   for (int i = 0; i < n && i < LC_COUNT; ++i) out[i] = dtf_launch_counters()[i];
   return 0;
-}
-
-DTF_API int* dtf_tickets(int n) {
-  constexpr int RING = 1 << 16;
-  static std::mutex mu;
-  static int* base[64] = {};
-  static int next[64] = {};
-  if (n <= 0 || n > RING / 4) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  if (!base[dev]) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(nullptr, &cs);
-    if (cs != hipStreamCaptureStatusNone) return nullptr;
-    int* p = nullptr;
-    if (hipMalloc(&p, sizeof(int) * RING) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, sizeof(int) * RING) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
-    base[dev] = p;
-  }
-  if (next[dev] + n > RING) next[dev] = 0;
-  int* r = base[dev] + next[dev];
-  next[dev] += n;
-  return r;
 }
 
 // Two-level deterministic reduction of `nrows` rows into out (or into row 0 if out == nullptr).
@@ -234,7 +205,6 @@ template <int BM, int BN, int WM, int WN, int AM, int BMODE, int PIPE = 2>
 static void launch_t(GemmArgs& a, hipStream_t st) {
   a.tiles_m = cdiv(a.M, BM);
   a.tiles_n = cdiv(a.N, BN);
-  prep_fin(a);
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, BMODE, 0, PIPE>), grid, dim3(NT), 0, st, a);
 }
@@ -298,33 +268,9 @@ static int tile256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn
   if (gemm_w4_try(a, amode, bmode, st, bn) == 0) return 0;
   return gemm256_try(a, amode, bmode, st, 0, bn);
 }
-int gemm8p_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn);  // gemm8p.hip
-
-// The 8-phase 256-row kernel (gemm8p.hip) for a K-contiguous conv / GEMM: forced by tiles 20 (256x256) and 21
-// (256x128); by default (DTF_G8P, 1 = on) when its tiles fill the chip: 256x256 with >= 256 tiles, else 256x128 with
-// >= 256 tiles. True if launched.
-static int g8p_mode() {
-  static const int m = [] {
-    const char* e = getenv("DTF_G8P");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-static bool try_gemm8p(GemmArgs& a, int am, int bm, int& tile, hipStream_t st) {
-  if (tile == 20 || tile == 21) {
-    if (gemm8p_try(a, am, bm, st, tile == 20 ? 256 : 128) == 0) return true;
-    tile = -1;
-    return false;
-  }
-  if (tile >= 0 || !g8p_mode() || a.atomic_out || a.splitk != 1) return false;
-  const long t256 = (long)cdiv(a.M, 256) * cdiv(a.N, 256) * a.batch, t128 = (long)cdiv(a.M, 256) * cdiv(a.N, 128) * a.batch;
-  const int bn = (a.N >= 256 && t256 >= 256) ? 256 : (a.N >= 128 && t128 >= 256) ? 128 : 0;
-  return bn && gemm8p_try(a, am, bm, st, bn) == 0;
-}
 int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool force);  // conv256.hip
 bool conv256_on();
 int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int C, int K, hipStream_t st);  // pwconv.hip
-bool pwconv_on();
 
 // The 256-row pipelined LDS-DMA kernel (conv256.hip) for a convolution GEMM: forced by tiles 11-14 (variant
 // tile - 11, see conv256.hip launch_cfg); by default whenever it is eligible and fills the chip. True if launched.
@@ -342,23 +288,14 @@ static bool try_conv256(GemmArgs& a, int am, int bm, int& tile, hipStream_t st) 
 int pick256(long M, long N, long K, long batch) {
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch, t2x1 = (long)cdiv(M, 256) * cdiv(N, 128) * batch,
              t128 = (long)cdiv(M, 128) * cdiv(N, 128) * batch;
-  static const long force_min = [] {  // tuning knob: take 256x256 whenever it has at least this many tiles
-    const char* e = getenv("DTF_G256_MIN");
-    return e ? atol(e) : 0L;
-  }();
-  static const int narrow = [] {  // opt-in (DTF_G256_NARROW=1): the 256x128 tiles are LDS-read bound with the 2x4
-    const char* e = getenv("DTF_G256_NARROW");  // wave layout: GPT-2-medium 218.5k -> 210.4k tok/s with them on
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  if (force_min > 0) return t256 >= force_min ? 256 : 0;
+  // (the 8-wave kernel's 256x128 tiles are LDS-read bound with its 2x4 wave layout: GPT-2-medium 218.5k -> 210.4k
+  // tok/s with them: not used)
   auto eff = [](long t, long slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
   const double base = 1.12 + 0.12 * (double)std::min<long>(K, 4096) / 4096.0;
   const double s256 = t256 >= 128 ? base * eff(t256, 256) : 0.0;
-  const double s2x1 = (narrow && t2x1 >= 128) ? 0.96 * base * eff(t2x1, 256) : 0.0;  // half the B reuse per tile
   const double s128 = eff(t128, 512);
-  if (s256 >= s2x1 && s256 > s128) return 256;
-  if (s2x1 > s128) return 128;
-  return 0;
+  (void)t2x1;
+  return s256 > s128 ? 256 : 0;
 }
 bool prefer256(long M, long N, long K, long batch) { return pick256(M, N, K, batch) == 256; }
 
@@ -381,31 +318,8 @@ static int pick_w4(long M, long N, long batch) {
 // LDS-DMA staged tiles for K-contiguous operands (both operand images filled by buffer_load ... lds):
 // 128x64 synchronous (occupancy hides the DMA) almost everywhere, 128x128 double-buffered when there are
 // few tiles and a long K (ResNet-50 stage 4). Measured per layer: tools/conv_roofline.py --tiles.
-static bool glds_on() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_GLDS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-static bool wgrad_glds_on() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_GLDS_WGRAD");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-static bool dense_glds_on() {
-  // opt-in: on BERT-base / GPT-2-medium the transformer GEMMs measured 1-3 % slower end to end with the
-  // LDS-DMA tiles than with the register-staged / 256x256 kernels (they mostly go to gemm256 anyway)
-  static const bool on = [] {
-    const char* e = getenv("DTF_GLDS_DENSE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 static int pick_glds_tile(const GemmArgs& a, int amode, int bmode) {
-  if (!glds_on() || !glds_mode(amode) || !glds_mode(bmode) || a.atomic_out) return -1;
+  if (!glds_mode(amode) || !glds_mode(bmode) || a.atomic_out) return -1;
   if (amode == OP_KCONTIG && (long)a.M * a.lda * 2 >= (1l << 31)) return -1;
   if (bmode == OP_KCONTIG && (long)a.N * a.ldb * 2 >= (1l << 31)) return -1;
   if (amode == OP_KOUTER && ((long)a.K * a.lda * 2 >= (1l << 31) || (a.M & 7))) return -1;
@@ -465,21 +379,9 @@ static uint64_t rowrep(int R, int S) {
 }
 
 // Tap-uniform gather eligibility (OP_IM2COL_T / OP_DGRAD_T): 64-channel K-tiles never straddle a tap, the tap
-// mask fits 32 bits, the gathered tensor's byte offsets fit 31 bits. Opt out with DTF_CONV_TAPS=0.
+// mask fits 32 bits, the gathered tensor's byte offsets fit 31 bits.
 static bool tap_uniform(int chans, int taps, long gathered_elems) {
-  static const bool on = [] {
-    const char* e = getenv("DTF_CONV_TAPS");
-    return !(e && e[0] == '0');
-  }();
-  return on && chans % 64 == 0 && taps <= 32 && gathered_elems * 2 < (1l << 31);
-}
-
-static bool rowmap_ok() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_WGRAD_ROWMAP");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  return chans % 64 == 0 && taps <= 32 && gathered_elems * 2 < (1l << 31);
 }
 
 // Split-K plan of an f32-output GEMM (a weight gradient: few output tiles over a long token K) on the 4-wave
@@ -507,14 +409,9 @@ static int plan_w4_split(long M, long N, long K, long batch, int& bn) {
 
 static int choose_splitk(long M, long N, long K, int tile_m, int tile_n, long batch) {
   long tiles = (long)cdiv(M, tile_m) * cdiv(N, tile_n) * batch;
-  static const long target = [] {
-    const char* e = getenv("DTF_SPLITK_BLOCKS");  // blocks a split-K launch aims for (2 per CU by default)
-    return e ? std::max(64L, atol(e)) : 512L;
-  }();
-  static const long full = [] {  // 128x128 tile count from which no split is taken (DTF_SPLITK_TILES)
-    const char* e = getenv("DTF_SPLITK_TILES");
-    return e ? std::max(16L, atol(e)) : 256L;
-  }();
+  // aim for 2 blocks per CU; no split from 256 128x128 tiles on (measured: more / less splitting lost on BERT
+  // and GPT-2, README "Measured and not adopted")
+  constexpr long target = 512, full = 256;
   if (tiles >= full || K <= 1024) return 1;
   long want = (target + tiles - 1) / tiles;
   if (want > 256) want = 256;
@@ -617,7 +514,6 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
       if (!big) {
         const int am = a_kouter ? OP_KOUTER : OP_KCONTIG, bm = b_kouter ? OP_KOUTER : OP_KCONTIG;
         int t = tile;
-        if (t < 0 && dense_glds_on() && a.batch == 1) t = pick_glds_tile(a, am, bm);
         dispatch(a, am, bm, t, (hipStream_t)stream);
       }
       count_launch(LC_SPLITK);
@@ -635,7 +531,6 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
                            bn256) == 0)
     return (int)hipGetLastError();
   const int am = a_kouter ? OP_KOUTER : OP_KCONTIG, bm = b_kouter ? OP_KOUTER : OP_KCONTIG;
-  if (tile < 0 && dense_glds_on() && a.batch == 1) tile = pick_glds_tile(a, am, bm);
   dispatch(a, am, bm, tile, (hipStream_t)stream);
   if (stat_rows) *stat_rows = a.tiles_m;
   return (int)hipGetLastError();
@@ -643,75 +538,47 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
 
 DTF_API int dtf_stem_fwd(const void* X, const void* Wt, void* Y, float* part, int* rows, int N, int Hs, int Ws, int C,
                          int K, int R, int S, int P, int Q, void* stream);  // stem.hip
-static bool stem_kernel_on() {  // DTF_STEM_KERNEL=0: the stem runs on the implicit-GEMM conv (A/B)
-  static const bool on = [] {
-    const char* e = getenv("DTF_STEM_KERNEL");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // NHWC conv forward: Y[N,P,Q,K] = X[N,H,W,C] * W[K,R,S,C] (+bias, act, BN stats of Y)
 // stats (optional): BN partial rows [tiles_m][2K] (capacity ceil(N*P*Q/64) rows); *stat_rows = tiles_m.
 static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
                          int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
-                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin);
+                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream);
 
 DTF_API int dtf_conv_fwd(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
                          int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
                          int pw, int dh, int dw, int act, int out_f32, int tile, void* stream) {
   return conv_fwd_impl(X, Wt, Y, bias, stats, stat_rows, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, act,
-                       out_f32, tile, stream, nullptr);
+                       out_f32, tile, stream);
 }
 
 DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float* beta, float* running_mean,
                             float* running_var, long M, int C, float momentum, float eps, float* scale,
                             float* shift, float* mean_out, float* invstd_out, void* stream);  // norm.hip
 
-// Opt-in (DTF_BN_FIN_FUSED=1 or dtf_set_bn_fin_fused): measured on MI355X, the in-launch finalize makes EVERY block
-// of the producing GEMM publish its partial row with an agent-scope release (an L2 write-back of its XCD) and the
-// ResNet-50 step went from 22.7 to 42.9 ms; the separate row-reduction + finalize launches stay the default.
-static int g_fin_on = [] {
-  const char* e = getenv("DTF_BN_FIN_FUSED");
-  return (e && e[0] == '1') ? 1 : 0;
-}();
-static bool fin_on() { return g_fin_on != 0; }
-DTF_API int dtf_set_bn_fin_fused(int on) {
-  g_fin_on = on ? 1 : 0;
-  return 0;
-}
-
-// Conv forward + training BatchNorm statistics AND their finalize: scale/shift/mean/invstd of the output's
-// BatchNorm and the running-statistics update, computed in the conv launch's own tail (BnFin) — or, when that is
-// not possible (split tiling, no ticket slots during a capture), by dtf_bn_finalize right after. stats: partial-row
-// scratch as for dtf_conv_fwd. *fused (optional): 1 when the conv launch finalized.
+// Conv forward + training BatchNorm statistics AND their finalize: the conv launch writes per-tile partial rows of
+// sum / sum of squares, dtf_bn_finalize reduces them in a fixed order and writes scale/shift/mean/invstd and the
+// running statistics. (An in-launch finalize by the last-arriving block measured slower and was removed in round 5:
+// profiles/r4_negative_results.txt.) *fused (optional) is always 0: the API keeps the slot.
 DTF_API int dtf_conv_fwd_bn(const void* X, const void* Wt, void* Y, float* stats, int N, int H, int W, int C, int K,
                             int R, int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int tile,
                             const float* gamma, const float* beta, float* rmean, float* rvar, float momentum,
                             float eps, float* scale, float* shift, float* mean, float* invstd, int* fused,
                             void* stream) {
-  int done = 0, rows = 0;
-  BnFin f{};
-  f.mode = fin_on() ? 1 : 0;
-  f.p0 = gamma; f.p1 = beta; f.p2 = rmean; f.p3 = rvar;
-  f.o0 = scale; f.o1 = shift; f.o2 = mean; f.o3 = invstd;
-  f.momentum = momentum; f.eps = eps;
-  f.count = (long)N * P * Q;
-  f.host_done = &done;
+  int rows = 0;
   int rc = conv_fwd_impl(X, Wt, Y, nullptr, stats, &rows, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, 0,
-                         tile, stream, &f);
+                         tile, stream);
   if (rc) return rc;
-  if (!done) rc = dtf_bn_finalize(stats, rows, gamma, beta, rmean, rvar, (long)N * P * Q, K, momentum, eps, scale,
-                                  shift, mean, invstd, stream);
-  if (fused) *fused = done;
+  rc = dtf_bn_finalize(stats, rows, gamma, beta, rmean, rvar, (long)N * P * Q, K, momentum, eps, scale, shift, mean,
+                       invstd, stream);
+  if (fused) *fused = 0;
   return rc;
 }
 
 static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bias, float* stats, int* stat_rows,
                          int N, int H, int W, int C, int K, int R, int S, int P, int Q, int sh, int sw, int ph,
-                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream, const BnFin* fin) {
+                         int pw, int dh, int dw, int act, int out_f32, int tile, void* stream) {
   if ((C & 7) || (K & 3)) return -1;
-  if (stats && !bias && !act && !out_f32 && tile < 0 && stem_kernel_on() && sh == 1 && sw == 1 && ph == 0 &&
+  if (stats && !bias && !act && !out_f32 && tile < 0 && sh == 1 && sw == 1 && ph == 0 &&
       pw == 0 && dh == 1 && dw == 1) {
     // the space-to-depth ResNet stem (C 16, K 64, 4x4): its own kernel (stem.hip); the finalize runs after
     int rows = 0;
@@ -722,7 +589,7 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
     }
   }
   const bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
-  if (pointwise && stats && !bias && !act && !out_f32 && (tile < 0 || tile == 30) && pwconv_on()) {
+  if (pointwise && stats && !bias && !act && !out_f32 && (tile < 0 || tile == 30)) {
     // channel-expanding 1x1 layers: the persistent register-resident-filter kernel (pwconv.hip); the BN finalize
     // then runs as its own launch over its <= 256 partial rows
     const int rows = pwconv_try(X, Wt, Y, stats, (long)N * P * Q, C, K, (hipStream_t)stream);
@@ -732,7 +599,6 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
     }
   }
   GemmArgs a{};
-  if (fin && stats) a.fin = *fin;
   a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
   a.g_rowrep = rowrep(a.g.R, a.g.S);
   a.A = (const bf16_t*)X; a.B = (const bf16_t*)Wt; a.C = Y; a.bias = bias; a.stats = stats;
@@ -741,7 +607,7 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
   a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
-  if (!try_gemm8p(a, am, OP_KCONTIG, tile, (hipStream_t)stream) && !try_conv256(a, am, OP_KCONTIG, tile, (hipStream_t)stream)) {
+  if (!try_conv256(a, am, OP_KCONTIG, tile, (hipStream_t)stream)) {
     if (tile < 0) tile = pick_glds_tile(a, am, OP_KCONTIG);
     dispatch(a, am, OP_KCONTIG, tile, (hipStream_t)stream);
   }
@@ -780,23 +646,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream, const BnFin* fin = nullptr);
-
-// The BnFin of a data gradient that also finalizes the backward of the BatchNorm whose output it is the gradient
-// of (mode 2): dgamma/dbeta (+= when accumulate) and the apply coefficients coef [3*C] of that BatchNorm (gamma,
-// mean, invstd: its forward's), computed in the dgrad launch's tail. Only a single-launch dgrad can do this.
-static BnFin bwd_fin(const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                     int accumulate, float* coef, long count, int* done) {
-  BnFin f{};
-  f.mode = (coef && invstd && mean && fin_on()) ? 2 : 0;
-  f.p0 = gamma; f.p1 = mean; f.p2 = const_cast<float*>(invstd);
-  f.o0 = dgamma; f.o1 = dbeta; f.o2 = coef;
-  f.accumulate = accumulate;
-  f.count = count;
-  f.host_done = done;
-  if (done) *done = 0;
-  return f;
-}
+                           const void* bsrc2, void* stream);
 
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
@@ -810,29 +660,6 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
 // dtf_conv_dgrad of a stride-1 pointwise conv whose result also adds bsrc2: the compact [N, H/2, W/2, C] data
 // gradient of a stride-2 1x1 projection shortcut of the same input, at the even pixels (the shortcut's full-size
 // gradient, 3/4 zeros, is never written or read). H and W even.
-// dtf_conv_dgrad with the BatchNorm-backward statistics finalized in the launch (see bwd_fin); *fused = 1 when it
-// did (else the caller reduces bnpart itself, as after dtf_conv_dgrad).
-DTF_API int dtf_conv_dgrad_bn(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
-                              int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, float beta,
-                              void* ws, long ws_bf16, const void* bnx, const void* bnmask, const float* bnmean,
-                              float* bnpart, int* bnrows, const void* betamask, const void* bsrc2,
-                              const float* gamma, const float* invstd, float* dgamma, float* dbeta, int accumulate,
-                              float* coef, int* fused, void* stream) {
-  int done = 0;
-  const BnFin f = bwd_fin(gamma, bnmean, invstd, dgamma, dbeta, accumulate, coef, (long)N * H * W, &done);
-  int rc;
-  if (bsrc2) {
-    if ((H & 1) || (W & 1)) return -11;
-    rc = conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, 1, 1, H, W, 1, 1, 0, 0, 1, 1, 0, 1.f, -1, ws, ws_bf16, bnx,
-                         bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, &f);
-  } else {
-    rc = conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, beta, -1, ws, ws_bf16,
-                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, &f);
-  }
-  if (fused) *fused = done;
-  return rc;
-}
-
 // The general bf16 data gradient of the ConvBN path: optional beta accumulate (+ deferred ReLU mask betamask), the
 // compact stride-2 shortcut gradient bsrc2 (pointwise stride-1 convs, H and W even), and the BN-backward statistics
 // of dX (bnx/bnmask/bnmean -> bnpart/bnrows).
@@ -843,10 +670,10 @@ DTF_API int dtf_conv_dgrad_x(const void* dY, const void* Wcrsk, void* dX, int N,
   if (bsrc2) {
     if ((H & 1) || (W & 1) || R != 1 || S != 1 || sh != 1 || sw != 1 || ph != 0 || pw != 0) return -11;
     return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, 1, 1, H, W, 1, 1, 0, 0, 1, 1, 0, 1.f, -1, ws, ws_bf16, bnx,
-                           bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, nullptr);
+                           bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream);
   }
   return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, beta, -1, ws, ws_bf16,
-                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, nullptr);
+                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream);
 }
 
 DTF_API int dtf_conv_dgrad_addsub2(const void* dY, const void* Wcrsk, void* dX, const void* bsrc2, int N, int H, int W,
@@ -862,7 +689,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream, const BnFin* fin) {
+                           const void* bsrc2, void* stream) {
   if ((C & 3) || (K & 7)) return -1;
   if (bnx && (out_f32 || (C & 7) || !bnpart || !bnmean || !bnrows)) return -9;
   if (betamask && (out_f32 || beta == 0.f || (C & 7) || sh > 1 || sw > 1)) return -10;
@@ -895,12 +722,11 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
     a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
     a.alpha = 1.f; a.beta = beta; a.act = 0; a.out_f32 = out_f32;
     bn_args(a);
-    if (fin && bnx) a.fin = *fin;  // single launch: it may finalize the BatchNorm backward itself
     bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
     int t = tile;
-    if (!try_gemm8p(a, am, OP_KCONTIG, t, st) && !try_conv256(a, am, OP_KCONTIG, t, st))
+    if (!try_conv256(a, am, OP_KCONTIG, t, st))
       dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
     if (bnrows) *bnrows = bnx ? a.tiles_m : 0;
     return (int)hipGetLastError();
@@ -946,7 +772,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
       const int am = pointwise ? OP_KCONTIG
                      : tap_uniform(K, nkh * nkw, (long)N * P * Q * K) ? OP_DGRAD_T : OP_DGRAD;
       int t = tile;
-      if (!try_gemm8p(a, am, OP_KCONTIG, t, st) && !try_conv256(a, am, OP_KCONTIG, t, st))
+      if (!try_conv256(a, am, OP_KCONTIG, t, st))
         dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
       prow += a.tiles_m;
     }
@@ -984,21 +810,15 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   const bool small = (long)N * H * W * C * 2 < (1l << 31) && (long)N * P * Q * K * 2 < (1l << 31);
   // spatial filters: LDS-DMA staged 128x128 (measured best for every ResNet-50 3x3 filter); 1x1 filters keep
   // the register-staged kernels (tools/conv_roofline.py --only wgrad --tiles)
-  const bool use_glds = small && wgrad_glds_on() && (tile >= 7 || (tile < 0 && R * S > 1));
+  const bool use_glds = small && (tile >= 7 || (tile < 0 && R * S > 1));
   // row-mapped / LDS-DMA loaders: one pixel decode per lane per K-tile row (spatial filters), buffer loads
-  const bool rowmap = small && (use_glds || (!pointwise && rowmap_ok()));
+  const bool rowmap = small && (use_glds || !pointwise);
   // Kout <= 64 spatial filters (ResNet's 56x56 stage and stem): a 128-row tile over Kout would be half empty;
   // compute dW^T [R*S*C][Kout] with the operands swapped on 128x64 tiles and transpose it into dW
-  static const bool swap_on = [] {
-    const char* e = getenv("DTF_WGRAD_SWAP");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool swap_on = true;
   // conv256: dW^T [R*S*C][Kout] = X^T . dY on the 256-row pipelined kernel (M = filter taps x channels, the long
   // dimension; N = Kout), split-K over the pixels into f32 slabs, reduced and transposed into dW
-  static const bool c256w = [] {
-    const char* e = getenv("DTF_CONV256_WGRAD");  // opt-in: slower than gemm_core.h on every ResNet-50 filter
-    return e && e[0] == '1';
-  }();
+  constexpr bool c256w = false;  // (default-on measured slower than gemm_core.h on every ResNet-50 filter)
   const bool c256_forced = tile >= 11 && tile <= 14;
   if (small && ws != nullptr && (c256_forced || (tile < 0 && c256w && conv256_on())) &&
       (pointwise || (C % 8 == 0 && (dh == 1 && dw == 1)))) {

@@ -507,16 +507,12 @@ int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int 
   if (fp8 && (amode != OP_KCONTIG || bmode != OP_KCONTIG)) return 1;
   a.tiles_m = cdiv(a.M, 256);
   a.tiles_n = cdiv(a.N, bn);
-  // pre-activation side output (aux, read again only by the backward), DTF_G256_AUX_NT bits: 0 = nontemporal
+  // pre-activation side output (aux, read again only by the backward), bits: 0 = nontemporal
   // stores (measured +-0); 1 = stored straight from the fragments in the main store pass instead of a second
   // LDS-staged pass (BERT-base +1.5%, GPT-2-medium +1.8%; FFN1 forward 167 -> 141 us / 123 -> 104 us); 2 = also
   // for the fp8 kernels (their own instantiation: 4 VGPR spills; GPT-2-medium fp8 erratic with it, 180-233k vs a
   // steady 231-234k tok/s without: off by default). Default 2 = bit 1
-  static const int aux_nt = [] {
-    const char* e = getenv("DTF_G256_AUX_NT");
-    return e ? atoi(e) : 2;
-  }();
-  a.aux_nt = aux_nt;
+  a.aux_nt = 2;
   count_launch(LC_GEMM256);
   if (bn == 256) launch256<256>(a, amode, bmode, st, fp8);
   else launch256<128>(a, amode, bmode, st, fp8);

@@ -60,34 +60,6 @@ struct ConvGeom {
   FastDiv dPQ, dQ, dHW, dW, dC, dS, dK;
 };
 
-// Fused BatchNorm finalize (mode != 0, on a launch that writes BN partial rows): the launch reduces its own partial
-// rows in its tail and writes the per-channel coefficients — no separate row-reduction / finalize launches on the
-// critical path. Two-level last-arriver hand-off (common.h last_arriver: write-through partial rows, a relaxed
-// ticket add per block, sc1 loads by the reducer; no release fences): the last block of each group of `gs`
-// M-tiles (per column tile) sums the group's rows into the group's first row, the last group of a column tile sums
-// the group rows and finalizes its channels; every sum runs in a fixed row order (deterministic).
-//   mode 1 (forward, stats = sum / sum of squares): scale, shift, mean, invstd (o0..o3), running statistics updated
-//          with `momentum`; p0 = gamma, p1 = beta, p2 = running_mean, p3 = running_var.
-//   mode 2 (backward, stats = sum dz / sum dz*(x-mean)): dgamma, dbeta (o0, o1; += when accumulate) and the apply
-//          coefficients (o2: 3*N floats); p0 = gamma, p1 = mean, p2 = invstd.
-struct BnFin {
-  int mode;
-  int gs;
-  int* tickets;  // zeroed slots: [ceil(tiles_m / gs) * tiles_n] group tickets, then [tiles_n] column-tile tickets
-  const float* p0;
-  const float* p1;
-  float* p2;
-  float* p3;
-  float* o0;
-  float* o1;
-  float* o2;
-  float* o3;
-  float momentum, eps;
-  int accumulate;
-  long count;      // rows reduced per channel (pixels)
-  int* host_done;  // host-side: set to 1 by prep_fin when the launch finalizes (never read on the device)
-};
-
 struct GemmArgs {
   const bf16_t* A;
   const bf16_t* B;
@@ -131,7 +103,6 @@ struct GemmArgs {
   int crm;
   FastDiv dRm1, dRm2;
   int rmH, rmW, rmsh, rmsw, rmh0, rmw0;
-  BnFin fin;
   // fp8 copies of the (bf16-rounded, post-activation / post-dact) output written by the staged epilogue of
   // gemm256.hip (host-checked; the bf16 C store is skipped when no_c): q8 [M][N] row-major, q8T [N][M] transposed,
   // q8col [M/128][N] per-128-row column sums of the values (a bias gradient's partials). Delayed scaling as
@@ -821,141 +792,6 @@ __device__ __forceinline__ v4f mfma_fp8_ab(const v8i& fb, const v8i& fa, const v
   return mfma_fp8x128<0, FP8 == 2 ? 1 : 0>(fb, fa, c);
 }
 
-// ---- fused BatchNorm finalize (BnFin) ------------------------------------------------------------------------------
-// Sum rows r0, r0 + stride, ... (cnt of them) of the [rows][2N] partial matrix over this block's column tile: float4
-// items (I4 = BN/2: both halves of BN columns), NTH / I4 threads per item each taking every (NTH/I4)-th row with four
-// independent loads in flight, combined through LDS in a fixed order. Returns the item's total in threads k == 0.
-template <int BN, int NTH>
-__device__ __forceinline__ float4 fin_sum_rows(const GemmArgs& a, const float* base, long stride, int cnt, int n0,
-                                              float4* red) {
-  constexpr int I4 = BN / 2, TPI = NTH / I4;
-  static_assert(NTH % I4 == 0, "BN/2 float4 items must divide the block");
-  const int item = threadIdx.x % I4, k = threadIdx.x / I4;
-  const int h = item / (BN / 4), c = n0 + (item % (BN / 4)) * 4;
-  float4 s[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) s[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (c < a.N) {
-    const float* p = base + (long)h * a.N + c;
-    int r = k;
-    for (; r + 3 * TPI < cnt; r += 4 * TPI) {
-      float4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = ld_wt4(p + (long)(r + u * TPI) * stride);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { s[u].x += v[u].x; s[u].y += v[u].y; s[u].z += v[u].z; s[u].w += v[u].w; }
-    }
-    for (; r < cnt; r += TPI) {  // (static index: a runtime-indexed s[] would live in scratch)
-      const float4 v = ld_wt4(p + (long)r * stride);
-      s[0].x += v.x; s[0].y += v.y; s[0].z += v.z; s[0].w += v.w;
-    }
-  }
-  float4 t;
-  t.x = (s[0].x + s[1].x) + (s[2].x + s[3].x);
-  t.y = (s[0].y + s[1].y) + (s[2].y + s[3].y);
-  t.z = (s[0].z + s[1].z) + (s[2].z + s[3].z);
-  t.w = (s[0].w + s[1].w) + (s[2].w + s[3].w);
-  __syncthreads();  // red may still be read by the previous round
-  red[threadIdx.x] = t;
-  __syncthreads();
-  float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (k == 0) {
-    for (int j = 0; j < TPI; ++j) {
-      const float4 q = red[j * I4 + item];
-      tot.x += q.x; tot.y += q.y; tot.z += q.z; tot.w += q.w;
-    }
-  }
-  return tot;
-}
-
-// The per-channel finalize math of norm.hip's bn_finalize / bn_bwd_finalize kernels (same formulas).
-__device__ __forceinline__ void fin_channel(const BnFin& f, int c, int C, float a, float b) {
-  if (f.mode == 1) {
-    const float mean = a / (float)f.count;
-    const float var = fmaxf(b / (float)f.count - mean * mean, 0.f);
-    const float inv = rsqrtf(var + f.eps);
-    const float gm = f.p0 ? f.p0[c] : 1.f, bt = f.p1 ? f.p1[c] : 0.f;
-    f.o0[c] = gm * inv;
-    f.o1[c] = bt - mean * gm * inv;
-    if (f.o2) f.o2[c] = mean;
-    if (f.o3) f.o3[c] = inv;
-    if (f.p2) {
-      const float unb = f.count > 1 ? var * (float)f.count / (float)(f.count - 1) : var;
-      f.p2[c] = f.p2[c] * f.momentum + mean * (1.f - f.momentum);
-      f.p3[c] = f.p3[c] * f.momentum + unb * (1.f - f.momentum);
-    }
-  } else {
-    const float is = f.p2[c];
-    const float sdz = a, sdx = b * is;
-    if (f.o0) f.o0[c] = (f.accumulate ? f.o0[c] : 0.f) + sdx;
-    if (f.o1) f.o1[c] = (f.accumulate ? f.o1[c] : 0.f) + sdz;
-    const float gm = f.p0 ? f.p0[c] : 1.f;
-    const float k1 = gm * is, k2 = sdz / (float)f.count, k3 = sdx / (float)f.count;
-    f.o2[c] = k1;
-    f.o2[C + c] = -k1 * k3 * is;
-    f.o2[2 * C + c] = k1 * (f.p1[c] * is * k3 - k2);
-  }
-}
-
-// Tail of a launch with BnFin: called by every block after its partial row (stats row tile_m, columns n0..n0+BN)
-// is written. smem: >= 16 + NTH*16 + 8*BN bytes of free LDS.
-template <int BN, int NTH>
-__device__ __forceinline__ void bn_fin_tail(const GemmArgs& a, char* smem, int tile_m, int n0) {
-  const BnFin& f = a.fin;
-  const int tn = n0 / BN, G = f.gs;
-  const int grp = tile_m / G, r0 = grp * G, r1 = min(a.tiles_m, r0 + G);
-  const int ngroups = (a.tiles_m + G - 1) / G;
-  const long rs = 2L * a.N;
-  int* flag = reinterpret_cast<int*>(smem);
-  float4* red = reinterpret_cast<float4*>(smem + 16);
-  float* fin = reinterpret_cast<float*>(smem + 16 + NTH * 16);
-  constexpr int I4 = BN / 2;
-  if (!last_arriver(f.tickets + grp * a.tiles_n + tn, r1 - r0, flag)) return;
-  // level 1: the group's rows -> its first row
-  const float4 g1 = fin_sum_rows<BN, NTH>(a, a.stats + (long)r0 * rs, rs, r1 - r0, n0, red);
-  const int item = threadIdx.x % I4, h = item / (BN / 4), c = n0 + (item % (BN / 4)) * 4;
-  if (threadIdx.x < I4 && c < a.N) {
-    float* p = a.stats + (long)r0 * rs + (long)h * a.N + c;
-    st_wt(p, g1.x); st_wt(p + 1, g1.y); st_wt(p + 2, g1.z); st_wt(p + 3, g1.w);
-  }
-  if (!last_arriver(f.tickets + ngroups * a.tiles_n + tn, ngroups, flag)) return;
-  // level 2: the group rows (stride G rows) -> finalize
-  const float4 g2 = fin_sum_rows<BN, NTH>(a, a.stats, (long)G * rs, ngroups, n0, red);
-  if (threadIdx.x < I4) {
-    const int cl = (item % (BN / 4)) * 4;
-    fin[h * BN + cl] = g2.x; fin[h * BN + cl + 1] = g2.y; fin[h * BN + cl + 2] = g2.z; fin[h * BN + cl + 3] = g2.w;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < BN; i += NTH) {
-    const int ch = n0 + i;
-    if (ch < a.N) fin_channel(f, ch, a.N, fin[i], fin[BN + i]);
-  }
-}
-
-// Host: arm a launch's BnFin once its tiling (tiles_m, tiles_n) is known — group size ~sqrt(tiles_m) so both
-// reduction levels read ~sqrt(rows) rows — or disarm it (no stats, split launch, no ticket slots: e.g. first use
-// inside a stream capture); *host_done tells the caller whether the finalize runs in the launch.
-inline void prep_fin(GemmArgs& a) {
-  int* host_done = a.fin.host_done;
-  if (host_done) *host_done = 0;
-  if (!a.fin.mode) return;
-  if (!a.stats || a.batch != 1 || a.splitk != 1 || a.tiles_m < 1 || (a.N & 3)) {
-    a.fin.mode = 0;
-    return;
-  }
-  int gs = 1;
-  while (gs * gs < a.tiles_m) ++gs;
-  const int ng = (a.tiles_m + gs - 1) / gs;
-  int* t = dtf_tickets(ng * a.tiles_n + a.tiles_n);
-  if (!t) {
-    a.fin.mode = 0;
-    return;
-  }
-  a.fin.gs = gs;
-  a.fin.tickets = t;
-  if (host_done) *host_done = 1;
-}
-
 // Shared epilogue of the MFMA GEMM kernels (gemm_kernel here, conv256_kernel in conv256.hip): the block's
 // BM x BN accumulator tile is held by WM x WN waves as acc[TM][TN] 16x16 fragments (wave (wm, wn) = (wave / WN,
 // wave % WN) owns rows wm*BM/WM.., cols wn*BN/WN..); NTH threads; SMEMB bytes of LDS at smem are free.
@@ -1105,13 +941,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
         if (n >= a.N) continue;
         float sv = 0.f, qv = 0.f;
         for (int t = nl >> 3; t < NTH; t += C8) { sv += red[t * 16 + (nl & 7)]; qv += red[t * 16 + 8 + (nl & 7)]; }
-        if (a.fin.mode) {  // read by this launch's last arriver: write-through
-          st_wt(prow + n, sv);
-          st_wt(prow + a.N + n, qv);
-        } else {
-          prow[n] = sv;
-          prow[a.N + n] = qv;
-        }
+        prow[n] = sv;
+        prow[a.N + n] = qv;
       }
     } else if (a.stats) {
       __syncthreads();  // the statistics reduction below reuses the LDS
@@ -1214,16 +1045,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
       float s = 0.f, q = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) { s += red[w * BN + nl]; q += red[WM * BN + w * BN + nl]; }
-      if (a.fin.mode) {  // read by this launch's last arriver: write-through
-        st_wt(prow + n, s);
-        st_wt(prow + a.N + n, q);
-      } else {
-        prow[n] = s;
-        prow[a.N + n] = q;
-      }
+      prow[n] = s;
+      prow[a.N + n] = q;
     }
   }
-  if (a.stats && a.fin.mode) bn_fin_tail<BN, NTH>(a, smem, tile_m, n0);
 }
 
 // Block -> (tile, z) over a grid of nwg tiles x gridDim.z (split-K slices / batch entries), gridDim.y == 1. The

@@ -311,25 +311,20 @@ DTF_API void dtf_sum_rows(float* rows, long stride, int nrows, long W, float* ou
 
 namespace dtf {
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int bn);  // gemm256.hip
-int pick256(long M, long N, long K, long batch);                                      // gemm.hip
 }  // namespace dtf
 
 using namespace dtf;
 
-// Tile policy of the fp8 GEMMs (DTF_FP8_TILES): 0 = the bf16 rule (pick256 with the fp8 K in bf16 units); 1 = the
-// 256-row pipelined kernel whenever it has >= 128 tiles, 256x128 tiles when only those fill the chip; 2 = as 1 but
-// 256x128 tiles whenever 256x256 would leave CUs idle in its last round. The scaled fp8 MFMA does twice the work per
-// staged byte of bf16, so the 128-row register-staged tiles are relatively more load/latency bound. Measured on
-// GPT-2-medium fp8 (interleaved A/B): mode 2 35.25 / 35.27 ms/step, mode 0 35.75 / 35.60, mode 1 35.84 / 35.94.
+// Tile policy of the fp8 GEMMs: the 256-row pipelined kernel whenever it has >= 128 tiles, 256x128 tiles whenever
+// 256x256 would leave CUs idle in its last round and 256x128 fill whole rounds. The scaled fp8 MFMA does twice the
+// work per staged byte of bf16, so the 128-row register-staged tiles are relatively more load/latency bound.
+// Measured on GPT-2-medium fp8 (interleaved A/B): 35.25 / 35.27 ms/step vs 35.75 / 35.60 with the bf16 rule and
+// 35.84 / 35.94 without the 256x128 preference.
 static int pick256_fp8(long M, long N, long K) {
-  static const int mode = [] {
-    const char* e = getenv("DTF_FP8_TILES");
-    return e ? atoi(e) : 2;
-  }();
-  if (mode == 0) return pick256(M, N, 2L * K, 1);
+  (void)K;
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256), t2x1 = (long)cdiv(M, 256) * cdiv(N, 128);
-  if (mode == 2 && t2x1 >= 128 && (t256 % 256) != 0 && t2x1 % 256 == 0) return 128;
-  if (t256 >= 128 && (mode != 2 || t256 % 256 == 0)) return 256;
+  if (t2x1 >= 128 && (t256 % 256) != 0 && t2x1 % 256 == 0) return 128;
+  if (t256 >= 128 && t256 % 256 == 0) return 256;
   if (t2x1 >= 128) return 128;
   return 0;
 }
@@ -453,26 +448,23 @@ DTF_API int dtf_gemm_fp8_ex(const void* A, const void* B, void* C, void* aux, co
   a.tiles_m = cdiv(M, 128);
   a.tiles_n = cdiv(N, big ? 128 : 64);
   dim3 grid(a.tiles_m * a.tiles_n, 1, 1);
-  // staging of the 128-row tiles (DTF_FP8_PIPE): 2 = register-staged double-buffered LDS, 3 / 4 = LDS-DMA single /
+  // staging of the 128-row tiles: 2 = register-staged double-buffered LDS, 3 / 4 = LDS-DMA single /
   // double buffered (both operand rows are 16-B aligned: host-checked above). 3 measured fastest standalone on the
   // GPT-2-medium projections (tools/bench_fp8_gemms.py: 0.602 vs 0.631 ms per layer for 2, 0.615 for 4) but slower in
   // the model step (35.89 vs 35.17 ms: the side-stream weight gradients share the CUs), so 2 stays the default
-  static const int pipe = [] {
-    const char* e = getenv("DTF_FP8_PIPE");
-    return e ? atoi(e) : 2;
-  }();
-#define DTF_FP8_L(BN_, F_, P_) hipLaunchKernelGGL((gemm_kernel<128, BN_, 2, 2, OP_KCONTIG, OP_KCONTIG, F_, P_>), grid, \
+  constexpr int pipe = 2;
+#define FP8_LAUNCH(BN_, F_, P_) hipLaunchKernelGGL((gemm_kernel<128, BN_, 2, 2, OP_KCONTIG, OP_KCONTIG, F_, P_>), grid, \
                                                   dim3(NT), 0, st, a)
-#define DTF_FP8_P(BN_, F_)                  \
-  if (pipe == 4) DTF_FP8_L(BN_, F_, 4);     \
-  else if (pipe == 3) DTF_FP8_L(BN_, F_, 3); \
-  else DTF_FP8_L(BN_, F_, 2);
-  if (big && fp8 == 2) { DTF_FP8_P(128, 2) }
-  else if (big) { DTF_FP8_P(128, 1) }
-  else if (fp8 == 2) { DTF_FP8_P(64, 2) }
-  else { DTF_FP8_P(64, 1) }
-#undef DTF_FP8_P
-#undef DTF_FP8_L
+#define FP8_PIPE_LAUNCH(BN_, F_)                  \
+  if (pipe == 4) FP8_LAUNCH(BN_, F_, 4);     \
+  else if (pipe == 3) FP8_LAUNCH(BN_, F_, 3); \
+  else FP8_LAUNCH(BN_, F_, 2);
+  if (big && fp8 == 2) { FP8_PIPE_LAUNCH(128, 2) }
+  else if (big) { FP8_PIPE_LAUNCH(128, 1) }
+  else if (fp8 == 2) { FP8_PIPE_LAUNCH(64, 2) }
+  else { FP8_PIPE_LAUNCH(64, 1) }
+#undef FP8_PIPE_LAUNCH
+#undef FP8_LAUNCH
   return (int)hipGetLastError();
 }
 

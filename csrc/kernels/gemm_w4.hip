@@ -418,7 +418,7 @@ void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
 // rows, K-outer operands with row counts % 8 == 0, operands < 2 GiB, and only the epilogue features w4_epilogue has.
 bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode) {
   if (a.atomic_out || a.stats || a.bnx || a.crm || a.bsrc || a.betamask || a.scales || a.q8 || a.q8T || a.q8col ||
-      a.zero_slot || a.fin.mode)
+      a.zero_slot)
     return false;
   if (a.out_f32 ? (a.bias || a.act || a.aux || a.dact || (a.ldc & 3) || ((uintptr_t)a.C & 15))
                 : ((a.N & 7) || (a.ldc & 7) || ((uintptr_t)a.C & 15)))

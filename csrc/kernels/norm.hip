@@ -892,37 +892,20 @@ int red_grid(long M, int C) {
 
 // leader rows left by the first (grouping) pass of a BN statistics reduction, which the finalize kernel then sums:
 // the grouping pass runs one block per leader row (more rows = more blocks reading the partials in parallel)
-static int bn_group_target() {
-  static const int t = [] {
-    const char* e = getenv("DTF_BN_GROUP_TARGET");  // (the finalize kernels sum up to ~256 rows themselves)
-    return e ? std::max(1, atoi(e)) : 256;
-  }();
-  return t;
-}
+static int bn_group_target() { return 256; }  // (the finalize kernels sum up to ~256 rows themselves)
 
 // Elementwise passes that consume a GEMM output sweep the rows last-to-first: the GEMM wrote them first-to-last,
 // so the most recently written rows (still in the 256 MiB Infinity Cache) are read first; the next GEMM then
-// reads this pass's output in its own first-to-last order, again most recent first. DTF_EW_REVERSE=1: on.
-static int ew_reverse() {
-  static const int on = [] {
-    const char* e = getenv("DTF_EW_REVERSE");  // opt-in: no measurable effect on ResNet-50 (b256)
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return on;
-}
+// reads this pass's output in its own first-to-last order, again most recent first. Measured: no effect on
+// ResNet-50 (b256): off.
+static int ew_reverse() { return 0; }
 
 // Variant of the streaming BN passes (tools/bench_bnb.py sweeps it; dtf_set_ew_variant): 0 = EU rows per trip,
 // 1 = + nontemporal hints, 2 = 8 rows per trip, 3 = 8 rows + nontemporal, 4 = 2 rows per trip
 // Measured (tools/bench_bnb.py, MI355X, ResNet-50 b256 shapes): 2 rows per trip is 3-9% faster than 4 on the
 // tensors that miss the Infinity Cache; nontemporal hints and 8 rows are not faster.
-int g_ew_variant = [] {
-  const char* e = getenv("DTF_EW_VARIANT");
-  return e ? atoi(e) : 4;
-}();
-int g_ew_apply_nu = [] {  // rows per trip of the forward apply pass (2, 4 or 8)
-  const char* e = getenv("DTF_EW_APPLY_NU");
-  return e ? atoi(e) : 2;
-}();
+int g_ew_variant = 4;
+int g_ew_apply_nu = 2;  // rows per trip of the forward apply pass (2, 4 or 8; 4 measured -0.4%)
 
 // elementwise channels-last passes: enough blocks to fill the chip, each with >= nu row trips when possible
 int ew_grid(long M, int C, int nu = EU) {
@@ -1072,18 +1055,18 @@ static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, con
                          (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, (bf16_t*)dx,
                          (bf16_t*)dz_out, (const bf16_t*)sc->x2, sc->mean2, sc->part2, ew_reverse());
   } else {
-#define DTF_BNB(NU, NT)                                                                                        \
+#define BNB_LAUNCH(NU, NT)                                                                                        \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<false, NU, NT>), dim3(ew_grid(M, C, NU)), dim3(256), 0, st,            \
                      (const bf16_t*)dy, (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, coef, M, C, \
                      (bf16_t*)dx, (bf16_t*)dz_out, nullptr, nullptr, nullptr, ew_reverse())
     switch (g_ew_variant) {
-      case 1: DTF_BNB(EU, true); break;
-      case 2: DTF_BNB(8, false); break;
-      case 3: DTF_BNB(8, true); break;
-      case 4: DTF_BNB(2, false); break;
-      default: DTF_BNB(EU, false); break;
+      case 1: BNB_LAUNCH(EU, true); break;
+      case 2: BNB_LAUNCH(8, false); break;
+      case 3: BNB_LAUNCH(8, true); break;
+      case 4: BNB_LAUNCH(2, false); break;
+      default: BNB_LAUNCH(EU, false); break;
     }
-#undef DTF_BNB
+#undef BNB_LAUNCH
   }
   return (int)hipGetLastError();
 }
@@ -1146,7 +1129,7 @@ DTF_API int dtf_maxpool_bn_bwd(const void* dy, const void* arg, const void* x, c
   return (int)hipGetLastError();
 }
 
-#define DTF_LN_DISPATCH(D, F) \
+#define LN_DISPATCH(D, F) \
   if ((D) <= 512) F(1); else if ((D) <= 1024) F(2); else if ((D) <= 1536) F(3); else F(4)
 
 DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
@@ -1155,7 +1138,7 @@ DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* be
 #define LNF(NC) \
   hipLaunchKernelGGL(ln_fwd_kernel<NC>, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream,             \
                       (const bf16_t*)x, gamma, beta, (bf16_t*)y, mean, rstd, M, D, eps)
-  DTF_LN_DISPATCH(D, LNF);
+  LN_DISPATCH(D, LNF);
 #undef LNF
   return (int)hipGetLastError();
 }
@@ -1176,12 +1159,8 @@ DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma
   if ((D & 7) || D > 2048) return -1;
   // ~48 rows (12 per wave) per block, 256..1024 blocks: long enough software-pipelined row walks per wave and a
   // smaller partial-row reduction; measured in the training step (the pass shares the CUs with the weight-gradient
-  // GEMMs): BERT-base 19.60 -> 19.17 ms/step vs 16 rows per block. DTF_LN_BWD_ROWS overrides the row count.
-  static const long rows_per_block = [] {
-    const char* e = getenv("DTF_LN_BWD_ROWS");
-    return e ? std::max(4L, atol(e)) : 0L;
-  }();
-  long blocks = rows_per_block ? cdiv(M, rows_per_block) : std::max<long>(256, cdiv(M, 48));
+  // GEMMs): BERT-base 19.60 -> 19.17 ms/step vs 16 rows per block.
+  long blocks = std::max<long>(256, cdiv(M, 48));
   blocks = std::max<long>(1, std::min<long>(blocks, std::min<long>(1024, cdiv(M, 4))));
   blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / (2L * D)));
   const size_t sh = sizeof(float) * 8 * D;
@@ -1189,7 +1168,7 @@ DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma
   hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3((unsigned)blocks), dim3(256), sh, (hipStream_t)stream,       \
                       (const bf16_t*)dy, (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, ws, M, D,            \
                       (const bf16_t*)res)
-  DTF_LN_DISPATCH(D, LNB);
+  LN_DISPATCH(D, LNB);
 #undef LNB
   dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, accumulate, stream);
   return (int)hipGetLastError();

@@ -203,208 +203,12 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
   }
 }
 
-// ---- forward BN apply by recomputation -----------------------------------------------------------------------
-// out = [relu]( bf16(X W^T) * scale + shift [+ res [* rscale + rshift]] ) with the 1-bit ReLU mask: the same
-// product as pw_conv_kernel (identical MFMA sequence: bit-identical bf16 y), recomputed from X instead of re-reading
-// the stored y — for C_in 64 the conv's input is 1/4 of its output, so the BatchNorm apply pass reads x (M x C)
-// instead of y (M x 4C). Same arithmetic as norm.hip bn_apply_kernel (bitwise equal output and mask).
-// The tile is staged through LDS and written as 16-B row chunks; each thread owns one 8-channel column chunk of the
-// 256-wide tile for the whole kernel (its scale / shift in registers) and loads its residual chunks at the top of
-// the iteration, waited for just before the epilogue.
-struct PwApplyArgs {
-  const bf16_t* X;
-  const bf16_t* W;
-  const float* scale;
-  const float* shift;
-  const bf16_t* res;     // optional [M][K]
-  const float* rscale;   // optional (with res): the residual is a BatchNorm input
-  const float* rshift;
-  bf16_t* out;           // [M][K]
-  uint8_t* mbits;        // optional [M*K/8]
-  int M, K, relu;
-  int tiles_m, tiles_n, nslots;
-};
-
-template <int LD, int RL, int ST>
-__device__ __forceinline__ void pa_wait(int nd, int nr, int ns) {
-#define DTF_PAW(D, R, S)                                                                \
-  if (nd == D && nr == R && ns == S) {                                                  \
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * LD + R * RL + S * ST) : "memory");     \
-    return;                                                                             \
-  }
-  DTF_PAW(0, 0, 0) DTF_PAW(1, 0, 0) DTF_PAW(2, 0, 0) DTF_PAW(0, 1, 0) DTF_PAW(1, 1, 0) DTF_PAW(0, 1, 1)
-  DTF_PAW(1, 1, 1) DTF_PAW(0, 1, 2) DTF_PAW(1, 1, 2) DTF_PAW(2, 1, 1) DTF_PAW(2, 1, 0) DTF_PAW(0, 0, 1)
-#undef DTF_PAW
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int C, int WMW>
-__global__ void __launch_bounds__(256 * WMW, 1) pw_apply_kernel(PwApplyArgs a) {
-  using G = PwGeo<C, WMW, true>;
-  constexpr int CH = G::ST;           // 16-B chunks per thread per tile
-  constexpr int STA = 2 * CH;         // stores per thread per tile: the chunks + their mask bytes
-  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wn = wave & 3, wm = wave >> 2;
-  const int b = blockIdx.x, xcd = b & 7, j8 = b >> 3;
-  const int tile_n = j8 % a.tiles_n;
-  const int slot = xcd + 8 * (j8 / a.tiles_n);
-  const int n0 = tile_n * 256 + wn * 64;
-
-  v8bf fb[4][C / 32];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int s = 0; s < C / 32; ++s)
-      fb[j][s] = *reinterpret_cast<const v8bf*>(a.W + (long)(n0 + 16 * j + (lane & 15)) * C + 32 * s +
-                                                  8 * (lane >> 4));
-  // this thread's 8-channel column chunk (fixed: NTH is a multiple of 32) and its coefficients
-  const int ch = t & 31, col = tile_n * 256 + ch * 8;
-  float sc[8], sh[8], rsc[8], rsh[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = a.scale[col + e];
-    sh[e] = a.shift[col + e];
-    rsc[e] = a.rscale ? a.rscale[col + e] : 1.f;
-    rsh[e] = a.rscale ? a.rshift[col + e] : 0.f;
-  }
-
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.X, (short)0, (int)((long)a.M * C * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t orr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)((long)a.M * a.K * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.res ? a.res : a.out), (short)0, a.res ? (int)((long)a.M * a.K * 2) : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.mbits ? (void*)a.mbits : (void*)a.out), (short)0, a.mbits ? (int)((long)a.M * a.K / 8) : 0,
-      0x00020000);
-  auto issue = [&](int mt, int buf) {
-    char* img = smem + buf * G::IMG;
-#pragma unroll
-    for (int i = 0; i < G::L; ++i) {
-      const int row = G::RPI * i + (t >> 3);
-      const int r = mt * G::BM + row;
-      const uint32_t base = r < a.M ? (uint32_t)r * (uint32_t)(C * 2) + (uint32_t)(((t & 7) ^ ((row >> 1) & 7)) * 16)
-                                    : 0x80000000u;
-#pragma unroll
-      for (int kt = 0; kt < G::NKT; ++kt)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            xr, (__attribute__((address_space(3))) void*)(img + kt * G::SUB + i * (G::RPI * 128) + wave * 1024), 16,
-            base + kt * 128, 0, 0, 0);
-    }
-  };
-  auto chunk_off = [&](int mt, int k) -> uint32_t {  // byte offset of chunk k of this thread in tile mt
-    const int row = (t + k * G::NTH) >> 5, m = mt * G::BM + row;
-    return m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)col) * 2u : 0x80000000u;
-  };
-
-  const int first = slot, step = a.nslots;
-  const int n_mine = first < a.tiles_m ? (a.tiles_m - first + step - 1) / step : 0;
-  char* stg = smem + G::NBUF * G::IMG;
-  // issue order: R0 D0 D1 | per iteration it: R(it+1) D(it+2) ... S(it)  (R = a tile's residual chunks into
-  // registers, one tile ahead; D = its activation DMA; S = its stores + mask bytes)
-  uint4 rv[2][CH];
-  auto load_res = [&](int tl, uint4 (&dst)[CH]) {
-#pragma unroll
-    for (int k = 0; k < CH; ++k)
-      dst[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rr, a.res ? chunk_off(first + tl * step, k) : 0x80000000u, 0, 0));
-  };
-  if (n_mine > 0) load_res(0, rv[0]);
-  if (n_mine > 0) issue(first, 0);
-  if (n_mine > 1) issue(first + step, 1);
-
-  for (int it = 0; it < n_mine; ++it) {
-    // after D(it): it 0: [D1]; it 1: R1 [D2] S0; it >= 2: S(it-2) R(it) [D(it+1)] S(it-1)
-    {
-      const int d1 = it + 1 < n_mine ? 1 : 0;
-      if (it == 0) pa_wait<G::LD, CH, STA>(d1, 0, 0);
-      else if (it == 1) pa_wait<G::LD, CH, STA>(d1, 1, 1);
-      else pa_wait<G::LD, CH, STA>(d1, 1, 2);
-    }
-    __syncthreads();
-    const int mt = first + it * step;
-    if (it + 1 < n_mine) load_res(it + 1, rv[(it + 1) & 1]);
-    if (it + 2 < n_mine) issue(first + (it + 2) * step, (it + 2) % G::NBUF);
-    const char* img = smem + (it % G::NBUF) * G::IMG;
-    v4f acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < G::NKT; ++kt)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        v8bf fa[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = frag_kcontig(img + kt * G::SUB, wm * 64 + 16 * i, kk, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][2 * kt + kk], fa[i], acc[i][j], 0, 0, 0);
-      }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ml = wm * 64 + 16 * i + (lane & 15), nl = wn * 64 + 16 * j + 4 * (lane >> 4);
-        uint2 o;
-        o.x = pack2bf(acc[i][j][0], acc[i][j][1]);
-        o.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-        *reinterpret_cast<uint2*>(stg + (ml * G::SROW + nl) * 2) = o;
-      }
-    // R(it) landed: after it come D(it+1) (issued an iteration ago), S(it-1), R(it+1), D(it+2) — those that exist
-    pa_wait<G::LD, CH, STA>((it + 1 < n_mine ? 1 : 0) + (it + 2 < n_mine ? 1 : 0), it + 1 < n_mine ? 1 : 0,
-                            it >= 1 ? 1 : 0);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < CH; ++k) {
-      const int row = (t + k * G::NTH) >> 5;
-      float f[8], r[8], o[8];
-      load8(reinterpret_cast<const bf16_t*>(stg) + row * G::SROW + ch * 8, f);
-      const uint4 rk = rv[it & 1][k];
-      const uint32_t rw[4] = {rk.x, rk.y, rk.z, rk.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        r[2 * q] = __uint_as_float(rw[q] << 16);
-        r[2 * q + 1] = __uint_as_float(rw[q] & 0xffff0000u);
-      }
-      uint32_t bits = 0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = fmaf(f[e], sc[e], sh[e]);
-        if (a.res) v += a.rscale ? fmaf(r[e], rsc[e], rsh[e]) : r[e];
-        if (a.relu) v = fmaxf(v, 0.f);
-        o[e] = v;
-        bits |= (uint32_t)(f2bf(v) != 0 && v > 0.f) << e;
-      }
-      uint4 ov;
-      ov.x = pack2bf(o[0], o[1]); ov.y = pack2bf(o[2], o[3]);
-      ov.z = pack2bf(o[4], o[5]); ov.w = pack2bf(o[6], o[7]);
-      const uint32_t off = chunk_off(mt, k);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, ov), orr, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mr, (a.mbits && off != 0x80000000u) ? off / 16u
-                                                                                                   : 0x80000000u, 0, 0);
-    }
-  }
-}
-
 template <int C, int WMW, bool STG = false>
 void launch_pw(const PwArgs& a, int grid, hipStream_t st) {
   hipLaunchKernelGGL((pw_conv_kernel<C, WMW, STG>), dim3(grid), dim3(256 * WMW), 0, st, a);
 }
 
 }  // namespace
-
-bool pwconv_on() {
-  static const bool on = [] {
-    const char* e = getenv("DTF_PWCONV");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 
 // Y[M][K] = X[M][C] . W[K][C]^T with the per-column BN statistics of Y as partial rows; C in {64, 128, 256},
 // K a multiple of 256 with K/256 in {1, 2, 4, 8}. Returns the number of partial rows written (> 0) or 0 when the
@@ -415,19 +219,11 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
   if (tiles_n != 1 && tiles_n != 2 && tiles_n != 4 && tiles_n != 8) return 0;
   if (M * C * 2 >= (1l << 31) || M * K * 2 >= (1l << 31)) return 0;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 15)) return 0;
-  // C 256: the 128-VGPR filter slice leaves room for one wave per SIMD; C 64 / 128: two row waves per block, or
-  // (DTF_PW_BPC = 2 or 3, C 64 only) several one-row-wave blocks per CU
-  static const int bpc = [] {
-    const char* e = getenv("DTF_PW_BPC");
-    return e ? std::max(1, std::min(3, atoi(e))) : 1;
-  }();
-  // DTF_PW_STAGE (default 1): the tile is stored through an LDS stage as row-contiguous 16-B chunks (C_in 128 then
-  // takes one row wave per block: the 3-deep ring plus the stage of a 128-row tile would exceed the LDS)
-  static const bool stage = [] {
-    const char* e = getenv("DTF_PW_STAGE");
-    return !(e && e[0] == '0');
-  }();
-  const int wmw = (C == 256 || (C == 64 && bpc > 1) || (C == 128 && stage)) ? 1 : 2;
+  // C 128 / 256: one row wave per block (the 128-VGPR filter slice; for C 128 the 3-deep ring plus the LDS store
+  // stage of a 128-row tile would exceed the LDS); C 64: two row waves per block. Every tile is stored through an
+  // LDS stage as row-contiguous 16-B chunks. (Measured alternatives, removed: several one-row-wave blocks per CU
+  // for C 64, direct fragment stores: profiles/r4_pointwise_conv_bw_probe.txt, r4_negative_results.txt.)
+  const int wmw = C == 64 ? 2 : 1;
   const int bm = 64 * wmw;
   PwArgs a{};
   a.X = (const bf16_t*)X; a.W = (const bf16_t*)W; a.Y = (bf16_t*)Y; a.stats = stats;
@@ -437,47 +233,16 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
   if (a.tiles_m < 8) return 0;
   // one block per CU (or bpc); fewer when there are fewer tiles (grid stays a multiple of 8 * tiles_n, and the
   // partial rows (one per row slot) never outnumber the M-tiles: the caller's scratch holds ceil(M/64) rows)
-  int grid = 256 * (wmw == 1 && C == 64 ? bpc : 1);
-  while (grid > 8 * tiles_n && grid / tiles_n > a.tiles_m) grid /= 2;
-  a.nslots = grid / tiles_n;
-  if (a.nslots > a.tiles_m && a.nslots > 8) return 0;
-  if (C == 64 && wmw == 1) launch_pw<64, 1>(a, grid, st);
-  else if (C == 64 && stage) launch_pw<64, 2, true>(a, grid, st);
-  else if (C == 64) launch_pw<64, 2>(a, grid, st);
-  else if (C == 128 && stage) launch_pw<128, 1, true>(a, grid, st);
-  else if (C == 128) launch_pw<128, 2>(a, grid, st);
-  else if (stage) launch_pw<256, 1, true>(a, grid, st);
-  else launch_pw<256, 1>(a, grid, st);
-  return hipGetLastError() == hipSuccess ? a.nslots : 0;
-}
-
-
-bool pwapply_try(const void* X, const void* W, const float* scale, const float* shift, const void* res,
-                 const float* rscale, const float* rshift, void* out, void* mbits, long M, int C, int K, int relu,
-                 hipStream_t st) {
-  if (!(C == 64 || C == 128 || C == 256) || (K % 256) || !scale || !shift) return false;
-  if ((rscale == nullptr) != (rshift == nullptr) || (rscale && !res)) return false;
-  const int tiles_n = K / 256;
-  if (tiles_n != 1 && tiles_n != 2 && tiles_n != 4 && tiles_n != 8) return false;
-  if (M * C * 2 >= (1l << 31) || M * K * 2 >= (1l << 31)) return false;
-  if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)out & 15) || ((uintptr_t)res & 15)) return false;
-  const int wmw = C == 64 ? 2 : 1;  // (LDS: the 3-deep ring + the staged 256-wide tile)
-  PwApplyArgs a{};
-  a.X = (const bf16_t*)X; a.W = (const bf16_t*)W; a.scale = scale; a.shift = shift;
-  a.res = (const bf16_t*)res; a.rscale = rscale; a.rshift = rshift;
-  a.out = (bf16_t*)out; a.mbits = (uint8_t*)mbits;
-  a.M = (int)M; a.K = K; a.relu = relu;
-  a.tiles_m = (int)((M + 64 * wmw - 1) / (64 * wmw));
-  a.tiles_n = tiles_n;
-  if (a.tiles_m < 8) return false;
   int grid = 256;
   while (grid > 8 * tiles_n && grid / tiles_n > a.tiles_m) grid /= 2;
   a.nslots = grid / tiles_n;
-  if (C == 64) hipLaunchKernelGGL((pw_apply_kernel<64, 2>), dim3(grid), dim3(512), 0, st, a);
-  else if (C == 128) hipLaunchKernelGGL((pw_apply_kernel<128, 1>), dim3(grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((pw_apply_kernel<256, 1>), dim3(grid), dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess;
+  if (a.nslots > a.tiles_m && a.nslots > 8) return 0;
+  if (C == 64) launch_pw<64, 2, true>(a, grid, st);
+  else if (C == 128) launch_pw<128, 1, true>(a, grid, st);
+  else launch_pw<256, 1, true>(a, grid, st);
+  return hipGetLastError() == hipSuccess ? a.nslots : 0;
 }
+
 
 }  // namespace dtf
 
@@ -487,14 +252,4 @@ DTF_API int dtf_pwconv_fwd(const void* X, const void* W, void* Y, float* stats, 
   const int r = dtf::pwconv_try(X, W, Y, stats, M, C, K, (hipStream_t)stream);
   if (rows) *rows = r;
   return r > 0 ? 0 : -1;
-}
-
-// out = [relu](BN(X W^T) [+ res]) with the ReLU mask, recomputing the pointwise product (see pw_apply_kernel): the
-// same shapes as dtf_pwconv_fwd. Returns 0 when launched, -1 when the shape is not handled.
-DTF_API int dtf_pwconv_apply(const void* X, const void* W, const float* scale, const float* shift, const void* res,
-                             const float* rscale, const float* rshift, void* out, void* mbits, long M, int C, int K,
-                             int relu, void* stream) {
-  return dtf::pwapply_try(X, W, scale, shift, res, rscale, rshift, out, mbits, M, C, K, relu, (hipStream_t)stream)
-             ? 0
-             : -1;
 }

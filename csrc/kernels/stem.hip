@@ -113,10 +113,7 @@ DTF_API int dtf_stem_fwd(const void* X, const void* Wt, void* Y, float* part, in
     return -1;
   if (((uintptr_t)X | (uintptr_t)Wt | (uintptr_t)Y) & 15) return -1;
   const int units = N * ((P + RG - 1) / RG);
-  static const int grid_cap = [] {
-    const char* e = getenv("DTF_STEM_GRID");
-    return e ? atoi(e) : 512;  // 2 blocks per CU (register-bound: the filter lives in VGPRs)
-  }();
+  constexpr int grid_cap = 512;  // 2 blocks per CU (register-bound: the filter lives in VGPRs)
   // the callers size `part` for the conv stats contract: ceil(N*P*Q/64) rows — never write more rows than that
   // (the units loop is persistent, so a smaller grid only means more units per block)
   const long cap_rows = ((long)N * P * Q + 63) / 64;

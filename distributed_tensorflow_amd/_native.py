@@ -26,14 +26,11 @@ _KERNEL_SIGS = {
     "dtf_gemm": [P, P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, L, L, L, F, F, I, I, I, I, P, L, P],
     "dtf_conv_fwd": [P, P, P, P, P, P] + [I] * 15 + [I, I, I, P],
     "dtf_pwconv_fwd": [P, P, P, P, P, L, I, I, P],
-    "dtf_pwconv_apply": [P, P, P, P, P, P, P, P, P, L, I, I, I, P],
     "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P, L, P, P, P, P, P, P, P],
     "dtf_conv_dgrad_addsub2": [P, P, P, P, I, I, I, I, I, I, P, L, P, P, P, P, P, P],
     "dtf_conv_fwd_bn": [P, P, P, P] + [I] * 15 + [I, P, P, P, P, F, F, P, P, P, P, P, P],
-    "dtf_conv_dgrad_bn": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P, P, P, P, I, P, P, P],
     "dtf_conv_dgrad_x": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P],
     "dtf_bn_bwd_apply_coef": [P, P, P, L, I, P, P, P, P, P, P, P, P],
-    "dtf_set_bn_fin_fused": [I],
     "dtf_set_ew_variant": [I],
     "dtf_set_ew_apply_nu": [I],
     "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P],
@@ -70,7 +67,6 @@ _KERNEL_SIGS = {
     "dtf_dropout": [P, P, L, F, U, P, P],
     "dtf_rng_advance": [P, P],
     "dtf_gemm256": [P, P, P, I, I, I, L, L, L, I, I, I, I, P, L, P],
-    "dtf_gemm8p": [P, P, P, I, I, I, L, L, L, I, I, P],
     "dtf_gemm_w4": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
     "dtf_gemm_w4_var": [P, P, P, I, I, I, I, I, P],
     "dtf_launch_counts": [P, I],

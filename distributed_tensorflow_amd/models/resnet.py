@@ -13,7 +13,6 @@ gradient and never influence the output).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -23,9 +22,9 @@ from ..keras.models import Model
 
 from ..ops.conv import ResidualGradLink
 
-RES_LINK = os.environ.get("DTF_RES_LINK", "1") != "0"
-FUSE_STEM = os.environ.get("DTF_FUSE_STEM", "1") != "0"  # stem BN + ReLU + MaxPool as one pass
-S2D_STEM = os.environ.get("DTF_S2D_STEM", "1") != "0"  # stem conv over the 2x2 space-to-depth image
+RES_LINK = True
+FUSE_STEM = True  # stem BN + ReLU + MaxPool as one pass
+S2D_STEM = True  # stem conv over the 2x2 space-to-depth image
 STAGES = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3), 26: (2, 2, 2, 2)}
 
 

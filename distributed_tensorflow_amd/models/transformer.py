@@ -21,10 +21,10 @@ from ..ops.conv import ResidualGradLink
 # post-LN blocks (BERT): the residual gradient of a sublayer's input is added by the sublayer's first projection's
 # data-gradient GEMM in its store pass, in place in the parked buffer (no clone, no add kernel): BERT-base 19.60 ->
 # 19.40 ms/step, bitwise-equal losses
-RES_LINK = __import__("os").environ.get("DTF_TF_RES_LINK", "1") == "1"
+RES_LINK = True
 # pre-LN blocks (GPT-2): the residual gradient is added in the LayerNorm backward's store pass (GPT-2-medium bf16
 # 35.50 -> 35.35, fp8 34.84 -> 34.48 ms/step, bitwise-equal results)
-LN_LINK = __import__("os").environ.get("DTF_TF_LN_LINK", "1") == "1"
+LN_LINK = True
 
 
 class _Proj(KL.Layer):
@@ -146,7 +146,7 @@ class GPT2Block(KL.Layer):
         self.ln2 = KL.LayerNormalization(epsilon=1e-5)
         self.fc = _Proj(4 * hidden, activation="gelu", fp8=fp8, single_consumer=True)
         self.proj = _Proj(hidden, fp8=fp8)
-        if fp8:  # FFN1's output feeds only FFN2: fp8 operands from FFN1's epilogue (ops.fp8 DTF_FP8_FUSE); untracked
+        if fp8:  # FFN1's output feeds only FFN2: fp8 operands from FFN1's epilogue (ops.fp8 _FUSE); untracked
             object.__setattr__(self.fc, "_fp8_next", self.proj)
         self.dropout = dropout
 

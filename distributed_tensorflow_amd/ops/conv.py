@@ -83,28 +83,6 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=N
         part = torch.empty(((N * H * W + 63) // 64 + sh * sw) * 2 * C, dtype=F32, device=dy.device)
         rows = IntOut()
     bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
-    if bn is not None and bn.invstd is not None and _FUSE_BN_FIN:
-        # the producing BatchNorm's backward is finalized in this launch's tail: dgamma/dbeta (straight into the
-        # arena gradients when they are direct) and the apply coefficients
-        Kb = C
-        tg, tb = direct_grad(bn.gamma_p), direct_grad(bn.beta_p)
-        direct = tg is not None and tb is not None
-        dgamma = tg if direct else torch.empty(Kb, dtype=F32, device=dy.device)
-        dbeta = tb if direct else torch.empty(Kb, dtype=F32, device=dy.device)
-        coef = torch.empty(3 * Kb, dtype=F32, device=dy.device)
-        fused = IntOut()
-        beta = 1.0 if (acc is not None or acc_sub2 is not None) else 0.0
-        if acc_sub2 is not None:
-            assert acc is None and (R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0)
-        call("dtf_conv_dgrad_bn", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
-             beta, ptr(ws), 2 * ws.numel(), *bn_ptrs, ptr(part), rows.addr,
-             ptr(acc_mask) if acc is not None else None, ptr(acc_sub2), ptr(bn.gamma), ptr(bn.invstd),
-             ptr(dgamma), ptr(dbeta), int(direct), ptr(coef), fused.addr, stream())
-        if fused.value:
-            bn.provide_fin(dx, coef, dgamma, dbeta, direct)
-        else:
-            bn.provide(dx, part, rows.value)
-        return dx
     if acc_sub2 is not None:  # + the compact gradient of a stride-2 1x1 shortcut at the even pixels
         assert acc is None and (R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0)
     call("dtf_conv_dgrad_x", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
@@ -231,54 +209,39 @@ class _BNSource:
     backward then skips its reduction pass (bn_bwd_reduce), provided the gradient it receives is exactly the
     tensor that dgrad wrote (same storage: autograd added nothing else to it)."""
     __slots__ = ("yc", "mbits", "mean", "invstd", "gamma", "gamma_p", "beta_p", "consumers", "part", "rows", "dptr",
-                 "fin", "__weakref__")
+                 "__weakref__")
 
     def __init__(self, yc, mbits, mean, invstd=None, gamma=None, params=(None, None)):
         self.yc, self.mbits, self.mean = yc, mbits, mean
-        # what the consumer's dgrad needs to FINALIZE this BatchNorm's backward too (gemm_core.h BnFin mode 2)
         self.invstd, self.gamma = invstd, gamma
         self.gamma_p, self.beta_p = params
         self.consumers = 0
         self.part = self.rows = self.dptr = None
-        self.fin = None
 
     def provide(self, dx, part, rows):
         self.part, self.rows, self.dptr = part, rows, dx.data_ptr()
-        self.fin = None
-
-    def provide_fin(self, dx, coef, dgamma, dbeta, direct):
-        self.part, self.rows, self.dptr = None, None, dx.data_ptr()
-        self.fin = (coef, dgamma, dbeta, direct)
 
     def take(self, dout):
-        """("partials", part, rows) for this gradient, ("coef", coef, dgamma, dbeta, direct) when the consumer's dgrad
-        already finalized it, or None (then the regular reduction runs)."""
-        part, rows, dptr, fin = self.part, self.rows, self.dptr, self.fin
-        self.part = self.rows = self.dptr = self.fin = None
+        """("partials", part, rows) for this gradient, or None (then the regular reduction runs)."""
+        part, rows, dptr = self.part, self.rows, self.dptr
+        self.part = self.rows = self.dptr = None
         if dptr is None or dout.data_ptr() != dptr or not dout.is_contiguous():
             return None
-        if fin is not None:
-            return ("coef",) + fin
         if part is None or rows < 1:
             return None
         return "partials", part, rows
 
 
-_FUSE_BN_BWD = __import__("os").environ.get("DTF_FUSE_BN_BWD", "1") != "0"
-# BatchNorm finalize (forward statistics, backward reductions) in the tail of the producing GEMM launch instead of
-# separate row-reduction + finalize launches (gemm_core.h BnFin). Opt-in (DTF_BN_FIN_FUSED=1, native side too): every
-# block of the producing launch publishes its partial row with an agent-scope release, and that made the ResNet-50
-# step 1.9x slower on MI355X (gemm.hip fin_on)
-_FUSE_BN_FIN = __import__("os").environ.get("DTF_BN_FIN_FUSED", "0") == "1"
-_LAZY_RES = __import__("os").environ.get("DTF_LAZY_RES", "1") != "0"
-# (Round 3 also built "lazy" BatchNorm outputs applied by the consuming conv's operand loaders; measured slower than
-# materialising on every configuration — profiles/r3_lazy_bn_modes.txt — and removed in round 4.)
-_DEFER_PROJ_BN = __import__("os").environ.get("DTF_DEFER_PROJ_BN", "1") != "0"
-_COMPACT_PROJ = __import__("os").environ.get("DTF_COMPACT_PROJ", "1") != "0"
-# BN apply of a channel-expanding 1x1 ConvBN by recomputing the product from its input (pwconv.hip pw_apply_kernel);
-# needs the pointwise forward kernel for the statistics pass (identical MFMA order: bit-identical y)
-_PW_APPLY = (__import__("os").environ.get("DTF_PW_APPLY", "0") == "1"
-             and __import__("os").environ.get("DTF_PWCONV", "1") != "0")
+# Fused BatchNorm backward reduction in the consumer's data-gradient GEMM (see _BNSource), lazy residual gradient
+# (parked with its ReLU mask on the link), deferred projection-shortcut BN and the compact stride-2 shortcut
+# gradient: module switches for tests (tests/test_resnet_gpu.py flips them to compare against the plain path).
+_FUSE_BN_BWD = True
+_LAZY_RES = True
+_DEFER_PROJ_BN = True
+_COMPACT_PROJ = True
+# (Measured and removed: "lazy" BatchNorm outputs applied by the consuming conv's operand loaders, r3 —
+# profiles/r3_lazy_bn_modes.txt; the BN finalize inside the producing GEMM launch and a BN apply that recomputes the
+# expanding 1x1 product, r4 — profiles/r4_negative_results.txt.)
 
 
 class _ConvBNFn(torch.autograd.Function):
@@ -323,16 +286,8 @@ class _ConvBNFn(torch.autograd.Function):
             out._dtf_affine = (scale, shift)
         else:
             out = torch.empty_like(yc)
-            done = False
-            if (_PW_APPLY and training and g[5:7] == (1, 1) and g[9:15] == (1, 1, 0, 0, 1, 1) and C in (64, 128, 256)
-                    and K % 256 == 0):
-                # channel-expanding 1x1 conv: recompute X W^T instead of re-reading its 4x larger output (pwconv.hip)
-                done = K_().dtf_pwconv_apply(ptr(x), ptr(bf16_shadow(w)), ptr(scale), ptr(shift), ptr(res),
-                                             ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, ptr(out),
-                                             ptr(mbits), M, C, K, int(relu), stream()) == 0
-            if not done:
-                call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
-                     ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, stream())
+            call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
+                 ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, stream())
         # backward needs the conv output and a 1-bit ReLU mask, not the bf16 BN output
         ctx.save_for_backward(x, w, gamma, yc, mbits, mean, invstd)
         ctx.bn_params = (gamma, beta)
@@ -376,14 +331,7 @@ class _ConvBNFn(torch.autograd.Function):
         if rsrc is not None:  # projection shortcut BN: its backward reduction rides on our apply pass
             part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=yc.device), IntOut()
             sc = (ptr(rsrc.yc), ptr(rsrc.mean), ptr(part2), rows2.addr)
-        if fused is not None and fused[0] == "coef":
-            # the consumer's dgrad launch reduced AND finalized this BatchNorm's backward: only the apply is left
-            coef, fg, fb, fdirect = fused[1:]
-            call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(mbits), ptr(yc), M, K, ptr(dyc), ptr(dres), ptr(coef), *sc,
-                 stream())
-            direct_bn = fdirect
-            dgamma, dbeta = fg, fb
-        elif fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
+        if fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
             coef = torch.empty(3 * K, dtype=F32, device=yc.device)
             call("dtf_bn_bwd_partials", ptr(dout), ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
                  ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(fused[1]), fused[2], ptr(coef),

@@ -40,9 +40,9 @@ X_SCALE, W_SCALE, G_SCALE, X_USED, X_AMAX, G_AMAX = range(6)
 X_AMAX2, G_AMAX2 = 6, 7
 # weights: delayed scaling too (the standard fp8 recipe) — each step's W/W^T quantize pass uses the amax the
 # previous step's pass recorded and records its own; the step's weight-gradient GEMM clears the slot just read.
-# One launch per weight and step instead of an absmax pass + the quantize pass. DTF_FP8_W_DELAYED=0: exact scale.
+# One launch per weight and step instead of an absmax pass + the quantize pass (False: exact scale; tests).
 W_AMAX, W_AMAX2 = 8, 9
-_W_DELAYED = os.environ.get("DTF_FP8_W_DELAYED", "1") != "0"
+_W_DELAYED = True
 
 
 def quantize(x, scale, amax=None, zero_amax=True):
@@ -82,12 +82,12 @@ def gemm_fp8(a, b, scales, out, *, fmt_a=0, out_f32=False, beta=0.0, splitk=1, b
     return out
 
 
-_WGRAD_SPLIT_MAX = int(os.environ.get("DTF_FP8_WGRAD_SPLITS", "1"))
+_WGRAD_SPLIT_MAX = 1
 
 
 def _wgrad_splits(M, N, K, ws_elems):
     """Split-K factor for the fp8 weight gradient (M x N output, K tokens) on the 256x256 kernel: about one
-    round of 1-block/CU tiles, >= 1024 tokens per split, at most DTF_FP8_WGRAD_SPLITS, slabs within the
+    round of 1-block/CU tiles, >= 1024 tokens per split, at most _WGRAD_SPLIT_MAX, slabs within the
     workspace. Default 1: the weight gradients run on the side stream next to the data-gradient chain, which
     already keeps the other CUs busy, so splitting only adds the slab write + reduction (GPT-2-medium fp8:
     34.89 ms/step unsplit vs 35.33 with 2 and 36.25 with 4 splits)."""
@@ -178,14 +178,14 @@ def _fp8_bwd_ok(M, K, N):
     return _FP8_BWD and M % 128 == 0 and K % 128 == 0 and N % 128 == 0
 
 
-# Producer-side quantization (DTF_FP8_FUSE, default on): a GELU projection whose only consumer is another fp8
+# Producer-side quantization (_FUSE, on; tests switch it off to compare): a GELU projection whose only consumer is another fp8
 # projection (GPT-2's FFN1 -> FFN2, linked by _Proj.fp8_next) writes FFN2's e4m3 input and its transpose from its own
 # GEMM epilogue, and FFN2's data-gradient GEMM writes FFN1's e5m2 gradient (GELU backward applied), its transpose and
 # the bias-gradient column sums from its epilogue: the bf16 GELU output and the bf16 gradient of it are never
 # written, and two quantize passes per layer and step leave the critical stream. Delayed scaling is unchanged (the
 # same amax slots, parities and scale publication as the quantize pass).
-_FUSE = os.environ.get("DTF_FP8_FUSE", "1") != "0"
-_FUSE_BWD = os.environ.get("DTF_FP8_FUSE_BWD", "1") != "0"  # the gradient half (FFN2's dgrad writes FFN1's e5m2 dZ)
+_FUSE = True
+_FUSE_BWD = True  # the gradient half (FFN2's dgrad writes FFN1's e5m2 dZ)
 
 
 def _placeholder(shape, dev):
@@ -404,7 +404,7 @@ class _DenseFP8(torch.autograd.Function):
 
 def dense_fp8(x, w, b, activation, layer, next_layer=None):
     """next_layer: the fp8 projection that is the ONLY consumer of this one's output (its operands may then be
-    written by this layer's epilogue; see DTF_FP8_FUSE)."""
+    written by this layer's epilogue; see _FUSE)."""
     from .linalg import act_code
     a = act_code(activation)
     st = _state(layer, x.device)

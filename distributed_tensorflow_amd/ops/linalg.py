@@ -125,11 +125,11 @@ def colsum(x2d, out=None, accumulate=False):
     return out
 
 
-# Dense weight gradients on the side stream (with SIDE_STREAM_ON); DTF_DENSE_WGRAD_STREAM=0: on the main stream.
+# Dense weight gradients on the side stream (with SIDE_STREAM_ON).
 # Every dense GEMM runs on the hand-written kernels (gemm.hip -> gemm_w4.hip for the 256-row tiles); the round-4
 # hipBLASLt routes for the plain projections were removed in round 5.
-DENSE_SIDE_ON = SIDE_STREAM_ON and __import__("os").environ.get("DTF_DENSE_WGRAD_STREAM", "1") != "0"
-_SPLIT_DGRAD_K = int(__import__("os").environ.get("DTF_SPLIT_DGRAD_K", "8192"))  # 0 disables the split route
+DENSE_SIDE_ON = SIDE_STREAM_ON
+_SPLIT_DGRAD_K = 8192  # data gradients over a K this long with few output tiles: split-K f32 route (0 disables)
 
 
 def dense_dgrad(dz, w16, acc=None):
@@ -177,7 +177,7 @@ class _ActSource:
         self.fused_ptr = None
 
 
-_FUSE_DACT = __import__("os").environ.get("DTF_FUSE_DACT", "1") != "0"
+_FUSE_DACT = True
 
 
 class _DenseFn(torch.autograd.Function):

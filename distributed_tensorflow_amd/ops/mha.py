@@ -21,11 +21,11 @@ from .nn import softmax
 _seed_counter = [0]
 
 # Backward through a dS^T scratch (dtf_attn_bwd_ds: the dK/dV kernel stores dS, dQ is a memory-bound GEMM over it)
-# instead of a dQ kernel that recomputes the scores, probabilities and dP. DTF_ATTN_DS: 1 always, 0 never, default
-# causal only — measured (tools/bench_attention.py, profiles/r4_attention_bench.txt): GPT-2-medium causal S=1024
+# instead of a dQ kernel that recomputes the scores, probabilities and dP: causal attention only (None; tests set True /
+# False to force a path) — measured (tools/bench_attention.py, profiles/r4_attention_bench.txt): GPT-2-medium causal S=1024
 # 178 -> 158 us (213 -> 183 with dropout); BERT-base S=512 203 -> 227 us (the dS round trip costs more than the
 # recompute saves when no tiles are skipped)
-_ATTN_DS = {"1": True, "0": False}.get(__import__("os").environ.get("DTF_ATTN_DS", ""), None)
+_ATTN_DS = None
 # The dS^T scratch is O(B*H*S^2) (GPT-2-medium S=1024 B=8: 268 MB per call); above this many bytes the backward takes
 # the O(S) recompute kernel instead, so a long-context run keeps flash attention's memory bound.
 DS_SCRATCH_MAX_BYTES = 1 << 30

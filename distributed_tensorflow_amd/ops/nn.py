@@ -138,7 +138,7 @@ def dropout(x, rate, training=True, seed=None):
     return torch.nn.functional.dropout(x, rate, True)
 
 
-_FUSE_ADD_DROPOUT = __import__("os").environ.get("DTF_FUSE_ADD_DROPOUT", "1") != "0"
+_FUSE_ADD_DROPOUT = True
 
 
 class _AddDropoutFn(torch.autograd.Function):

@@ -28,7 +28,7 @@ import torch.distributed as dist
 from .. import _native
 
 MAX_RANKS = 8
-NBLK = int(os.environ.get("DTF_P2P_BLOCKS", "64"))  # blocks per rank and call
+NBLK = 64  # blocks per rank and call
 # buckets up to this size (bytes, f32) take the P2P path when it is available (DTF_P2P_MAX_KB; 0 disables)
 MAX_BYTES = int(float(os.environ.get("DTF_P2P_MAX_KB", "4096")) * 1024)
 # a spinning block gives up after this long (a peer rank far behind, e.g. writing a checkpoint, is waited for)

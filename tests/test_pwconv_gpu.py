@@ -47,35 +47,3 @@ def test_conv_fwd_routes_pointwise_to_pwconv(cuda):
     # the general kernel leaves one partial row per 128-row M-tile; the persistent kernel one per row slot (<= 256)
     R = _run(cuda, 40000, 64, 256, via_conv=True)
     assert R <= 3 * 256
-
-
-
-@pytest.mark.parametrize("M,C,K,res,raff,relu", [(1000, 64, 256, True, False, True), (5000, 128, 512, True, True, True),
-                                                 (3001, 256, 1024, True, False, True), (4099, 64, 512, False, False, False)])
-def test_pwconv_apply_bitwise_equals_conv_then_bn_apply(cuda, M, C, K, res, raff, relu):
-    """The recompute-based BN apply (dtf_pwconv_apply) against the statistics pass (dtf_pwconv_fwd) followed by the
-    ordinary apply pass (dtf_bn_apply) on its stored output: output and 1-bit ReLU mask bitwise equal."""
-    g = torch.Generator(device="cpu").manual_seed(M + C + K)
-    x = (torch.rand(M, C, generator=g) * 2 - 1).to(BF).to(cuda)
-    w = ((torch.rand(K, C, generator=g) * 2 - 1) * 0.1).to(BF).to(cuda)
-    r = (torch.rand(M, K, generator=g) * 2 - 1).to(BF).to(cuda) if res else None
-    sc = (torch.rand(K, generator=g) + 0.5).to(cuda)
-    sh = (torch.rand(K, generator=g) - 0.5).to(cuda)
-    rsc = (torch.rand(K, generator=g) + 0.5).to(cuda) if raff else None
-    rsh = (torch.rand(K, generator=g) - 0.5).to(cuda) if raff else None
-    y = torch.empty(M, K, dtype=BF, device=cuda)
-    part = torch.empty(((M + 63) // 64) * 2 * K, dtype=torch.float32, device=cuda)
-    rows = IntOut()
-    call("dtf_pwconv_fwd", ptr(x), ptr(w), ptr(y), ptr(part), rows.addr, M, C, K, stream())
-    ref = torch.empty_like(y)
-    ref_bits = torch.zeros(M * K // 8, dtype=torch.uint8, device=cuda)
-    call("dtf_bn_apply", ptr(y), ptr(sc), ptr(sh), ptr(r), ptr(ref), M, K, int(relu), ptr(ref_bits) if relu else None,
-         ptr(rsc), ptr(rsh), stream())
-    out = torch.full_like(y, float("nan"))
-    bits = torch.full((M * K // 8,), 0xAA, dtype=torch.uint8, device=cuda)
-    call("dtf_pwconv_apply", ptr(x), ptr(w), ptr(sc), ptr(sh), ptr(r), ptr(rsc), ptr(rsh), ptr(out),
-         ptr(bits) if relu else None, M, C, K, int(relu), stream())
-    torch.cuda.synchronize()
-    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
-    if relu:
-        assert torch.equal(bits, ref_bits)
