@@ -158,22 +158,24 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     exposed = [b.exposed_ms() for b in bucketers if hasattr(b, "exposed_ms")]
-    # after the timed region: the host time to issue ONE step into an idle GPU queue (min of 3). In the timed loop
-    # the host is throttled by the queue once it runs ahead, so its issue time there equals the GPU time either way;
-    # this one says whether Python + launches alone would keep up with the GPU.
-    single = []
-    for _ in range(3):
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        logs = step()
-        single.append(time.perf_counter() - t1)
-    torch.cuda.synchronize()
     exposed = [e for e in exposed if e is not None]
+    # the loss and the replica checksum describe exactly the warmup + timed steps (taken before the probe below)
     loss = float(logs["loss"])
     # proof that the N replicas trained in lock step: an exact checksum of every trainable f32 master (the bit
     # patterns summed as integers), compared across ranks (min == max); the world size the process group reports
     arena = getattr(model, "_arena", None)
     csum = int(arena.flat.detach().view(torch.int32).to(torch.int64).sum().item()) if arena is not None else 0
+    # after the timed region: the host time to issue ONE step into an idle GPU queue (min of 3). In the timed loop
+    # the host is throttled by the queue once it runs ahead, so its issue time there equals the GPU time either way;
+    # this one says whether Python + launches alone would keep up with the GPU. (These 3 extra steps change the
+    # weights after the loss / checksum above were taken.)
+    single = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        single.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
     rccl_world = dist.get_world_size() if dist.is_initialized() else 1
     backend = dist.get_backend() if dist.is_initialized() else None
     identical = True
