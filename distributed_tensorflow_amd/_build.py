@@ -6,7 +6,7 @@
 * ``lib/libdtf_runtime.so`` — the host-side C++ runtime (``csrc/runtime/*.cc``):
   tensor-bundle checkpoint IO, TFRecord/event writer, CRC32C, the TCP
   rendezvous / KV store, the parameter-server transport and the CPU
-  shared-memory all-reduce.
+  shared-memory all-reduce, and the RCCL communicator (librccl bound at run time).
 
 The reference has no native code of its own; these are the
 MI355X-native equivalents of the TF runtime pieces it relies on.
@@ -110,7 +110,7 @@ def build_runtime(verbose=True, jobs=None):
         objs = list(ex.map(lambda s: _compile(flags, s, os.path.join(OBJDIR, "runtime",
                                                                      os.path.basename(s) + ".o"), hdrs, verbose),
                            srcs))
-    return _link([cxx, "-shared", "-fPIC", "-pthread"], objs, RUNTIME_SO, verbose)
+    return _link([cxx, "-shared", "-fPIC", "-pthread", "-ldl"], objs, RUNTIME_SO, verbose)
 
 
 def build(verbose=True):

@@ -75,6 +75,23 @@ SIGS = {
     "dtfrt_shm_allreduce_f32": (I, [P, P, U64]),
     "dtfrt_shm_barrier": (I, [P]),
     "dtfrt_shm_close": (None, [P, I]),
+    # RCCL communicator (rccl_comm.cc)
+    "dtfrt_rccl_available": (I, [P]),
+    "dtfrt_rccl_version": (I, []),
+    "dtfrt_rccl_error_string": (S, [I]),
+    "dtfrt_rccl_unique_id": (I, [P]),
+    "dtfrt_rccl_comm_init": (P, [P, I, I, I, I, S, P]),
+    "dtfrt_rccl_comm_destroy": (I, [P, I]),
+    "dtfrt_rccl_comm_info": (I, [P, P, P, P, P]),
+    "dtfrt_rccl_async_error": (I, [P]),
+    "dtfrt_rccl_all_reduce": (I, [P, P, P, I64, I, I, P]),
+    "dtfrt_rccl_reduce_scatter": (I, [P, P, P, I64, I, I, P]),
+    "dtfrt_rccl_all_gather": (I, [P, P, P, I64, I, P]),
+    "dtfrt_rccl_broadcast": (I, [P, P, P, I64, I, I, P]),
+    "dtfrt_rccl_send": (I, [P, P, I64, I, I, P]),
+    "dtfrt_rccl_recv": (I, [P, P, I64, I, I, P]),
+    "dtfrt_rccl_group_start": (I, []),
+    "dtfrt_rccl_group_end": (I, []),
 }
 
 

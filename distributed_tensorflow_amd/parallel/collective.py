@@ -64,7 +64,8 @@ def world():
 class GradientBucketer:
     """Bucketed, backward-overlapped SUM all-reduce of a ParamArena's gradient buffer."""
 
-    def __init__(self, arena, group=None, bucket_mb=None, average=False, wire_dtype=None, collective=True):
+    def __init__(self, arena, group=None, bucket_mb=None, average=False, wire_dtype=None, collective=True,
+                 implementation=None):
         self.arena = arena
         self.group = group
         # collective=False: no all-reduce (one replica) — the bucketer only drives the per-bucket optimizer update
@@ -105,7 +106,16 @@ class GradientBucketer:
         # small buckets (<= p2p.MAX_BYTES) on one node: the one-shot P2P all-reduce over IPC-mapped peer arenas
         # instead of RCCL (collective setup: every rank constructs its bucketer at the same point)
         self.p2p = None
-        self.paths = {"rccl": 0, "p2p": 0}
+        self.rccl = None  # the framework's own RCCL communicator (rccl.RcclCommunicator), else torch's process group
+        self.paths = {"rccl": 0, "p2p": 0, "rccl_native": 0}
+        if collective and arena.grad.is_cuda and type(self) is GradientBucketer and dist.get_backend(group) == "nccl":
+            from . import rccl
+            if rccl.wanted(implementation):
+                try:
+                    self.rccl = rccl.RcclCommunicator(group, device=arena.grad.device)
+                except (RuntimeError, OSError, ValueError) as e:
+                    print(f"[dtf] native RCCL communicator unavailable ({e}); torch.distributed for the buckets",
+                          flush=True)
         if collective and arena.grad.is_cuda and self.wire == "f32" and type(self) is GradientBucketer:
             from . import p2p
             spans = [(lo, hi) for lo, hi in self.buckets if (hi - lo) * 4 <= p2p.MAX_BYTES]
@@ -183,6 +193,20 @@ class GradientBucketer:
             with comm_stream_ctx(t.device):
                 self.p2p.all_reduce_(lo, hi)
             self.paths["p2p"] += 1
+        elif self.collective and self.rccl is not None:
+            # the native communicator: stream-ordered on the communication stream (it waits for the main and
+            # weight-gradient streams as they are now), so neither compute stream waits for the collective
+            from ..ops._util import comm_stream_ctx
+            with comm_stream_ctx(t.device):
+                if self.wire == "bf16":
+                    if self._wirebuf is None:
+                        self._wirebuf = torch.empty(self.arena.grad.numel(), dtype=torch.bfloat16, device=t.device)
+                    _cast(t, self._wirebuf[lo:hi])
+                    self.rccl.all_reduce_(self._wirebuf[lo:hi])
+                    _cast(self._wirebuf[lo:hi], t)
+                else:
+                    self.rccl.all_reduce_(t)
+            self.paths["rccl_native"] += 1
         elif self.collective:
             ctx = contextlib.nullcontext()
             if t.is_cuda:  # the bucket's weight gradients may still be in flight on the side stream
@@ -238,11 +262,12 @@ class GradientBucketer:
             for w in self._works:
                 if w is not None:
                     w.wait()  # GPU: the main stream waits for the collective's RCCL stream
-            if self.p2p is not None and self.arena.grad.is_cuda:
+            if self.arena.grad.is_cuda:
                 from ..ops._util import join_comm_stream
-                join_comm_stream(self.arena.grad.device)  # P2P buckets were reduced by kernels on the comm stream
-                self.p2p.poll()
-            if self.wire == "bf16" and self.collective:
+                join_comm_stream(self.arena.grad.device)  # P2P / native RCCL buckets ran on the comm stream
+                if self.p2p is not None:
+                    self.p2p.poll()
+            if self.wire == "bf16" and self.collective and self.rccl is None:
                 for lo, hi in self.buckets:
                     _cast(self._wirebuf[lo:hi], self.arena.grad[lo:hi])
             if self.average and self.collective:

@@ -202,14 +202,27 @@ class OneDeviceStrategy(Strategy):
         return self._device
 
 
+class CommunicationImplementation(enum.Enum):
+    """tf.distribute.experimental.CommunicationImplementation. On GPUs every choice is RCCL over xGMI: NCCL drives
+    the framework's own communicator (parallel/rccl.py, C++ csrc/runtime/rccl_comm.cc, channel count set at
+    creation), RING torch.distributed's ProcessGroupNCCL, AUTO the former unless DTF_COMM=torch. CPU replicas use
+    gloo / the shared-memory all-reduce whatever is asked."""
+    AUTO = "AUTO"
+    RING = "RING"
+    NCCL = "NCCL"
+
+
 class CommunicationOptions:
     """tf.distribute.experimental.CommunicationOptions: ``bytes_per_pack`` is the gradient bucket cap (0 = the
-    framework default, DTF_BUCKET_MB); ``wire_dtype`` ("f32" / "bf16", an extension) the all-reduce payload
-    type; ``implementation`` is accepted for API compatibility (the collective is always RCCL on GPUs)."""
+    framework default, DTF_BUCKET_MB); ``implementation`` a CommunicationImplementation; ``wire_dtype`` ("f32" /
+    "bf16", an extension) the all-reduce payload type."""
 
-    def __init__(self, bytes_per_pack=0, timeout_seconds=None, implementation=None, wire_dtype=None):
+    def __init__(self, bytes_per_pack=0, timeout_seconds=None, implementation=CommunicationImplementation.AUTO,
+                 wire_dtype=None):
         self.bytes_per_pack = int(bytes_per_pack or 0)
         self.timeout_seconds = timeout_seconds
+        if isinstance(implementation, str):
+            implementation = CommunicationImplementation(implementation.upper())
         self.implementation = implementation
         self.wire_dtype = wire_dtype
 
@@ -229,6 +242,8 @@ class MultiWorkerMirroredStrategy(Strategy):
         if bucket_mb is None and co is not None and co.bytes_per_pack:
             bucket_mb = co.bytes_per_pack / float(1 << 20)
         self.wire_dtype = getattr(co, "wire_dtype", None)
+        impl = getattr(co, "implementation", None)
+        self.implementation = None if impl in (None, CommunicationImplementation.AUTO) else impl
         self.bucket_mb = bucket_mb
         if cluster_resolver is None:
             if TorchrunClusterResolver.active():
@@ -307,7 +322,8 @@ class MultiWorkerMirroredStrategy(Strategy):
             b = collective.ShmAllReduce(arena, self._rank, self._world, obj[0])
         else:
             b = collective.GradientBucketer(arena, bucket_mb=self.bucket_mb,
-                                            wire_dtype=getattr(self, "wire_dtype", None)).install()
+                                            wire_dtype=getattr(self, "wire_dtype", None),
+                                            implementation=getattr(self, "implementation", None)).install()
         self._bucketers[id(arena)] = b
 
     def backward(self, loss, arena, optimizer=None):

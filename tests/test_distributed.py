@@ -323,3 +323,17 @@ def test_agree_exchanges_only_every_nth_call(monkeypatch):
     monkeypatch.setattr(S.dist, "broadcast", lambda t, src=0: calls.append(int(t.item())))
     out = [s.agree(True, every=4) for _ in range(8)]
     assert out == [False, False, False, True] * 2 and len(calls) == 2
+
+
+def test_native_rccl_binding_and_selection():
+    """The C++ RCCL communicator binds librccl at run time (PyTorch's copy when loaded) on any host; the bucketer's
+    communicator choice follows CommunicationImplementation (NCCL -> ours, RING -> torch's process group)."""
+    from distributed_tensorflow_amd.parallel import rccl, CommunicationOptions, CommunicationImplementation
+    ok, where = rccl.available()
+    assert ok, where
+    assert rccl.version() >= 22000
+    assert rccl.wanted(CommunicationImplementation.NCCL) and not rccl.wanted(CommunicationImplementation.RING)
+    assert rccl.wanted("rccl") and not rccl.wanted("torch")
+    co = CommunicationOptions(implementation="nccl")
+    assert co.implementation is CommunicationImplementation.NCCL
+    assert CommunicationOptions().implementation is CommunicationImplementation.AUTO

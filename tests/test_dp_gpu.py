@@ -143,9 +143,10 @@ def test_two_rank_resnet_replicas_stay_identical(cuda):
     assert all(x == x for x in res[0][2])
 
 
-def _worker_rccl1(port, jit, wire, q, zero=False):
+def _worker_rccl1(port, jit, wire, q, zero=False, impl="AUTO"):
     """One replica on the REAL RCCL backend (world size 1, DTF_FORCE_COLLECTIVE): process group, bucketed
-    all-reduces from post-accumulate hooks, optionally the bf16 wire and hipGraph capture of the whole step."""
+    all-reduces from post-accumulate hooks, optionally the bf16 wire and hipGraph capture of the whole step.
+    impl: CommunicationImplementation — NCCL / AUTO the framework's C++ communicator, RING torch's process group."""
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       DTF_FORCE_COLLECTIVE="1")
     os.environ.pop("DTF_COLLECTIVE_BACKEND", None)
@@ -154,7 +155,7 @@ def _worker_rccl1(port, jit, wire, q, zero=False):
         from distributed_tensorflow_amd import parallel
         s = parallel.MultiWorkerMirroredStrategy(bucket_mb=0.25,
                                                  communication_options=parallel.CommunicationOptions(
-                                                     wire_dtype=wire), shard_optimizer=zero)
+                                                     wire_dtype=wire, implementation=impl), shard_optimizer=zero)
         assert dist.get_backend() == "nccl"
         with s.scope():
             m = _gpt2(100)
@@ -164,29 +165,34 @@ def _worker_rccl1(port, jit, wire, q, zero=False):
         torch.cuda.synchronize()
         b = s._bucketers[id(m._arena)]
         q.put((type(fn).__name__, [w.detach().float().cpu().numpy() for w in m.trainable_variables], losses,
-               len(b.buckets)))
+               len(b.buckets), dict(b.paths)))
         dist.destroy_process_group()
     except Exception:
-        q.put((None, None, traceback.format_exc(), 0))
+        q.put((None, None, traceback.format_exc(), 0, None))
 
 
-@pytest.mark.parametrize("jit,wire,zero", [(False, "f32", False), (True, "f32", False), (False, "bf16", False),
-                                           (False, "f32", True)])
-def test_rccl_bucketer_world1_matches_single_process(cuda, jit, wire, zero):
+@pytest.mark.parametrize("jit,wire,zero,impl", [(False, "f32", False, "AUTO"), (True, "f32", False, "AUTO"),
+                                                (False, "bf16", False, "AUTO"), (False, "f32", True, "AUTO"),
+                                                (False, "f32", False, "RING"), (True, "f32", False, "RING")])
+def test_rccl_bucketer_world1_matches_single_process(cuda, jit, wire, zero, impl):
     """zero=True: ZeRO-1 on RCCL (reduce_scatter_tensor into the compact shard gradient, segment-wise fused
-    AdamW, in-place all_gather_into_tensor of the masters, bf16 refresh)."""
+    AdamW, in-place all_gather_into_tensor of the masters, bf16 refresh). impl AUTO: the buckets go through the
+    framework's own RCCL communicator (parallel/rccl.py) on the communication stream; RING: torch's process group."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker_rccl1, args=(_port(), jit, wire, q, zero))
+    p = ctx.Process(target=_worker_rccl1, args=(_port(), jit, wire, q, zero, impl))
     p.start()
     try:
-        kind, ws, losses, nb = q.get(timeout=100)
+        kind, ws, losses, nb, paths = q.get(timeout=100)
     finally:
         p.join(30)
         if p.is_alive():
             p.kill()
     assert ws is not None, losses
     assert nb > 3 and kind == ("CapturedStep" if jit else "method")
+    if not zero:  # which communicator carried the buckets
+        native = impl == "AUTO"
+        assert (paths["rccl_native"] > 0) == native and (paths["rccl"] > 0) == (not native), paths
     m = _gpt2(100)
     ref = [float(m.train_step((x, y))["loss"]) for x, y in _batches("gpt2", cuda, steps=5)]
     torch.cuda.synchronize()
