@@ -1,0 +1,76 @@
+// Shared pieces of the 4-wave 256-row GEMM kernels (gemm_w4.hip: bf16; gemm_w4_fp8.hip: fp8 on the block-scaled
+// MFMA): the pinned barrier / LDS-wait helpers and the loop-invariant LDS-DMA operand loader.
+#pragma once
+#include "gemm_core.h"
+
+namespace dtf {
+namespace {
+
+constexpr int W4_THREADS = 256;
+constexpr int W4_A = 256 * BK * 2;  // A image of one stage: 256 rows x 128 bytes (64 bf16 / 128 fp8 k) = 32 KiB
+
+// raw s_barrier pinned in the schedule: register-only MFMAs may not move across it (an inline-asm wait alone does
+// not order them: cdna_hip_programming.md §5.4 rule 18)
+__device__ __forceinline__ void w4_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// pad for the first VALU read of an accumulator after the last inline-asm MFMA (hipcc inserts no hazard padding
+// after inline asm)
+__device__ __forceinline__ void w4_mfma_drain() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+}
+
+// wait for this wave's outstanding LDS reads (inline-asm reads hipcc does not track), pinned in the schedule
+__device__ __forceinline__ void w4_lgkm0() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS-DMA loader of one R-row (K-contiguous: [R rows][64 k]) or R-column (K-outer: [64 k][R cols]) operand image
+// per K-tile, R/32 wave instructions per thread, in the lane-linear layouts frag_kcontig / frag_kouter<R> read (the
+// XOR swizzle is applied on the source side, as gemm_core.h GldsLoader / GldsKOuter). Everything per-lane is
+// loop-invariant: the k position of a tile goes into the instruction's SGPR offset and the LDS destination is a
+// scalar (M0). Rows / columns past the operand get an out-of-range VGPR offset and read zeros. Every issued tile is
+// a real one (the caller clamps the tile index), so in-range rows never read past their own row.
+template <int R, int MODE>
+struct W4Loader {
+  static_assert(MODE == OP_KCONTIG || MODE == OP_KOUTER, "plain operands only");
+  static constexpr int L = R / 32;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff[L];
+  int kstep;  // bytes per unit of k in the global operand: 2 (K-contiguous) or 2 * ld (K-outer)
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot, int t) {
+    const uint32_t bytes = MODE == OP_KCONTIG ? (uint32_t)((long)Rtot * ld * 2) : (uint32_t)((long)a.K * ld * 2);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+    kstep = MODE == OP_KCONTIG ? 2 : (int)(ld * 2);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      if constexpr (MODE == OP_KCONTIG) {
+        const int row = 32 * i + (t >> 3);
+        const int c = (t & 7) ^ ((row >> 1) & 7);
+        voff[i] = r0 + row < Rtot ? (int)((long)(r0 + row) * ld * 2) + c * 16 : (int)0x80000000;
+      } else {
+        const int P = i * 4096 + t * 16;
+        const int kr = P / (2 * R);
+        const int c = ((P % (2 * R)) >> 4) ^ (kouter_swz<R>(kr) << 1);
+        const int col = r0 + c * 8;
+        voff[i] = col < Rtot ? (int)((long)kr * ld * 2) + col * 2 : (int)0x80000000;
+      }
+    }
+  }
+  // piece i of the K-tile starting at k0 into the stage image at LDS byte address lds (wave-uniform)
+  __device__ __forceinline__ void issue1(int k0, uint32_t lds, int i) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 4096),
+                                             16, (uint32_t)voff[i], k0 * kstep, 0, 0);
+  }
+};
+
+}  // namespace
+}  // namespace dtf

@@ -25,13 +25,11 @@
 // Epilogue: w4_epilogue (LDS-staged 16-B row stores for bf16 outputs).
 // Reference op family: MatMul and its gradients in the TF graph the reference builds (SURVEY §2.4.b K3;
 // /root/reference/trainer/task.py:137-139).
-#include "gemm_core.h"
+#include "gemm_w4.h"
 
 namespace dtf {
 namespace {
 
-constexpr int W4_THREADS = 256;
-constexpr int W4_A = 256 * BK * 2;  // A image of one stage: 256 rows x 64 k (32 KiB)
 
 template <int BN>
 struct W4Geo {
@@ -45,16 +43,6 @@ struct W4Geo {
   static constexpr int NG = 8 + BN / 32;                // LDS-DMA pieces per K-tile (A 8, B BN/32)
 };
 
-// raw s_barrier pinned in the schedule: register-only MFMAs may not move across it (an inline-asm wait alone does
-// not order them: cdna_hip_programming.md §5.4 rule 18)
-__device__ __forceinline__ void w4_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 // acc += B . A on the MFMA, accumulating IN PLACE. Written as inline asm with a tied AGPR operand because the builtin
 // lets the register allocator give the result a new register tuple: with all 256 AGPRs holding accumulators there is
 // no free tuple, and hipcc then rotated accumulators through VGPRs (50-470 v_accvgpr moves per K-tile depending on
@@ -66,10 +54,6 @@ __device__ __forceinline__ void w4_barrier() {
 __device__ __forceinline__ void w4_mfma(v4f& c, const v8bf& b, const v8bf& a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
 }
-__device__ __forceinline__ void w4_mfma_drain() {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-}
-
 // Transposed fragment of a K-outer [64 k][R cols] image (frag_kouter<R>'s addressing) read by inline-asm
 // ds_read_b64_tr_b16: the builtin makes hipcc wait vmcnt for the in-flight LDS-DMA of the OTHER stage before every
 // such read (it cannot tell the two apart), which drained the prefetch every K-tile (NN / TN 0.4-0.5x of NT). hipcc
@@ -93,12 +77,6 @@ __device__ __forceinline__ v8bf w4_frag(const char* lds, int rb, int kk, int lan
   if constexpr (MODE == OP_KOUTER) return w4_frag_kouter<R>(lds, rb, kk, lane);
   else return frag_kcontig(lds, rb, kk, lane);
 }
-__device__ __forceinline__ void w4_lgkm0() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 // Epilogue. gemm_core.h's generic gemm_epilogue serves every fused feature through runtime branches; instantiated
 // over 64 fragments per lane it compiled to ~57k instructions with ~7.7k SGPR-spill lane moves and cost ~20 us per
 // 256x256 tile (3x the tile's MFMA time at K = 768: tools/bench_gemm_w4.py --sweepk). This one covers what the dense
@@ -204,46 +182,6 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
     *reinterpret_cast<uint4*>(C + e) = val;
   }
 }
-
-// LDS-DMA loader of one R-row (K-contiguous: [R rows][64 k]) or R-column (K-outer: [64 k][R cols]) operand image
-// per K-tile, R/32 wave instructions per thread, in the lane-linear layouts frag_kcontig / frag_kouter<R> read (the
-// XOR swizzle is applied on the source side, as gemm_core.h GldsLoader / GldsKOuter). Everything per-lane is
-// loop-invariant: the k position of a tile goes into the instruction's SGPR offset and the LDS destination is a
-// scalar (M0). Rows / columns past the operand get an out-of-range VGPR offset and read zeros. Every issued tile is
-// a real one (the caller clamps the tile index), so in-range rows never read past their own row.
-template <int R, int MODE>
-struct W4Loader {
-  static_assert(MODE == OP_KCONTIG || MODE == OP_KOUTER, "plain operands only");
-  static constexpr int L = R / 32;
-  __amdgpu_buffer_rsrc_t rsrc;
-  int voff[L];
-  int kstep;  // bytes per unit of k in the global operand: 2 (K-contiguous) or 2 * ld (K-outer)
-
-  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot, int t) {
-    const uint32_t bytes = MODE == OP_KCONTIG ? (uint32_t)((long)Rtot * ld * 2) : (uint32_t)((long)a.K * ld * 2);
-    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
-    kstep = MODE == OP_KCONTIG ? 2 : (int)(ld * 2);
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-      if constexpr (MODE == OP_KCONTIG) {
-        const int row = 32 * i + (t >> 3);
-        const int c = (t & 7) ^ ((row >> 1) & 7);
-        voff[i] = r0 + row < Rtot ? (int)((long)(r0 + row) * ld * 2) + c * 16 : (int)0x80000000;
-      } else {
-        const int P = i * 4096 + t * 16;
-        const int kr = P / (2 * R);
-        const int c = ((P % (2 * R)) >> 4) ^ (kouter_swz<R>(kr) << 1);
-        const int col = r0 + c * 8;
-        voff[i] = col < Rtot ? (int)((long)kr * ld * 2) + col * 2 : (int)0x80000000;
-      }
-    }
-  }
-  // piece i of the K-tile starting at k0 into the stage image at LDS byte address lds (wave-uniform)
-  __device__ __forceinline__ void issue1(int k0, uint32_t lds, int i) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 4096),
-                                             16, (uint32_t)voff[i], k0 * kstep, 0, 0);
-  }
-};
 
 // VAR (ablation builds for tools/bench_gemm_w4.py --var; 0 = the kernel): 1 no LDS-DMA in the loop, 2 no fragment
 // reads in the loop (MFMAs on stale fragments), 3 both, 4 no epilogue — timing only, results are wrong for VAR != 0.

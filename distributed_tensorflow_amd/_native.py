@@ -70,6 +70,14 @@ _KERNEL_SIGS = {
     "dtf_gemm_w4": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
     "dtf_gemm_w4_var": [P, P, P, I, I, I, I, I, P],
     "dtf_launch_counts": [P, I],
+    # per-stream hipGraph executor (graph_sync.hip)
+    "dtf_xs_epoch_inc": [P, I, P],
+    "dtf_xs_signal": [P, I, P, I, P],
+    "dtf_xs_wait": [P, I, P, I, P, I, P],
+    "dtf_event_create": [],
+    "dtf_event_destroy": [P],
+    "dtf_event_record_external": [P, P],
+    "dtf_stream_wait_external": [P, P],
     "dtf_gemm256_bn": [P, P, P, I, I, I, L, L, L, I, I, I, I, P],
     "dtf_gemm_dact": [P, P, P, P, I, I, I, I, L, L, L, I, I, P],
     "dtf_quant_fp8_exact": [P, P, L, P, P, P],
@@ -102,7 +110,7 @@ _KERNEL_SIGS = {
 }
 
 
-_RESTYPES = {"dtf_stream_create": P}
+_RESTYPES = {"dtf_stream_create": P, "dtf_event_create": P}
 
 
 class NativeMissing(RuntimeError):

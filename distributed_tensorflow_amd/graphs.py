@@ -1,9 +1,14 @@
 """hipGraph capture of training steps (the tf.function / XLA-free answer to per-op launch overhead).
 
-``CapturedStep(fn)`` runs ``fn`` eagerly for ``warmup`` calls, then captures one call into a
-hipGraph (``torch.cuda.CUDAGraph`` = hipGraph on ROCm) and afterwards only replays it: every HIP
-kernel of forward, backward, (single-rank) gradient reduction and the fused optimizer update is
-issued by ONE graph launch. Inputs are copied into static buffers; per-step scalars that the graph
+``CapturedStep(fn)`` runs ``fn`` eagerly for ``warmup`` calls, then captures one call into
+hipGraphs (``torch.cuda.CUDAGraph`` = hipGraph on ROCm) and afterwards only replays them: every HIP
+kernel of forward, backward, gradient reduction and the fused optimizer update is issued by graph
+launches, one per stream the step uses ("split" capture, the default): the main (data-gradient) stream's
+graph, then the weight-gradient side stream's, then the communication stream's, each launched into its own
+stream so the kernels keep the hardware queue and the overlap they have eagerly. Cross-stream edges become
+external event nodes (earlier-launched graph -> later one) or bounded device-flag waits (the joins back into
+main): csrc/kernels/graph_sync.hip. ``split=False`` (or torch.distributed process-group collectives in the
+step) captures ONE multi-branch graph instead, whose branches the HIP runtime maps onto queues itself. Inputs are copied into static buffers; per-step scalars that the graph
 cannot bake in (bias-corrected learning rate, gradient scale) are published by
 ``Optimizer.graph_prestep`` into the pinned buffers the captured memcpy nodes read; derived weight
 layouts are invalidated after every replay. Restrictions (as for any graph capture): static shapes,
@@ -38,28 +43,39 @@ def _rebuild(template, it):
     return template
 
 
+SPLIT_DEFAULT = __import__("os").environ.get("DTF_GRAPH_SPLIT", "1") != "0"
+
+
 class CapturedStep:
-    def __init__(self, fn, warmup=2, optimizers=(), pool=None):
+    def __init__(self, fn, warmup=2, optimizers=(), pool=None, split=None):
         self.fn = fn
         self.warmup = warmup
         self.optimizers = list(optimizers)
         self.pool = pool
+        self.split = SPLIT_DEFAULT if split is None else bool(split)
         self.graph = None
+        self.sc = None        # ops._util.SplitCapture of a per-stream capture
         self.calls = 0
         self.static_in = None
         self.out = None
+        self._errbuf = None
 
     def _capture(self, args):
         from .ops import _util
         flat = _flat(args, [])
         self.static_in = [t.clone() for t in flat]
+        self._src = self._sources(flat)
         static_args = _rebuild(args, iter(self.static_in))
         for o in self.optimizers:
             o.graph_prepare()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
-            out = self.fn(static_args)
+        if self.split and _util.split_capture_ok():
+            out = self._capture_split(g, static_args)
+        else:
+            self.sc = None
+            with torch.cuda.graph(g, pool=self.pool):
+                out = self.fn(static_args)
         self.graph = g
         # keep the raw (device) log values: each replay hands out a fresh lazy view of them
         self._log_type = type(out) if isinstance(out, dict) else None
@@ -68,6 +84,54 @@ class CapturedStep:
         for o in self.optimizers:
             o._host_iter -= 1
         _util.bump_weights_epoch()
+
+    def _capture_split(self, g, static_args):
+        import gc
+        from .ops import _util
+        dev = torch.device("cuda", torch.cuda.current_device())
+        pool = self.pool if self.pool is not None else torch.cuda.graph_pool_handle()
+        self.pool = pool
+        sc = _util.SplitCapture(dev, pool)
+        cap = torch.cuda.Stream(device=dev)
+        cap.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.synchronize()
+        gc.collect()
+        with torch.cuda.stream(cap):
+            g.capture_begin(pool=pool, capture_error_mode="relaxed")
+            ok = False
+            try:
+                sc.begin(cap)
+                _util.set_split_capture(sc)
+                out = self.fn(static_args)
+                sc.finish()
+                ok = True
+            finally:
+                _util.set_split_capture(None)
+                if not ok:
+                    sc.abort()
+                g.capture_end()
+        torch.cuda.current_stream(dev).wait_stream(cap)
+        self.sc = sc
+        return out
+
+    @staticmethod
+    def _sources(flat):
+        import weakref
+        out = []
+        for t in flat:
+            try:
+                out.append((weakref.ref(t), t._version))
+            except TypeError:
+                out.append(None)
+        return out
+
+    def check(self):
+        """Raise if a cross-stream flag wait of the per-stream graphs ever timed out (a broken edge; its replay's
+        results are not to be trusted). Synchronises the device."""
+        if self.sc is not None:
+            e = int(self.sc.err.item())
+            if e:
+                raise RuntimeError(f"hipGraph per-stream replay: cross-stream wait {e - 1} timed out")
 
     def __call__(self, args):
         self.calls += 1
@@ -83,13 +147,26 @@ class CapturedStep:
                 return r
             self._capture(args)
         else:
-            for s, t in zip(self.static_in, _flat(args, [])):
-                if s.data_ptr() != t.data_ptr():
+            flat = _flat(args, [])
+            for i, (s, t) in enumerate(zip(self.static_in, flat)):
+                # the very tensor whose contents the static buffer already holds (same object, no in-place write
+                # since: torch's version counter, shared by its views): no copy (e.g. a fixed benchmark batch)
+                src = self._src[i]
+                if s.data_ptr() != t.data_ptr() and not (src is not None and src[0]() is t and t._version == src[1]):
                     s.copy_(t, non_blocking=True)
+            self._src = self._sources(flat)
         # per-step scalars go to a pinned ring (Optimizer.graph_prestep): no host sync between replays
         for o in self.optimizers:
             o.graph_prestep()
         self.graph.replay()
+        if self.sc is not None:
+            self.sc.replay_others()
+            if self.calls % 256 == 0:  # a timed-out flag wait (never expected): checked without a host sync
+                if self._errbuf is not None and int(self._errbuf[0]):
+                    raise RuntimeError("hipGraph per-stream replay: a cross-stream wait timed out")
+                if self._errbuf is None:
+                    self._errbuf = torch.zeros(1, dtype=torch.int32).pin_memory()
+                self._errbuf.copy_(self.sc.err, non_blocking=True)
         for o in self.optimizers:
             o.graph_poststep()
         from .ops import _util
@@ -100,11 +177,12 @@ class CapturedStep:
         for o in self.optimizers:
             o._graph = None
         self.graph = None
+        self.sc = None
         self.calls = 0
 
 
-def function(fn=None, warmup=2, optimizers=()):
-    """Decorator: ``@dtf.function`` captures a (static-shape) step into a hipGraph after `warmup` calls."""
+def function(fn=None, warmup=2, optimizers=(), split=None):
+    """Decorator: ``@dtf.function`` captures a (static-shape) step into hipGraphs after `warmup` calls."""
     def wrap(f):
-        return CapturedStep(f, warmup=warmup, optimizers=optimizers)
+        return CapturedStep(f, warmup=warmup, optimizers=optimizers, split=split)
     return wrap(fn) if fn is not None else wrap

@@ -110,6 +110,9 @@ def before_overwrite(t):
     _PARKED.discard(p)
     ev = _SIDE_READS.pop(p, None)
     if ev is not None:
+        if isinstance(ev, tuple):  # a per-stream capture's flag mark (SplitCapture.mark)
+            _SPLIT.wait_mark(torch.cuda.current_stream(t.device), ev)
+            return
         torch.cuda.current_stream(t.device).wait_event(ev)
         if torch.cuda.is_current_stream_capturing():
             _CAPTURE_KEEP.append(ev)
@@ -131,7 +134,7 @@ def _drop_holds():
     """Forget the held side reads (the main stream is ordered after them now). Inside a capture the events stay
     alive until the capture is over: destroying an event a captured node records crashes the graph's capture end."""
     if _SIDE_HOLD and torch.cuda.is_current_stream_capturing():
-        _CAPTURE_KEEP.extend(h[0] for h in _SIDE_HOLD)
+        _CAPTURE_KEEP.extend(h[0] for h in _SIDE_HOLD if h[0] is not None)
     elif _CAPTURE_KEEP and not torch.cuda.is_current_stream_capturing():
         _CAPTURE_KEEP.clear()
     _SIDE_HOLD.clear()
@@ -140,7 +143,7 @@ def _drop_holds():
 def _release_side_holds():
     if not _SIDE_HOLD or torch.cuda.is_current_stream_capturing():
         return
-    keep = [h for h in _SIDE_HOLD if not h[0].query()]
+    keep = [h for h in _SIDE_HOLD if h[0] is not None and not h[0].query()]
     _SIDE_HOLD[:] = keep
 
 
@@ -151,20 +154,26 @@ def fork_side(device, *tensors):
     among them are protected from their in-place overwrite (before_overwrite)."""
     _release_side_holds()
     side = side_stream(device)
-    side.wait_stream(torch.cuda.current_stream(device))
+    stream_wait(side, torch.cuda.current_stream(device))
     held = [t for t in tensors if t is not None]
     for t in held:
         t.record_stream(side)
     _SIDE_USED.add(device.index)
     with torch.cuda.stream(side):
         yield side
+    parked = [t for t in held if _sptr(t) in _PARKED] if _PARKED else []
+    if _SPLIT is not None:
+        _SIDE_HOLD.append((None, held))
+        if parked:
+            mk = _SPLIT.mark(side)
+            for t in parked:
+                _SIDE_READS[_sptr(t)] = mk
+        return
     ev = torch.cuda.Event()
     ev.record(side)
     _SIDE_HOLD.append((ev, held))
-    if _PARKED:
-        for t in held:
-            if _sptr(t) in _PARKED:
-                _SIDE_READS[_sptr(t)] = ev
+    for t in parked:
+        _SIDE_READS[_sptr(t)] = ev
 
 
 def collective_ctx(device):
@@ -178,7 +187,7 @@ def collective_ctx(device):
     if device.type != "cuda":
         return contextlib.nullcontext()
     side = side_stream(device)
-    side.wait_stream(torch.cuda.current_stream(device))
+    stream_wait(side, torch.cuda.current_stream(device))
     _SIDE_USED.add(device.index)
     return torch.cuda.stream(side)
 
@@ -204,9 +213,9 @@ def comm_stream_ctx(device):
     if device.type != "cuda":
         return contextlib.nullcontext()
     comm = comm_stream(device)
-    comm.wait_stream(torch.cuda.current_stream(device))  # = record an event on main, make comm wait on it
+    stream_wait(comm, torch.cuda.current_stream(device))  # = record an event on main, make comm wait on it
     if device.index in _SIDE_USED:
-        comm.wait_stream(_SIDE[device.index])
+        stream_wait(comm, _SIDE[device.index])
     _COMM_USED.add(device.index)
     return torch.cuda.stream(comm)
 
@@ -214,7 +223,7 @@ def comm_stream_ctx(device):
 def join_comm_stream(device):
     """The current stream waits for everything issued on the communication stream (a no-op when unused)."""
     if device.type == "cuda" and device.index in _COMM_USED:
-        torch.cuda.current_stream(device).wait_stream(_COMM[device.index])
+        stream_wait(torch.cuda.current_stream(device), _COMM[device.index])
         _COMM_USED.discard(device.index)
 
 
@@ -229,18 +238,18 @@ def update_stream_ctx(device, extra_wait=None):
     u = _UPD.get(device.index)
     if u is None:
         u = _UPD[device.index] = torch.cuda.Stream(device=device)
-    u.wait_stream(torch.cuda.current_stream(device))
+    stream_wait(u, torch.cuda.current_stream(device))
     if device.index in _SIDE_USED:
-        u.wait_stream(_SIDE[device.index])
-    if device.index in _COMM_USED:  # a bucket reduced on the communication stream (P2P all-reduce)
-        u.wait_stream(_COMM[device.index])
+        stream_wait(u, _SIDE[device.index])
+    if device.index in _COMM_USED:  # a bucket reduced on the communication stream (P2P / native RCCL)
+        stream_wait(u, _COMM[device.index])
     return torch.cuda.stream(u)
 
 
 def join_update_stream(device):
     u = _UPD.get(device.index)
     if u is not None:
-        torch.cuda.current_stream(device).wait_stream(u)
+        stream_wait(torch.cuda.current_stream(device), u)
 
 
 def join_side_streams():
@@ -253,9 +262,173 @@ def join_side_streams():
         _drop_holds()
         return
     for idx in list(_SIDE_USED):
-        torch.cuda.current_stream(idx).wait_stream(_SIDE[idx])
+        stream_wait(torch.cuda.current_stream(idx), _SIDE[idx])
     _SIDE_USED.clear()
     _drop_holds()  # the main stream is ordered after every side read now
+
+
+# ---------------------------------------------------------------- per-stream hipGraph capture
+# graphs.CapturedStep captures a multi-stream step as one hipGraph PER STREAM (csrc/kernels/graph_sync.hip explains
+# why and how the graphs are ordered). While such a capture runs, every cross-stream dependency of the framework goes
+# through stream_wait / SplitCapture.mark + wait_mark instead of torch's wait_stream / wait_event, which inside a
+# capture would merge the streams into one multi-branch graph.
+_SPLIT = None
+XS_TIMEOUT_MS = 20000
+_SPLIT_BLOCKERS = __import__("weakref").WeakSet()  # objects whose stream use the per-stream capture cannot express
+
+
+def block_split_capture(obj):
+    """`obj` issues cross-stream work outside the framework's stream helpers (torch.distributed process-group
+    collectives: their Work.wait() orders on RCCL's internal stream): hipGraph capture keeps one multi-branch graph
+    while it lives."""
+    _SPLIT_BLOCKERS.add(obj)
+
+
+def split_capture_ok():
+    return len(_SPLIT_BLOCKERS) == 0
+
+
+class SplitCapture:
+    """State of one per-stream capture: the streams in launch order (main first), each non-main stream's CUDAGraph
+    (capture begun lazily at the stream's first use), the external events and the device flag / epoch arrays."""
+    MAX_SLOTS = 4096
+
+    def __init__(self, device, pool):
+        self.device, self.pool = device, pool
+        self.lib = _native.kernels()
+        self.streams, self.index, self.graphs = [], {}, []
+        self.events = []
+        self.nslot = 0
+        self.flags = torch.zeros(self.MAX_SLOTS, dtype=torch.int32, device=device)
+        self.epochs = torch.zeros(16, dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.counts = {"event": 0, "flag": 0}
+        self.activity = {}   # position -> count of waits it took (work is issued on a stream after its waits)
+        self.joined = {}     # (consumer, producer) -> producer's activity when consumer last waited for all of it
+
+    def _call(self, name, *args):
+        rc = getattr(self.lib, name)(*args)
+        if rc:
+            raise RuntimeError(f"{name} failed during a per-stream capture: {rc}")
+
+    def begin(self, main):
+        """`main` is capturing already (the caller's CUDAGraph); it becomes position 0."""
+        self.index[main.cuda_stream] = 0
+        self.streams.append(main)
+        self.graphs.append(None)
+        self._call("dtf_xs_epoch_inc", ptr(self.epochs), 0, main.cuda_stream)
+
+    def ensure(self, s):
+        pos = self.index.get(s.cuda_stream)
+        if pos is not None:
+            return pos
+        pos = len(self.streams)
+        if pos >= self.epochs.numel():
+            raise RuntimeError("per-stream capture: too many streams")
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):  # a private memory pool per stream graph (one pool cannot record two captures)
+            g.capture_begin(capture_error_mode="relaxed")
+        self.index[s.cuda_stream] = pos
+        self.streams.append(s)
+        self.graphs.append(g)
+        self._call("dtf_xs_epoch_inc", ptr(self.epochs), pos, s.cuda_stream)
+        return pos
+
+    def _slot(self):
+        if self.nslot >= self.MAX_SLOTS:
+            raise RuntimeError("per-stream capture: out of flag slots")
+        self.nslot += 1
+        return self.nslot - 1
+
+    def mark(self, producer):
+        """A point on `producer`'s stream that any stream can wait for later (wait_mark)."""
+        pp = self.ensure(producer)
+        if pp == 0:
+            ev = self.lib.dtf_event_create()
+            self.events.append(ev)
+            self._call("dtf_event_record_external", ev, producer.cuda_stream)
+            return ("ev", ev)
+        slot = self._slot()
+        self._call("dtf_xs_signal", ptr(self.flags), slot, ptr(self.epochs), pp, producer.cuda_stream)
+        return ("flag", slot)
+
+    def wait_mark(self, consumer, mk):
+        pc = self.ensure(consumer)
+        if mk[0] == "ev":
+            self.counts["event"] += 1
+            self._call("dtf_stream_wait_external", consumer.cuda_stream, mk[1])
+        else:
+            self.counts["flag"] += 1
+            self._call("dtf_xs_wait", ptr(self.flags), mk[1], ptr(self.epochs), pc, ptr(self.err), XS_TIMEOUT_MS,
+                       consumer.cuda_stream)
+
+    def wait(self, consumer, producer):
+        if consumer.cuda_stream == producer.cuda_stream:
+            return
+        pp = self.index.get(producer.cuda_stream)
+        if pp is None:
+            return  # nothing issued on the producer in this capture
+        pc = self.ensure(consumer)
+        act = self.activity.get(pp, 0)
+        if pp > 0 and self.joined.get((pc, pp)) == act:
+            return  # the producer took no new work since the consumer last waited for all of it
+        self.joined[(pc, pp)] = act
+        self.activity[pc] = self.activity.get(pc, 0) + 1
+        if pp < pc:  # the producer's graph is enqueued first: an external event pair
+            ev = self.lib.dtf_event_create()
+            self.events.append(ev)
+            self._call("dtf_event_record_external", ev, producer.cuda_stream)
+            self.counts["event"] += 1
+            self._call("dtf_stream_wait_external", consumer.cuda_stream, ev)
+        else:
+            self.wait_mark(consumer, self.mark(producer))
+
+    def finish(self):
+        """Join every other stream into main (the next replay's main graph must not overwrite buffers a late stream
+        still reads) and end their captures."""
+        main = self.streams[0]
+        for s in self.streams[1:]:
+            self.wait(main, s)
+        for s, g in zip(self.streams[1:], self.graphs[1:]):
+            with torch.cuda.stream(s):
+                g.capture_end()
+        self.graphs_done = True
+
+    def abort(self):
+        for s, g in zip(self.streams[1:], self.graphs[1:]):
+            try:
+                with torch.cuda.stream(s):
+                    g.capture_end()
+            except RuntimeError:
+                pass
+
+    def replay_others(self):
+        """After the main graph was launched on the current stream: every other stream's graph, in order."""
+        for s, g in zip(self.streams[1:], self.graphs[1:]):
+            with torch.cuda.stream(s):
+                g.replay()
+
+    def __del__(self):
+        lib = getattr(self, "lib", None)
+        for ev in getattr(self, "events", ()):
+            try:
+                lib.dtf_event_destroy(ev)
+            except Exception:
+                pass
+
+
+def set_split_capture(sc):
+    global _SPLIT
+    _SPLIT = sc
+
+
+def stream_wait(consumer, producer):
+    """`consumer` waits for the work issued on `producer` so far (torch's wait_stream, or its per-stream-capture
+    form while one runs)."""
+    if _SPLIT is not None:
+        _SPLIT.wait(consumer, producer)
+    else:
+        consumer.wait_stream(producer)
 
 
 _RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
@@ -442,12 +615,18 @@ def crsk_shadow(param, K, RS, C):
             tiles += rs * ((k + 63) // 64) * ((c + 63) // 64)
         tkey = (param.device.index, tuple(rows))
         table = _CRSK_TABLES.get(tkey)
-        if table is None:
-            if len(_CRSK_TABLES) > 64:
-                _CRSK_TABLES.clear()
-            table = torch.tensor(rows, dtype=torch.int64).to(param.device)
-            _CRSK_TABLES[tkey] = table
-        call("dtf_filters_to_crsk", ptr(table), len(rows), tiles, stream())
+        if table is None and torch.cuda.is_current_stream_capturing():
+            # a filter set first seen inside a hipGraph capture (no host->device copy allowed): one launch each
+            for p in live:
+                k, rs, c = p._dtf_crsk_geom
+                call("dtf_filter_to_crsk", ptr(bf16_shadow(p)), ptr(p._dtf_crsk), k, rs, c, stream())
+        else:
+            if table is None:
+                if len(_CRSK_TABLES) > 64:
+                    _CRSK_TABLES.clear()
+                table = torch.tensor(rows, dtype=torch.int64).to(param.device)
+                _CRSK_TABLES[tkey] = table
+            call("dtf_filters_to_crsk", ptr(table), len(rows), tiles, stream())
     for p in live:
         p._dtf_crsk_key = _crsk_key(p)
     return s

@@ -116,6 +116,11 @@ class GradientBucketer:
                 except (RuntimeError, OSError, ValueError) as e:
                     print(f"[dtf] native RCCL communicator unavailable ({e}); torch.distributed for the buckets",
                           flush=True)
+        if collective and arena.grad.is_cuda and self.rccl is None:
+            # process-group collectives order through Work.wait() on RCCL's own stream: hipGraph capture keeps the
+            # single multi-branch graph for this configuration
+            from ..ops._util import block_split_capture
+            block_split_capture(self)
         if collective and arena.grad.is_cuda and self.wire == "f32" and type(self) is GradientBucketer:
             from . import p2p
             spans = [(lo, hi) for lo, hi in self.buckets if (hi - lo) * 4 <= p2p.MAX_BYTES]
