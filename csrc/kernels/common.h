@@ -152,6 +152,9 @@ enum LaunchCounter : int {
   LC_GEMM_DACT = 4,   // dtf_gemm_dact (activation backward in the data-gradient epilogue)
   LC_BETA_BF16 = 5,   // bf16 GEMM accumulating into C (beta != 0)
   LC_SPLITK = 6,      // split-K GEMM (f32 slabs + ordered reduction)
+  LC_W4F8_256 = 7,    // gemm_w4_fp8.hip, 256x256 tiles
+  LC_W4F8_128 = 8,    // gemm_w4_fp8.hip, 256x128 tiles
+  LC_GEMM256_FP8 = 9, // gemm256.hip with fp8 operands
   LC_COUNT = 16
 };
 DTF_API long* dtf_launch_counters();

@@ -513,7 +513,7 @@ int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int 
   // for the fp8 kernels (their own instantiation: 4 VGPR spills; GPT-2-medium fp8 erratic with it, 180-233k vs a
   // steady 231-234k tok/s without: off by default). Default 2 = bit 1
   a.aux_nt = 2;
-  count_launch(LC_GEMM256);
+  count_launch(fp8 ? LC_GEMM256_FP8 : LC_GEMM256);
   if (bn == 256) launch256<256>(a, amode, bmode, st, fp8);
   else launch256<128>(a, amode, bmode, st, fp8);
   return 0;

@@ -7,6 +7,8 @@
 //  * dtf_gemm_fp8: C[M][N] = (sa*sb) * A_q[M][K] . B_q[N][K]^T (+bias, act, pre-activation aux), bf16 out,
 //    on v_mfma_f32_16x16x32_fp8_fp8 with the same LDS-staged, swizzled pipeline as the bf16 GEMM
 //    (gemm_core.h) — half the staged bytes per FLOP.
+#include <cstdlib>
+
 #include "gemm_core.h"
 
 namespace {
@@ -320,6 +322,27 @@ using namespace dtf;
 // work per staged byte of bf16, so the 128-row register-staged tiles are relatively more load/latency bound.
 // Measured on GPT-2-medium fp8 (interleaved A/B): 35.25 / 35.27 ms/step vs 35.75 / 35.60 with the bf16 rule and
 // 35.84 / 35.94 without the 256x128 preference.
+namespace dtf {
+int gemm_w4_fp8_try(GemmArgs& a, int fp8, hipStream_t st, int bn);  // gemm_w4_fp8.hip
+}
+// The 4-wave fp8 kernel (gemm_w4_fp8.hip) first: DTF_FP8_W4=0 keeps the 8-wave gemm256 / 128-row kernels (A/B).
+static int g_fp8_w4 = -1;
+static bool fp8_w4_on() {
+  if (g_fp8_w4 < 0) {
+    const char* e = getenv("DTF_FP8_W4");
+    g_fp8_w4 = e ? atoi(e) : 1;
+  }
+  return g_fp8_w4 != 0;
+}
+DTF_API void dtf_fp8_w4_enable(int on) { g_fp8_w4 = on ? 1 : 0; }  // A/B switch for benchmarks and tests
+// Its tile width: 256x256 unless 256x128 tiles fill the 256 CUs' rounds clearly better (as pick_w4 in gemm.hip).
+static int pick_w4_fp8(long M, long N, long batch_splits) {
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch_splits, t2x1 = (long)cdiv(M, 256) * cdiv(N, 128) * batch_splits;
+  auto eff = [](long t, long slots) { return (double)t / (double)(((t + slots - 1) / slots) * slots); };
+  const double s256 = N > 128 ? eff(t256, 256) : 0.0, s2x1 = 0.8 * eff(t2x1, 256);
+  return s256 >= s2x1 ? 256 : 128;
+}
+
 static int pick256_fp8(long M, long N, long K) {
   (void)K;
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256), t2x1 = (long)cdiv(M, 256) * cdiv(N, 128);
@@ -435,12 +458,15 @@ DTF_API int dtf_gemm_fp8_ex(const void* A, const void* B, void* C, void* aux, co
     a.C = ws;
     a.slab = (long)M * N;
     a.beta = 0.f;
-    if (gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8, 256)) return -5;
+    if (!(fp8_w4_on() && gemm_w4_fp8_try(a, fp8, st, pick_w4_fp8(M, N, splitk)) == 0) &&
+        gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8, 256))
+      return -5;
     dtf_sum_rows(ws, (long)M * N, splitk, (long)M * N, (float*)C, beta != 0.f ? 1 : 0, stream);
     return (int)hipGetLastError();
   }
   a.splitk = 1;
   a.kchunk = (a.K + BK - 1) / BK * BK;
+  if (fp8_w4_on() && gemm_w4_fp8_try(a, fp8, st, pick_w4_fp8(M, N, 1)) == 0) return (int)hipGetLastError();
   const int bn = pick256_fp8(M, N, K);
   if (bn && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, st, fp8, bn) == 0) return (int)hipGetLastError();
   const long b128 = (long)cdiv(M, 128) * cdiv(N, 128);
@@ -480,6 +506,8 @@ DTF_API int dtf_gemm_fp8(const void* A, const void* B, void* C, void* aux, const
   a.lda = lda / 2; a.ldb = ldb / 2; a.ldc = ldc;
   a.batch = 1; a.splitk = 1; a.kchunk = (a.K + BK - 1) / BK * BK;
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = 0;
+  if (tile < 0 && fp8_w4_on() && gemm_w4_fp8_try(a, 1, (hipStream_t)stream, pick_w4_fp8(M, N, 1)) == 0)
+    return (int)hipGetLastError();
   // the 256x256 glds pipeline when its tiling fills the chip (fp8 halves its staged bytes per FLOP)
   const int bn = tile < 0 ? pick256_fp8(M, N, K) : 0;
   if (bn && gemm256_try(a, OP_KCONTIG, OP_KCONTIG, (hipStream_t)stream, 1, bn) == 0)

@@ -95,7 +95,14 @@ def build_kernels(verbose=True, jobs=None):
         objs = list(ex.map(lambda s: _compile(flags, s, os.path.join(OBJDIR, "kernels",
                                                                      os.path.basename(s) + ".o"), hdrs, verbose),
                            srcs))
-    return _link([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"], objs, KERNELS_SO, verbose)
+    so = _link([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"], objs, KERNELS_SO, verbose)
+    # a declaration in the wrong namespace links fine into a shared library and fails only at dlopen on the GPU box:
+    # refuse undefined C++ symbols of our own here
+    r = subprocess.run(["nm", "-u", "-C", so], capture_output=True, text=True)
+    bad = [ln.strip() for ln in r.stdout.splitlines() if "dtf" in ln or "GemmArgs" in ln]
+    if bad:
+        raise RuntimeError(f"{so}: undefined symbols of our own: {bad[:8]}")
+    return so
 
 
 def build_runtime(verbose=True, jobs=None):

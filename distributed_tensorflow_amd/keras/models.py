@@ -269,10 +269,12 @@ class Model(Layer):
         arena = self._ensure_arena()
         with prof.phase("backward"), direct_grads():  # includes the overlapped bucket all-reduces
             # per-bucket update during backward when the model asks for it (overlap_update) or DTF_OVERLAP_UPDATE
-            # forces it; a hipGraph-captured step (and its eager warmups) keeps the single update after backward
+            # forces it; a step captured as ONE multi-branch hipGraph (and its eager warmups) keeps the single update
+            # after backward, the per-stream capture (graphs.SPLIT_DEFAULT) keeps the per-bucket one
             from ..parallel import strategy as _S
+            from .. import graphs as _G
             ovl = _S._OVERLAP_UPDATE in ("1", "force") or (_S._OVERLAP_UPDATE == "" and self.overlap_update)
-            graph_ok = not getattr(self, "_graph_step", False)
+            graph_ok = not getattr(self, "_graph_step", False) or _G.SPLIT_DEFAULT
             strat.backward(loss, arena, optimizer=self.optimizer if ovl and graph_ok else None)
             join_side_streams()  # weight gradients issued on the side stream are in the arena
         with prof.phase("optimizer"):

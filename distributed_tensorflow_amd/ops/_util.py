@@ -516,7 +516,8 @@ def call_log():
         _CALL_LOG.remove(c)
 
 
-LAUNCH_COUNTERS = ("w4_256", "w4_128", "gemm256", "gemm_tile", "gemm_dact", "beta_bf16", "splitk")
+LAUNCH_COUNTERS = ("w4_256", "w4_128", "gemm256", "gemm_tile", "gemm_dact", "beta_bf16", "splitk", "w4f8_256", "w4f8_128",
+                   "gemm256_fp8")
 
 
 def launch_counts():

@@ -41,7 +41,8 @@ _OVERLAP_UPDATE = os.environ.get("DTF_OVERLAP_UPDATE", "")
 # update on its own stream the stem's bucket diverges from the first replay, with the update on the capture stream
 # (or the weight gradients on the main stream) the first replay's forward already differs — while the same buckets
 # updated after backward (finalize) replay bit-identically; the optimizer is one ~120 us launch per ResNet-50 step,
-# so the capture keeps the single fused update after backward).
+# so the capture keeps the single fused update after backward). The per-stream capture (graphs.py, split) records the
+# update stream as a graph of its own with explicit event / flag edges and keeps the per-bucket update.
 
 
 class ReduceOp(enum.Enum):
@@ -124,7 +125,9 @@ class Strategy:
         if not arena.grad.is_cuda and _OVERLAP_UPDATE != "force":
             return None
         if arena.grad.is_cuda and torch.cuda.is_current_stream_capturing():
-            return None  # a captured step keeps the single update after backward (see above)
+            from ..ops import _util
+            if _util._SPLIT is None:
+                return None  # a single-graph capture keeps the single update after backward (see above)
         b = self._bucketers.get(id(arena))
         if b is None:  # one replica: a bucketer without collectives, only to time the bucket updates
             b = collective.GradientBucketer(arena, collective=False).install()

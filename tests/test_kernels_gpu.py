@@ -647,11 +647,28 @@ def test_fp8_backward_matches_bf16(cuda):
     assert rels[0] < 1e-6 and max(rels) < 0.06, rels
 
 
+@pytest.mark.parametrize("w4", [True, False])
 @pytest.mark.parametrize("fmt_a,out_f32,splitk,M,N,K", [(0, False, 1, 256, 128, 256), (1, False, 1, 256, 128, 256),
                                                         (1, False, 1, 1024, 1024, 1024),
+                                                        (0, False, 1, 1000, 392, 384),
                                                         (1, True, 1, 256, 128, 512), (1, True, 4, 512, 512, 4096)])
-def test_fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K):
-    """dtf_gemm_fp8_ex: e4m3 / e5m2 A x e4m3 B on the scaled MFMA vs the torch decode of the same bytes."""
+def test_fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K, w4):
+    """dtf_gemm_fp8_ex: e4m3 / e5m2 A x e4m3 B on the scaled MFMA vs the torch decode of the same bytes; w4: the
+    4-wave kernel on v_mfma_scale_f32_32x32x64_f8f6f4 (gemm_w4_fp8.hip, the default), else the 8-wave / 128-row
+    kernels on the 16x16x128 form — pinned through the launch counters."""
+    from distributed_tensorflow_amd.ops import fp8, _util
+    from distributed_tensorflow_amd._native import kernels
+    kernels().dtf_fp8_w4_enable(int(w4))
+    before = _util.launch_counts()
+    try:
+        _fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K)
+    finally:
+        kernels().dtf_fp8_w4_enable(1)
+    d = _util.launch_delta(before)
+    assert (d["w4f8_256"] + d["w4f8_128"] > 0) == w4, d
+
+
+def _fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K):
     from distributed_tensorflow_amd.ops import fp8
     torch.manual_seed(0)
     da = torch.float8_e5m2 if fmt_a else torch.float8_e4m3fn
@@ -668,6 +685,33 @@ def test_fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K):
         out = torch.empty((M, N), dtype=BF, device=cuda)
         fp8.gemm_fp8(a.view(torch.uint8), b.view(torch.uint8), scales, out, fmt_a=fmt_a)
     close(out, ref, 1e-2)
+
+
+@pytest.mark.parametrize("bn", [256, 128])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_w4_fp8_epilogue(cuda, bn, act):
+    """The 4-wave fp8 kernel's bf16 epilogue (device scales, bias, activation with the pre-activation side output)
+    through dtf_gemm_fp8, and its direct entry at both tile widths, vs f32 references of the decoded bytes."""
+    from distributed_tensorflow_amd.ops._util import call, ptr, stream, launch_counts, launch_delta
+    torch.manual_seed(1)
+    M, N, K = 1280, 648, 640
+    a = (torch.randn(M, K, device=cuda) * 2).to(torch.float8_e4m3fn)
+    b = (torch.randn(N, K, device=cuda) * 2).to(torch.float8_e4m3fn)
+    z = a.float() @ b.float().t()
+    out = torch.empty((M, N), dtype=F32, device=cuda)
+    before = launch_counts()
+    call("dtf_gemm_w4_fp8", ptr(a), ptr(b), ptr(out), M, N, K, K, K, N, 0, 1, bn, stream())
+    assert launch_delta(before)["w4f8_%d" % bn] == 1
+    close(out, z, 1e-4)
+    scales = torch.tensor([0.5, 0.125], device=cuda)
+    bias = torch.randn(N, device=cuda)
+    y = torch.empty((M, N), dtype=BF, device=cuda)
+    pre = torch.empty((M, N), dtype=BF, device=cuda)
+    call("dtf_gemm_fp8", ptr(a), ptr(b), ptr(y), ptr(pre), ptr(bias), ptr(scales), M, N, K, K, K, N, act, -1, stream())
+    p = z * 0.0625 + bias
+    close(pre, p, 1e-2)
+    ref = torch.relu(p) if act == 1 else torch.nn.functional.gelu(p, approximate="tanh") if act == 2 else p
+    close(y, ref, 1e-2)
 
 
 @pytest.mark.parametrize("ak,bk", [(False, False), (False, True), (True, False), (True, True)])

@@ -25,7 +25,7 @@ def main():
     dev = torch.device("cuda")
     T = 8192
     sc = torch.ones(2, device=dev)
-    tot = {"bf16": 0.0, "fp8": 0.0, "quant": 0.0}
+    tot = {"bf16": 0.0, "fp8": 0.0, "fp8_8wave": 0.0, "quant": 0.0}
     for name, kin, kout in SHAPES:
         x = torch.randn(T, kin, device=dev).to(BF)
         w = (torch.randn(kout, kin, device=dev) * 0.05).to(BF)
@@ -45,13 +45,20 @@ def main():
             "dW": (lambda: ops.gemm(dz, x, a_kouter=True, b_kouter=True, out_dtype=torch.float32),
                    lambda: F.gemm_fp8(gqT, xqT, sc, dw, fmt_a=1, out_f32=True, beta=1.0)),
         }
+        from distributed_tensorflow_amd._native import kernels
         for role, (fb, f8) in roles.items():
             fl = 2.0 * T * kin * kout
-            tb, t8 = timeit(fb), timeit(f8)
+            tb = timeit(fb)
+            kernels().dtf_fp8_w4_enable(0)
+            t8o = timeit(f8)
+            kernels().dtf_fp8_w4_enable(1)
+            t8 = timeit(f8)
             tot["bf16"] += tb
             tot["fp8"] += t8
+            tot["fp8_8wave"] += t8o
             line = (f"{name:4s} {role:3s} T={T} {kin}->{kout}: bf16 {tb * 1e6:6.1f}us {fl / tb / 1e12:6.0f} TF | "
-                    f"fp8 {t8 * 1e6:6.1f}us {fl / t8 / 1e12:6.0f} TF ({tb / t8:4.2f}x)")
+                    f"fp8 4-wave {t8 * 1e6:6.1f}us {fl / t8 / 1e12:6.0f} TF ({tb / t8:4.2f}x bf16) | "
+                    f"fp8 8-wave {t8o * 1e6:6.1f}us {fl / t8o / 1e12:6.0f} TF")
             if hasattr(torch, "_scaled_mm") and hasattr(torch, "float8_e4m3fn") and role == "fwd":
                 try:
                     a8 = x.to(torch.float8_e4m3fn)
