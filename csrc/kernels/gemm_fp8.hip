@@ -326,15 +326,20 @@ namespace dtf {
 int gemm_w4_fp8_try(GemmArgs& a, int fp8, hipStream_t st, int bn);  // gemm_w4_fp8.hip
 }
 // The 4-wave fp8 kernel (gemm_w4_fp8.hip) first: DTF_FP8_W4=0 keeps the 8-wave gemm256 / 128-row kernels (A/B).
+// 0 off, 1 every fp8 GEMM, 2 (default) every one except the producer-quantizing (q8) GEMMs: their epilogue (LDS
+// transposes for the K-outer copy, column sums, amax) on the 4-wave kernel is faster standalone (FFN1 forward 87 vs
+// 106 us, FFN2 data gradient 54 vs 65 us: tools/bench_fp8_gemms.py) but 1.7% slower in the GPT-2-medium fp8 step next
+// to the side-stream weight gradients (interleaved, 246.7-247.2k vs 251.0-251.2k tok/s: profiles/r5_fp8_w4.txt)
 static int g_fp8_w4 = -1;
 static bool fp8_w4_on() {
   if (g_fp8_w4 < 0) {
     const char* e = getenv("DTF_FP8_W4");
-    g_fp8_w4 = e ? atoi(e) : 1;
+    g_fp8_w4 = e ? atoi(e) : 2;
   }
   return g_fp8_w4 != 0;
 }
-DTF_API void dtf_fp8_w4_enable(int on) { g_fp8_w4 = on ? 1 : 0; }  // A/B switch for benchmarks and tests
+// A/B switch for benchmarks and tests (-1: back to DTF_FP8_W4 / the default)
+DTF_API void dtf_fp8_w4_enable(int on) { g_fp8_w4 = on; }
 // Its tile width: 256x256 unless 256x128 tiles fill the 256 CUs' rounds clearly better (as pick_w4 in gemm.hip).
 static int pick_w4_fp8(long M, long N, long batch_splits) {
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * batch_splits, t2x1 = (long)cdiv(M, 256) * cdiv(N, 128) * batch_splits;
@@ -558,6 +563,9 @@ DTF_API int dtf_gemm_fp8_q8(const void* A, const void* B, void* C, void* aux, co
   a.q8 = (uint8_t*)q8; a.q8T = (uint8_t*)q8T; a.q8col = q8col; a.q8fmt = q8fmt;
   a.q8scale = q8scale; a.q8amax = q8amax; a.q8amax_prev = q8amax_prev; a.q8used = q8used; a.q8used2 = q8used2;
   a.no_c = C ? 0 : 1;
+  if (fp8_w4_on() && g_fp8_w4 != 2 &&
+      gemm_w4_fp8_try(a, fmt_a == 1 ? 2 : 1, (hipStream_t)stream, pick_w4_fp8(M, N, 1)) == 0)
+    return (int)hipGetLastError();
   if (gemm256_try(a, OP_KCONTIG, OP_KCONTIG, (hipStream_t)stream, fmt_a == 1 ? 2 : 1, bn)) return -6;
   return (int)hipGetLastError();
 }

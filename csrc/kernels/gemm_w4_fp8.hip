@@ -29,7 +29,7 @@ template <int BN>
 struct W8Geo {
   static constexpr int JN = BN / 64;                    // B fragments (32 columns each) per wave per substep
   static constexpr int STAGE = W4_A + BN * 128;
-  static constexpr int EPI = 256 * (BN + 8) * 2;        // the epilogue's staged bf16 C tile
+  static constexpr int EPI = 256 * (BN + 8) * 2 + 16 * BN * 4;  // staged bf16 C tile + q8 column-sum partials
   static constexpr int SMEM = EPI > 2 * STAGE ? EPI : 2 * STAGE;
   static constexpr int NSTEP = 2 * JN;                  // 2-MFMA steps per substep (4 x JN MFMAs)
   static constexpr int NREAD = 4 + JN;                  // fragments per substep
@@ -138,18 +138,118 @@ __device__ __forceinline__ void w8_epilogue(const GemmArgs& a, v16f (&acc)[4][BN
       }
     }
   __syncthreads();
+  // fp8 copies of the final bf16 values for the next fp8 layer (GemmArgs::q8*, as gemm256.hip's staged epilogue):
+  // the delayed scale (block 0 publishes the one used), row-major copy, transposed copy and per-128-row column sums
+  // from a column pass over the LDS tile, and the block's max |value| into the amax slot
+  const bool q8on = a.q8 || a.q8T || a.q8col;
+  const bool q8tp = a.q8T || a.q8col;
+  const float q8fmax = a.q8fmt ? 57344.f : 448.f;
+  float q8inv = 0.f, q8max = 0.f;
+  if (q8on) {
+    const float ap = a.q8amax_prev ? a.q8amax_prev[0] : 0.f;
+    const float s8 = ap > 0.f ? ap / q8fmax : fmaxf(a.q8scale[0], 1e-30f);
+    q8inv = 1.f / s8;
+    if (a.q8used && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+      a.q8used[0] = s8;
+      if (a.q8used2) a.q8used2[0] = s8;
+    }
+  }
+  auto q8v = [&](float f) { return fminf(fmaxf(f * q8inv, -q8fmax), q8fmax); };
   constexpr int TPR = BN / 8, RPP = W4_THREADS / TPR;
   const int c8 = threadIdx.x % TPR, r0 = threadIdx.x / TPR;
   const int n = n0 + c8 * 8;
-  if (n >= a.N) return;
   bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
+  if (n < a.N) {
 #pragma unroll 4
-  for (int it = 0; it < 256 / RPP; ++it) {
-    const int ml = r0 + RPP * it;
-    const int m = m0 + ml;
-    if (m >= a.M) break;
-    const uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8 * 8);
-    *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = val;
+    for (int it = 0; it < 256 / RPP; ++it) {
+      const int ml = r0 + RPP * it;
+      const int m = m0 + ml;
+      if (m >= a.M) break;
+      const long e = (long)m * a.ldc + n;
+      uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8 * 8);
+      if (a.dact) val = dact8(val, *reinterpret_cast<const uint4*>(a.dact_src + e), a.dact);
+      if (!a.no_c) *reinterpret_cast<uint4*>(C + e) = val;
+      if (q8on) {
+        const uint32_t vw[4] = {val.x, val.y, val.z, val.w};
+        float f[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f[2 * q] = __uint_as_float(vw[q] << 16);
+          f[2 * q + 1] = __uint_as_float(vw[q] & 0xffff0000u);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) q8max = fmaxf(q8max, fabsf(f[r]));
+        if (a.q8)
+          *reinterpret_cast<uint2*>(a.q8 + (long)m * a.N + n) =
+              make_uint2(q8pack4(a.q8fmt, q8v(f[0]), q8v(f[1]), q8v(f[2]), q8v(f[3])),
+                         q8pack4(a.q8fmt, q8v(f[4]), q8v(f[5]), q8v(f[6]), q8v(f[7])));
+        if (q8tp && a.dact) *reinterpret_cast<uint4*>(ct + ml * CS + c8 * 8) = val;  // the column pass's values
+      }
+    }
+  }
+  if (q8tp) {
+    __syncthreads();
+    // transposed copy + column sums from 16-row x 8-column blocks: a thread reads its block's 16 rows as 16-B LDS
+    // chunks (consecutive threads: consecutive chunks of a row), writes the 8 transposed 16-B pieces and its 8
+    // partial column sums (row order within the block) to LDS; the sums of each 128-row half are then folded over
+    // the 8 blocks in block order (deterministic)
+    constexpr int NC8 = BN / 8;
+    float* part = reinterpret_cast<float*>(smem + 256 * CS * 2);  // [16 row blocks][BN]
+    for (int task = threadIdx.x; task < 16 * NC8; task += W4_THREADS) {
+      const int cc = task % NC8, rg = task / NC8;
+      uint4 v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const uint4*>(ct + (rg * 16 + i) * CS + cc * 8);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float f[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t w = c < 2 ? v[i].x : c < 4 ? v[i].y : c < 6 ? v[i].z : v[i].w;
+          f[i] = __uint_as_float((c & 1) ? (w & 0xffff0000u) : (w << 16));
+        }
+        float cs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) cs += f[i];
+        part[rg * BN + cc * 8 + c] = cs;
+        const int nn = n0 + cc * 8 + c;
+        if (a.q8T && nn < a.N) {
+          uint4 qv;
+          qv.x = q8pack4(a.q8fmt, q8v(f[0]), q8v(f[1]), q8v(f[2]), q8v(f[3]));
+          qv.y = q8pack4(a.q8fmt, q8v(f[4]), q8v(f[5]), q8v(f[6]), q8v(f[7]));
+          qv.z = q8pack4(a.q8fmt, q8v(f[8]), q8v(f[9]), q8v(f[10]), q8v(f[11]));
+          qv.w = q8pack4(a.q8fmt, q8v(f[12]), q8v(f[13]), q8v(f[14]), q8v(f[15]));
+          *reinterpret_cast<uint4*>(a.q8T + (long)nn * a.M + m0 + rg * 16) = qv;
+        }
+      }
+    }
+    if (a.q8col) {
+      __syncthreads();
+      for (int t = threadIdx.x; t < 2 * BN; t += W4_THREADS) {
+        const int nl = t % BN, h = t / BN;
+        if (n0 + nl >= a.N) continue;
+        float cs = 0.f;
+#pragma unroll
+        for (int rg = 0; rg < 8; ++rg) cs += part[(h * 8 + rg) * BN + nl];
+        a.q8col[(long)((m0 + h * 128) >> 7) * a.N + n0 + nl] = cs;
+      }
+    }
+  }
+  if (q8on && a.q8amax) {  // block max |value| -> the amax slot (relaxed check first: most blocks lose)
+    float mx = q8max;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) red[wave] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int i = 1; i < W4_THREADS / 64; ++i) mx = fmaxf(mx, red[i]);
+      unsigned int* am = reinterpret_cast<unsigned int*>(a.q8amax);
+      const unsigned int cur = __hip_atomic_load(am, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__float_as_uint(mx) > cur) atomicMax(am, __float_as_uint(mx));
+    }
   }
 }
 
@@ -284,11 +384,13 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_fp8_kernel(GemmArgs a) 
 
 // True if the fp8 4-wave kernel can run these arguments (fp8 entry-point convention: 2-byte units).
 bool gemm_w4_fp8_ok(const GemmArgs& a) {
-  if (a.atomic_out || a.stats || a.bnx || a.crm || a.bsrc || a.betamask || a.q8 || a.q8T || a.q8col || a.dact ||
-      a.batch > 1)
+  if (a.atomic_out || a.stats || a.bnx || a.crm || a.bsrc || a.betamask || a.batch > 1) return false;
+  const bool q8 = a.q8 || a.q8T || a.q8col;
+  if (a.out_f32 ? (a.bias || a.act || a.aux || a.dact || q8 || (a.ldc & 3) || ((uintptr_t)a.C & 15))
+                : (a.beta != 0.f || (a.N & 7) || (a.ldc & 7) || ((uintptr_t)a.C & 15) || ((uintptr_t)a.dact_src & 15)))
     return false;
-  if (a.out_f32 ? (a.bias || a.act || a.aux || (a.ldc & 3) || ((uintptr_t)a.C & 15))
-                : (a.beta != 0.f || (a.N & 7) || (a.ldc & 7) || ((uintptr_t)a.C & 15)))
+  if (q8 && ((a.M & 255) || !a.q8scale || a.slab > 0 || (a.q8 && ((uintptr_t)a.q8 & 7)) ||
+             (a.q8T && ((uintptr_t)a.q8T & 15)) || (a.dact && a.ldc != a.N)))
     return false;
   if (a.kchunk % BK || a.K % BK || (a.lda & 7) || (a.ldb & 7)) return false;
   if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return false;

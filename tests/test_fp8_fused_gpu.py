@@ -28,8 +28,24 @@ def _q8(a, b, scales, C, M, N, Kd, *, fmt_a, act=0, aux=None, bias=None, dact_sr
                                stream())
 
 
+@pytest.fixture(params=[2, 1], ids=["q8-gemm256", "q8-w4"])
+def q8_kernel(request):
+    """The producer-quantizing GEMM on the 8-wave gemm256 epilogue (default) or on the 4-wave fp8 kernel's
+    (gemm_w4_fp8.hip w8_epilogue), pinned through the launch counters."""
+    from distributed_tensorflow_amd.ops._util import launch_counts, launch_delta
+    K().dtf_fp8_w4_enable(request.param)
+    before = launch_counts()
+    yield request.param
+    K().dtf_fp8_w4_enable(-1)
+    d = launch_delta(before)
+    if request.param == 1:
+        assert d["w4f8_256"] + d["w4f8_128"] > 0 and d["gemm256_fp8"] == 0, d
+    else:
+        assert d["gemm256_fp8"] > 0, d
+
+
 @pytest.mark.parametrize("M,N,Kd", [(512, 1024, 256), (768, 512, 384)])
-def test_q8_forward_epilogue_matches_quantize_pass(cuda, M, N, Kd):
+def test_q8_forward_epilogue_matches_quantize_pass(cuda, M, N, Kd, q8_kernel):
     """GELU projection: the fp8 copies (q, q^T), the delayed scale it used and the recorded amax are bit-identical
     to quantizing the bf16 output of the same GEMM with the transposing quantizer; the pre-activation side output is
     unchanged and no bf16 output is written."""
@@ -59,7 +75,7 @@ def test_q8_forward_epilogue_matches_quantize_pass(cuda, M, N, Kd):
     assert torch.equal(buf[3:5], ref_buf[3:5]) and buf[3].item() > 0  # scale used (both slots)
 
 
-def test_q8_backward_epilogue_gelu_grad(cuda):
+def test_q8_backward_epilogue_gelu_grad(cuda, q8_kernel):
     """Data-gradient GEMM (e5m2 x e4m3) whose output is the gradient of a GELU: e5m2 copy of dZ = (dY W) * gelu'(pre)
     with its transpose and per-128-row column sums vs the bf16 GEMM + the transposing quantizer (which applies the
     GELU backward in f32; the fused epilogue rounds dZ to bf16 first: bytes may differ by one e5m2 step)."""

@@ -663,7 +663,7 @@ def test_fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K, w4):
     try:
         _fp8_gemm_formats(cuda, fmt_a, out_f32, splitk, M, N, K)
     finally:
-        kernels().dtf_fp8_w4_enable(1)
+        kernels().dtf_fp8_w4_enable(-1)
     d = _util.launch_delta(before)
     assert (d["w4f8_256"] + d["w4f8_128"] > 0) == w4, d
 

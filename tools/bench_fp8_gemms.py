@@ -51,7 +51,7 @@ def main():
             tb = timeit(fb)
             kernels().dtf_fp8_w4_enable(0)
             t8o = timeit(f8)
-            kernels().dtf_fp8_w4_enable(1)
+            kernels().dtf_fp8_w4_enable(-1)
             t8 = timeit(f8)
             tot["bf16"] += tb
             tot["fp8"] += t8
@@ -78,6 +78,37 @@ def main():
         print(f"{name:4s} quantize: x [{T},{kin}] e4m3 (+T) {tq * 1e6:6.1f}us  dZ [{T},{kout}] e5m2 (+T) "
               f"{tg * 1e6:6.1f}us", flush=True)
     print({k: round(v * 1e3, 3) for k, v in tot.items()}, "ms per layer (fwd + dX + dW of the 4 projections)")
+    # the two producer-quantizing GEMMs of a block (dtf_gemm_fp8_q8): FFN1 forward (GELU, pre-activation side output,
+    # e4m3 copy + transpose of the output for FFN2) and FFN2's data gradient (GELU backward, e5m2 copy + transpose +
+    # bias-gradient column sums for FFN1)
+    from distributed_tensorflow_amd.ops._util import K as KL, ptr, stream
+    from distributed_tensorflow_amd._native import kernels
+    buf = torch.tensor([1.0, 0.0, 1.0, 0.0, 0.0], device=dev)
+    for name, M, N, Kd, fmt_a, dact in (("ffn1 fwd q8", T, 4096, 1024, 0, 0), ("ffn2 dX q8", T, 1024, 4096, 1, 2)):
+        a = torch.randint(0, 120, (M, Kd), dtype=torch.uint8, device=dev)
+        b = torch.randint(0, 120, (N, Kd), dtype=torch.uint8, device=dev)
+        aux = torch.empty(M, N, dtype=BF, device=dev)
+        pre = torch.randn(M, N, device=dev).to(BF)
+        bias = torch.zeros(N, device=dev)
+        q = torch.empty(M, N, dtype=torch.uint8, device=dev)
+        qT = torch.empty(N, M, dtype=torch.uint8, device=dev)
+        cp = torch.empty(M // 128, N, dtype=torch.float32, device=dev)
+
+        def f():
+            rc = KL().dtf_gemm_fp8_q8(ptr(a), ptr(b), None, ptr(aux) if not dact else None,
+                                      ptr(bias) if not dact else None, ptr(sc), M, N, Kd, Kd, Kd, 0 if dact else 2,
+                                      fmt_a, ptr(pre) if dact else None, dact, None, ptr(q), ptr(qT),
+                                      ptr(cp) if dact else None, fmt_a, ptr(buf[0:1]), ptr(buf[1:2]), ptr(buf[2:3]),
+                                      ptr(buf[3:4]), ptr(buf[4:5]), stream())
+            assert rc == 0, rc
+        kernels().dtf_fp8_w4_enable(0)
+        to = timeit(f)
+        kernels().dtf_fp8_w4_enable(1)
+        t4 = timeit(f)
+        kernels().dtf_fp8_w4_enable(-1)
+        fl = 2.0 * M * N * Kd
+        print(f"{name}: 4-wave {t4 * 1e6:6.1f}us {fl / t4 / 1e12:6.0f} TF | 8-wave {to * 1e6:6.1f}us "
+              f"{fl / to / 1e12:6.0f} TF", flush=True)
 
 
 if __name__ == "__main__":
