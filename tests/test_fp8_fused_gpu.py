@@ -28,10 +28,11 @@ def _q8(a, b, scales, C, M, N, Kd, *, fmt_a, act=0, aux=None, bias=None, dact_sr
                                stream())
 
 
-@pytest.fixture(params=[2, 1], ids=["q8-gemm256", "q8-w4"])
+@pytest.fixture(params=[0, 1], ids=["q8-gemm256", "q8-w4"])
 def q8_kernel(request):
-    """The producer-quantizing GEMM on the 8-wave gemm256 epilogue (default) or on the 4-wave fp8 kernel's
-    (gemm_w4_fp8.hip w8_epilogue), pinned through the launch counters."""
+    """The producer-quantizing GEMM on the 8-wave gemm256 epilogue (the default for q8 GEMMs) or on the 4-wave fp8
+    kernel's (gemm_w4_fp8.hip w8_epilogue), pinned through the launch counters. The plain reference GEMM of a test runs
+    on the same kernel family (its accumulation order is part of what is compared bit for bit)."""
     from distributed_tensorflow_amd.ops._util import launch_counts, launch_delta
     K().dtf_fp8_w4_enable(request.param)
     before = launch_counts()

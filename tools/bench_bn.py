@@ -45,7 +45,19 @@ def main():
                                     ptr(dx), None, ptr(dg), ptr(db), 0, ptr(work), None, None, None, None, None, None, stream()))
         t_bwdr = timeit(lambda: call("dtf_bn_bwd", ptr(dy), None, ptr(mb), ptr(x), ptr(mean), ptr(inv), ptr(gm), M,
                                      C, ptr(dx), ptr(dz), ptr(dg), ptr(db), 0, ptr(work), None, None, None, None, None, None, stream()))
+        rows = max(1, M // 128)
+        part = torch.randn(rows, 2 * C, device=dev) * 0.01
+        coef = torch.empty(3 * C, device=dev)
+        # the apply-only backward the model runs when the consumer's dgrad epilogue already reduced (bn_bwd_apply)
+        t_bp = timeit(lambda: call("dtf_bn_bwd_partials", ptr(dy), ptr(mb), ptr(x), ptr(mean), ptr(inv), ptr(gm), M, C,
+                                   ptr(dx), None, ptr(dg), ptr(db), 0, ptr(part), rows, ptr(coef), None, None, None,
+                                   None, stream()))
+        t_bpr = timeit(lambda: call("dtf_bn_bwd_partials", ptr(dy), ptr(mb), ptr(x), ptr(mean), ptr(inv), ptr(gm), M,
+                                    C, ptr(dx), ptr(dz), ptr(dg), ptr(db), 0, ptr(part), rows, ptr(coef), None, None,
+                                    None, None, stream()))
         gb = lambda b, t: b / t / 1e9  # noqa: E731
+        print(f"M={M:8d} C={C:5d} bwd apply-only {t_bp * 1e6:7.1f}us {gb(3.0625 * n, t_bp):6.0f} GB/s | "
+              f"+dres {t_bpr * 1e6:7.1f}us {gb(4.0625 * n, t_bpr):6.0f} GB/s", flush=True)
         print(f"M={M:8d} C={C:5d} copy {gb(2 * n, t_copy):6.0f} GB/s | apply {t_app * 1e6:7.1f}us "
               f"{gb(2.0625 * n, t_app):6.0f} GB/s | apply+res {t_res * 1e6:7.1f}us {gb(3.0625 * n, t_res):6.0f} | "
               f"bwd {t_bwd * 1e6:7.1f}us {gb(5.125 * n, t_bwd):6.0f} | bwd+dz {t_bwdr * 1e6:7.1f}us "
