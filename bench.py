@@ -25,6 +25,10 @@ sys.path.insert(0, ROOT)
 
 DEFAULT_BATCH = {"resnet50": 256, "resnet101": 256, "resnet152": 256, "bert_base": 32, "gpt2_medium_fp8": 8,
                  "gpt2_medium": 8}
+# hipGraph replay (graphs.py per-stream capture) vs eager, interleaved on one MI355X (profiles/r5_hipgraph_default.txt):
+# ResNet-50 +1.4%, BERT-base +0.7%, GPT-2-medium fp8 +0.3%, GPT-2-medium bf16 -1.8% (its many side->main joins are
+# device-flag waits in the replay). Multi-rank runs stay eager unless DTF_GRAPH_DIST=1 (keras Model.make_train_function).
+GRAPH_DEFAULT = {"resnet50": 1, "resnet101": 1, "resnet152": 1, "bert_base": 1, "gpt2_medium_fp8": 1, "gpt2_medium": 0}
 
 
 def _relaunch(args):
@@ -97,8 +101,9 @@ def main():
                     help="gradient all-reduce payload type (default f32; bf16 halves the xGMI bytes)")
     ap.add_argument("--zero", type=int, default=0,
                     help="1: ZeRO-1 sharded optimizer update (reduce-scatter + 1/N update + all-gather of masters)")
-    ap.add_argument("--graph", type=int, default=0,
-                    help="1: capture the whole train step in a hipGraph (compile(jit_compile=True))")
+    ap.add_argument("--graph", type=int, default=None,
+                    help="1: capture the train step as per-stream hipGraphs (compile(jit_compile=True)), 0: eager; "
+                         "default: per model from the interleaved A/B (profiles/r5_hipgraph_default.txt)")
     ap.add_argument("--ar-sweep", type=int, default=1,
                     help="N>1: after the timed steps, time f32 all-reduces of 1-128 MB and report RCCL bus bandwidth")
     ap.add_argument("--hiprio", type=int, default=0,
@@ -107,6 +112,10 @@ def main():
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
+    if args.graph is None:
+        # the capture is the third call of the step (two eager warmups first): with fewer than 3 warmup steps it
+        # would land in the timed region, so the default is eager then
+        args.graph = GRAPH_DEFAULT.get(args.model, 0) if args.warmup >= 3 else 0
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world == 1 and "RANK" not in os.environ:
         return _relaunch(args)  # before anything touches the GPU
