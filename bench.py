@@ -150,6 +150,10 @@ def main():
 
     for _ in range(args.warmup):
         logs = step()
+    sc = getattr(train_fn, "sc", None)
+    if sc is not None:  # the per-stream capture: graphs (streams) and cross-stream edges by kind
+        cfg["graph_streams"] = len(sc.streams)
+        cfg["graph_edges"] = dict(sc.counts)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
