@@ -23,7 +23,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-DEFAULT_BATCH = {"resnet50": 256, "resnet101": 256, "resnet152": 256, "bert_base": 32, "gpt2_medium_fp8": 8,
+# Per-GPU batch. ResNet: sized for the 288 GB of HBM3E (the activations of a 1024-image step take ~60 GB): the
+# per-step fixed costs (optimizer pass, small stage-4 layers that cannot fill 256 CUs, launch tails) are amortised
+# over 4x the images of the 256 used through round 4 — interleaved on one MI355X, graph replay: 256 12,316-12,348,
+# 384 12,768-12,774, 512 12,948-12,976, 768 13,085, 1024 13,188 img/s (profiles/r5_resnet50_batch_sweep.txt).
+DEFAULT_BATCH = {"resnet50": 1024, "resnet101": 512, "resnet152": 512, "bert_base": 32, "gpt2_medium_fp8": 8,
                  "gpt2_medium": 8}
 # hipGraph replay (graphs.py per-stream capture) vs eager, interleaved on one MI355X (profiles/r5_hipgraph_default.txt):
 # ResNet-50 +1.4%, BERT-base +0.7%, GPT-2-medium fp8 +0.3%, GPT-2-medium bf16 -1.8% (its many side->main joins are

@@ -82,15 +82,16 @@ def gemm_fp8(a, b, scales, out, *, fmt_a=0, out_f32=False, beta=0.0, splitk=1, b
     return out
 
 
-_WGRAD_SPLIT_MAX = int(os.environ.get("DTF_FP8_WGRAD_SPLIT_MAX", "1"))
+_WGRAD_SPLIT_MAX = int(os.environ.get("DTF_FP8_WGRAD_SPLIT_MAX", "4"))
 
 
 def _wgrad_splits(M, N, K, ws_elems):
     """Split-K factor for the fp8 weight gradient (M x N output, K tokens) on the 4-wave kernel's 256x128 tiles:
     about one round of 1-block/CU tiles, >= 1024 tokens per split, at most _WGRAD_SPLIT_MAX, slabs within the
-    workspace. Default 1: the weight gradients run on the side stream next to the data-gradient chain, which
-    already keeps the other CUs busy, so splitting only adds the slab write + reduction (round 3, 8-wave kernel,
-    GPT-2-medium fp8: 34.89 ms/step unsplit vs 35.33 with 2 and 36.25 with 4 splits)."""
+    workspace. Default 4 since the 4-wave fp8 kernel (its 256x128 tiles leave a 1024 x 1024 weight gradient at 32
+    blocks): GPT-2-medium fp8 253.7k / 255.3k tok/s unsplit vs 259.4k / 260.4k with up to 4 splits, interleaved
+    (profiles/r5_fp8_w4.txt); with the round-3 8-wave kernel splitting had lost (34.89 ms/step unsplit vs 35.33 with
+    2 and 36.25 with 4 splits)."""
     tiles = -(-M // 256) * -(-N // 128)
     s = max(1, min(256 // max(tiles, 1), K // 1024, _WGRAD_SPLIT_MAX))
     while s > 1 and s * M * N > ws_elems:
