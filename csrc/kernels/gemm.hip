@@ -1,4 +1,6 @@
 // MFMA GEMM + implicit-GEMM convolution for gfx950: host API (kernels in gemm_core.h).
+#include <cstdlib>
+
 #include "gemm_core.h"
 
 // Deterministic grouped row sums (split-K slabs, BN partial rows): see common.h.
@@ -402,6 +404,33 @@ static int plan_w4_split(long M, long N, long K, long batch, int& bn) {
     for (long sp = 1; sp <= std::min<long>(16, K / 1024); ++sp) {
       const double sc = speed * eff(t * sp, 256) - 0.03 * (double)(sp - 1);
       if (sc > best) { best = sc; best_s = (int)sp; bn = w; }
+    }
+  }
+  return best_s;
+}
+
+// Split-K plan for a very long K (a 1x1-conv weight gradient over up to millions of pixels) on the 4-wave
+// kernels: the tile width (256x256 or 256x128) and split count s (<= 64) that minimise a time model —
+//   rounds of 1-block/CU tiles  x  K-tiles per split  x  per-K-tile time (256 CUs at ~1.5 PF: 1.43 us for a
+//   256x256x64 tile, 256x128 at 0.8 of that rate)  +  for s > 1 the f32 slab round trip (8 s M N bytes at 5 TB/s)
+//   and the reduction launch (5 us).
+// Returns s (1 = no split) and the tile width in bn; bn = 0 when K is too short to consider splitting (the caller's
+// usual rule then applies).
+static int plan_w4_split_long(long M, long N, long K, long batch, int& bn) {
+  bn = 0;
+  if (K < 2048) return 0;
+  const long kt = (K + BK - 1) / BK;
+  double best = 1e30;
+  int best_s = 1;
+  for (int w : {256, 128}) {
+    if (w == 256 && N <= 128) continue;
+    const long t = (long)cdiv(M, 256) * cdiv(N, w) * batch;
+    const double tau = w == 256 ? 1.43e-6 : 0.89e-6;
+    for (long sp = 1; sp <= std::min<long>(64, kt / 16); ++sp) {
+      const double rounds = (double)((t * sp + 255) / 256);
+      double tm = rounds * (double)((kt + sp - 1) / sp) * tau;
+      if (sp > 1) tm += 8.0 * (double)sp * (double)M * (double)N * (double)batch / 5e12 + 5e-6;
+      if (tm < best) { best = tm; best_s = (int)sp; bn = w; }
     }
   }
   return best_s;
@@ -851,6 +880,36 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
     }
   }
   if (c256_forced) tile = -1;
+  // 1x1 filters of >= 4 256x128 tiles: the plain TN GEMM dW = dY^T . X over the pixels on the 4-wave kernel (K-outer
+  // operands through ds_read_b64_tr_b16), split-K into f32 slabs by plan_w4_split_long (the pixel count is the long
+  // K), reduced in a fixed order into dW (smaller filters keep the 128-row tiles: one tile over millions of pixels
+  // cannot fill the chip without more slab traffic than it saves)
+  // (ResNet-50 b1024: 13,285 / 13,213 vs 13,236 / 13,154 img/s with the 128-row tiles, interleaved; stage-3/4 filters
+  // 40-42 vs 46-49 us at b256: profiles/r5_wgrad_w4.txt)
+  if (pointwise && tile < 0 && ws != nullptr && K >= 128 && C >= 128 && (long)K * C >= 4 * 256 * 128) {
+    int bn = 0;
+    const int s = plan_w4_split_long(a.M, a.N, a.K, 1, bn);
+    if (bn && s >= 1 && (s == 1 || (long)s * mn <= ws_elems)) {
+      GemmArgs b = a;
+      b.splitk = s;
+      b.kchunk = ((b.K + s - 1) / s + BK - 1) / BK * BK;
+      if (s > 1) {
+        b.C = ws;
+        b.slab = mn;
+        b.beta = 0.f;
+      } else {
+        b.C = dW;
+        b.beta = accumulate ? 1.f : 0.f;
+      }
+      if (tile256_try(b, OP_KOUTER, OP_KOUTER, st, bn) == 0) {
+        if (s > 1) {
+          count_launch(LC_SPLITK);
+          dtf_sum_rows(ws, mn, s, mn, dW, accumulate, st);
+        }
+        return (int)hipGetLastError();
+      }
+    }
+  }
   if (swap_on && use_glds && tile < 0 && K <= 64 && R * S > 1 && ws != nullptr) {
     GemmArgs b = a;
     b.A = (const bf16_t*)X; b.B = (const bf16_t*)dY;
