@@ -23,16 +23,19 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Per-GPU batch. ResNet: sized for the 288 GB of HBM3E (the activations of a 1024-image step take ~60 GB): the
-# per-step fixed costs (optimizer pass, small stage-4 layers that cannot fill 256 CUs, launch tails) are amortised
-# over 4x the images of the 256 used through round 4 — interleaved on one MI355X, graph replay: 256 12,316-12,348,
-# 384 12,768-12,774, 512 12,948-12,976, 768 13,085, 1024 13,188 img/s (profiles/r5_resnet50_batch_sweep.txt).
-DEFAULT_BATCH = {"resnet50": 1024, "resnet101": 512, "resnet152": 512, "bert_base": 32, "gpt2_medium_fp8": 8,
-                 "gpt2_medium": 8}
+# Per-GPU batch, sized for the 288 GB of HBM3E (round 5; rounds 1-4 ran ResNet 256, BERT 32, GPT-2 8): per-step fixed
+# costs (the optimizer pass over 110-355M parameters, embedding / loss, small layers and GEMM tile rounds that cannot
+# fill 256 CUs, launch tails) are amortised over more samples. Measured on one MI355X (graph replay unless noted;
+# profiles/r5_batch_sweeps.txt): ResNet-50 256 12,316-12,348 | 512 12,948-12,976 | 1024 13,188 img/s; BERT-base
+# 32 878k | 64 919k | 128 1,014k tok/s; GPT-2-medium bf16 (eager) 8 238k | 16 291k | 32 309k, fp8 8 260k | 16 319k |
+# 32 334k tok/s.
+DEFAULT_BATCH = {"resnet50": 1024, "resnet101": 512, "resnet152": 512, "bert_base": 128, "gpt2_medium_fp8": 32,
+                 "gpt2_medium": 32}
 # hipGraph replay (graphs.py per-stream capture) vs eager, interleaved on one MI355X (profiles/r5_hipgraph_default.txt):
-# ResNet-50 +1.4%, BERT-base +0.7%, GPT-2-medium fp8 +0.3%, GPT-2-medium bf16 -1.8% (its many side->main joins are
-# device-flag waits in the replay). Multi-rank runs stay eager unless DTF_GRAPH_DIST=1 (keras Model.make_train_function).
-GRAPH_DEFAULT = {"resnet50": 1, "resnet101": 1, "resnet152": 1, "bert_base": 1, "gpt2_medium_fp8": 1, "gpt2_medium": 0}
+# ResNet-50 +1.4%, BERT-base +0.7%, GPT-2-medium fp8 +0.3..2%; GPT-2-medium bf16 -1.8% at batch 8 (its many
+# side->main joins are device-flag waits in the replay), -0.3% at the default batch 32. Multi-rank runs stay eager
+# unless DTF_GRAPH_DIST=1 (keras Model.make_train_function).
+GRAPH_DEFAULT = {"resnet50": 1, "resnet101": 1, "resnet152": 1, "bert_base": 1, "gpt2_medium_fp8": 1, "gpt2_medium": 1}
 
 
 def _relaunch(args):
