@@ -25,6 +25,8 @@
 // Epilogue: w4_epilogue (LDS-staged 16-B row stores for bf16 outputs).
 // Reference op family: MatMul and its gradients in the TF graph the reference builds (SURVEY §2.4.b K3;
 // /root/reference/trainer/task.py:137-139).
+#include <cstdlib>
+
 #include "gemm_w4.h"
 
 namespace dtf {
@@ -182,6 +184,7 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
     *reinterpret_cast<uint4*>(C + e) = val;
   }
 }
+
 
 // VAR (ablation builds for tools/bench_gemm_w4.py --var; 0 = the kernel): 1 no LDS-DMA in the loop, 2 no fragment
 // reads in the loop (MFMAs on stale fragments), 3 both, 4 no epilogue — timing only, results are wrong for VAR != 0.
