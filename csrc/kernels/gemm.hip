@@ -470,6 +470,48 @@ DTF_API int dtf_gemm(const void* A, const void* B, void* C, void* aux, const flo
                    sC, alpha, beta, act, out_f32, splitk, tile, ws, ws_elems, stream);
 }
 
+// Weight gradient with its bias gradient fused (the BiasAddGrad of a dense layer): dW[M][N] (f32, += when beta = 1)
+// = dY^T X over K tokens with dY [K][M] and X [K][N] both K-outer, and db[M] += the column sums of dY, taken by the
+// 4-wave kernel from the dY fragments it already holds (GemmArgs::rowsum: 4 v_dot2c per fragment, no separate pass
+// over dY). Split-K by plan_w4_split into f32 slabs of ws (splitk * M * N, then splitk * M row-sum partials), both
+// reduced in a fixed order. Returns -1 when the 4-wave kernel cannot take the shape (nothing launched: the caller runs
+// the plain GEMM + a column-sum pass).
+DTF_API int dtf_gemm_wgrad_bias(const void* dY, const void* X, float* dW, float* db, int M, int N, int K, long lda,
+                                long ldb, long ldc, float beta, float* ws, long ws_elems, void* stream) {
+  if (!db || (beta != 0.f && beta != 1.f) || (M & 7) || (N & 7) || (K % BK) || ldc != N) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  GemmArgs a{};
+  a.A = (const bf16_t*)dY; a.B = (const bf16_t*)X; a.C = dW;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.batch = 1; a.alpha = 1.f; a.beta = beta; a.out_f32 = 1;
+  int bn = 0;
+  int s = plan_w4_split(M, N, K, 1, bn);
+  if (s <= 0 || !bn) {
+    s = 1;
+    bn = pick_w4(M, N, 1);
+    if (!bn) bn = 128;
+  }
+  const long mn = (long)M * N;
+  if (!ws || (long)s * mn + (long)s * M > ws_elems) s = 1;
+  if (!ws || (long)M > ws_elems - (s > 1 ? (long)s * mn : 0)) return -1;
+  a.splitk = s;
+  a.kchunk = ((K + s - 1) / s + BK - 1) / BK * BK;
+  float* rows = ws + (s > 1 ? (long)s * mn : 0);
+  a.rowsum = rows;
+  if (s > 1) {
+    a.C = ws;
+    a.slab = mn;
+    a.beta = 0.f;
+  }
+  if (gemm_w4_try(a, OP_KOUTER, OP_KOUTER, st, bn)) return -1;
+  if (s > 1) {
+    count_launch(LC_SPLITK);
+    dtf_sum_rows(ws, mn, s, mn, dW, beta != 0.f ? 1 : 0, stream);
+  }
+  dtf_sum_rows(rows, M, s, M, db, 1, stream);
+  return (int)hipGetLastError();
+}
+
 // Data-gradient GEMM with the activation backward fused: C[M][N] (bf16) = (A . B^T) * act'(pre), pre [M][N] with
 // row stride ldc (act 1 relu, 2 gelu-tanh). The product is rounded to bf16 before the multiply, exactly as the
 // unfused GEMM + dtf_act pair would.

@@ -119,6 +119,9 @@ struct GemmArgs {
   int q8fmt;
   int no_c;
   int aux_nt;  // gemm256.hip staged epilogue: nontemporal stores for the aux (pre-activation) output
+  // optional row sums of A over each split's K range (gemm_w4.hip, K-outer A, f32 out): rowsum[split][M] — the bias
+  // gradient of a weight-gradient GEMM dW = dY^T X is the row sum of its A operand dY^T (written by the N-tile-0 blocks)
+  float* rowsum;
 };
 
 // 4 floats -> 4 packed OCP fp8 bytes (fmt 0 e4m3, 1 e5m2), values already scaled and clamped

@@ -229,6 +229,13 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < JN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
   v8bf fa0[8], fb0[JN], fa1[8], fb1[JN];
+  // VAR bit 8: row sums of A (the fused bias gradient of a weight gradient, GemmArgs::rowsum): each A fragment
+  // (16 rows x 32 k, 8 k per lane) is summed once per substep with 4 v_dot2c_f32_bf16 against 1.0 — VALU work that
+  // issues beside the MFMAs, no extra LDS traffic
+  constexpr bool RS = (VAR & 8) != 0;
+  float rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rs[i] = 0.f;
 
   // piece s (0..NG-1) of tile t's LDS-DMA: A instruction s, then B instruction s - 8. Tiles past the last one load
   // the last tile again (into the stage t would use, which nothing reads any more): no branch in the loop body.
@@ -258,6 +265,19 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
     const int i = s / SPR, j0 = (s % SPR) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) w4_mfma(acc[i][j0 + j], fb[j0 + j], fa[i]);
+    if constexpr (RS) {
+      if (s % SPR == 0) {
+        typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+        const bf2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+        const v8bf f = fa[i];
+        float r = rs[i];
+        r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 0, 1), one, r, false);
+        r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 2, 3), one, r, false);
+        r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 4, 5), one, r, false);
+        r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(f, f, 6, 7), one, r, false);
+        rs[i] = r;
+      }
+    }
   };
   // the fragment reads of a substep go out in the first half of the next one's steps (NREAD over NSTEP/2 steps),
   // so the explicit lgkmcnt(0) ahead of the substep that consumes them finds them done
@@ -320,6 +340,18 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
     for (int s = 0; s < NSTEP; ++s) mma4(fa1, fb1, s);
   }
   w4_mfma_drain();
+  if constexpr (RS) {  // lanes l, l^16, l^32, l^48 hold the same row's k-groups: fold them, lanes 0..15 write
+    if (tile_n == 0 && wn == 0 && a.rowsum) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v = rs[i];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int m = m0 + wm * 128 + i * 16 + lane;
+        if (lane < 16 && m < a.M) a.rowsum[(long)z * a.M + m] = v;
+      }
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the epilogue reuses the LDS
   if constexpr ((VAR & 4) != 0) {  // ablation: no epilogue (one store of a value that depends on every accumulator)
@@ -341,6 +373,10 @@ void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
   dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
   if constexpr (VAR != 0) {  // ablation builds: NT only
     hipLaunchKernelGGL((gemm_w4_kernel<OP_KCONTIG, OP_KCONTIG, BN, VAR>), grid, dim3(W4_THREADS), 0, st, a);
+    return;
+  }
+  if (a.rowsum) {  // (gemm_w4_ok: K-outer operands, f32 out)
+    hipLaunchKernelGGL((gemm_w4_kernel<OP_KOUTER, OP_KOUTER, BN, 8>), grid, dim3(W4_THREADS), 0, st, a);
     return;
   }
   if (amode == OP_KCONTIG && bmode == OP_KCONTIG)
@@ -365,6 +401,7 @@ bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode) {
                 : ((a.N & 7) || (a.ldc & 7) || ((uintptr_t)a.C & 15)))
     return false;
   if ((amode != OP_KCONTIG && amode != OP_KOUTER) || (bmode != OP_KCONTIG && bmode != OP_KOUTER)) return false;
+  if (a.rowsum && (!a.out_f32 || amode != OP_KOUTER || bmode != OP_KOUTER || a.batch > 1)) return false;
   if (a.kchunk % BK || a.K % BK || (a.lda & 7) || (a.ldb & 7)) return false;
   if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return false;
   auto fits = [](long elems) { return elems * 2 < (1l << 31); };

@@ -71,6 +71,7 @@ _KERNEL_SIGS = {
     "dtf_gemm_w4_var": [P, P, P, I, I, I, I, I, P],
     "dtf_gemm_w4_fp8": [P, P, P, I, I, I, L, L, L, I, I, I, P],
     "dtf_fp8_w4_enable": [I],
+    "dtf_gemm_wgrad_bias": [P, P, P, P, I, I, I, L, L, L, F, P, L, P],
     "dtf_launch_counts": [P, I],
     # per-stream hipGraph executor (graph_sync.hip)
     "dtf_xs_epoch_inc": [P, I, P],

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, bf16_shadow, call, direct_grad, fork_side, on_gpu, ptr,
+from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, K, bf16_shadow, call, direct_grad, fork_side, on_gpu, ptr,
                     stream, workspace)
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
@@ -149,6 +149,20 @@ def dense_dgrad(dz, w16, acc=None):
     return gemm(dz, w16, b_kouter=True, out=acc, beta=1.0)
 
 
+def dense_wgrad_bias(dz, x2, out, bias_out):
+    """dW += dZ^T X and db += column sums of dZ in ONE 4-wave GEMM launch (the bias gradient from the dZ fragments the
+    weight-gradient kernel already holds: gemm.hip dtf_gemm_wgrad_bias); False when that kernel cannot take the shape
+    (nothing ran: use dense_wgrad + colsum)."""
+    if not (dz.is_cuda and out.dtype == F32 and out.is_contiguous() and bias_out.is_contiguous()):
+        return False
+    T, M = dz.shape
+    N = x2.shape[1]
+    ws = workspace(dz.device)
+    rc = K().dtf_gemm_wgrad_bias(ptr(dz), ptr(x2), ptr(out), ptr(bias_out), M, N, T, dz.stride(0), x2.stride(0), N,
+                                 1.0, ptr(ws), ws.numel(), stream())
+    return rc == 0
+
+
 def dense_wgrad(dz, x2, out=None):
     """dW[out, in] = dZ^T X in f32; accumulated into `out` (an arena gradient view) when given."""
     if out is not None:
@@ -178,6 +192,9 @@ class _ActSource:
 
 
 _FUSE_DACT = True
+# the bias gradient of an arena-accumulated Dense layer inside its weight-gradient GEMM (dense_wgrad_bias) instead of a
+# separate column-sum pass over dZ
+_FUSE_BIAS_GRAD = True
 
 
 class _DenseFn(torch.autograd.Function):
@@ -248,9 +265,10 @@ class _DenseFn(torch.autograd.Function):
             # arena-accumulated weight / bias gradients on the side stream: off the dgrad critical path, and their
             # blocks fill the partial last wave of the data-gradient GEMMs (and vice versa)
             with fork_side(dz.device, dz, x2):
-                dense_wgrad(dz, x2, out=tw)
-                if tb is not None:
-                    colsum(dz, out=tb, accumulate=True)
+                if not (tb is not None and _FUSE_BIAS_GRAD and dense_wgrad_bias(dz, x2, tw, tb)):
+                    dense_wgrad(dz, x2, out=tw)
+                    if tb is not None:
+                        colsum(dz, out=tb, accumulate=True)
             if ctx.has_b and ctx.needs_input_grad[2] and tb is None:
                 db = colsum(dz)
             ctx.link = None

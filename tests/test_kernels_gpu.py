@@ -810,3 +810,30 @@ def test_row_reductions_large(cuda, T, W, stride):
     out = torch.ones(W, device=cuda)
     _util.K().dtf_sum_rows(_util.ptr(rows), stride, T, W, _util.ptr(out), 1, _util.stream())
     torch.testing.assert_close(out.double(), ref + 1.0, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("T,M,N", [(4096, 768, 1024), (8192, 1024, 4096), (1024, 264, 136)])
+def test_dense_wgrad_bias_fused(cuda, T, M, N):
+    """dW += dZ^T X and db += colsum(dZ) in one 4-wave GEMM launch (the bias gradient from the dZ fragments by
+    v_dot2c against 1.0, GemmArgs::rowsum) vs the weight-gradient GEMM + the column-sum pass: dW bit for bit (same
+    kernel, split plan and slab reduction), db to f32 rounding; both vs the f32 reference."""
+    from distributed_tensorflow_amd.ops import linalg as LA
+    from distributed_tensorflow_amd.ops._util import launch_counts, launch_delta
+    torch.manual_seed(0)
+    dz = rnd(T, M, dev=cuda)
+    x = rnd(T, N, dev=cuda)
+    w0 = torch.randn(M, N, device=cuda)
+    b0 = torch.randn(M, device=cuda)
+    tw, tb = w0.clone(), b0.clone()
+    before = launch_counts()
+    assert LA.dense_wgrad_bias(dz, x, tw, tb)
+    d = launch_delta(before)
+    assert d["w4_256"] + d["w4_128"] == 1, d
+    uw, ub = w0.clone(), b0.clone()
+    LA.dense_wgrad(dz, x, out=uw)
+    LA.colsum(dz, out=ub, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(tw, uw)
+    torch.testing.assert_close(tb, ub, rtol=1e-5, atol=1e-3)
+    close(tw, w0 + dz.float().t() @ x.float(), 1e-3)
+    close(tb, b0 + dz.float().sum(0), 1e-4)
