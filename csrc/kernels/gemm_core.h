@@ -885,8 +885,26 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, v4f (&acc)[BM /
       bmu[0] = m0v.x; bmu[1] = m0v.y; bmu[2] = m0v.z; bmu[3] = m0v.w;
       bmu[4] = m1v.x; bmu[5] = m1v.y; bmu[6] = m1v.z; bmu[7] = m1v.w;
     }
+    // full tile, nothing to combine: U LDS reads back to back, then their U stores (the general loop below waits for
+    // every read right before its store, behind the beta / dact / BN-backward branches)
+    const bool plain = a.beta == 0.f && !a.dact && !bn_bwd && !a.crm && m0 + BM <= a.M && n0 + c8t * 8 < a.N;
+    if (plain) {
+      constexpr int RPP = NTH / C8, IT = BM / RPP, U = IT < 8 ? IT : 8;
+      const int r0 = threadIdx.x / C8;
+      bf16_t* cp = reinterpret_cast<bf16_t*>(a.C) + cbase + (long)(m0 + r0) * a.ldc + n0 + c8t * 8;
+#pragma unroll
+      for (int i0 = 0; i0 < IT; i0 += U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const uint4*>(ct + (r0 + RPP * (i0 + u)) * CS + c8t * 8);
+#pragma unroll
+        for (int u = 0; u < U; ++u) *reinterpret_cast<uint4*>(cp + (long)RPP * (i0 + u) * a.ldc) = v[u];
+        __builtin_amdgcn_sched_group_barrier(0x100, U, 0);
+        __builtin_amdgcn_sched_group_barrier(0x040, U, 0);
+      }
+    }
 #pragma unroll 4
-    for (int c = threadIdx.x; c < BM * C8; c += NTH) {
+    for (int c = plain ? BM * C8 : threadIdx.x; c < BM * C8; c += NTH) {
       const int ml = c / C8;
       const int m = m0 + ml, n = n0 + c8t * 8;
       if (m >= a.M || n >= a.N) continue;

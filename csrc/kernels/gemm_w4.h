@@ -32,6 +32,24 @@ __device__ __forceinline__ void w4_lgkm0() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Staged bf16 rows -> C for a full tile with nothing to combine (no beta, no activation backward): the LDS reads of
+// 8 rows go out back to back, then their 16-B stores, so neither waits on the other row by row (the general loop's
+// beta / dact branches made hipcc wait lgkmcnt(0) before every single store).
+template <int BN, int ROWS>
+__device__ __forceinline__ void w4_store_rows(const bf16_t* ct, bf16_t* c, long ldc, int r0, int c8) {
+  constexpr int CS = BN + 8, RPP = W4_THREADS / (BN / 8), IT = ROWS / RPP, U = IT < 8 ? IT : 8;
+#pragma unroll
+  for (int i0 = 0; i0 < IT; i0 += U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const uint4*>(ct + (r0 + RPP * (i0 + u)) * CS + c8 * 8);
+#pragma unroll
+    for (int u = 0; u < U; ++u) *reinterpret_cast<uint4*>(c + (long)(r0 + RPP * (i0 + u)) * ldc) = v[u];
+    __builtin_amdgcn_sched_group_barrier(0x100, U, 0);  // the U LDS reads first,
+    __builtin_amdgcn_sched_group_barrier(0x040, U, 0);  // then the U global stores
+  }
+}
+
 // LDS-DMA loader of one R-row (K-contiguous: [R rows][64 k]) or R-column (K-outer: [64 k][R cols]) operand image
 // per K-tile, R/32 wave instructions per thread, in the lane-linear layouts frag_kcontig / frag_kouter<R> read (the
 // XOR swizzle is applied on the source side, as gemm_core.h GldsLoader / GldsKOuter). Everything per-lane is

@@ -161,6 +161,10 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
   const int n = n0 + c8 * 8;
   if (n >= a.N) return;
   bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + cbase;
+  if (a.beta == 0.f && !a.dact && m0 + 256 <= a.M) {
+    w4_store_rows<BN, 256>(ct, C + (long)m0 * a.ldc + n, a.ldc, r0, c8);
+    return;
+  }
 #pragma unroll 4
   for (int it = 0; it < 256 / RPP; ++it) {
     const int ml = r0 + RPP * it;
@@ -184,7 +188,6 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
     *reinterpret_cast<uint4*>(C + e) = val;
   }
 }
-
 
 // VAR (ablation builds for tools/bench_gemm_w4.py --var; 0 = the kernel): 1 no LDS-DMA in the loop, 2 no fragment
 // reads in the loop (MFMAs on stale fragments), 3 both, 4 no epilogue — timing only, results are wrong for VAR != 0.
@@ -366,27 +369,28 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
   w4_epilogue<BN>(a, acc, smem, m0, n0, z, bz);
 }
 
+template <int AM, int BMODE, int BN, int VAR>
+void w4_go(GemmArgs& a, hipStream_t st) {
+  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
+  hipLaunchKernelGGL((gemm_w4_kernel<AM, BMODE, BN, VAR>), grid, dim3(W4_THREADS), 0, st, a);
+}
+
 template <int BN, int VAR = 0>
 void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
   a.tiles_m = cdiv(a.M, 256);
   a.tiles_n = cdiv(a.N, BN);
-  dim3 grid(a.tiles_m * a.tiles_n, 1, a.batch * a.splitk);
   if constexpr (VAR != 0) {  // ablation builds: NT only
-    hipLaunchKernelGGL((gemm_w4_kernel<OP_KCONTIG, OP_KCONTIG, BN, VAR>), grid, dim3(W4_THREADS), 0, st, a);
+    w4_go<OP_KCONTIG, OP_KCONTIG, BN, VAR>(a, st);
     return;
   }
   if (a.rowsum) {  // (gemm_w4_ok: K-outer operands, f32 out)
-    hipLaunchKernelGGL((gemm_w4_kernel<OP_KOUTER, OP_KOUTER, BN, 8>), grid, dim3(W4_THREADS), 0, st, a);
+    w4_go<OP_KOUTER, OP_KOUTER, BN, 8>(a, st);
     return;
   }
-  if (amode == OP_KCONTIG && bmode == OP_KCONTIG)
-    hipLaunchKernelGGL((gemm_w4_kernel<OP_KCONTIG, OP_KCONTIG, BN, VAR>), grid, dim3(W4_THREADS), 0, st, a);
-  else if (amode == OP_KCONTIG)
-    hipLaunchKernelGGL((gemm_w4_kernel<OP_KCONTIG, OP_KOUTER, BN, VAR>), grid, dim3(W4_THREADS), 0, st, a);
-  else if (bmode == OP_KCONTIG)
-    hipLaunchKernelGGL((gemm_w4_kernel<OP_KOUTER, OP_KCONTIG, BN, VAR>), grid, dim3(W4_THREADS), 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_w4_kernel<OP_KOUTER, OP_KOUTER, BN, VAR>), grid, dim3(W4_THREADS), 0, st, a);
+  if (amode == OP_KCONTIG && bmode == OP_KCONTIG) w4_go<OP_KCONTIG, OP_KCONTIG, BN, VAR>(a, st);
+  else if (amode == OP_KCONTIG) w4_go<OP_KCONTIG, OP_KOUTER, BN, VAR>(a, st);
+  else if (bmode == OP_KCONTIG) w4_go<OP_KOUTER, OP_KCONTIG, BN, VAR>(a, st);
+  else w4_go<OP_KOUTER, OP_KOUTER, BN, VAR>(a, st);
 }
 
 }  // namespace

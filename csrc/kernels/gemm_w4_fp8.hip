@@ -159,7 +159,9 @@ __device__ __forceinline__ void w8_epilogue(const GemmArgs& a, v16f (&acc)[4][BN
   const int c8 = threadIdx.x % TPR, r0 = threadIdx.x / TPR;
   const int n = n0 + c8 * 8;
   bf16_t* C = reinterpret_cast<bf16_t*>(a.C);
-  if (n < a.N) {
+  if (n < a.N && !q8on && !a.dact && !a.no_c && m0 + 256 <= a.M) {
+    w4_store_rows<BN, 256>(ct, C + (long)m0 * a.ldc + n, a.ldc, r0, c8);
+  } else if (n < a.N) {
 #pragma unroll 4
     for (int it = 0; it < 256 / RPP; ++it) {
       const int ml = r0 + RPP * it;

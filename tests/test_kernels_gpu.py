@@ -837,3 +837,4 @@ def test_dense_wgrad_bias_fused(cuda, T, M, N):
     torch.testing.assert_close(tb, ub, rtol=1e-5, atol=1e-3)
     close(tw, w0 + dz.float().t() @ x.float(), 1e-3)
     close(tb, b0 + dz.float().sum(0), 1e-4)
+
