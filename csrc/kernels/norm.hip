@@ -1170,6 +1170,20 @@ DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma
                       (const bf16_t*)res)
   LN_DISPATCH(D, LNB);
 #undef LNB
-  dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, accumulate, stream);
+  if (dgb) dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, accumulate, stream);
   return (int)hipGetLastError();
+}
+
+// The data-gradient half of dtf_layernorm_bwd2: dx and the per-block [dgamma | dbeta] partial rows in part (>= 2D
+// floats per row, part_elems in all); *rows = the partial row count. The caller reduces the rows where it likes
+// (ops/norm.py: on the weight-gradient side stream, off the dgrad chain).
+DTF_API int dtf_layernorm_bwd_part(const void* dy, const void* x, const float* gamma, const float* mean,
+                                   const float* rstd, void* dx, float* part, long part_elems, long M, int D,
+                                   const void* res, int* rows, void* stream) {
+  if ((D & 7) || D > 2048 || part_elems < 2L * D) return -1;
+  const long blocks = std::max<long>(
+      1, std::min<long>(std::min<long>(std::max<long>(256, cdiv(M, 48)), std::min<long>(1024, cdiv(M, 4))),
+                        part_elems / (2L * D)));
+  *rows = (int)blocks;
+  return dtf_layernorm_bwd2(dy, x, gamma, mean, rstd, dx, nullptr, part, blocks * 2L * D, M, D, 0, res, stream);
 }

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from ._util import BF16, F32, IntOut, call, direct_grad, on_gpu, ptr, stream, workspace
+from ._util import BF16, F32, SIDE_STREAM_ON, IntOut, call, direct_grad, fork_side, on_gpu, ptr, stream, workspace
 
 
 def batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training):
@@ -119,6 +119,17 @@ class _LNFn(torch.autograd.Function):
             res = res.to(BF16).contiguous()
         g_p, b_p = ctx.ln_params
         tg, tb = direct_grad(g_p), direct_grad(b_p)
+        if tg is not None and tb is not None and tb.data_ptr() == tg.data_ptr() + 4 * D and SIDE_STREAM_ON:
+            # gamma and beta are adjacent in the arena: dx here, and the [dgamma | dbeta] partial rows reduced into
+            # their gradients on the weight-gradient side stream — the reduction launches leave the dgrad chain,
+            # where they waited for CUs held by side-stream GEMM blocks
+            part = torch.empty(1024 * 2 * D, dtype=F32, device=x.device)
+            rows = IntOut()
+            call("dtf_layernorm_bwd_part", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(part),
+                 part.numel(), M, D, ptr(res), rows.addr, stream())
+            with fork_side(x.device, part):
+                call("dtf_sum_rows", ptr(part), 2 * D, rows.value, 2 * D, ptr(tg), 1, stream())
+            return dx, None, None, None, None
         if tg is not None and tb is not None and tb.data_ptr() == tg.data_ptr() + 4 * D:
             # gamma and beta are adjacent in the arena: accumulate [dgamma | dbeta] into their gradients
             call("dtf_layernorm_bwd2", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(tg), ptr(ws),
