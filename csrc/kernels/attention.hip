@@ -80,14 +80,23 @@ __device__ __forceinline__ uint32_t drop_salt(const AttnArgs& a, int bh) {
   }
   return fmix32(s ^ ((uint32_t)bh * 0x9E3779B9u));
 }
-// 4 x 16-bit uniforms for keys 4 kq .. 4 kq + 3 of query q
+// 4 x 16-bit uniforms for keys 4 kq .. 4 kq + 3 of query q: the counter's full fmix32, and a second word from it by
+// one xor-shift-multiply round (its low half mixes both halves of the first word, its high half every bit of it)
 __device__ __forceinline__ uint2 drop_bits(const AttnArgs& a, uint32_t salt, int q, int kq) {
   const uint32_t x = fmix32(((uint32_t)q * (uint32_t)a.nkq + (uint32_t)kq) ^ salt);
-  return make_uint2(x, fmix32(x + 0x9E3779B9u));
+  return make_uint2(x, (x ^ (x >> 16)) * 0x45D9F3Bu);
 }
-__device__ __forceinline__ bool keep_field(uint2 b, int j, uint32_t thr) {
-  const uint32_t w = j < 2 ? b.x : b.y;
-  return ((w >> (16 * (j & 1))) & 0xFFFFu) < thr;
+// keep test of field j (compile-time) against thr (< 65536 whenever dropout is on): the high field of a word is
+// compared whole against thr << 16, the low one after a shift — one or two VALU ops, no field extraction
+template <int J>
+__device__ __forceinline__ bool keep_j(uint2 b, uint32_t thr) {
+  const uint32_t w = J < 2 ? b.x : b.y;
+  return (J & 1) ? w < (thr << 16) : (w << 16) < (thr << 16);
+}
+// lanes 4 g .. 4 g + 3 (a DPP quad) all take lane 4 g + r's value: a VALU move, no LDS round trip
+template <int R>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, R * 0x55, 0xF, 0xF, false);
 }
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -255,13 +264,21 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a, const int qblk,
         for (int kt = 0; kt < 4; ++kt) {
           uint2 bits = make_uint2(0, 0);
           if (drop) bits = drop_bits(a, salt, qi, (k0 >> 2) + 4 * kt + G);
+          float p[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float p = ex2(fmaf(s[kt][qt][r], c, -mnew));
-            ls += p;
-            if (drop) p = keep_field(bits, r, a.thr) ? p * a.inv_keep : 0.f;
-            s[kt][qt][r] = p;
+            p[r] = ex2(fmaf(s[kt][qt][r], c, -mnew));
+            ls += p[r];
           }
+          // dropped probabilities are zeroed here; the 1/keep scale is applied once, to the output row
+          if (drop) {
+            p[0] = keep_j<0>(bits, a.thr) ? p[0] : 0.f;
+            p[1] = keep_j<1>(bits, a.thr) ? p[1] : 0.f;
+            p[2] = keep_j<2>(bits, a.thr) ? p[2] : 0.f;
+            p[3] = keep_j<3>(bits, a.thr) ? p[3] : 0.f;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[kt][qt][r] = p[r];
         }
         l[qt] = l[qt] * alpha + ls;
         if (__any(alpha != 1.f)) {  // the running max moved for some query of the wave
@@ -299,13 +316,20 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a, const int qblk,
       for (int kt = 0; kt < 4; ++kt) {
         uint2 bits = make_uint2(0, 0);
         if (drop) bits = drop_bits(a, salt, qi, (k0 >> 2) + 4 * kt + G);
+        float p[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = ex2(s[kt][qt][r] - ms);
-          ls += p;
-          if (drop) p = keep_field(bits, r, a.thr) ? p * a.inv_keep : 0.f;
-          s[kt][qt][r] = p;
+          p[r] = ex2(s[kt][qt][r] - ms);
+          ls += p[r];
         }
+        if (drop) {
+          p[0] = keep_j<0>(bits, a.thr) ? p[0] : 0.f;
+          p[1] = keep_j<1>(bits, a.thr) ? p[1] : 0.f;
+          p[2] = keep_j<2>(bits, a.thr) ? p[2] : 0.f;
+          p[3] = keep_j<3>(bits, a.thr) ? p[3] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kt][qt][r] = p[r];
       }
       l[qt] = l[qt] * alpha + ls;
 #pragma unroll
@@ -330,7 +354,7 @@ __device__ __forceinline__ void attn_fwd_body(const AttnArgs& a, const int qblk,
   for (int qt = 0; qt < QT; ++qt) {
     float L = l[qt] + __shfl_xor(l[qt], 16, 64);
     L += __shfl_xor(L, 32, 64);
-    const float inv = L > 0.f ? 1.f / L : 0.f;
+    const float inv = L > 0.f ? (drop ? a.inv_keep : 1.f) / L : 0.f;
     const int qi = q0 + 16 * qt + i;
     if (qi < a.Sq) {
 #pragma unroll
@@ -492,6 +516,19 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
           const int key = k0w + 16 * kt + i;
           uint2 mine = make_uint2(0, 0);
           if (drop) mine = drop_bits(a, salt, q0 + 16 * qs + 4 * G + fld, key >> 2);
+          // query row r's bits live in the quad lane whose field index is r (DPP quad broadcast); this lane's key is
+          // field fld of that word: the word by fld >> 1, the half by fld & 1 (lane constants)
+          uint32_t wsel[4] = {0u, 0u, 0u, 0u};
+          if (drop) {
+            const uint32_t b0x = quad_bcast<0>(mine.x), b0y = quad_bcast<0>(mine.y);
+            const uint32_t b1x = quad_bcast<1>(mine.x), b1y = quad_bcast<1>(mine.y);
+            const uint32_t b2x = quad_bcast<2>(mine.x), b2y = quad_bcast<2>(mine.y);
+            const uint32_t b3x = quad_bcast<3>(mine.x), b3y = quad_bcast<3>(mine.y);
+            wsel[0] = fld < 2 ? b0x : b0y;
+            wsel[1] = fld < 2 ? b1x : b1y;
+            wsel[2] = fld < 2 ? b2x : b2y;
+            wsel[3] = fld < 2 ? b3x : b3y;
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ql = 16 * qs + 4 * G + r, qi = q0 + ql;
@@ -500,12 +537,8 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
             const float p = ex2(x - slse[ql]);
             float pd = p, dpv = dp[r];
             if (drop) {
-              // bits of row r live in the quad lane whose field index is r
-              uint2 rb;
-              rb.x = (uint32_t)__shfl((int)mine.x, quad | r, 64);
-              rb.y = (uint32_t)__shfl((int)mine.y, quad | r, 64);
-              const bool z = keep_field(rb, fld, a.thr);
-              pd = z ? p * a.inv_keep : 0.f;
+              const bool z = ((fld & 1) ? wsel[r] : (wsel[r] << 16)) < (a.thr << 16);
+              pd = z ? p : 0.f;  // (the 1/keep scale of dV is applied once, at its store)
               dpv = z ? dpv * a.inv_keep : 0.f;
             }
             P[hh][kt][r] = pd;
@@ -551,7 +584,7 @@ __device__ __forceinline__ void attn_dkdv_body(const AttnArgs& a, const int kblk
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         store4(dK + (long)key * a.kss + 16 * dt + 4 * G, dk[dt][kt], a.scale);
-        store4(dV + (long)key * a.kss + 16 * dt + 4 * G, dv[dt][kt], 1.f);
+        store4(dV + (long)key * a.kss + 16 * dt + 4 * G, dv[dt][kt], drop ? a.inv_keep : 1.f);
       }
     }
   }
@@ -666,7 +699,11 @@ __device__ __forceinline__ void attn_dq_body(const AttnArgs& a, const int qblk, 
           if (diag && k0 + 16 * kt + 4 * G + r > qi + off) x = -INFINITY;
           const float p = ex2(x - lse[qt]);
           float dpv = dp[r];
-          if (drop) dpv = keep_field(bits, r, a.thr) ? dpv * a.inv_keep : 0.f;
+          if (drop) {
+            const bool kp = r == 0 ? keep_j<0>(bits, a.thr) : r == 1 ? keep_j<1>(bits, a.thr)
+                            : r == 2 ? keep_j<2>(bits, a.thr) : keep_j<3>(bits, a.thr);
+            dpv = kp ? dpv * a.inv_keep : 0.f;
+          }
           dS[kt][qt][r] = p * (dpv - dd[qt]);
         }
       }

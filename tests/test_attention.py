@@ -45,7 +45,7 @@ def keep_mask(seed, B, H, Sq, Sk, keep):
         k = np.arange(Sk, dtype=np.uint32)[None, None, :]
         salt = _fmix32(s32 ^ (bh * np.uint32(0x9E3779B9)))
         x = _fmix32((q * np.uint32(nkq) + (k >> np.uint32(2))) ^ salt)
-        y = _fmix32(x + np.uint32(0x9E3779B9))
+        y = (x ^ (x >> np.uint32(16))) * np.uint32(0x45D9F3B)
         j = k & np.uint32(3)
         w = np.where(j < 2, x, y)
         u = (w >> (np.uint32(16) * (j & np.uint32(1)))) & np.uint32(0xFFFF)
