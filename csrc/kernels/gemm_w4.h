@@ -1,6 +1,8 @@
 // Shared pieces of the 4-wave 256-row GEMM kernels (gemm_w4.hip: bf16; gemm_w4_fp8.hip: fp8 on the block-scaled
 // MFMA): the pinned barrier / LDS-wait helpers and the loop-invariant LDS-DMA operand loader.
 #pragma once
+#include <type_traits>
+
 #include "gemm_core.h"
 
 namespace dtf {
@@ -89,6 +91,61 @@ struct W4Loader {
                                              16, (uint32_t)voff[i], k0 * kstep, 0, 0);
   }
 };
+
+// Implicit-GEMM (convolution forward, OP_IM2COL_T) A operand for the 4-wave kernels: row r = output pixel (n, p, q),
+// k = (tap, channel) with C % 64 == 0, so a 64-deep K-tile is ONE filter tap x 64 channels. Per lane and piece: the
+// row's input base offset and its in-image tap mask (loop-invariant); per K-tile: the tap's wave-uniform offset, and
+// rows whose tap falls in the padding get an out-of-range offset (the buffer range check supplies zeros). Same LDS
+// image and piece layout as W4Loader<R, OP_KCONTIG>.
+template <int R>
+struct W4Im2col {
+  static constexpr int L = R / 32;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int roff[L];
+  uint32_t tmask[L];
+  FastDiv dC, dS;  // (copies: the per-K-tile tap decode stays in scalar registers, no loads of the arguments)
+  int tsh, tsw;    // byte offsets of one filter row / column step in the input
+
+  __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long, int r0, int Rtot, int t) {
+    dC = a.g.dC;
+    dS = a.g.dS;
+    tsh = a.g.dh * a.g.W * a.g.C * 2;
+    tsw = a.g.dw * a.g.C * 2;
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)((long)a.g.N * a.g.H * a.g.W * a.g.C * 2),
+                                             0x00020000);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int row = 32 * i + (t >> 3);
+      const int c = (t & 7) ^ ((row >> 1) & 7);
+      const int r = r0 + row;
+      uint32_t m = 0u;
+      int off = 0;
+      if (r < Rtot) {
+        uint32_t n, rem, y, x;
+        fdivmod((uint32_t)r, a.g.dPQ, n, rem);
+        fdivmod(rem, a.g.dQ, y, x);
+        const int hb = (int)y * a.g.sh - a.g.ph, wb = (int)x * a.g.sw - a.g.pw;
+        off = (((int)n * a.g.H + hb) * a.g.W + wb) * a.g.C * 2;
+        m = tap_mask(a.g.R, a.g.S, max(0, -hb), min(a.g.R - 1, a.g.H - 1 - hb), max(0, -wb),
+                     min(a.g.S - 1, a.g.W - 1 - wb), a.g_rowrep);
+      }
+      roff[i] = off + c * 16;
+      tmask[i] = m;
+    }
+  }
+  __device__ __forceinline__ void issue1(int k0, uint32_t lds, int i) {
+    uint32_t tap, c0, kh, kw;
+    fdivmod((uint32_t)k0, dC, tap, c0);
+    fdivmod(tap, dS, kh, kw);
+    const int toff = (int)kh * tsh + (int)kw * tsw + (int)c0 * 2;
+    const uint32_t off = ((tmask[i] >> tap) & 1u) ? (uint32_t)(roff[i] + toff) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 4096),
+                                             16, off, 0, 0, 0);
+  }
+};
+
+template <int R, int MODE>
+using W4LoaderFor = typename std::conditional<MODE == OP_IM2COL_T, W4Im2col<R>, W4Loader<R, MODE>>::type;
 
 }  // namespace
 }  // namespace dtf

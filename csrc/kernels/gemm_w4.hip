@@ -40,6 +40,7 @@ struct W4Geo {
   static constexpr int STAGE = W4_A + B_BYTES;
   static constexpr int EPI = 256 * (BN + 8) * 2;        // the epilogue's staged bf16 C tile
   static constexpr int SMEM = EPI > 2 * STAGE ? EPI : 2 * STAGE;
+  static constexpr int SMEM_ST = EPI + 16 * BN > 2 * STAGE ? EPI + 16 * BN : 2 * STAGE;  // + BN statistics partials
   static constexpr int NSTEP = 2 * JN;                  // 4-MFMA steps per substep (8 x JN MFMAs)
   static constexpr int NREAD = 8 + JN;                  // fragments per substep
   static constexpr int NG = 8 + BN / 32;                // LDS-DMA pieces per K-tile (A 8, B BN/32)
@@ -87,7 +88,10 @@ __device__ __forceinline__ v8bf w4_frag(const char* lds, int rb, int kk, int lan
 //           backward (dact: C *= act'(pre)); staged through LDS so every global access is a whole 16-B row chunk;
 //   f32 C:  alpha, beta, split-K slabs; 16-B row pieces straight from the fragments.
 // Lane l of wave (wm, wn) holds acc[i][j][r] = C[m0 + 128 wm + 16 i + (l & 15)][n0 + BN/2 wn + 16 j + 4 (l >> 4) + r].
-template <int BN>
+// ST: also the training BatchNorm statistics of the stored bf16 values (a convolution forward's epilogue): one partial
+// row per 256-row tile, stats[tile][0, N) = column sums, [N, 2N) = sums of squares, reduced over the tile's 16-lane
+// row groups (DPP) and its two wave rows (LDS) in a fixed order.
+template <int BN, bool ST = false>
 __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN / 32], char* smem, int m0, int n0,
                                             int z, int bz) {
   constexpr int JN = BN / 32, WTN = BN / 2;
@@ -119,6 +123,13 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
   // bf16: fragments -> LDS tile [256][BN + 8] (16-B row pad) with bias / aux / activation applied
   constexpr int CS = BN + 8;
   bf16_t* ct = reinterpret_cast<bf16_t*>(smem);
+  float csum[ST ? JN : 1][4], csq[ST ? JN : 1][4];
+  if constexpr (ST) {
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) csum[j][r] = csq[j][r] = 0.f;
+  }
   float4 bias[JN];
 #pragma unroll
   for (int j = 0; j < JN; ++j) {
@@ -152,9 +163,44 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
       o.x = pack2bf(v[0], v[1]);
       o.y = pack2bf(v[2], v[3]);
       *reinterpret_cast<uint2*>(ct + ml * CS + nl) = o;
+      if constexpr (ST) {
+        if (m < a.M) {
+          const float f[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                              __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            csum[j][r] += f[r];
+            csq[j][r] = fmaf(f[r], f[r], csq[j][r]);
+          }
+        }
+      }
     }
   }
+  float* red = reinterpret_cast<float*>(smem + 256 * CS * 2);  // [sum | sq][wm][BN]
+  if constexpr (ST) {
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float sv = row16_sum(csum[j][r]), qv = row16_sum(csq[j][r]);
+        const int nl = wn * WTN + j * 16 + (lane >> 4) * 4 + r;
+        if ((lane & 15) == 0) {
+          red[wm * BN + nl] = sv;
+          red[2 * BN + wm * BN + nl] = qv;
+        }
+      }
+  }
   __syncthreads();
+  if constexpr (ST) {
+    float* prow = a.stats + (long)(m0 / 256) * 2 * a.N;
+    for (int nl = threadIdx.x; nl < BN; nl += W4_THREADS) {
+      const int n = n0 + nl;
+      if (n < a.N) {
+        prow[n] = red[nl] + red[BN + nl];
+        prow[a.N + n] = red[2 * BN + nl] + red[3 * BN + nl];
+      }
+    }
+  }
   // LDS -> C in whole 16-B chunks: a row is BN/8 consecutive threads
   constexpr int TPR = BN / 8, RPP = W4_THREADS / TPR;
   const int c8 = threadIdx.x % TPR, r0 = threadIdx.x / TPR;
@@ -196,7 +242,8 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
   using G = W4Geo<BN>;
   constexpr int JN = G::JN, WTN = BN / 2, NSTEP = G::NSTEP, NREAD = G::NREAD, NG = G::NG;
   constexpr int SPR = JN / 4;  // steps per accumulator row
-  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  constexpr bool ST = (VAR & 16) != 0;  // BN statistics epilogue (convolution forward)
+  __shared__ __attribute__((aligned(16))) char smem[ST ? G::SMEM_ST : G::SMEM];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
@@ -218,7 +265,7 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
   const int kend = min(a.K, kbeg + a.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  W4Loader<256, AM> la;
+  W4LoaderFor<256, AM> la;
   W4Loader<BN, BMODE> lb;
   la.init(a, a.A + (long)bz * a.sA, a.lda, m0, a.M, threadIdx.x);
   lb.init(a, a.B + (long)bz * a.sB, a.ldb, n0, a.N, threadIdx.x);
@@ -366,7 +413,7 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
     if (x == 12345.f) reinterpret_cast<float*>(a.C)[threadIdx.x] = x;
     return;
   }
-  w4_epilogue<BN>(a, acc, smem, m0, n0, z, bz);
+  w4_epilogue<BN, ST>(a, acc, smem, m0, n0, z, bz);
 }
 
 template <int AM, int BMODE, int BN, int VAR>
@@ -387,6 +434,12 @@ void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
     w4_go<OP_KOUTER, OP_KOUTER, BN, 8>(a, st);
     return;
   }
+  if (amode == OP_IM2COL_T) {  // (gemm_w4_ok: convolution forward, with or without BN statistics)
+    if (a.stats) w4_go<OP_IM2COL_T, OP_KCONTIG, BN, 16>(a, st);
+    else w4_go<OP_IM2COL_T, OP_KCONTIG, BN, 0>(a, st);
+    return;
+  }
+
   if (amode == OP_KCONTIG && bmode == OP_KCONTIG) w4_go<OP_KCONTIG, OP_KCONTIG, BN, VAR>(a, st);
   else if (amode == OP_KCONTIG) w4_go<OP_KCONTIG, OP_KOUTER, BN, VAR>(a, st);
   else if (bmode == OP_KCONTIG) w4_go<OP_KOUTER, OP_KCONTIG, BN, VAR>(a, st);
@@ -398,9 +451,21 @@ void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
 // True if the 4-wave kernel can run C = A . B^T with these arguments: K % 64 == 0 per split, 16-B aligned operand
 // rows, K-outer operands with row counts % 8 == 0, operands < 2 GiB, and only the epilogue features w4_epilogue has.
 bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode) {
-  if (a.atomic_out || a.stats || a.bnx || a.crm || a.bsrc || a.betamask || a.scales || a.q8 || a.q8T || a.q8col ||
-      a.zero_slot)
+  if (a.atomic_out || a.bnx || a.crm || a.bsrc || a.betamask || a.scales || a.q8 || a.q8T || a.q8col || a.zero_slot)
     return false;
+  // BN statistics: convolution forward only (bf16 out, nothing else in the epilogue, one tile row per stats row)
+  if (a.stats && (amode != OP_IM2COL_T || a.out_f32 || a.beta != 0.f || a.bias || a.act || a.aux || a.dact ||
+                  a.batch > 1 || a.splitk > 1))
+    return false;
+  if (amode == OP_IM2COL_T) {  // tap-uniform K-tiles, gathered input < 2 GiB, plain K-contiguous filters
+    const ConvGeom& g = a.g;
+    if (bmode != OP_KCONTIG || (g.C & 63) || g.R * g.S > 32 || (long)g.N * g.H * g.W * g.C * 2 >= (1l << 31) ||
+        a.batch > 1 || a.splitk > 1 || a.out_f32 || (a.N & 7) || (a.ldc & 7) || ((uintptr_t)a.C & 15) ||
+        (a.K % BK) || (a.ldb & 7) || ((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15) ||
+        (long)a.N * a.ldb * 2 >= (1l << 31))
+      return false;
+    return true;
+  }
   if (a.out_f32 ? (a.bias || a.act || a.aux || a.dact || (a.ldc & 3) || ((uintptr_t)a.C & 15))
                 : ((a.N & 7) || (a.ldc & 7) || ((uintptr_t)a.C & 15)))
     return false;

@@ -580,16 +580,49 @@ def test_conv_wgrad_conv256_matches_reference(cuda, case, tile):
     close((dw - base).permute(0, 3, 1, 2), wr.grad, 1e-2)
 
 
-def test_conv256_default_path_bn_stats(cuda):
-    """A layer on the default conv256 route (>= 192 blocks of 256 rows, N >= 256, K >= 1024: ResNet-50 stage 3):
+@pytest.mark.parametrize("case", [(64, 28, 128, 256, 1), (8, 28, 128, 256, 2), (4, 13, 256, 512, 1),
+                                  (3, 14, 512, 512, 2)])
+def test_conv_fwd_w4_im2col_bn_stats(cuda, case):
+    """3x3 convolutions with >= 128 output channels take the 4-wave kernel with the implicit-GEMM loader
+    (gemm_w4.hip W4Im2col: per-row tap masks, padding read as zeros by the buffer range check) and its BN-statistics
+    epilogue: output against the f32 reference and the partial rows against the column sums / sums of squares, on
+    strided, odd-sized (partial 256-row tiles) and 256- / 128-wide tile shapes; launch-counted."""
+    from distributed_tensorflow_amd.ops import conv as C
+    from distributed_tensorflow_amd.ops._util import launch_counts, launch_delta
+    N, H, Cin, K, st = case
+    x = rnd(N, H, H, Cin, dev=cuda)
+    w = torch.randn(K, 3, 3, Cin, device=cuda) / math.sqrt(9 * Cin)
+    g = C._geom(x, w, (st, st), (1, 1), (1, 1))
+    before = launch_counts()
+    y, part, rows = C.conv_fwd_raw(x, w.to(BF), g, stats=True)
+    torch.cuda.synchronize()
+    d = launch_delta(before)
+    assert d["w4_256"] + d["w4_128"] == 1, d
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.to(BF).float().permute(0, 3, 1, 2), padding=1,
+                                    stride=st)
+    close(y.permute(0, 3, 1, 2).float(), yr, 1e-2)
+    p = part[:rows * 2 * K].view(rows, 2 * K).sum(0)
+    yf = y.float().reshape(-1, K)
+    close(p[:K], yf.sum(0), 1e-3)
+    close(p[K:], (yf * yf).sum(0), 1e-3)
+
+
+def test_conv256_forced_bn_stats(cuda):
+    """The 256-row 8-wave conv256 kernel (forced tile 12: 256 x 256, 8 waves), still the route of 3x3 data gradients:
     forward with the BN statistics epilogue against the f32 reference, partial rows summing to the column sums /
     sums of squares."""
     from distributed_tensorflow_amd.ops import conv as C
+    from distributed_tensorflow_amd.ops._util import IntOut, call, ptr, stream
     N, H, W, Cin, K = 64, 28, 28, 128, 256
     x = rnd(N, H, W, Cin, dev=cuda)
     w = torch.randn(K, 3, 3, Cin, device=cuda) / math.sqrt(9 * Cin)
-    g = C._geom(x, w, (1, 1), (1, 1), (1, 1))
-    y, part, rows = C.conv_fwd_raw(x, w.to(BF), g, stats=True)
+    M = N * H * W
+    y = torch.empty(N, H, W, K, device=cuda, dtype=BF)
+    part = torch.empty(((M + 63) // 64) * 2 * K, dtype=F32, device=cuda)
+    ro = IntOut()
+    call("dtf_conv_fwd", ptr(x), ptr(w.to(BF)), ptr(y), None, ptr(part), ro.addr, N, H, W, Cin, K, 3, 3, H, W, 1, 1,
+         1, 1, 1, 1, 0, 0, 12, stream())
+    rows = ro.value
     yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.to(BF).float().permute(0, 3, 1, 2), padding=1)
     close(y.permute(0, 3, 1, 2).float(), yr, 1e-2)
     p = part[:rows * 2 * K].view(rows, 2 * K).sum(0)

@@ -61,13 +61,18 @@ def main():
     ap.add_argument("--tiles", action="store_true", help="also time every forced tile shape")
     ap.add_argument("--only", default=None)
     ap.add_argument("--tile-list", default=None, help="comma-separated tiles for --tiles")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--match", default=None, help="only layers whose name contains this")
     args = ap.parse_args()
-    global TILES
+    global TILES, NB
+    NB = args.batch
     TILES = [int(t) for t in args.tile_list.split(",")] if args.tile_list else None
     dev = torch.device("cuda")
     torch.manual_seed(0)
     tot = {"fwd": [0.0, 0.0, 0.0], "dgrad": [0.0, 0.0, 0.0], "wgrad": [0.0, 0.0, 0.0]}
     for name, H, Cin, K, R, s, cnt in layers():
+        if args.match and args.match not in name:
+            continue
         p = R // 2
         x = torch.randn(NB, H, H, Cin, device=dev).to(BF)
         w = torch.randn(K, R, R, Cin, device=dev) * 0.05
