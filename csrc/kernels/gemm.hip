@@ -681,7 +681,7 @@ static int conv_fwd_impl(const void* X, const void* Wt, void* Y, const float* bi
   a.alpha = 1.f; a.beta = 0.f; a.act = act; a.out_f32 = out_f32;
   const int am = pointwise ? OP_KCONTIG : tap_uniform(C, R * S, (long)N * H * W * C) ? OP_IM2COL_T : OP_IM2COL;
   // tap-uniform convolutions with >= 256 output channels (ResNet-50 3x3, stages 3-4): the 4-wave 256-row kernel with
-  // the implicit-GEMM loader and the BN-statistics epilogue (gemm_w4.hip W4Im2col), tile width by pick_w4. Per layer
+  // the implicit-GEMM loader and the BN-statistics epilogue (gemm_w4.h W4Gather), tile width by pick_w4. Per layer
   // at batch 1024 (profiles/r5_conv3x3_w4.txt): stage 3 287 / 253 us vs 324 / 299 on conv256, stage 4 219 / 215 vs
   // 255 / 251; stage 2 (128 channels, 256x128 tiles) 412 / 340 vs 375 / 297 on the 128x64 LDS-DMA tile: not taken.
   // (1x1 layers stay off it: strided projections 393-605 vs 350-508 us, the 2048-channel expansion 179 vs 150,
@@ -812,6 +812,15 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
     int t = tile;
+    // stride-1 3x3 data gradients into >= 256 channels (ResNet-50 stages 3-4): the 4-wave kernel with the dY gather
+    // loader and the BN-backward statistics epilogue (profiles/r5_conv3x3_w4.txt)
+    if (am == OP_DGRAD_T && R * S > 1 && t < 0 && C >= 256 && !out_f32 && beta == 0.f && !betamask && !bsrc2) {
+      const int bn = pick_w4(a.M, a.N, 1);
+      if (bn && gemm_w4_try(a, am, OP_KCONTIG, st, bn) == 0) {
+        if (bnrows) *bnrows = bnx ? a.tiles_m : 0;
+        return (int)hipGetLastError();
+      }
+    }
     if (!try_conv256(a, am, OP_KCONTIG, t, st))
       dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
     if (bnrows) *bnrows = bnx ? a.tiles_m : 0;

@@ -92,27 +92,37 @@ struct W4Loader {
   }
 };
 
-// Implicit-GEMM (convolution forward, OP_IM2COL_T) A operand for the 4-wave kernels: row r = output pixel (n, p, q),
-// k = (tap, channel) with C % 64 == 0, so a 64-deep K-tile is ONE filter tap x 64 channels. Per lane and piece: the
-// row's input base offset and its in-image tap mask (loop-invariant); per K-tile: the tap's wave-uniform offset, and
-// rows whose tap falls in the padding get an out-of-range offset (the buffer range check supplies zeros). Same LDS
-// image and piece layout as W4Loader<R, OP_KCONTIG>.
-template <int R>
-struct W4Im2col {
+// Implicit-GEMM A operand for the 4-wave kernels. OP_IM2COL_T (convolution forward): row r = output pixel (n, p, q),
+// k = (tap, input channel), C % 64 == 0. OP_DGRAD_T (stride-1 data gradient): row r = input pixel (n, h, w), k = (tap,
+// output channel) gathered from dY, Kout % 64 == 0. Either way a 64-deep K-tile is ONE filter tap x 64 channels. Per
+// lane and piece: the row's base offset and its in-image tap mask (loop-invariant); per K-tile: the tap's wave-uniform
+// offset, and rows whose tap falls outside the image get an out-of-range offset (the buffer range check supplies
+// zeros). Same LDS image and piece layout as W4Loader<R, OP_KCONTIG>.
+template <int R, int MODE>
+struct W4Gather {
+  static_assert(MODE == OP_IM2COL_T || MODE == OP_DGRAD_T, "gathered operands only");
   static constexpr int L = R / 32;
   __amdgpu_buffer_rsrc_t rsrc;
   int roff[L];
   uint32_t tmask[L];
-  FastDiv dC, dS;  // (copies: the per-K-tile tap decode stays in scalar registers, no loads of the arguments)
-  int tsh, tsw;    // byte offsets of one filter row / column step in the input
+  FastDiv dCh, dS;  // (copies: the per-K-tile tap decode stays in scalar registers, no loads of the arguments)
+  int tsh, tsw;     // byte offsets of one filter row / column step in the gathered tensor
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long, int r0, int Rtot, int t) {
-    dC = a.g.dC;
-    dS = a.g.dS;
-    tsh = a.g.dh * a.g.W * a.g.C * 2;
-    tsw = a.g.dw * a.g.C * 2;
-    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)((long)a.g.N * a.g.H * a.g.W * a.g.C * 2),
-                                             0x00020000);
+    const ConvGeom& g = a.g;
+    dS = g.dS;
+    if constexpr (MODE == OP_IM2COL_T) {
+      dCh = g.dC;
+      tsh = g.dh * g.W * g.C * 2;
+      tsw = g.dw * g.C * 2;
+      rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)((long)g.N * g.H * g.W * g.C * 2), 0x00020000);
+    } else {
+      dCh = g.dK;
+      tsh = -(g.dh * g.Q * g.Kout * 2);
+      tsw = -(g.dw * g.Kout * 2);
+      rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)((long)g.N * g.P * g.Q * g.Kout * 2),
+                                               0x00020000);
+    }
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       const int row = 32 * i + (t >> 3);
@@ -122,12 +132,21 @@ struct W4Im2col {
       int off = 0;
       if (r < Rtot) {
         uint32_t n, rem, y, x;
-        fdivmod((uint32_t)r, a.g.dPQ, n, rem);
-        fdivmod(rem, a.g.dQ, y, x);
-        const int hb = (int)y * a.g.sh - a.g.ph, wb = (int)x * a.g.sw - a.g.pw;
-        off = (((int)n * a.g.H + hb) * a.g.W + wb) * a.g.C * 2;
-        m = tap_mask(a.g.R, a.g.S, max(0, -hb), min(a.g.R - 1, a.g.H - 1 - hb), max(0, -wb),
-                     min(a.g.S - 1, a.g.W - 1 - wb), a.g_rowrep);
+        if constexpr (MODE == OP_IM2COL_T) {
+          fdivmod((uint32_t)r, g.dPQ, n, rem);
+          fdivmod(rem, g.dQ, y, x);
+          const int hb = (int)y * g.sh - g.ph, wb = (int)x * g.sw - g.pw;
+          off = (((int)n * g.H + hb) * g.W + wb) * g.C * 2;
+          m = tap_mask(g.R, g.S, max(0, -hb), min(g.R - 1, g.H - 1 - hb), max(0, -wb), min(g.S - 1, g.W - 1 - wb),
+                       a.g_rowrep);
+        } else {
+          fdivmod((uint32_t)r, g.dHW, n, rem);
+          fdivmod(rem, g.dW, y, x);
+          const int hb = (int)y + g.ph, wb = (int)x + g.pw;
+          off = (((int)n * g.P + hb) * g.Q + wb) * g.Kout * 2;
+          m = tap_mask(g.R, g.S, max(0, hb - g.P + 1), min(g.R - 1, hb), max(0, wb - g.Q + 1), min(g.S - 1, wb),
+                       a.g_rowrep);
+        }
       }
       roff[i] = off + c * 16;
       tmask[i] = m;
@@ -135,7 +154,7 @@ struct W4Im2col {
   }
   __device__ __forceinline__ void issue1(int k0, uint32_t lds, int i) {
     uint32_t tap, c0, kh, kw;
-    fdivmod((uint32_t)k0, dC, tap, c0);
+    fdivmod((uint32_t)k0, dCh, tap, c0);
     fdivmod(tap, dS, kh, kw);
     const int toff = (int)kh * tsh + (int)kw * tsw + (int)c0 * 2;
     const uint32_t off = ((tmask[i] >> tap) & 1u) ? (uint32_t)(roff[i] + toff) : 0x80000000u;
@@ -145,7 +164,8 @@ struct W4Im2col {
 };
 
 template <int R, int MODE>
-using W4LoaderFor = typename std::conditional<MODE == OP_IM2COL_T, W4Im2col<R>, W4Loader<R, MODE>>::type;
+using W4LoaderFor = typename std::conditional<MODE == OP_IM2COL_T || MODE == OP_DGRAD_T, W4Gather<R, MODE>,
+                                              W4Loader<R, MODE>>::type;
 
 }  // namespace
 }  // namespace dtf

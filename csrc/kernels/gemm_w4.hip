@@ -40,7 +40,7 @@ struct W4Geo {
   static constexpr int STAGE = W4_A + B_BYTES;
   static constexpr int EPI = 256 * (BN + 8) * 2;        // the epilogue's staged bf16 C tile
   static constexpr int SMEM = EPI > 2 * STAGE ? EPI : 2 * STAGE;
-  static constexpr int SMEM_ST = EPI + 16 * BN > 2 * STAGE ? EPI + 16 * BN : 2 * STAGE;  // + BN statistics partials
+  static constexpr int SMEM_ST = EPI + 16384 > 2 * STAGE ? EPI + 16384 : 2 * STAGE;  // + BN statistics partials
   static constexpr int NSTEP = 2 * JN;                  // 4-MFMA steps per substep (8 x JN MFMAs)
   static constexpr int NREAD = 8 + JN;                  // fragments per substep
   static constexpr int NG = 8 + BN / 32;                // LDS-DMA pieces per K-tile (A 8, B BN/32)
@@ -164,7 +164,7 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
       o.y = pack2bf(v[2], v[3]);
       *reinterpret_cast<uint2*>(ct + ml * CS + nl) = o;
       if constexpr (ST) {
-        if (m < a.M) {
+        if (m < a.M && !a.bnx) {
           const float f[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
                               __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
 #pragma unroll
@@ -184,27 +184,87 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
       for (int r = 0; r < 4; ++r) {
         const float sv = row16_sum(csum[j][r]), qv = row16_sum(csq[j][r]);
         const int nl = wn * WTN + j * 16 + (lane >> 4) * 4 + r;
-        if ((lane & 15) == 0) {
+        if ((lane & 15) == 0 && !a.bnx) {
           red[wm * BN + nl] = sv;
           red[2 * BN + wm * BN + nl] = qv;
         }
       }
   }
   __syncthreads();
-  if constexpr (ST) {
-    float* prow = a.stats + (long)(m0 / 256) * 2 * a.N;
-    for (int nl = threadIdx.x; nl < BN; nl += W4_THREADS) {
-      const int n = n0 + nl;
-      if (n < a.N) {
-        prow[n] = red[nl] + red[BN + nl];
-        prow[a.N + n] = red[2 * BN + nl] + red[3 * BN + nl];
-      }
-    }
-  }
   // LDS -> C in whole 16-B chunks: a row is BN/8 consecutive threads
   constexpr int TPR = BN / 8, RPP = W4_THREADS / TPR;
   const int c8 = threadIdx.x % TPR, r0 = threadIdx.x / TPR;
   const int n = n0 + c8 * 8;
+  if constexpr (ST) {
+    float* prow = a.stats + (long)(m0 / 256) * 2 * a.N;
+    if (!a.bnx) {
+      for (int nl = threadIdx.x; nl < BN; nl += W4_THREADS) {
+        const int nn = n0 + nl;
+        if (nn < a.N) {
+          prow[nn] = red[nl] + red[BN + nl];
+          prow[a.N + nn] = red[2 * BN + nl] + red[3 * BN + nl];
+        }
+      }
+    } else {
+      // data gradient of a BatchNorm(+ReLU) output (bnx: the BN input, bnmask: its ReLU bits, bnmean): the BN
+      // backward reduction of the stored values, sum dz and sum dz * (x - mean) with dz = the masked gradient, taken
+      // from whole 16-B chunks in the store pass; the RPP threads of a chunk column are folded in a fixed order
+      float bs[8], bq[8], mu[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) bs[r] = bq[r] = mu[r] = 0.f;
+      bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + cbase;
+      if (n < a.N) {
+        const float4 m0v = *reinterpret_cast<const float4*>(a.bnmean + n);
+        const float4 m1v = *reinterpret_cast<const float4*>(a.bnmean + n + 4);
+        mu[0] = m0v.x; mu[1] = m0v.y; mu[2] = m0v.z; mu[3] = m0v.w;
+        mu[4] = m1v.x; mu[5] = m1v.y; mu[6] = m1v.z; mu[7] = m1v.w;
+#pragma unroll 4
+        for (int it = 0; it < 256 / RPP; ++it) {
+          const int ml = r0 + RPP * it;
+          const int m = m0 + ml;
+          if (m >= a.M) break;
+          const uint4 val = *reinterpret_cast<const uint4*>(ct + ml * CS + c8 * 8);
+          const long e = (long)m * a.ldc + n;
+          *reinterpret_cast<uint4*>(C + e) = val;
+          const uint4 xr = *reinterpret_cast<const uint4*>(a.bnx + e);
+          const uint32_t bits = a.bnmask ? (uint32_t)a.bnmask[e >> 3] : 0xFFu;  // e % 8 == 0
+          const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int r = 2 * q + h;
+              const float dv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
+              const float xv = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
+              const float dz = ((bits >> r) & 1u) ? dv : 0.f;
+              bs[r] += dz;
+              bq[r] = fmaf(dz, xv - mu[r], bq[r]);
+            }
+        }
+      }
+      float* red2 = reinterpret_cast<float*>(smem + 256 * CS * 2);  // [thread][sum 8 | sq 8]
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        red2[threadIdx.x * 16 + r] = bs[r];
+        red2[threadIdx.x * 16 + 8 + r] = bq[r];
+      }
+      __syncthreads();
+      for (int nl = threadIdx.x; nl < BN; nl += W4_THREADS) {
+        const int nn = n0 + nl;
+        if (nn >= a.N) continue;
+        float sv = 0.f, qv = 0.f;
+#pragma unroll
+        for (int k = 0; k < RPP; ++k) {
+          const int t = (nl >> 3) + k * TPR;
+          sv += red2[t * 16 + (nl & 7)];
+          qv += red2[t * 16 + 8 + (nl & 7)];
+        }
+        prow[nn] = sv;
+        prow[a.N + nn] = qv;
+      }
+      return;
+    }
+  }
   if (n >= a.N) return;
   bf16_t* C = reinterpret_cast<bf16_t*>(a.C) + cbase;
   if (a.beta == 0.f && !a.dact && m0 + 256 <= a.M) {
@@ -439,6 +499,11 @@ void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
     else w4_go<OP_IM2COL_T, OP_KCONTIG, BN, 0>(a, st);
     return;
   }
+  if (amode == OP_DGRAD_T) {  // stride-1 data gradient, with or without the BN-backward statistics
+    if (a.stats) w4_go<OP_DGRAD_T, OP_KCONTIG, BN, 16>(a, st);
+    else w4_go<OP_DGRAD_T, OP_KCONTIG, BN, 0>(a, st);
+    return;
+  }
 
   if (amode == OP_KCONTIG && bmode == OP_KCONTIG) w4_go<OP_KCONTIG, OP_KCONTIG, BN, VAR>(a, st);
   else if (amode == OP_KCONTIG) w4_go<OP_KCONTIG, OP_KOUTER, BN, VAR>(a, st);
@@ -451,15 +516,21 @@ void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
 // True if the 4-wave kernel can run C = A . B^T with these arguments: K % 64 == 0 per split, 16-B aligned operand
 // rows, K-outer operands with row counts % 8 == 0, operands < 2 GiB, and only the epilogue features w4_epilogue has.
 bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode) {
-  if (a.atomic_out || a.bnx || a.crm || a.bsrc || a.betamask || a.scales || a.q8 || a.q8T || a.q8col || a.zero_slot)
+  if (a.atomic_out || a.crm || a.bsrc || a.betamask || a.scales || a.q8 || a.q8T || a.q8col || a.zero_slot)
     return false;
-  // BN statistics: convolution forward only (bf16 out, nothing else in the epilogue, one tile row per stats row)
-  if (a.stats && (amode != OP_IM2COL_T || a.out_f32 || a.beta != 0.f || a.bias || a.act || a.aux || a.dact ||
-                  a.batch > 1 || a.splitk > 1))
+  // BN statistics: convolution forward (IM2COL_T) or the BN-backward reduction of a data gradient (DGRAD_T + bnx);
+  // bf16 out, nothing else in the epilogue, one tile row per stats row
+  if (a.stats && ((amode != OP_IM2COL_T && amode != OP_DGRAD_T) || (amode == OP_DGRAD_T) != (a.bnx != nullptr) ||
+                  a.out_f32 || a.beta != 0.f || a.bias || a.act || a.aux || a.dact || a.batch > 1 || a.splitk > 1 ||
+                  (a.bnx && (a.N & 7))))
     return false;
-  if (amode == OP_IM2COL_T) {  // tap-uniform K-tiles, gathered input < 2 GiB, plain K-contiguous filters
+  if (a.bnx && !a.stats) return false;
+  if (amode == OP_IM2COL_T || amode == OP_DGRAD_T) {  // tap-uniform K-tiles, gathered tensor < 2 GiB, K-contiguous B
     const ConvGeom& g = a.g;
-    if (bmode != OP_KCONTIG || (g.C & 63) || g.R * g.S > 32 || (long)g.N * g.H * g.W * g.C * 2 >= (1l << 31) ||
+    const bool fwd = amode == OP_IM2COL_T;
+    if (bmode != OP_KCONTIG || ((fwd ? g.C : g.Kout) & 63) || g.R * g.S > 32 ||
+        (fwd ? (long)g.N * g.H * g.W * g.C : (long)g.N * g.P * g.Q * g.Kout) * 2 >= (1l << 31) ||
+        (!fwd && (g.sh != 1 || g.sw != 1)) ||
         a.batch > 1 || a.splitk > 1 || a.out_f32 || (a.N & 7) || (a.ldc & 7) || ((uintptr_t)a.C & 15) ||
         (a.K % BK) || (a.ldb & 7) || ((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15) ||
         (long)a.N * a.ldb * 2 >= (1l << 31))

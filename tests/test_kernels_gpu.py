@@ -871,3 +871,49 @@ def test_dense_wgrad_bias_fused(cuda, T, M, N):
     close(tw, w0 + dz.float().t() @ x.float(), 1e-3)
     close(tb, b0 + dz.float().sum(0), 1e-4)
 
+
+
+@pytest.mark.parametrize("case", [(4, 14, 14, 256, 256), (3, 9, 11, 512, 128), (2, 7, 7, 512, 512)])
+@pytest.mark.parametrize("with_bn", [True, False])
+def test_conv_dgrad_w4_gather_bn_stats(cuda, case, with_bn):
+    """Stride-1 3x3 data gradients into >= 256 channels take the 4-wave kernel with the dY gather loader
+    (gemm_w4.h W4Gather<OP_DGRAD_T>): dX against the f32 autograd reference on odd / partial-tile shapes, and with a
+    BatchNorm(+ReLU) input the BN-backward partial rows (sum dz, sum dz * (x - mean), dz = dX * mask) of the stored
+    values; launch-counted."""
+    from distributed_tensorflow_amd.ops import conv as C
+    from distributed_tensorflow_amd.ops._util import IntOut, call, crsk_shadow, launch_counts, launch_delta, ptr, \
+        stream, workspace
+    N, H, W, Cin, K = case
+    R = S = 3
+    dy = rnd(N, H, W, K, dev=cuda)
+    w = torch.randn(K, R, S, Cin, device=cuda) / math.sqrt(R * S * Cin)
+    x = rnd(N, H, W, Cin, dev=cuda)
+    g = C._geom(x, w, (1, 1), (1, 1), (1, 1))
+    M = N * H * W
+    yc = rnd(N, H, W, Cin, dev=cuda)
+    mask = torch.rand(M * Cin, device=cuda) > 0.4
+    bits = (mask.view(-1, 8).to(torch.uint8) << torch.arange(8, device=cuda, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    mean = torch.randn(Cin, device=cuda) * 0.1
+    dx = torch.empty(N, H, W, Cin, device=cuda, dtype=BF)
+    part = torch.empty(((M + 63) // 64 + 1) * 2 * Cin, dtype=torch.float32, device=cuda)
+    rows = IntOut()
+    ws = workspace(cuda)
+    wc = crsk_shadow(w, K, R * S, Cin)
+    before = launch_counts()
+    bn = (ptr(yc), ptr(bits), ptr(mean), ptr(part), rows.addr) if with_bn else (None, None, None, None, None)
+    call("dtf_conv_dgrad", ptr(dy), ptr(wc), ptr(dx), N, H, W, Cin, K, R, S, g[7], g[8], 1, 1, 1, 1, 1, 1, 0,
+         0.0, -1, ptr(ws), 2 * ws.numel(), *bn, None, stream())
+    torch.cuda.synchronize()
+    d = launch_delta(before)
+    assert d["w4_256"] + d["w4_128"] == 1, d
+    xr = torch.zeros(N, Cin, H, W, device=cuda, requires_grad=True)
+    torch.nn.functional.conv2d(xr, w.to(BF).float().permute(0, 3, 1, 2), padding=1).backward(
+        dy.float().permute(0, 3, 1, 2))
+    close(dx.permute(0, 3, 1, 2).float(), xr.grad, 1e-2)
+    if with_bn:
+        T = rows.value
+        assert T == (M + 255) // 256
+        p = part[:T * 2 * Cin].view(T, 2 * Cin).sum(0)
+        dz = dx.float().reshape(M, Cin) * mask.view(M, Cin).float()
+        close(p[:Cin], dz.sum(0), 1e-3)
+        close(p[Cin:], (dz * (yc.float().reshape(M, Cin) - mean)).sum(0), 1e-3)
