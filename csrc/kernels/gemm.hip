@@ -866,9 +866,13 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
       const bool pointwise = nkh == 1 && nkw == 1 && ch == 0 && cw == 0 && Hs == P && Ws == Q;
       const int am = pointwise ? OP_KCONTIG
                      : tap_uniform(K, nkh * nkw, (long)N * P * Q * K) ? OP_DGRAD_T : OP_DGRAD;
+      // (the phase launches stay on the 128-row LDS-DMA tiles: conv256 on the 4-tap phase measured slower, stride-2
+      // stage-3/4 layers 433 / 384 us vs 368 / 323 at batch 1024, profiles/r5_conv3x3_w4.txt)
       int t = tile;
-      if (!try_conv256(a, am, OP_KCONTIG, t, st))
+      if (t >= 0 && try_conv256(a, am, OP_KCONTIG, t, st)) {
+      } else {
         dispatch(a, am, OP_KCONTIG, t < 0 ? pick_glds_tile(a, am, OP_KCONTIG) : t, st);
+      }
       prow += a.tiles_m;
     }
   }
