@@ -2,6 +2,7 @@
 // (SURVEY §2.4.b K1, K2, K7, K8, K17, K18). Every kernel is 16-B vectorized and
 // grid-stride (Guideline 13: scalar bf16 loads cost 2-2.5x on CDNA).
 #include "common.h"
+#include "dropout_mask.h"
 
 namespace {
 
@@ -157,31 +158,7 @@ __global__ void act_kernel(const bf16_t* x, const bf16_t* dy, bf16_t* y, long n8
 // Per-step dropout stream: the host seed identifies the call site within a step, the device counter `ctr`
 // (advanced once per training step by dtf_rng_advance, inside the captured graph when the step is a hipGraph)
 // identifies the step, so a replayed graph draws fresh masks although its kernel arguments are frozen.
-__device__ __forceinline__ uint64_t step_seed(uint64_t seed, const uint64_t* ctr) {
-  return ctr ? seed ^ (*ctr * 0xD1B54A32D192ED03ull) : seed;
-}
-
 __global__ void rng_advance_kernel(uint64_t* ctr) { *ctr += 1; }
-
-// Dropout mask of an 8-element chunk: two 64-bit counter hashes give eight 16-bit uniforms; element j is kept
-// when its uniform is below thr = round(keep * 65536), and kept values are scaled by 65536 / thr (the exact
-// inverse of the realised keep probability). 4x fewer hashes than one per element.
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-__device__ __forceinline__ uint32_t keep_bits8(uint64_t seed, long chunk, uint32_t thr) {
-  const uint64_t h0 = mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(2 * chunk + 1));
-  const uint64_t h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(2 * chunk + 2));
-  uint32_t bits = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    bits |= (uint32_t)(((h0 >> (16 * j)) & 0xFFFFu) < thr) << j;
-    bits |= (uint32_t)(((h1 >> (16 * j)) & 0xFFFFu) < thr) << (4 + j);
-  }
-  return bits;
-}
 
 // dropout: y = x * mask / keep ; mask regenerated from (seed, chunk index)
 __global__ void dropout_kernel(const bf16_t* x, bf16_t* y, long n8, uint32_t thr, uint64_t seed, const uint64_t* ctr) {
@@ -523,10 +500,6 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const bf16_t* __restri
 
 #define GRID(n) dim3(stream_grid((n), 256)), dim3(256), 0, (hipStream_t)stream
 
-static uint32_t keep_threshold(float keep) {  // 16-bit keep threshold of the dropout kernels (>= 1)
-  long t = lrintf(keep * 65536.f);
-  return (uint32_t)(t < 1 ? 1 : (t > 65536 ? 65536 : t));
-}
 
 DTF_API int dtf_cast_f32_bf16(const float* x, void* y, long n, void* stream) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, GRID(n / 8 + 1), x, (bf16_t*)y, n);

@@ -11,6 +11,7 @@
 //   residual branch). All passes are 16-B vectorized and grid-stride; reductions
 //   write one partial row per block (no same-address atomics: deterministic).
 #include "common.h"
+#include "dropout_mask.h"
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -781,10 +782,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, bf16_t* __restrict__ dx,
                                                      float* __restrict__ part, long M, int D,
-                                                     const bf16_t* __restrict__ res) {
+                                                     const bf16_t* __restrict__ res, bf16_t* __restrict__ dfo,
+                                                     uint32_t thr, uint64_t seed, const uint64_t* ctr) {
   extern __shared__ float sred[];  // [4][2D]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int d8 = D / 8;
+  // dfo: the input x was y = x0 + dropout(f) (ops.add_dropout); the branch gradient df = dropout(dx) with that mask
+  // (elementwise.hip dropout_kernel: same chunk hashes, same roundings) is written in the same store pass
+  const uint64_t sd = dfo ? step_seed(seed, ctr) : 0ull;
+  const float dinv = 65536.f / (float)thr;
   float gm[NC][8], ag[NC][8], ab[NC][8];
 #pragma unroll
   for (int k = 0; k < NC; ++k) {
@@ -861,6 +867,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
           for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(o[j])) + rv[j];
         }
         store8(dx + row * D + c * 8, o);
+        if (dfo) {
+          const uint32_t kb = keep_bits8(sd, row * d8 + c, thr);
+          float q[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) q[j] = ((kb >> j) & 1u) ? bf2f(f2bf(o[j])) * dinv : 0.f;
+          store8(dfo + row * D + c * 8, q);
+        }
       }
     }
   }
@@ -1153,9 +1166,18 @@ DTF_API int dtf_layernorm_bwd(const void* dy, const void* x, const float* gamma,
   return dtf_layernorm_bwd2(dy, x, gamma, mean, rstd, dx, dgb, ws, ws_elems, M, D, accumulate, nullptr, stream);
 }
 // res (optional, bf16 [M][D]): another gradient of the LayerNorm's input (the residual branch), added to dx
+static int ln_bwd_impl(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
+                       void* dx, float* dgb, float* ws, long ws_elems, long M, int D, int accumulate, const void* res,
+                       void* dfo, uint32_t thr, unsigned long long seed, const void* ctr, void* stream);
 DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma, const float* mean,
                                const float* rstd, void* dx, float* dgb, float* ws, long ws_elems, long M, int D,
                                int accumulate, const void* res, void* stream) {
+  return ln_bwd_impl(dy, x, gamma, mean, rstd, dx, dgb, ws, ws_elems, M, D, accumulate, res, nullptr, 65536u, 0ull,
+                     nullptr, stream);
+}
+static int ln_bwd_impl(const void* dy, const void* x, const float* gamma, const float* mean, const float* rstd,
+                       void* dx, float* dgb, float* ws, long ws_elems, long M, int D, int accumulate, const void* res,
+                       void* dfo, uint32_t thr, unsigned long long seed, const void* ctr, void* stream) {
   if ((D & 7) || D > 2048) return -1;
   // ~48 rows (12 per wave) per block, 256..1024 blocks: long enough software-pipelined row walks per wave and a
   // smaller partial-row reduction; measured in the training step (the pass shares the CUs with the weight-gradient
@@ -1167,7 +1189,7 @@ DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma
 #define LNB(NC) \
   hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3((unsigned)blocks), dim3(256), sh, (hipStream_t)stream,       \
                       (const bf16_t*)dy, (const bf16_t*)x, gamma, mean, rstd, (bf16_t*)dx, ws, M, D,            \
-                      (const bf16_t*)res)
+                      (const bf16_t*)res, (bf16_t*)dfo, thr, (uint64_t)seed, (const uint64_t*)ctr)
   LN_DISPATCH(D, LNB);
 #undef LNB
   if (dgb) dtf_sum_rows(ws, 2L * D, (int)blocks, 2L * D, dgb, accumulate, stream);
@@ -1177,13 +1199,17 @@ DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma
 // The data-gradient half of dtf_layernorm_bwd2: dx and the per-block [dgamma | dbeta] partial rows in part (>= 2D
 // floats per row, part_elems in all); *rows = the partial row count. The caller reduces the rows where it likes
 // (ops/norm.py: on the weight-gradient side stream, off the dgrad chain).
+// dfo (optional): also the gradient of a dropped-out branch that the LayerNorm input was the residual sum of
+// (ops.add_dropout: x = x0 + dropout(f, keep, seed, ctr)): df = dropout(dx) with the same mask, in the same pass.
 DTF_API int dtf_layernorm_bwd_part(const void* dy, const void* x, const float* gamma, const float* mean,
                                    const float* rstd, void* dx, float* part, long part_elems, long M, int D,
-                                   const void* res, int* rows, void* stream) {
+                                   const void* res, int* rows, void* dfo, float keep, unsigned long long seed,
+                                   const void* ctr, void* stream) {
   if ((D & 7) || D > 2048 || part_elems < 2L * D) return -1;
   const long blocks = std::max<long>(
       1, std::min<long>(std::min<long>(std::max<long>(256, cdiv(M, 48)), std::min<long>(1024, cdiv(M, 4))),
                         part_elems / (2L * D)));
   *rows = (int)blocks;
-  return dtf_layernorm_bwd2(dy, x, gamma, mean, rstd, dx, nullptr, part, blocks * 2L * D, M, D, 0, res, stream);
+  return ln_bwd_impl(dy, x, gamma, mean, rstd, dx, nullptr, part, blocks * 2L * D, M, D, 0, res, dfo,
+                     dfo ? keep_threshold(keep) : 65536u, seed, ctr, stream);
 }

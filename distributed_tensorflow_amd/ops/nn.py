@@ -141,8 +141,29 @@ def dropout(x, rate, training=True, seed=None):
 _FUSE_ADD_DROPOUT = True
 
 
+class DropSource:
+    """What a LayerNorm consuming an add_dropout output needs to apply that dropout's backward in its own store pass
+    (norm.hip ln_bwd_kernel dfo): the mask parameters; the LayerNorm backward leaves df here and add_dropout's backward
+    takes it when the gradient it receives is exactly the tensor that LayerNorm backward wrote (its only consumer, or
+    the residual joined inside the LayerNorm backward) — otherwise it runs its own dropout pass."""
+    __slots__ = ("keep", "seed", "ctr", "df", "dptr", "__weakref__")
+
+    def __init__(self, keep, seed, ctr):
+        self.keep, self.seed, self.ctr = keep, seed, ctr
+        self.df = self.dptr = None
+
+    def provide(self, dx, df):
+        self.df, self.dptr = df, dx.data_ptr()
+
+    def take(self, dy):
+        df, dptr = self.df, self.dptr
+        self.df = self.dptr = None
+        return df if (df is not None and dy.data_ptr() == dptr and dy.is_contiguous()) else None
+
+
 class _AddDropoutFn(torch.autograd.Function):
-    """y = x + dropout(f): one pass forward; backward dx = dy, df = dropout(dy) with the same mask."""
+    """y = x + dropout(f): one pass forward; backward dx = dy, df = dropout(dy) with the same mask (or df from the
+    consuming LayerNorm's backward, DropSource)."""
 
     @staticmethod
     def forward(ctx, x, f, keep, seed, ctr, link):
@@ -150,16 +171,27 @@ class _AddDropoutFn(torch.autograd.Function):
         y = torch.empty_like(x)
         call("dtf_add_dropout", ptr(x), ptr(f), ptr(y), x.numel(), float(keep), int(seed), ctr, stream())
         ctx.keep, ctx.seed, ctx.ctr, ctx.link = keep, seed, ctr, link
+        ctx.src = DropSource(keep, seed, ctr) if _FUSE_LN_DROPOUT_BWD else None
+        if ctx.src is not None:
+            y._dtf_dropsrc = ctx.src
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dy = dy.to(BF16).contiguous()
-        df = torch.empty_like(dy)
-        call("dtf_dropout", ptr(dy), ptr(df), dy.numel(), float(ctx.keep), int(ctx.seed), ctx.ctr, stream())
+        df = ctx.src.take(dy) if ctx.src is not None else None
+        ctx.src = None
+        if df is None:
+            df = torch.empty_like(dy)
+            call("dtf_dropout", ptr(dy), ptr(df), dy.numel(), float(ctx.keep), int(ctx.seed), ctx.ctr, stream())
         dx = ctx.link.park(dy) if ctx.link is not None else dy  # None: the branch's first GEMM adds it
         ctx.link = None
         return dx, df, None, None, None, None
+
+
+# A LayerNorm whose input is an add_dropout output applies the dropout's backward in its own store pass (module
+# switch for tests: tests/test_model_training_gpu.py compares both).
+_FUSE_LN_DROPOUT_BWD = True
 
 
 def add_dropout(x, f, rate, training=True, seed=None, link=None):

@@ -103,6 +103,7 @@ class _LNFn(torch.autograd.Function):
              stream())
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.ln_params = (gamma, beta)
+        ctx.dsrc = getattr(x, "_dtf_dropsrc", None)  # x = x0 + dropout(f): apply that dropout's backward too
         return y
 
     @staticmethod
@@ -125,8 +126,13 @@ class _LNFn(torch.autograd.Function):
             # where they waited for CUs held by side-stream GEMM blocks
             part = torch.empty(1024 * 2 * D, dtype=F32, device=x.device)
             rows = IntOut()
+            src, ctx.dsrc = ctx.dsrc, None
+            df = torch.empty_like(dx) if src is not None else None
             call("dtf_layernorm_bwd_part", ptr(dy), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), ptr(dx), ptr(part),
-                 part.numel(), M, D, ptr(res), rows.addr, stream())
+                 part.numel(), M, D, ptr(res), rows.addr, ptr(df), float(src.keep) if src else 1.0,
+                 int(src.seed) if src else 0, src.ctr if src else None, stream())
+            if src is not None:
+                src.provide(dx, df)
             with fork_side(x.device, part):
                 call("dtf_sum_rows", ptr(part), 2 * D, rows.value, 2 * D, ptr(tg), 1, stream())
             return dx, None, None, None, None
