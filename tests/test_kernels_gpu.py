@@ -917,3 +917,4 @@ def test_conv_dgrad_w4_gather_bn_stats(cuda, case, with_bn):
         dz = dx.float().reshape(M, Cin) * mask.view(M, Cin).float()
         close(p[:Cin], dz.sum(0), 1e-3)
         close(p[Cin:], (dz * (yc.float().reshape(M, Cin) - mean)).sum(0), 1e-3)
+
