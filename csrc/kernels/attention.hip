@@ -392,23 +392,28 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a, int nblk) 
 // ------------------------------------------------------------------------------------------------ backward
 // D[q] = sum_d dO[q][d] * O[q][d]: 8 lanes per (bh, q) row, 16 B each, rows visited in memory order (heads
 // innermost for the packed [B, S, H, 64] layout) so a wave reads 8 consecutive 128-B rows
+// (32-bit row decode: the host guarantees B * H * Sq < 2^31; 64-bit divisions by the runtime H and Sq cost ~4x the
+// whole pass on GPT-2-medium b32)
 __global__ void __launch_bounds__(256) attn_dvec_kernel(AttnArgs a) {
-  const long n = (long)a.B * a.H * a.Sq;
+  const int n = a.B * a.H * a.Sq;
   const int sub = threadIdx.x & 7;
   const bool hfast = a.osh == HD;
-  const long step = ((long)gridDim.x * blockDim.x) >> 3;
-  for (long r = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 3; r < n; r += step) {
+  const int step = (int)((gridDim.x * blockDim.x) >> 3);
+  const uint32_t H = (uint32_t)a.H, Sq = (uint32_t)a.Sq;
+  for (int r = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 3); r < n; r += step) {
     int b, h, q;
     if (hfast) {
-      h = (int)(r % a.H);
-      const long t = r / a.H;
-      q = (int)(t % a.Sq);
-      b = (int)(t / a.Sq);
+      const uint32_t t = (uint32_t)r / H;
+      h = (int)((uint32_t)r - t * H);
+      const uint32_t t2 = t / Sq;
+      q = (int)(t - t2 * Sq);
+      b = (int)t2;
     } else {
-      q = (int)(r % a.Sq);
-      const long t = r / a.Sq;
-      h = (int)(t % a.H);
-      b = (int)(t / a.H);
+      const uint32_t t = (uint32_t)r / Sq;
+      q = (int)((uint32_t)r - t * Sq);
+      const uint32_t t2 = t / H;
+      h = (int)(t - t2 * H);
+      b = (int)t2;
     }
     const long base = b * a.osb + h * a.osh + (long)q * a.oss + sub * 8;
     float x[8], y[8];
@@ -947,6 +952,7 @@ DTF_API int dtf_attn_bwd_ds(const void* q, const void* k, const void* v, const l
   a.dv = (bf16_t*)dv;
   a.ds = (bf16_t*)ds;
   a.dsld = (Sq + 63) / 64 * 64;
+  if ((long)B * H * Sq >= (1l << 31)) return -1;
   const long blocks = ((long)B * H * Sq + 31) / 32;  // 32 rows per block
   hipLaunchKernelGGL(attn_dvec_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, st, a);
   const int nkb = (Sk + 127) / 128, nqt = (Sq + 63) / 64;
