@@ -731,15 +731,22 @@ __global__ void __launch_bounds__(256) maxpool_bn_bwd_apply_kernel(const bf16_t*
 // ---------------- LayerNorm: one wave per row, D % 8 == 0, D <= 512 * NC ----------------
 // The row lives in registers (NC 16-byte chunks per lane): one HBM read, one write.
 template <int NC>
+// fb (optional): the LayerNorm input is the residual sum x + dropout(fb) of ops.add_dropout, formed here (same mask,
+// same roundings as elementwise.hip add_dropout_kernel) and stored to ysum for the backward — one pass instead of
+// the add kernel's write and this kernel's re-read of the sum.
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, bf16_t* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     long M, int D, float eps) {
+                                                     long M, int D, float eps, const bf16_t* __restrict__ fb,
+                                                     bf16_t* __restrict__ ysum, uint32_t thr, uint64_t seed,
+                                                     const uint64_t* ctr) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const bf16_t* xr = x + row * D;
   const int d8 = D / 8;
+  const uint64_t sd = fb ? step_seed(seed, ctr) : 0ull;
+  const float dinv = 65536.f / (float)thr;
   float f[NC][8];
   float s = 0.f;
 #pragma unroll
@@ -747,6 +754,15 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
     const int c = lane + 64 * k;
     if (c < d8) {
       load8(xr + c * 8, f[k]);
+      if (fb) {
+        float b[8];
+        load8(fb + row * D + c * 8, b);
+        const uint32_t kb = keep_bits8(sd, row * d8 + c, thr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          f[k][j] = bf2f(f2bf(f[k][j] + (((kb >> j) & 1u) ? bf2f(f2bf(b[j] * dinv)) : 0.f)));
+        store8(ysum + row * D + c * 8, f[k]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += f[k][j];
     }
@@ -1145,15 +1161,31 @@ DTF_API int dtf_maxpool_bn_bwd(const void* dy, const void* arg, const void* x, c
 #define LN_DISPATCH(D, F) \
   if ((D) <= 512) F(1); else if ((D) <= 1024) F(2); else if ((D) <= 1536) F(3); else F(4)
 
-DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
-                              float* rstd, long M, int D, float eps, void* stream) {
+static int ln_fwd_impl(const void* x, const float* gamma, const float* beta, void* y, float* mean, float* rstd,
+                       long M, int D, float eps, const void* fb, void* ysum, uint32_t thr, unsigned long long seed,
+                       const void* ctr, void* stream) {
   if ((D & 7) || D > 2048) return -1;
 #define LNF(NC) \
   hipLaunchKernelGGL(ln_fwd_kernel<NC>, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream,             \
-                      (const bf16_t*)x, gamma, beta, (bf16_t*)y, mean, rstd, M, D, eps)
+                      (const bf16_t*)x, gamma, beta, (bf16_t*)y, mean, rstd, M, D, eps, (const bf16_t*)fb,    \
+                      (bf16_t*)ysum, thr, (uint64_t)seed, (const uint64_t*)ctr)
   LN_DISPATCH(D, LNF);
 #undef LNF
   return (int)hipGetLastError();
+}
+
+DTF_API int dtf_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y, float* mean,
+                              float* rstd, long M, int D, float eps, void* stream) {
+  return ln_fwd_impl(x, gamma, beta, y, mean, rstd, M, D, eps, nullptr, nullptr, 65536u, 0ull, nullptr, stream);
+}
+
+// LayerNorm of ysum = x + dropout(f, keep, seed, ctr) (ops.add_dropout deferred to its LayerNorm): ysum is written
+// too (the LayerNorm input the backward needs, the residual stream of pre-LN blocks).
+DTF_API int dtf_add_dropout_layernorm_fwd(const void* x, const void* f, void* ysum, const float* gamma,
+                                          const float* beta, void* y, float* mean, float* rstd, long M, int D,
+                                          float eps, float keep, unsigned long long seed, const void* ctr,
+                                          void* stream) {
+  return ln_fwd_impl(x, gamma, beta, y, mean, rstd, M, D, eps, f, ysum, keep_threshold(keep), seed, ctr, stream);
 }
 
 DTF_API int dtf_layernorm_bwd2(const void* dy, const void* x, const float* gamma, const float* mean,

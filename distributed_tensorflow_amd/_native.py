@@ -43,6 +43,7 @@ _KERNEL_SIGS = {
     "dtf_layernorm_fwd": [P, P, P, P, P, P, L, I, F, P],
     "dtf_layernorm_bwd": [P, P, P, P, P, P, P, P, L, L, I, I, P],
     "dtf_layernorm_bwd2": [P, P, P, P, P, P, P, P, L, L, I, I, P, P],
+    "dtf_add_dropout_layernorm_fwd": [P, P, P, P, P, P, P, P, L, I, F, F, U, P, P],
     "dtf_layernorm_bwd_part": [P, P, P, P, P, P, P, L, L, I, P, P, P, F, U, P, P],
     "dtf_maxpool_fwd": [P, P, P] + [I] * 12 + [P],
     "dtf_maxpool_bwd": [P, P, P] + [I] * 12 + [P],

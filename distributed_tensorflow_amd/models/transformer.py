@@ -77,9 +77,10 @@ class BertLayer(KL.Layer):
         l1, l2 = (ResidualGradLink(), ResidualGradLink()) if (RES_LINK and training and x.is_cuda
                                                               and torch.is_grad_enabled()) else (None, None)
         a = self.att(x, mask, training=training, link=l1)
-        x = self.ln1(ops.add_dropout(x, a, self.dropout, bool(training), link=l1))
+        # (into_ln: each residual sum is formed inside the LayerNorm pass that reads it first)
+        x = self.ln1(ops.add_dropout(x, a, self.dropout, bool(training), link=l1, into_ln=True))
         f = self.ff2(self.ff1(x, link=l2))
-        return self.ln2(ops.add_dropout(x, f, self.dropout, bool(training), link=l2))
+        return self.ln2(ops.add_dropout(x, f, self.dropout, bool(training), link=l2, into_ln=True))
 
 
 class BertModel(Model):
@@ -149,14 +150,18 @@ class GPT2Block(KL.Layer):
         if fp8:  # FFN1's output feeds only FFN2: fp8 operands from FFN1's epilogue (ops.fp8 _FUSE); untracked
             object.__setattr__(self.fc, "_fp8_next", self.proj)
         self.dropout = dropout
+        object.__setattr__(self, "out_into_ln", False)  # set by GPT2: the output's first reader is a LayerNorm
 
     def call(self, x, training=None):
         # the residual gradient of each half-block's input joins its LayerNorm's backward (ResidualGradLink)
         l1, l2 = (ResidualGradLink(), ResidualGradLink()) if (LN_LINK and training and x.is_cuda
                                                               and torch.is_grad_enabled()) else (None, None)
+        # (into_ln: the residual sum is formed inside the LayerNorm pass that reads it first — ln2 here; the block
+        # output only when the owning GPT2 feeds it to the next block's ln1 or ln_f, out_into_ln)
         x = ops.add_dropout(x, self.att(self.ln1(x, link=l1), training=training), self.dropout, bool(training),
-                            link=l1)
-        return ops.add_dropout(x, self.proj(self.fc(self.ln2(x, link=l2))), self.dropout, bool(training), link=l2)
+                            link=l1, into_ln=True)
+        return ops.add_dropout(x, self.proj(self.fc(self.ln2(x, link=l2))), self.dropout, bool(training), link=l2,
+                               into_ln=self.out_into_ln)
 
 
 class GPT2(Model):
@@ -175,6 +180,8 @@ class GPT2(Model):
         self.wte = self.add_weight("wte", (self.vocab_p, hidden), TruncatedNormal(0.0, 0.02))
         self.wpe = self.add_weight("wpe", (ctx, hidden), TruncatedNormal(0.0, 0.01))
         self.blocks = [GPT2Block(hidden, heads, dropout, fp8) for _ in range(layers)]
+        for b in self.blocks:  # each block output is read first by the next block's ln1 or by ln_f
+            object.__setattr__(b, "out_into_ln", True)
         self.ln_f = KL.LayerNormalization(epsilon=1e-5)
         pad = torch.zeros(self.vocab_p)
         pad[vocab:] = -1e9  # padded vocab entries never receive probability mass

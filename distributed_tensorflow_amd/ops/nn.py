@@ -166,10 +166,14 @@ class _AddDropoutFn(torch.autograd.Function):
     consuming LayerNorm's backward, DropSource)."""
 
     @staticmethod
-    def forward(ctx, x, f, keep, seed, ctr, link):
+    def forward(ctx, x, f, keep, seed, ctr, link, defer=False):
         x, f = x.contiguous(), f.contiguous()
         y = torch.empty_like(x)
-        call("dtf_add_dropout", ptr(x), ptr(f), ptr(y), x.numel(), float(keep), int(seed), ctr, stream())
+        if defer:
+            # formed by the LayerNorm this output feeds (ops.norm.layer_norm resolves it: one fused pass)
+            y._dtf_pending = PendingAddDropout(x, f, keep, seed, ctr)
+        else:
+            call("dtf_add_dropout", ptr(x), ptr(f), ptr(y), x.numel(), float(keep), int(seed), ctr, stream())
         ctx.keep, ctx.seed, ctx.ctr, ctx.link = keep, seed, ctr, link
         ctx.src = DropSource(keep, seed, ctr) if _FUSE_LN_DROPOUT_BWD else None
         if ctx.src is not None:
@@ -186,7 +190,29 @@ class _AddDropoutFn(torch.autograd.Function):
             call("dtf_dropout", ptr(dy), ptr(df), dy.numel(), float(ctx.keep), int(ctx.seed), ctx.ctr, stream())
         dx = ctx.link.park(dy) if ctx.link is not None else dy  # None: the branch's first GEMM adds it
         ctx.link = None
-        return dx, df, None, None, None, None
+        return dx, df, None, None, None, None, None
+
+
+class PendingAddDropout:
+    """An add_dropout output whose values are formed by the LayerNorm that consumes it (the model promises that the
+    LayerNorm is its first reader: models.transformer passes defer=True only there). resolve() forms them with the
+    plain add kernel when that LayerNorm cannot fuse."""
+    __slots__ = ("x", "f", "keep", "seed", "ctr")
+
+    def __init__(self, x, f, keep, seed, ctr):
+        self.x, self.f, self.keep, self.seed, self.ctr = x, f, keep, seed, ctr
+
+    def resolve(self, y):
+        call("dtf_add_dropout", ptr(self.x), ptr(self.f), ptr(y), y.numel(), float(self.keep), int(self.seed), self.ctr,
+             stream())
+
+
+def take_pending(y):
+    """The PendingAddDropout of y (cleared), or None."""
+    p = getattr(y, "_dtf_pending", None)
+    if p is not None:
+        y._dtf_pending = None
+    return p
 
 
 # A LayerNorm whose input is an add_dropout output applies the dropout's backward in its own store pass (module
@@ -194,16 +220,22 @@ class _AddDropoutFn(torch.autograd.Function):
 _FUSE_LN_DROPOUT_BWD = True
 
 
-def add_dropout(x, f, rate, training=True, seed=None, link=None):
+# add_dropout(..., into_ln=True) leaves its sum to the LayerNorm it feeds (one fused pass forward)
+_FUSE_ADD_LN = True
+
+
+def add_dropout(x, f, rate, training=True, seed=None, link=None, into_ln=False):
     """Residual connection around a dropped-out branch: x + dropout(f, rate) (fused on GPU). link: a
     ResidualGradLink shared with the branch's first Dense layer (ops.dense(..., link=)): the residual gradient
-    of x is then added inside that layer's data-gradient GEMM instead of by autograd."""
+    of x is then added inside that layer's data-gradient GEMM instead of by autograd. into_ln: the caller feeds the
+    result to ops.layer_norm before anything else reads it; the sum is then formed in the LayerNorm's pass."""
     if not training or rate <= 0.0:
         return add(x, f)
     if _FUSE_ADD_DROPOUT and on_gpu(x) and x.dtype == BF16 and f.dtype == BF16 and x.shape == f.shape \
             and x.numel() % 8 == 0:
         s, ctr = _auto_seed(seed, x.device)
-        return _AddDropoutFn.apply(x, f, 1.0 - rate, s, ctr, link)
+        defer = bool(into_ln and _FUSE_ADD_LN and x.shape[-1] % 8 == 0 and x.shape[-1] <= 2048)
+        return _AddDropoutFn.apply(x, f, 1.0 - rate, s, ctr, link, defer)
     return add(x, dropout(f, rate, training, seed))
 
 

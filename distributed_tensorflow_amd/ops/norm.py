@@ -4,6 +4,7 @@ from __future__ import annotations
 import torch
 
 from ._util import BF16, F32, SIDE_STREAM_ON, IntOut, call, direct_grad, fork_side, on_gpu, ptr, stream, workspace
+from .nn import take_pending
 
 
 def batch_norm_ref(y, gamma, beta, rmean, rvar, momentum, eps, training):
@@ -93,14 +94,19 @@ class _LNFn(torch.autograd.Function):
         # link: ops.conv.ResidualGradLink on which the residual add of the same input parks its gradient; the
         # backward adds it in its store pass (pre-LN blocks: x feeds LN and the residual connection)
         ctx.link = link
+        pend = take_pending(x)  # x = x0 + dropout(f) still to be formed (ops.add_dropout(..., into_ln=True))
         x = x.contiguous()
         D = x.shape[-1]
         M = x.numel() // D
         y = torch.empty_like(x)
         mean = torch.empty(M, dtype=F32, device=x.device)
         rstd = torch.empty(M, dtype=F32, device=x.device)
-        call("dtf_layernorm_fwd", ptr(x), ptr(gamma), ptr(beta), ptr(y), ptr(mean), ptr(rstd), M, D, float(eps),
-             stream())
+        if pend is not None:
+            call("dtf_add_dropout_layernorm_fwd", ptr(pend.x), ptr(pend.f), ptr(x), ptr(gamma), ptr(beta), ptr(y),
+                 ptr(mean), ptr(rstd), M, D, float(eps), float(pend.keep), int(pend.seed), pend.ctr, stream())
+        else:
+            call("dtf_layernorm_fwd", ptr(x), ptr(gamma), ptr(beta), ptr(y), ptr(mean), ptr(rstd), M, D, float(eps),
+                 stream())
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.ln_params = (gamma, beta)
         ctx.dsrc = getattr(x, "_dtf_dropsrc", None)  # x = x0 + dropout(f): apply that dropout's backward too
@@ -150,6 +156,11 @@ class _LNFn(torch.autograd.Function):
 def layer_norm(x, gamma, beta, eps=1e-5, link=None):
     """link: a ResidualGradLink shared with the residual add of the same input (ops.add_dropout(..., link=)):
     that add parks its gradient of x and this backward returns the sum (no autograd add kernel)."""
+    if on_gpu(x) and x.shape[-1] % 8 == 0 and x.dtype == BF16:
+        return _LNFn.apply(x, gamma, beta, float(eps), link)
+    pend = take_pending(x)
+    if pend is not None:  # (an input this LayerNorm cannot fuse: form the sum first)
+        pend.resolve(x)
     if on_gpu(x) and x.shape[-1] % 8 == 0:
         return _LNFn.apply(x.to(BF16), gamma, beta, float(eps), link)
     return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), gamma, beta, eps).to(

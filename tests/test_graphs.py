@@ -201,12 +201,16 @@ def test_gpt2_layernorm_residual_join_bitwise(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("switch,launch", [("_FUSE_LN_DROPOUT_BWD", "dtf_dropout"),
+                                           ("_FUSE_ADD_LN", "dtf_add_dropout")])
 @pytest.mark.parametrize("model", ["gpt2", "bert"])
-def test_layernorm_applies_dropout_backward_bitwise(cuda, model, monkeypatch):
+def test_layernorm_applies_dropout_backward_bitwise(cuda, model, switch, launch, monkeypatch):
     """A LayerNorm whose input is an add_dropout output writes the dropped-out branch's gradient in its own store pass
-    (norm.hip ln_bwd_kernel dfo, ops.nn.DropSource) instead of a separate dropout pass over its output: the same
-    losses and weights as with the separate pass (bit for bit on GPT-2, whose pre-LN residual joins inside the LayerNorm
-    backward; within the run-to-run spread on post-LN BERT) — and the separate dropout passes really disappear."""
+    (norm.hip ln_bwd_kernel dfo, ops.nn.DropSource) instead of a separate dropout pass over its output
+    (_FUSE_LN_DROPOUT_BWD), and forms the residual sum x + dropout(f) in its own forward pass instead of reading it
+    from the add kernel (_FUSE_ADD_LN, ln_fwd_kernel fb): the same losses and weights as without the fusion (bit for
+    bit on GPT-2, whose pre-LN residual joins inside the LayerNorm backward; within the run-to-run spread on post-LN
+    BERT) — and the separate passes really disappear."""
     from distributed_tensorflow_amd.keras import initializers
     from distributed_tensorflow_amd.models import transformer as T
     from distributed_tensorflow_amd.ops import _util, mha, nn
@@ -225,7 +229,7 @@ def test_layernorm_applies_dropout_backward_bitwise(cuda, model, monkeypatch):
             batches.append((x, torch.randint(0, V, (B, P), device=cuda)))
     res = []
     for on in (False, False, True):
-        monkeypatch.setattr(nn, "_FUSE_LN_DROPOUT_BWD", on)
+        monkeypatch.setattr(nn, switch, on)
         initializers.set_seed(5)
         nn._seed_counter[0] = mha._seed_counter[0] = 0  # same dropout seeds and step counters in both runs
         _util._RNG.clear()
@@ -237,7 +241,7 @@ def test_layernorm_applies_dropout_backward_bitwise(cuda, model, monkeypatch):
         with _util.call_log() as calls:
             ls = [float(m.train_step(b)["loss"]) for b in batches]
         torch.cuda.synchronize()
-        res.append((ls, [w.detach().clone() for w in m.trainable_variables], calls["dtf_dropout"]))
+        res.append((ls, [w.detach().clone() for w in m.trainable_variables], calls[launch]))
     assert res[2][2] < res[0][2], (res[0][2], res[2][2])
     if model == "gpt2":
         assert res[0][0] == res[2][0]
