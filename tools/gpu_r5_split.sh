@@ -1,11 +1,11 @@
+# split-K penalty of the dense weight-gradient plan (gemm.hip plan_w4_split, native:dtf_set_split_penalty), interleaved
+# bash tools/gpu_r5_split.sh <tag>
 set -o pipefail
 mkdir -p gpurun_out
-tag=${1:-r5s}
-for i in 1 2; do
-  for v in 0 1; do
-    for m in bert_base gpt2_medium; do
-      DTF_SPLIT_MODEL=$v timeout -k 10 300 python -u bench.py --model $m --steps 10 --warmup 5 > gpurun_out/${tag}_${m}_${v}_$i.log 2>&1 || { tail -20 gpurun_out/${tag}_${m}_${v}_$i.log; exit 1; }
-      echo "$m DTF_SPLIT_MODEL=$v run $i $(tail -n 1 gpurun_out/${tag}_${m}_${v}_$i.log | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
-    done
+tag=${1:-r5sp}
+for m in gpt2_medium bert_base; do
+  for pen in ${PENS:-30 80 200 30 80 200}; do
+    timeout -k 10 300 python -u tools/bench_with.py native:dtf_set_split_penalty=$pen -- --model $m --steps 20 --warmup 5 > gpurun_out/${tag}_${m}_$pen.log 2>&1 || { tail -20 gpurun_out/${tag}_${m}_$pen.log; exit 1; }
+    echo "$m pen=$pen $(tail -n 1 gpurun_out/${tag}_${m}_$pen.log | cut -c1-110)"
   done
 done
