@@ -155,7 +155,6 @@ enum LaunchCounter : int {
   LC_W4F8_256 = 7,    // gemm_w4_fp8.hip, 256x256 tiles
   LC_W4F8_128 = 8,    // gemm_w4_fp8.hip, 256x128 tiles
   LC_GEMM256_FP8 = 9, // gemm256.hip with fp8 operands
-  LC_SPLITK_FIXUP = 10,  // split-K reduced inside the 4-wave GEMM (GemmArgs::fix_cnt), no reduction launch
   LC_COUNT = 16
 };
 DTF_API long* dtf_launch_counters();

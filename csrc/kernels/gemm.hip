@@ -1,7 +1,5 @@
 // MFMA GEMM + implicit-GEMM convolution for gfx950: host API (kernels in gemm_core.h).
 #include <cstdlib>
-#include <map>
-#include <mutex>
 
 #include "gemm_core.h"
 
@@ -266,59 +264,6 @@ static int pick_tile(long M, long N, long batch_splits, long K = 1 << 30) {
 
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8 = 0, int bn = 256);  // gemm256.hip
 int gemm_w4_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn);  // gemm_w4.hip
-bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode);                      // gemm_w4.hip
-
-// Split-K fixup (GemmArgs::fix_cnt, gemm_w4.hip w4_fixup) for split counts up to this (dtf_set_split_fixup; 0 = off)
-static int g_fixup_max = 16;
-
-// Arrival counters of the split-K fixup: one zeroed slice of FIX_CAP per (device, stream), taken from a per-device
-// pool allocated and cleared on first use. Launches on one stream are serial and the last block of every tile resets
-// its counter, so a slice is all zeros whenever the next launch on that stream starts. nullptr = no fixup: too many
-// tiles, pool full, or a stream being captured (a graph replays on other streams, possibly beside eager work on the
-// capture stream: its launches keep the separate reduction pass).
-static unsigned* fixup_counters(hipStream_t st, long tiles) {
-  constexpr long FIX_CAP = 16384, SLICES = 64;
-  if (tiles > FIX_CAP) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  static std::mutex mu;
-  static std::map<int, unsigned*> pool;
-  static std::map<std::pair<int, hipStream_t>, unsigned*> slice;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = slice.find({dev, st});
-  if (it != slice.end()) return it->second;
-  unsigned*& base = pool[dev];
-  if (!base) {
-    if (hipMalloc(&base, FIX_CAP * SLICES * sizeof(unsigned)) != hipSuccess) {
-      base = nullptr;
-      return nullptr;
-    }
-    if (hipMemset(base, 0, FIX_CAP * SLICES * sizeof(unsigned)) != hipSuccess) return nullptr;
-  }
-  long used = 0;
-  for (auto& kv : slice) used += kv.first.first == dev;
-  if (used >= SLICES) return nullptr;
-  unsigned* p = base + used * FIX_CAP;
-  slice[{dev, st}] = p;
-  return p;
-}
-
-// Sets the fixup fields of a 4-wave split-K launch (f32 slabs in a.C, a.slab set) that reduces into out; false (fields
-// cleared) when the kernel or the counters cannot take it — the caller then reduces the slabs itself.
-static bool w4_fixup_arm(GemmArgs& a, int amode, int bmode, int bn, float* out, bool accumulate, hipStream_t st) {
-  a.fix_out = nullptr; a.fix_cnt = nullptr; a.fix_acc = 0;
-  if (a.splitk < 2 || a.splitk > g_fixup_max || a.batch != 1 || a.slab <= 0) return false;
-  unsigned* cnt = fixup_counters(st, (long)cdiv(a.M, 256) * cdiv(a.N, bn));
-  if (!cnt) return false;
-  a.fix_out = out; a.fix_cnt = cnt; a.fix_acc = accumulate ? 1 : 0;
-  if (!gemm_w4_ok(a, amode, bmode)) {
-    a.fix_out = nullptr; a.fix_cnt = nullptr; a.fix_acc = 0;
-    return false;
-  }
-  return true;
-}
 // 256-row tiles: the 4-wave kernel (gemm_w4.hip: 1.0-1.25x gemm256 on every transformer shape, profiles/
 // r5_gemm_vs_hipblaslt.txt) when its epilogue covers the call, else the 8-wave gemm256 kernel.
 static int tile256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int bn = 256) {
@@ -473,12 +418,9 @@ static int plan_w4_split(long M, long N, long K, long batch, int& bn) {
 // Returns s (1 = no split) and the tile width in bn; bn = 0 when K is too short to consider splitting (the caller's
 // usual rule then applies).
 }  // namespace dtf
+// (profiles/r5_gemm_vs_hipblaslt.txt: 0.005-0.2 measured, 0.03 kept)
 DTF_API int dtf_set_split_penalty(int permille) {
   dtf::g_split_penalty = permille / 1000.0;
-  return 0;
-}
-DTF_API int dtf_set_split_fixup(int max_splits) {
-  dtf::g_fixup_max = max_splits;
   return 0;
 }
 namespace dtf {
@@ -565,17 +507,13 @@ DTF_API int dtf_gemm_wgrad_bias(const void* dY, const void* X, float* dW, float*
   a.kchunk = ((K + s - 1) / s + BK - 1) / BK * BK;
   float* rows = ws + (s > 1 ? (long)s * mn : 0);
   a.rowsum = rows;
-  bool fixed = false;
   if (s > 1) {
     a.C = ws;
     a.slab = mn;
     a.beta = 0.f;
-    fixed = w4_fixup_arm(a, OP_KOUTER, OP_KOUTER, bn, dW, beta != 0.f, st);
   }
   if (gemm_w4_try(a, OP_KOUTER, OP_KOUTER, st, bn)) return -1;
-  if (fixed) {
-    count_launch(LC_SPLITK_FIXUP);
-  } else if (s > 1) {
+  if (s > 1) {
     count_launch(LC_SPLITK);
     dtf_sum_rows(ws, mn, s, mn, dW, beta != 0.f ? 1 : 0, stream);
   }
@@ -633,21 +571,12 @@ static int gemm_impl(const void* A, const void* B, void* C, void* aux, const flo
       a.C = ws;
       a.slab = (long)M * N;  // z = batch*splitk + split -> slab index
       a.beta = 0.f;
-      bool big = false, fixed = false;
+      bool big = false;
       if (w4bn) {  // the split chosen for the 4-wave kernel
         GemmArgs b = a;
-        const int am = a_kouter ? OP_KOUTER : OP_KCONTIG, bm = b_kouter ? OP_KOUTER : OP_KCONTIG;
-        if (w4_fixup_arm(b, am, bm, w4bn, (float*)C, beta != 0.f, (hipStream_t)stream) &&
-            gemm_w4_try(b, am, bm, (hipStream_t)stream, w4bn) == 0) {
-          big = fixed = true;
-        } else {
-          b.fix_out = nullptr; b.fix_cnt = nullptr; b.fix_acc = 0;
-          if (tile256_try(b, am, bm, (hipStream_t)stream, w4bn) == 0) big = true;
-        }
-      }
-      if (fixed) {
-        count_launch(LC_SPLITK_FIXUP);
-        return (int)hipGetLastError();
+        if (tile256_try(b, a_kouter ? OP_KOUTER : OP_KCONTIG, b_kouter ? OP_KOUTER : OP_KCONTIG, (hipStream_t)stream,
+                        w4bn) == 0)
+          big = true;
       }
       if (!big && tile < 0 && M >= 256 && N >= 256) {  // 256x256 tiles: re-split for them (>= ~1 block per CU)
         GemmArgs b = a;

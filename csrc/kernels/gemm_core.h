@@ -78,11 +78,6 @@ struct GemmArgs {
   int out_f32;          // C is float
   int atomic_out;       // atomicAdd into float C (split-K / accumulate)
   long slab;            // >0: split-K partials go to slab (blockIdx.z) of this many elements (plain stores)
-  // split-K fixup (4-wave kernel, f32 slabs, batch 1): the last split of each tile to finish (per-tile arrival counter
-  // fix_cnt, zero on entry and reset by that block) sums the tile's slabs in split order into fix_out (+= when fix_acc)
-  float* fix_out;
-  unsigned* fix_cnt;
-  int fix_acc;
   ConvGeom g;
   // optional output-row remap (strided dgrad phases): row m = (n, hh, ww) over an rmHs x rmWs grid is stored
   // at pixel (n, rmsh*hh + rmh0, rmsw*ww + rmw0) of an rmH x rmW image

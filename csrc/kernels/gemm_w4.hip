@@ -91,76 +91,6 @@ __device__ __forceinline__ v8bf w4_frag(const char* lds, int rb, int kk, int lan
 // ST: also the training BatchNorm statistics of the stored bf16 values (a convolution forward's epilogue): one partial
 // row per 256-row tile, stats[tile][0, N) = column sums, [N, 2N) = sums of squares, reduced over the tile's 16-lane
 // row groups (DPP) and its two wave rows (LDS) in a fixed order.
-// Split-K fixup (GemmArgs::fix_cnt): after its slab stores every split of a tile releases them (device-scope fence)
-// and counts itself in on the tile's arrival counter; the split that arrives last acquires the others' slabs and sums
-// all of them in split order — rows s < S & ~3 into four interleaved accumulators, the rest into the first, combined
-// as (a0 + a1) + (a2 + a3), then + the old value when accumulating: exactly dtf_group_rows4_kernel's association, so
-// the result is bit-identical to the separate reduction pass it replaces, which re-read every slab from HBM in its
-// own launch after the GEMM. No block waits for another (no spin): a block that is not last just exits.
-template <int BN>
-__device__ __noinline__ void w4_fixup(const float* __restrict__ slabs, long slab, float* __restrict__ out,
-                                      unsigned* cnt, int S, int M, int N, long ldc, int tiles_n, int accumulate,
-                                      int m0, int n0) {
-  // (not inlined, scalar arguments: the kernel's registers are spent; acc is dead here)
-  constexpr int JN = BN / 32, WTN = BN / 2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  __shared__ int last;
-  const int tile = (m0 / 256) * tiles_n + n0 / BN;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(cnt + tile, 1u) == (unsigned)(S - 1);
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (threadIdx.x == 0) atomicExch(cnt + tile, 0u);  // ready for the next launch on this stream
-  const int S4 = S & ~3;
-  // one 16-row fragment row x 4 fragment columns at a time (64 accumulator registers: the kernel's budget is spent)
-#pragma unroll 1
-  for (int ij = 0; ij < 8 * (JN / 4); ++ij) {
-    const int i = ij / (JN / 4), j0 = (ij % (JN / 4)) * 4;
-    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
-    if (m >= M) continue;
-    const int nb = n0 + wn * WTN + j0 * 16 + (lane >> 4) * 4;
-    const long roff = (long)m * ldc + nb;
-    float4 q[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) q[j][u] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 1
-    for (int s = 0; s < S; ++s) {
-      const float* src = slabs + (long)s * slab + roff;
-      const int u = s < S4 ? (s & 3) : 0;
-      float4 v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        v[j] = nb + j * 16 < N ? *reinterpret_cast<const float4*>(src + j * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-          if (w == u) { q[j][w].x += v[j].x; q[j][w].y += v[j].y; q[j][w].z += v[j].z; q[j][w].w += v[j].w; }
-      }
-    }
-    float* orow = out + roff;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (nb + j * 16 >= N) continue;
-      float4 r;
-      r.x = (q[j][0].x + q[j][1].x) + (q[j][2].x + q[j][3].x);
-      r.y = (q[j][0].y + q[j][1].y) + (q[j][2].y + q[j][3].y);
-      r.z = (q[j][0].z + q[j][1].z) + (q[j][2].z + q[j][3].z);
-      r.w = (q[j][0].w + q[j][1].w) + (q[j][2].w + q[j][3].w);
-      if (accumulate) {
-        const float4 o = *reinterpret_cast<const float4*>(orow + j * 16);
-        r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
-      }
-      *reinterpret_cast<float4*>(orow + j * 16) = r;
-    }
-  }
-}
-
 template <int BN, bool ST = false>
 __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN / 32], char* smem, int m0, int n0,
                                             int z, int bz) {
@@ -188,9 +118,6 @@ __device__ __forceinline__ void w4_epilogue(const GemmArgs& a, v4f (&acc)[8][BN 
         *reinterpret_cast<float4*>(crow + n) = v;
       }
     }
-    if (a.fix_cnt)
-      w4_fixup<BN>(reinterpret_cast<const float*>(a.C), a.slab, a.fix_out, a.fix_cnt, a.splitk, a.M, a.N, a.ldc,
-                   a.tiles_n, a.fix_acc, m0, n0);
     return;
   }
   // bf16: fragments -> LDS tile [256][BN + 8] (16-B row pad) with bias / aux / activation applied
@@ -615,9 +542,6 @@ bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode) {
     return false;
   if ((amode != OP_KCONTIG && amode != OP_KOUTER) || (bmode != OP_KCONTIG && bmode != OP_KOUTER)) return false;
   if (a.rowsum && (!a.out_f32 || amode != OP_KOUTER || bmode != OP_KOUTER || a.batch > 1)) return false;
-  if (a.fix_cnt && (!a.out_f32 || a.splitk < 2 || a.slab <= 0 || a.batch > 1 || !a.fix_out || a.beta != 0.f ||
-                    ((uintptr_t)a.fix_out & 15)))
-    return false;
   if (a.kchunk % BK || a.K % BK || (a.lda & 7) || (a.ldb & 7)) return false;
   if (((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15)) return false;
   auto fits = [](long elems) { return elems * 2 < (1l << 31); };

@@ -517,7 +517,7 @@ def call_log():
 
 
 LAUNCH_COUNTERS = ("w4_256", "w4_128", "gemm256", "gemm_tile", "gemm_dact", "beta_bf16", "splitk", "w4f8_256", "w4f8_128",
-                   "gemm256_fp8", "splitk_fixup")
+                   "gemm256_fp8")
 
 
 def launch_counts():
