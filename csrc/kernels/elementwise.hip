@@ -319,6 +319,80 @@ __global__ void __launch_bounds__(256) embed_bwd_small_kernel(const bf16_t* __re
   for (int i = threadIdx.x; i < VD; i += blockDim.x) part[(long)blockIdx.x * VD + i] = acc[i];
 }
 
+// Embedding gradient for tables of V <= VR <= 4 rows (BERT's token types): one wave per block, each lane's columns
+// (NC 8-column chunks) accumulated in registers per table row over the block's tokens in token order, 4 tokens' loads
+// in flight, then the wave's [V][D] partial row to part[block] — deterministic (no atomics; dtf_sum_rows finishes in
+// a fixed order). The LDS-atomic form above raced its 4 waves on the same rows (2 token types) and took 257 us for
+// BERT-base b128's 65k tokens.
+template <int VR, int NC>
+__global__ void __launch_bounds__(64) embed_bwd_regs_kernel(const bf16_t* __restrict__ dy,
+                                                            const long* __restrict__ idx, long T, int D, int V,
+                                                            long rpb, float* __restrict__ part) {
+  const int lane = threadIdx.x;
+  const int d8 = D / 8;
+  float acc[VR][NC][8];
+#pragma unroll
+  for (int u = 0; u < VR; ++u)
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[u][k][j] = 0.f;
+  const long r0 = (long)blockIdx.x * rpb, r1 = min(T, r0 + rpb);
+  long t = r0;
+  for (; t + 4 <= r1; t += 4) {
+    int vv[4];
+    float f[4][NC][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      vv[q] = (int)idx[t + q];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        const int c = lane + 64 * k;
+        if (c < d8) load8(dy + (t + q) * D + c * 8, f[q][k]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int u = 0; u < VR; ++u)
+        if (vv[q] == u) {
+#pragma unroll
+          for (int k = 0; k < NC; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[u][k][j] += f[q][k][j];
+        }
+  }
+  for (; t < r1; ++t) {
+    const int v = (int)idx[t];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + 64 * k;
+      if (c >= d8) continue;
+      float f[8];
+      load8(dy + t * D + c * 8, f);
+#pragma unroll
+      for (int u = 0; u < VR; ++u)
+        if (v == u) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[u][k][j] += f[j];
+        }
+    }
+  }
+  float* prow = part + (long)blockIdx.x * V * D;
+#pragma unroll
+  for (int u = 0; u < VR; ++u) {
+    if (u >= V) break;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + 64 * k;
+      if (c >= d8) continue;
+      float4* o = reinterpret_cast<float4*>(prow + (long)u * D + c * 8);
+      o[0] = make_float4(acc[u][k][0], acc[u][k][1], acc[u][k][2], acc[u][k][3]);
+      o[1] = make_float4(acc[u][k][4], acc[u][k][5], acc[u][k][6], acc[u][k][7]);
+    }
+  }
+}
+
 // Fused softmax cross-entropy over rows (logits f32 or bf16), int64 labels.
 // loss[r] = logsumexp(x) - x[label]; dlogits = (softmax - onehot) * gscale (written in the fwd pass).
 // label < 0 => ignored row (loss 0, grad 0). label_smoothing eps spreads eps/V over all classes.
@@ -599,6 +673,26 @@ DTF_API int dtf_embed_bwd_small(const void* dy, const long* idx, float* out, lon
   if ((D & 7) || V < 1 || V * D > 16384) return -1;
   hipStream_t st = (hipStream_t)stream;
   const long VD = (long)V * D;
+  const int d8 = D / 8;
+  if (V <= 4 && d8 <= 256 && T > 0 && ws_elems >= VD) {
+    long blocks = std::max<long>(1, std::min<long>((T + 31) / 32, 2048));
+    blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / VD));
+    const long rpb = (T + blocks - 1) / blocks;
+    blocks = (T + rpb - 1) / rpb;
+    const int nc = (d8 + 63) / 64;
+#define EBR(VR, NC) \
+  hipLaunchKernelGGL((embed_bwd_regs_kernel<VR, NC>), dim3((unsigned)blocks), dim3(64), 0, st, (const bf16_t*)dy, idx, \
+                     T, D, V, rpb, ws)
+#define EBR_NC(VR) \
+  if (nc == 1) EBR(VR, 1); else if (nc == 2) EBR(VR, 2); else EBR(VR, 4)
+    if (V == 1) EBR_NC(1);
+    else if (V == 2) EBR_NC(2);
+    else EBR_NC(4);
+#undef EBR_NC
+#undef EBR
+    dtf_sum_rows(ws, VD, (int)blocks, VD, out, accumulate, stream);
+    return (int)hipGetLastError();
+  }
   long blocks = std::max<long>(1, std::min<long>((T + 63) / 64, 1024));
   blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / VD));
   const long rpb = (T + blocks - 1) / blocks;

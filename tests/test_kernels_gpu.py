@@ -918,3 +918,26 @@ def test_conv_dgrad_w4_gather_bn_stats(cuda, case, with_bn):
         close(p[:Cin], dz.sum(0), 1e-3)
         close(p[Cin:], (dz * (yc.float().reshape(M, Cin) - mean)).sum(0), 1e-3)
 
+
+
+@pytest.mark.parametrize("T,D,V", [(65536, 768, 2), (4099, 1024, 3), (1001, 200, 1), (777, 2048, 4), (3000, 256, 9)])
+def test_embed_bwd_small_table(cuda, T, D, V):
+    """Gradient of a small embedding table (BERT's token types): out[v] (+)= sum of dy over the tokens of type v —
+    register accumulators per wave for V <= 4 (elementwise.hip embed_bwd_regs_kernel), the LDS form above; vs the f32
+    reference, accumulating, and the same bits on a second run (no atomics on the register path)."""
+    from distributed_tensorflow_amd.ops._util import call, ptr, stream, workspace
+    torch.manual_seed(0)
+    dy = rnd(T, D, dev=cuda)
+    idx = torch.randint(0, V, (T,), device=cuda)
+    ws = workspace(cuda)
+    base = torch.randn(V, D, device=cuda)
+    outs = []
+    for _ in range(2):
+        out = base.clone()
+        call("dtf_embed_bwd_small", ptr(dy), ptr(idx), ptr(out), T, D, V, 1, ptr(ws), ws.numel(), stream())
+        outs.append(out)
+    torch.cuda.synchronize()
+    ref = base + torch.zeros(V, D, device=cuda).index_add_(0, idx, dy.float())
+    close(outs[0], ref, 1e-4)
+    if V <= 4:
+        assert torch.equal(outs[0], outs[1])
