@@ -294,40 +294,16 @@ __global__ void __launch_bounds__(256) embed_bwd_sorted_kernel(const bf16_t* __r
   }
 }
 
-// Embedding gradient for SMALL tables (V <= 16, e.g. token types): LDS-resident [V][D] accumulators per block
-// (LDS atomics; lanes of one instruction hit distinct columns), block partials to part[block][V*D].
-__global__ void __launch_bounds__(256) embed_bwd_small_kernel(const bf16_t* __restrict__ dy,
-                                                              const long* __restrict__ idx, long T, int D, int V,
-                                                              long rpb, float* __restrict__ part) {
-  extern __shared__ float acc[];
-  const int VD = V * D;
-  for (int i = threadIdx.x; i < VD; i += blockDim.x) acc[i] = 0.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int d8 = D / 8;
-  const long r0 = (long)blockIdx.x * rpb, r1 = min(T, r0 + rpb);
-  for (long t = r0 + w; t < r1; t += 4) {
-    const long v = idx[t];
-    for (int c = lane; c < d8; c += 64) {
-      float f[8];
-      load8(dy + t * D + c * 8, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(&acc[v * D + c * 8 + j], f[j]);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < VD; i += blockDim.x) part[(long)blockIdx.x * VD + i] = acc[i];
-}
-
-// Embedding gradient for tables of V <= VR <= 4 rows (BERT's token types): one wave per block, each lane's columns
-// (NC 8-column chunks) accumulated in registers per table row over the block's tokens in token order, 4 tokens' loads
-// in flight, then the wave's [V][D] partial row to part[block] — deterministic (no atomics; dtf_sum_rows finishes in
-// a fixed order). The LDS-atomic form above raced its 4 waves on the same rows (2 token types) and took 257 us for
-// BERT-base b128's 65k tokens.
+// Embedding gradient for small tables (V <= 16 rows, e.g. BERT's token types): one wave per block, each lane's
+// columns (NC 8-column chunks) accumulated in registers per table row over the block's tokens in token order, 4
+// tokens' loads in flight, then the wave's partial rows to part[block][V][D] — deterministic (no atomics; dtf_sum_rows
+// finishes in a fixed order). One launch covers table rows [vbase, vbase + VR); larger tables take ceil(V / 4)
+// launches. (Round 4's form accumulated in LDS with float atomics raced by 4 waves on the same rows, 257 us for
+// BERT-base b128's 65k tokens: 28 us now.)
 template <int VR, int NC>
 __global__ void __launch_bounds__(64) embed_bwd_regs_kernel(const bf16_t* __restrict__ dy,
                                                             const long* __restrict__ idx, long T, int D, int V,
-                                                            long rpb, float* __restrict__ part) {
+                                                            int vbase, long rpb, float* __restrict__ part) {
   const int lane = threadIdx.x;
   const int d8 = D / 8;
   float acc[VR][NC][8];
@@ -344,7 +320,7 @@ __global__ void __launch_bounds__(64) embed_bwd_regs_kernel(const bf16_t* __rest
     float f[4][NC][8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      vv[q] = (int)idx[t + q];
+      vv[q] = (int)idx[t + q] - vbase;
 #pragma unroll
       for (int k = 0; k < NC; ++k) {
         const int c = lane + 64 * k;
@@ -363,7 +339,7 @@ __global__ void __launch_bounds__(64) embed_bwd_regs_kernel(const bf16_t* __rest
         }
   }
   for (; t < r1; ++t) {
-    const int v = (int)idx[t];
+    const int v = (int)idx[t] - vbase;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       const int c = lane + 64 * k;
@@ -378,10 +354,10 @@ __global__ void __launch_bounds__(64) embed_bwd_regs_kernel(const bf16_t* __rest
         }
     }
   }
-  float* prow = part + (long)blockIdx.x * V * D;
+  float* prow = part + (long)blockIdx.x * V * D + (long)vbase * D;
 #pragma unroll
   for (int u = 0; u < VR; ++u) {
-    if (u >= V) break;
+    if (vbase + u >= V) break;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       const int c = lane + 64 * k;
@@ -670,35 +646,28 @@ DTF_API int dtf_embed_bwd_sorted(const void* dy, const long* sid, const long* pe
 // Small-table (V <= 16) embedding gradient: out[V][D] (+)= sum over tokens.
 DTF_API int dtf_embed_bwd_small(const void* dy, const long* idx, float* out, long T, int D, int V, int accumulate,
                                 float* ws, long ws_elems, void* stream) {
-  if ((D & 7) || V < 1 || V * D > 16384) return -1;
+  if ((D & 7) || V < 1 || V > 16 || D > 2048 || T <= 0) return T <= 0 ? 0 : -1;
   hipStream_t st = (hipStream_t)stream;
   const long VD = (long)V * D;
-  const int d8 = D / 8;
-  if (V <= 4 && d8 <= 256 && T > 0 && ws_elems >= VD) {
-    long blocks = std::max<long>(1, std::min<long>((T + 31) / 32, 2048));
-    blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / VD));
-    const long rpb = (T + blocks - 1) / blocks;
-    blocks = (T + rpb - 1) / rpb;
-    const int nc = (d8 + 63) / 64;
-#define EBR(VR, NC) \
-  hipLaunchKernelGGL((embed_bwd_regs_kernel<VR, NC>), dim3((unsigned)blocks), dim3(64), 0, st, (const bf16_t*)dy, idx, \
-                     T, D, V, rpb, ws)
-#define EBR_NC(VR) \
-  if (nc == 1) EBR(VR, 1); else if (nc == 2) EBR(VR, 2); else EBR(VR, 4)
-    if (V == 1) EBR_NC(1);
-    else if (V == 2) EBR_NC(2);
-    else EBR_NC(4);
-#undef EBR_NC
-#undef EBR
-    dtf_sum_rows(ws, VD, (int)blocks, VD, out, accumulate, stream);
-    return (int)hipGetLastError();
-  }
-  long blocks = std::max<long>(1, std::min<long>((T + 63) / 64, 1024));
+  if (ws_elems < VD) return -1;
+  long blocks = std::max<long>(1, std::min<long>((T + 31) / 32, 2048));
   blocks = std::min<long>(blocks, std::max<long>(1, ws_elems / VD));
   const long rpb = (T + blocks - 1) / blocks;
   blocks = (T + rpb - 1) / rpb;
-  hipLaunchKernelGGL(embed_bwd_small_kernel, dim3((unsigned)blocks), dim3(256), sizeof(float) * VD, st,
-                     (const bf16_t*)dy, idx, T, D, V, rpb, ws);
+  const int nc = (D / 8 + 63) / 64;
+#define EBR(VR, NC) \
+  hipLaunchKernelGGL((embed_bwd_regs_kernel<VR, NC>), dim3((unsigned)blocks), dim3(64), 0, st, (const bf16_t*)dy, idx, \
+                     T, D, V, vb, rpb, ws)
+#define EBR_NC(VR) \
+  if (nc == 1) EBR(VR, 1); else if (nc == 2) EBR(VR, 2); else EBR(VR, 4)
+  for (int vb = 0; vb < V; vb += 4) {
+    const int vr = V - vb;
+    if (vr == 1) EBR_NC(1);
+    else if (vr == 2) EBR_NC(2);
+    else EBR_NC(4);
+  }
+#undef EBR_NC
+#undef EBR
   dtf_sum_rows(ws, VD, (int)blocks, VD, out, accumulate, stream);
   return (int)hipGetLastError();
 }

@@ -304,7 +304,7 @@ class _EmbedFn(torch.autograd.Function):
         if yshape is not None:
             acc = int(direct[2] is not None)
             dy_ = direct[2] if acc else torch.zeros(yshape, dtype=F32, device=dy.device)
-            if tid is not None and yshape[0] <= 16:
+            if tid is not None and yshape[0] <= 16 and D <= 2048:
                 call("dtf_embed_bwd_small", ptr(dy), ptr(tid), ptr(dy_), T, D, yshape[0], acc, ptr(ws), ws.numel(),
                      stream())
             elif tid is not None:
