@@ -9,8 +9,10 @@ with the bucketed all-reduce, and the fused optimizer update — bracketed by a 
 ``torch.cuda.synchronize()``; the max over ranks is reported by rank 0 as one JSON line.
 Data: synthetic (random inputs + labels resident on each GPU); weights random-init.
 
-Other BASELINE.json configs: ``--model bert_base`` (seq 512, MultiWorkerMirroredStrategy, tokens/s)
-and ``--model gpt2_medium_fp8`` (ctx 1024, fp8 projections, MirroredStrategy, tokens/s).
+Other BASELINE.json configs: ``--model bert_base`` (seq 512, MultiWorkerMirroredStrategy, tokens/s),
+``--model gpt2_medium_fp8`` (ctx 1024, fp8 projections, MirroredStrategy, tokens/s) and ``--model resnet50_ps``
+(ParameterServerStrategy: 2 PS + 6 trainers, one task per GPU, with ``--gpus 8``; 1 PS + 3 trainers on one GPU with
+``--gpus 1``; distributed_tensorflow_amd/cli/ps_bench.py).
 """
 import argparse
 import json
@@ -29,12 +31,14 @@ sys.path.insert(0, ROOT)
 # profiles/r5_batch_sweeps.txt): ResNet-50 256 12,316-12,348 | 512 12,948-12,976 | 1024 13,188 img/s; BERT-base
 # 32 878k | 64 919k | 128 1,014k tok/s; GPT-2-medium bf16 (eager) 8 238k | 16 291k | 32 309k, fp8 8 260k | 16 319k |
 # 32 334k tok/s.
-DEFAULT_BATCH = {"resnet50": 1024, "resnet101": 512, "resnet152": 512, "bert_base": 128, "gpt2_medium_fp8": 32,
+DEFAULT_BATCH = {"resnet50_ps": 256, "resnet50": 1024, "resnet101": 512, "resnet152": 512, "bert_base": 128, "gpt2_medium_fp8": 32,
                  "gpt2_medium": 32}
 # hipGraph replay (graphs.py per-stream capture) vs eager, interleaved on one MI355X (profiles/r5_hipgraph_default.txt):
 # ResNet-50 +1.4%, BERT-base +0.7%, GPT-2-medium fp8 +0.3..2%; GPT-2-medium bf16 -1.8% at batch 8 (its many
-# side->main joins are device-flag waits in the replay), -0.3% at the default batch 32. Multi-rank runs stay eager
-# unless DTF_GRAPH_DIST=1 (keras Model.make_train_function).
+# side->main joins are device-flag waits in the replay), -0.3% at the default batch 32. Multi-rank runs are captured
+# the same way when the gradient buckets go through the framework's RCCL communicator (the default): the bucket
+# all-reduces are nodes of the communication stream's graph (keras Model.make_train_function; DTF_GRAPH_DIST=0 keeps
+# them eager).
 GRAPH_DEFAULT = {"resnet50": 1, "resnet101": 1, "resnet152": 1, "bert_base": 1, "gpt2_medium_fp8": 1, "gpt2_medium": 1}
 
 
@@ -119,9 +123,16 @@ def main():
                          "frees up — the 4-wave GEMM blocks of the side stream hold a whole CU's registers); interleaved "
                          "on one MI355X: ResNet-50 13,386 / 13,459 vs 13,317 / 13,337 img/s, GPT-2 +0.3%, BERT +-0 "
                          "(profiles/r5_hipgraph_default.txt)")
+    ap.add_argument("--ps", type=int, default=None, help="resnet50_ps: parameter-server tasks (default: see ps_bench)")
+    ap.add_argument("--trainers", type=int, default=None, help="resnet50_ps: trainer tasks")
+    ap.add_argument("--ps-cpu", action="store_true", help="resnet50_ps: PS shards in host shared memory")
+    ap.add_argument("--ps-timeout", type=float, default=1500, help="resnet50_ps: whole-cluster time limit (s)")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
+    if args.model.endswith("_ps"):  # its own launcher (one task per GPU), never torchrun's
+        from distributed_tensorflow_amd.cli import ps_bench
+        return ps_bench.main(args, sys.argv[1:])
     if args.graph is None:
         # the capture is the third call of the step (two eager warmups first): with fewer than 3 warmup steps it
         # would land in the timed region, so the default is eager then
@@ -151,7 +162,6 @@ def main():
     model, data, unit, cfg = build(args, strategy, dev, rank)
     model._jit = bool(args.graph)
     train_fn = model.make_train_function(force=True)
-    cfg["hipgraph"] = type(train_fn).__name__ == "CapturedStep"
     cfg["hiprio"] = bool(args.hiprio)
 
     def step():
@@ -160,6 +170,7 @@ def main():
 
     for _ in range(args.warmup):
         logs = step()
+    cfg["hipgraph"] = bool(getattr(train_fn, "captured", False))
     sc = getattr(train_fn, "sc", None)
     if sc is not None:  # the per-stream capture: graphs (streams) and cross-stream edges by kind
         cfg["graph_streams"] = len(sc.streams)
@@ -180,6 +191,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if hasattr(train_fn, "check"):
+        train_fn.check()  # a timed-out cross-stream wait of the graph replay fails the run (not a slow or wrong one)
     exposed = [b.exposed_ms() for b in bucketers if hasattr(b, "exposed_ms")]
     exposed = [e for e in exposed if e is not None]
     # the loss and the replica checksum describe exactly the warmup + timed steps (taken before the probe below)
@@ -213,7 +226,7 @@ def main():
     # after the timed region (it changes nothing that was measured): the collective's own bus bandwidth on this
     # node at bucket-sized messages, so the bucket cap and wire dtype can be chosen from a measurement on the
     # hardware the scaling run used (RCCL over xGMI on an 8-GPU node)
-    ar_sweep = _allreduce_sweep(dist, dev, world) if (world > 1 and args.ar_sweep) else None
+    ar_sweep = _allreduce_sweep(dist, dev, world, bucketers) if (world > 1 and args.ar_sweep) else None
     ms = dt / args.steps * 1e3
     global_batch = args.batch * world
     per_sample = getattr(args, "tokens_per_sample", 1)
@@ -274,27 +287,49 @@ def _paths(bucketers):
     return out or None
 
 
-def _allreduce_sweep(dist, dev, world, sizes_mb=(1, 4, 16, 32, 64, 128), iters=5):
-    """Bus bandwidth (GB/s, the nccl-tests convention: bytes * 2 (n-1) / n / time) of f32 all-reduces on the default
-    process group, slowest rank's time per size."""
+def _allreduce_sweep(dist, dev, world, bucketers, sizes_mb=(1, 4, 16, 32, 64, 128), iters=5,
+                     min_channels=(4, 8, 16)):
+    """Bus bandwidth (GB/s, the nccl-tests convention: bytes * 2 (n-1) / n / time) of f32 all-reduces, slowest rank's
+    time per size, on the communicator the gradient buckets actually use — the framework's RCCL communicator
+    (parallel/rccl.py) at the bucketer's channel setting — plus the same communicator type at min_channels 4 / 8 / 16
+    (the bucket cap and channel count are chosen from this table) and torch's ProcessGroupNCCL for comparison."""
     import torch
-    out = {}
-    for mb in sizes_mb:
-        x = torch.ones(mb * (1 << 20) // 4, dtype=torch.float32, device=dev)
-        sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
-        for _ in range(2):
-            dist.all_reduce(x)
-        sync()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            dist.all_reduce(x)
-        sync()
-        el = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        out[f"{mb}MB"] = round(mb * (1 << 20) * 2 * (world - 1) / world / float(el.item()) / 1e9, 1)
-        del x
-    return out
+    from distributed_tensorflow_amd.parallel import rccl
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+
+    def sweep(fn):
+        out = {}
+        for mb in sizes_mb:
+            x = torch.ones(mb * (1 << 20) // 4, dtype=torch.float32, device=dev)
+            for _ in range(2):
+                fn(x)
+            sync()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn(x)
+            sync()
+            el = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            out[f"{mb}MB"] = round(mb * (1 << 20) * 2 * (world - 1) / world / float(el.item()) / 1e9, 1)
+            del x
+        return out
+
+    res = {}
+    used = next((b.rccl for b in bucketers if getattr(b, "rccl", None) is not None), None)
+    if used is not None:
+        res["buckets"] = {"communicator": "native", "min_channels": used.min_channels,
+                          "max_channels": used.max_channels, "busbw": sweep(used.all_reduce_)}
+    if dev.type == "cuda" and dist.get_backend() == "nccl" and rccl.available()[0]:
+        for mc in min_channels:
+            c = rccl.RcclCommunicator(device=dev, min_channels=mc, max_channels=max(mc, rccl.DEFAULT_MAX_CHANNELS),
+                                      name=f"sweep{mc}")
+            try:
+                res[f"native_min{mc}"] = sweep(c.all_reduce_)
+            finally:
+                c.destroy()
+    res["torch_process_group"] = sweep(lambda x: dist.all_reduce(x))
+    return res
 
 
 if __name__ == "__main__":

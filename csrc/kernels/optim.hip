@@ -42,6 +42,7 @@ struct OptArgs {
   int nesterov, zero_grad;
   const float* hp;
   const float* sumsq;
+  const int* abort;  // per-stream hipGraph replay: nonzero after a timed-out cross-stream wait -> apply nothing
 };
 
 template <int KIND>
@@ -100,6 +101,9 @@ __device__ __forceinline__ void st_nt(float* p, long i, float4 v) {
 template <int KIND, int NS>
 __global__ void __launch_bounds__(256) optim_kernel(OptArgs a) {
   constexpr int U = 2;
+  // a join of this step timed out (graph_sync.hip xs_wait): its gradients may be incomplete, so the weights must not
+  // move; the host raises at its next check (graphs.CapturedStep)
+  if (a.abort && __hip_atomic_load(a.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const float lr = a.hp[0];
   float gs = a.hp[1];
   if (a.sumsq && a.hp[2] > 0.f) {
@@ -196,12 +200,12 @@ DTF_API int dtf_hp_ring_select(const float* table, int R, int n, int* ctr, float
 
 DTF_API int dtf_optim_apply(int kind, float* p, float* g, float* s1, float* s2, void* p16, long n, float b1,
                             float b2, float eps, float wd, float mom, float l1, float l2, int nesterov,
-                            int zero_grad, const float* hp, const float* sumsq, void* stream) {
+                            int zero_grad, const float* hp, const float* sumsq, const int* abort, void* stream) {
   if (n <= 0) return 0;
   OptArgs a;
   a.p = p; a.g = g; a.s1 = s1; a.s2 = s2; a.p16 = (bf16_t*)p16; a.n = n; a.kind = kind;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.mom = mom; a.l1 = l1; a.l2 = l2;
-  a.nesterov = nesterov; a.zero_grad = zero_grad; a.hp = hp; a.sumsq = sumsq;
+  a.nesterov = nesterov; a.zero_grad = zero_grad; a.hp = hp; a.sumsq = sumsq; a.abort = abort;
   hipStream_t st = (hipStream_t)stream;
   switch (kind) {
     case OPT_SGD: launch_optim<OPT_SGD>(a, st); break;

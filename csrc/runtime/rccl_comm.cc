@@ -30,7 +30,10 @@ typedef void* ncomm_t;
 struct NUid {
   char internal[128];
 };
-// ncclConfig_t (RCCL 2.26 / 2.27 layout; fields after nvlsCTAs are not used)
+// ncclConfig_t as laid out by RCCL 2.26 and 2.27 (fields after nvlsCTAs are not used). The layout is NOT a stable ABI
+// across releases: load() refuses any other version (kMinVersion..kMaxVersion), and the framework then falls back
+// to torch.distributed's process group.
+constexpr int kMinVersion = 22600, kMaxVersion = 22799;
 struct NConfig {
   size_t size;
   unsigned int magic;
@@ -115,6 +118,11 @@ void load() {
     return;
   }
   if (a.GetVersion(&a.version) != 0) a.version = 0;
+  if (a.version < kMinVersion || a.version > kMaxVersion) {
+    g_err = "RCCL version " + std::to_string(a.version) + " outside the ncclConfig_t layouts this binding knows (" +
+            std::to_string(kMinVersion) + ".." + std::to_string(kMaxVersion) + ")";
+    return;
+  }
   a.lib = lib;
 }
 

@@ -57,7 +57,7 @@ _KERNEL_SIGS = {
     "dtf_maxpool_bn_bwd": [P, P, P, P, P, P] + [I] * 12 + [P, P, P, I, P, P],
     "dtf_gap_fwd": [P, P, I, I, I, I, P],
     "dtf_gap_bwd": [P, I, P, I, I, I, P],
-    "dtf_optim_apply": [I, P, P, P, P, P, L, F, F, F, F, F, F, F, I, I, P, P, P],
+    "dtf_optim_apply": [I, P, P, P, P, P, L, F, F, F, F, F, F, F, I, I, P, P, P, P],
     "dtf_sumsq": [P, L, P, I, P],
     "dtf_hp_ring_select": [P, I, I, P, P, P],
     "dtf_cast_f32_bf16": [P, P, L, P],

@@ -53,6 +53,24 @@ def _pump(prefix, stream, out):
         out.flush()
 
 
+def task_list(num_ps, num_workers, num_chief, chief_job="master"):
+    """Launch order of the tasks: PS tasks, then the chief, then the workers."""
+    return [("ps", i) for i in range(num_ps)] + [(chief_job, i) for i in range(num_chief)] + \
+        [("worker", i) for i in range(num_workers)]
+
+
+def assign_devices(tasks, gpu_list, ps_gpus=False):
+    """{task: device ordinal string}: the GPU tasks (chief/worker, and PS when ps_gpus) take `gpu_list` round-robin in
+    launch order; a task not in the result runs on the host (HIP_VISIBLE_DEVICES='')."""
+    out = {}
+    gi = 0
+    for t, i in tasks:
+        if gpu_list and (t != "ps" or ps_gpus):
+            out[(t, i)] = gpu_list[gi % len(gpu_list)]
+            gi += 1
+    return out
+
+
 def launch(cmd, num_ps=1, num_workers=1, num_chief=1, gpus=None, ps_gpus=False, chief_job="master", env=None,
            timeout=None, log=sys.stdout, host_kv=False, max_restarts=0):
     """Start every task and supervise them.
@@ -64,16 +82,15 @@ def launch(cmd, num_ps=1, num_workers=1, num_chief=1, gpus=None, ps_gpus=False, 
     coordination service down with it)."""
     import time
     cluster = make_cluster(num_ps, num_workers, num_chief, chief_job)
-    tasks = [("ps", i) for i in range(num_ps)] + [(chief_job, i) for i in range(num_chief)] + \
-            [("worker", i) for i in range(num_workers)]
+    tasks = task_list(num_ps, num_workers, num_chief, chief_job)
     gpu_list = [g for g in (gpus.split(",") if gpus else []) if g != ""]
+    ordinals = assign_devices(tasks, gpu_list, ps_gpus)
     kv_server = None
     if host_kv or max_restarts:
         from ..parallel.kv import KVServer
         kv_server = KVServer("127.0.0.1", 0)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     envs = {}
-    gi = 0
     for t, i in tasks:
         e = dict(os.environ, **(env or {}))
         e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
@@ -81,12 +98,11 @@ def launch(cmd, num_ps=1, num_workers=1, num_chief=1, gpus=None, ps_gpus=False, 
         e["DTF_ROLE"] = f"{t}{i}"
         if kv_server is not None:
             e["DTF_KV_ADDR"] = f"127.0.0.1:{kv_server.port}"
-        if gpu_list and (t != "ps" or ps_gpus):
+        if (t, i) in ordinals:
             # every GPU of the launcher's own visible set stays visible (a PS shard in one GPU's HBM is mapped by
             # the trainers on the others); the task's device is selected by its ordinal WITHIN that set, so
             # --gpus indexes the caller's HIP_VISIBLE_DEVICES (left untouched), never raw physical ids
-            e["DTF_DEVICE_ORDINAL"] = gpu_list[gi % len(gpu_list)]
-            gi += 1
+            e["DTF_DEVICE_ORDINAL"] = ordinals[(t, i)]
         else:
             e["HIP_VISIBLE_DEVICES"] = ""
             e["CUDA_VISIBLE_DEVICES"] = ""

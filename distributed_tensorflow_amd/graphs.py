@@ -47,8 +47,18 @@ SPLIT_DEFAULT = __import__("os").environ.get("DTF_GRAPH_SPLIT", "1") != "0"
 
 
 class CapturedStep:
-    def __init__(self, fn, warmup=2, optimizers=(), pool=None, split=None):
+    def __init__(self, fn, warmup=2, optimizers=(), pool=None, split=None, static_inputs=False, require_split=False):
         self.fn = fn
+        # require_split=True (multi-rank steps): capture only as per-stream graphs; when the step issues collectives
+        # the per-stream capture cannot order (torch.distributed process-group Work objects), run eagerly instead of
+        # capturing one multi-branch graph around them
+        self.require_split = bool(require_split)
+        self.eager = False
+        # static_inputs=True: the caller promises that a replay argument which is the same tensor object as last
+        # time, with an unchanged version counter, still holds the same values, so its copy into the static buffer is
+        # skipped. Off by default: writes through .data, DLPack, numpy views of pinned staging buffers or native
+        # kernels do not bump the version counter, and a skipped copy would then train on a stale batch.
+        self.static_inputs = bool(static_inputs)
         self.warmup = warmup
         self.optimizers = list(optimizers)
         self.pool = pool
@@ -58,10 +68,13 @@ class CapturedStep:
         self.calls = 0
         self.static_in = None
         self.out = None
-        self._errbuf = None
+        self._errq = []  # (pinned copy of the capture's error flag, event after the copy) per replay in flight
 
     def _capture(self, args):
         from .ops import _util
+        if self.require_split and not (self.split and _util.split_capture_ok()):
+            self.eager = True
+            return False
         flat = _flat(args, [])
         self.static_in = [t.clone() for t in flat]
         self._src = self._sources(flat)
@@ -84,6 +97,7 @@ class CapturedStep:
         for o in self.optimizers:
             o._host_iter -= 1
         _util.bump_weights_epoch()
+        return True
 
     def _capture_split(self, g, static_args):
         import gc
@@ -133,8 +147,34 @@ class CapturedStep:
             if e:
                 raise RuntimeError(f"hipGraph per-stream replay: cross-stream wait {e - 1} timed out")
 
+    ERR_DEPTH = 2  # replays the host may run ahead of the last error-flag check
+
+    def _post_err_check(self):
+        """Every replay copies the error flag to pinned memory behind an event; the copy of the replay ERR_DEPTH
+        calls back is waited for and checked here. A timed-out cross-stream wait therefore raises within ERR_DEPTH
+        replays (and the optimizer launches skipped their update since: ops.optim step_abort_ptr), while the host
+        still runs up to ERR_DEPTH steps ahead of the GPU."""
+        q = self._errq
+        if len(q) >= self.ERR_DEPTH:
+            buf, ev = q.pop(0)
+            ev.synchronize()
+            if int(buf[0]):
+                raise RuntimeError(f"hipGraph per-stream replay: cross-stream wait {int(buf[0]) - 1} timed out; the "
+                                   "step's optimizer update was skipped")
+        else:
+            buf, ev = torch.zeros(1, dtype=torch.int32).pin_memory(), torch.cuda.Event()
+        buf.copy_(self.sc.err, non_blocking=True)
+        ev.record()
+        q.append((buf, ev))
+
+    @property
+    def captured(self):
+        return self.graph is not None
+
     def __call__(self, args):
         self.calls += 1
+        if self.eager:
+            return self.fn(args)
         if self.graph is None:
             if self.calls <= self.warmup:
                 # warm up on a side stream (lazy inits, allocator pools) as graph capture requires
@@ -145,28 +185,25 @@ class CapturedStep:
                     r = self.fn(args)
                 cur.wait_stream(side)
                 return r
-            self._capture(args)
+            if not self._capture(args):
+                return self.fn(args)
         else:
             flat = _flat(args, [])
             for i, (s, t) in enumerate(zip(self.static_in, flat)):
                 # the very tensor whose contents the static buffer already holds (same object, no in-place write
                 # since: torch's version counter, shared by its views): no copy (e.g. a fixed benchmark batch)
-                src = self._src[i]
+                src = self._src[i] if self.static_inputs else None
                 if s.data_ptr() != t.data_ptr() and not (src is not None and src[0]() is t and t._version == src[1]):
                     s.copy_(t, non_blocking=True)
-            self._src = self._sources(flat)
+            if self.static_inputs:
+                self._src = self._sources(flat)
         # per-step scalars go to a pinned ring (Optimizer.graph_prestep): no host sync between replays
         for o in self.optimizers:
             o.graph_prestep()
         self.graph.replay()
         if self.sc is not None:
             self.sc.replay_others()
-            if self.calls % 256 == 0:  # a timed-out flag wait (never expected): checked without a host sync
-                if self._errbuf is not None and int(self._errbuf[0]):
-                    raise RuntimeError("hipGraph per-stream replay: a cross-stream wait timed out")
-                if self._errbuf is None:
-                    self._errbuf = torch.zeros(1, dtype=torch.int32).pin_memory()
-                self._errbuf.copy_(self.sc.err, non_blocking=True)
+            self._post_err_check()
         for o in self.optimizers:
             o.graph_poststep()
         from .ops import _util
@@ -179,10 +216,12 @@ class CapturedStep:
         self.graph = None
         self.sc = None
         self.calls = 0
+        self.eager = False
+        self._errq = []
 
 
-def function(fn=None, warmup=2, optimizers=(), split=None):
+def function(fn=None, warmup=2, optimizers=(), split=None, static_inputs=False):
     """Decorator: ``@dtf.function`` captures a (static-shape) step into hipGraphs after `warmup` calls."""
     def wrap(f):
-        return CapturedStep(f, warmup=warmup, optimizers=optimizers, split=split)
+        return CapturedStep(f, warmup=warmup, optimizers=optimizers, split=split, static_inputs=static_inputs)
     return wrap(fn) if fn is not None else wrap

@@ -282,20 +282,23 @@ class Model(Layer):
         return self._update_metrics(loss, y, y_pred)
 
     def make_train_function(self, force=False):
-        """The per-batch step fit() drives. With ``compile(jit_compile=True)`` on one GPU rank it is a
-        hipGraph-captured step (graphs.CapturedStep): eager warmup, one capture, then one graph launch
-        per step. Multi-rank capture of the RCCL bucket all-reduces is opt-in (DTF_GRAPH_DIST=1)."""
+        """The per-batch step fit() drives. With ``compile(jit_compile=True)`` on a GPU it is a hipGraph-captured
+        step (graphs.CapturedStep): eager warmup, one capture, then one graph launch per stream per step. A
+        multi-rank step is captured too when its gradient collectives run on the framework's RCCL communicator
+        (the per-stream capture puts them in the communication stream's graph); with torch.distributed
+        process-group collectives (CommunicationImplementation.RING, ZeRO-1) it stays eager. DTF_GRAPH_DIST=0
+        keeps every multi-rank step eager. In-process replicas are never captured."""
         if getattr(self, "_train_fn", None) is not None and not force:
             return self._train_fn
         strat = self.distribute_strategy
         fn = self.train_step
         dev = self._device()
-        multi = getattr(strat, "_world", 1) > 1 or bool(strat.inproc_replicas() if hasattr(
-            strat, "inproc_replicas") else None)
-        if getattr(self, "_jit", False) and dev.type == "cuda" and (
-                not multi or os.environ.get("DTF_GRAPH_DIST", "0") == "1"):
+        inproc = bool(strat.inproc_replicas() if hasattr(strat, "inproc_replicas") else None)
+        multi = getattr(strat, "_world", 1) > 1 or bool(getattr(strat, "_force", False))
+        if getattr(self, "_jit", False) and dev.type == "cuda" and not inproc and (
+                not multi or os.environ.get("DTF_GRAPH_DIST", "1") != "0"):
             from ..graphs import CapturedStep
-            fn = CapturedStep(self.train_step, warmup=2, optimizers=[self.optimizer])
+            fn = CapturedStep(self.train_step, warmup=2, optimizers=[self.optimizer], require_split=multi)
         self._graph_step = type(fn).__name__ == "CapturedStep"
         self._train_fn = fn
         return fn

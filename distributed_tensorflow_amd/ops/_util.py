@@ -273,7 +273,12 @@ def join_side_streams():
 # through stream_wait / SplitCapture.mark + wait_mark instead of torch's wait_stream / wait_event, which inside a
 # capture would merge the streams into one multi-branch graph.
 _SPLIT = None
-XS_TIMEOUT_MS = 20000
+# A join that waits on a stream holding cross-rank collectives waits as long as a peer may legitimately lag (rank 0
+# alone checkpointing or evaluating): the same bound as the P2P all-reduce (parallel/p2p.py). On a timeout the wait
+# sets SplitCapture.err; the captured optimizer launch reads that flag and applies nothing (step_abort_ptr), and the
+# executor raises at its next per-replay check (graphs.CapturedStep), so a late peer can never make a replica apply
+# an unreduced gradient.
+XS_TIMEOUT_MS = 300000
 _SPLIT_BLOCKERS = __import__("weakref").WeakSet()  # objects whose stream use the per-stream capture cannot express
 
 
@@ -415,6 +420,12 @@ class SplitCapture:
                 lib.dtf_event_destroy(ev)
             except Exception:
                 pass
+
+
+def step_abort_ptr():
+    """Device address of the running per-stream capture's error flag (None outside such a capture): kernels that
+    commit a step's result (the fused optimizer) skip their work when it is set."""
+    return ptr(_SPLIT.err) if _SPLIT is not None else None
 
 
 def set_split_capture(sc):

@@ -208,24 +208,26 @@ class _BNSource:
     gradient) lets the GEMM epilogue write sum(dz), sum(dz*(x-mean)) partial rows; the producing ConvBN's
     backward then skips its reduction pass (bn_bwd_reduce), provided the gradient it receives is exactly the
     tensor that dgrad wrote (same storage: autograd added nothing else to it)."""
-    __slots__ = ("yc", "mbits", "mean", "invstd", "gamma", "gamma_p", "beta_p", "consumers", "part", "rows", "dptr",
-                 "__weakref__")
+    __slots__ = ("yc", "mbits", "mean", "invstd", "gamma", "gamma_p", "beta_p", "consumers", "part", "rows", "dx",
+                 "ver", "__weakref__")
 
     def __init__(self, yc, mbits, mean, invstd=None, gamma=None, params=(None, None)):
         self.yc, self.mbits, self.mean = yc, mbits, mean
         self.invstd, self.gamma = invstd, gamma
         self.gamma_p, self.beta_p = params
         self.consumers = 0
-        self.part = self.rows = self.dptr = None
+        self.part = self.rows = self.dx = self.ver = None
 
     def provide(self, dx, part, rows):
-        self.part, self.rows, self.dptr = part, rows, dx.data_ptr()
+        # dx itself is held (not its address), with its version: see nn.same_unmodified
+        self.part, self.rows, self.dx, self.ver = part, rows, dx, dx._version
 
     def take(self, dout):
         """("partials", part, rows) for this gradient, or None (then the regular reduction runs)."""
-        part, rows, dptr = self.part, self.rows, self.dptr
-        self.part = self.rows = self.dptr = None
-        if dptr is None or dout.data_ptr() != dptr or not dout.is_contiguous():
+        from .nn import same_unmodified
+        part, rows, dx, ver = self.part, self.rows, self.dx, self.ver
+        self.part = self.rows = self.dx = self.ver = None
+        if not same_unmodified(dout, dx, ver):
             return None
         if part is None or rows < 1:
             return None

@@ -146,19 +146,27 @@ class DropSource:
     (norm.hip ln_bwd_kernel dfo): the mask parameters; the LayerNorm backward leaves df here and add_dropout's backward
     takes it when the gradient it receives is exactly the tensor that LayerNorm backward wrote (its only consumer, or
     the residual joined inside the LayerNorm backward) — otherwise it runs its own dropout pass."""
-    __slots__ = ("keep", "seed", "ctr", "df", "dptr", "__weakref__")
+    __slots__ = ("keep", "seed", "ctr", "df", "dx", "ver", "__weakref__")
 
     def __init__(self, keep, seed, ctr):
         self.keep, self.seed, self.ctr = keep, seed, ctr
-        self.df = self.dptr = None
+        self.df = self.dx = self.ver = None
 
     def provide(self, dx, df):
-        self.df, self.dptr = df, dx.data_ptr()
+        # hold dx itself (not only its address): a freed dx whose address a later gradient reuses can never match
+        self.df, self.dx, self.ver = df, dx, dx._version
 
     def take(self, dy):
-        df, dptr = self.df, self.dptr
-        self.df = self.dptr = None
-        return df if (df is not None and dy.data_ptr() == dptr and dy.is_contiguous()) else None
+        df, dx, ver = self.df, self.dx, self.ver
+        self.df = self.dx = self.ver = None
+        return df if (df is not None and same_unmodified(dy, dx, ver)) else None
+
+
+def same_unmodified(t, src, ver):
+    """t is (a view of) the very buffer `src` that a fused backward wrote, with no in-place write since (the version
+    counter is shared by all views of a storage: an autograd accumulation into it bumps it)."""
+    return (src is not None and t.data_ptr() == src.data_ptr() and t.shape == src.shape and t.is_contiguous()
+            and src._version == ver and t._version == ver)
 
 
 class _AddDropoutFn(torch.autograd.Function):

@@ -108,7 +108,7 @@ class GradientBucketer:
         self.p2p = None
         self.rccl = None  # the framework's own RCCL communicator (rccl.RcclCommunicator), else torch's process group
         self.paths = {"rccl": 0, "p2p": 0, "rccl_native": 0}
-        if collective and arena.grad.is_cuda and type(self) is GradientBucketer and dist.get_backend(group) == "nccl":
+        if collective and arena.grad.is_cuda and dist.get_backend(group) == "nccl":
             from . import rccl
             if rccl.wanted(implementation):
                 try:
@@ -156,6 +156,14 @@ class GradientBucketer:
         for h in self._handles:
             h.remove()
         self._handles = []
+
+    def close(self):
+        """Tear the bucketer down: hooks off and the native communicator released (a collective: every rank of the
+        group closes its bucketer at the same point, after the last step)."""
+        self.remove()
+        if self.rccl is not None:
+            self.rccl.destroy()
+            self.rccl = None
 
     def _on_grad(self, i):
         if not self.enabled:
@@ -253,7 +261,7 @@ class GradientBucketer:
             self._launch(self._next)
             self._next += 1
         ev0 = None
-        if self.timing and self.arena.grad.is_cuda:
+        if self.timing and self.arena.grad.is_cuda and not torch.cuda.is_current_stream_capturing():
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()  # backward compute is done here; what follows on this stream is waiting on RCCL
         if self._opt is not None:
@@ -346,8 +354,9 @@ class ShardedGradientBucketer(GradientBucketer):
         ctx = contextlib.nullcontext()
         g = self.arena.grad[lo:hi]
         if g.is_cuda:
-            from ..ops._util import collective_ctx
-            ctx = collective_ctx(g.device)
+            from ..ops._util import collective_ctx, comm_stream_ctx
+            # native communicator: stream-ordered on the communication stream (hipGraph-capturable, no Work)
+            ctx = comm_stream_ctx(g.device) if self.rccl is not None else collective_ctx(g.device)
         with ctx:
             inp = g
             if b in self._send:
@@ -357,8 +366,13 @@ class ShardedGradientBucketer(GradientBucketer):
                 else:
                     inp[:hi - lo].copy_(g)
             out = self._recv.get(b, self.sgrad[c:c + s])
-            self._works[b] = dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group,
-                                                        async_op=True)
+            if self.rccl is not None:
+                self.rccl.reduce_scatter(inp, out)
+                self.paths["rccl_native"] += 1
+            else:
+                self._works[b] = dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group,
+                                                            async_op=True)
+                self.paths["rccl"] += 1
 
     def finalize(self):
         if self.arena.grad.is_cuda:
@@ -368,12 +382,15 @@ class ShardedGradientBucketer(GradientBucketer):
             self._launch(self._next)
             self._next += 1
         ev0 = None
-        if self.timing and self.arena.grad.is_cuda:
+        if self.timing and self.arena.grad.is_cuda and not torch.cuda.is_current_stream_capturing():
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         for w in self._works:
             if w is not None:
                 w.wait()
+        if self.rccl is not None and self.arena.grad.is_cuda:
+            from ..ops._util import join_comm_stream
+            join_comm_stream(self.arena.grad.device)
         for b, r in self._recv.items():
             s, _, _, c = self.shards[b]
             _cast(r, self.sgrad[c:c + s])
@@ -396,6 +413,8 @@ class ShardedGradientBucketer(GradientBucketer):
 
     def _all_gather_(self, buf):
         """In-place all-gather of this rank's chunks of ``buf`` (an arena-shaped f32 buffer), bucket by bucket."""
+        if self.rccl is not None:
+            return self._all_gather_native(buf)
         works = []
         for b, (lo, hi) in enumerate(self.buckets):
             s, own_lo, own_hi, _ = self.shards[b]
@@ -415,6 +434,22 @@ class ShardedGradientBucketer(GradientBucketer):
             if b is not None:
                 lo, hi = self.buckets[b]
                 buf[lo:hi].copy_(self._gather[b][:hi - lo])
+
+    def _all_gather_native(self, buf):
+        """_all_gather_ on the framework's communicator, stream-ordered on the current stream."""
+        for b, (lo, hi) in enumerate(self.buckets):
+            s, own_lo, own_hi, _ = self.shards[b]
+            if (hi - lo) == s * self.world:
+                self.rccl.all_gather(buf[own_lo:own_lo + s], buf[lo:hi])  # in place: the input is our slice
+            else:
+                img = self._gather.get(b)
+                if img is None:
+                    img = self._gather[b] = torch.zeros(s * self.world, dtype=buf.dtype, device=buf.device)
+                mine = img[self.rank * s:(self.rank + 1) * s]
+                mine.zero_()
+                mine[:own_hi - own_lo].copy_(buf[own_lo:own_hi])
+                self.rccl.all_gather(mine, img)
+                buf[lo:hi].copy_(img[:hi - lo])
 
     def gather_params(self):
         """All-gather the updated f32 masters and refresh the bf16 compute copies."""

@@ -20,9 +20,11 @@ use it); SURVEY §1.2 "RCCL over xGMI", VERDICT r4 "an RCCL communicator owned b
 """
 from __future__ import annotations
 
+import atexit
+import collections
 import ctypes
-import itertools
 import os
+import weakref
 
 import torch
 
@@ -33,7 +35,16 @@ _DT = {torch.float32: 7, torch.bfloat16: 9, torch.float16: 6, torch.int32: 2, to
 _OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
 DEFAULT_MIN_CHANNELS = 8
 DEFAULT_MAX_CHANNELS = 16
-_SEQ = itertools.count()
+_SEQ = collections.Counter()   # communicators created so far per group (ranks tuple): the unique-id store key
+_LIVE = weakref.WeakSet()      # communicators to release at interpreter exit
+
+
+@atexit.register
+def _release_all():
+    # local teardown only (ncclCommAbort frees this rank's resources without waiting for peers): a finalize at exit
+    # could block on a peer that is already gone
+    for c in list(_LIVE):
+        c.destroy(abort=True)
 
 
 def available():
@@ -75,11 +86,16 @@ class RcclCommunicator:
         self.max_channels = int(max_channels if max_channels is not None else DEFAULT_MAX_CHANNELS)
         if 0 < self.max_channels < self.min_channels:
             raise ValueError(f"max_channels {self.max_channels} < min_channels {self.min_channels}")
-        seq = next(_SEQ)
+        # the store key names the group by its global ranks plus the number of communicators this process created for
+        # that group before (every member creates them in the same order): disjoint groups whose rank 0s publish at
+        # the same time can never read each other's id
+        ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(self.world))
+        seq = _SEQ[ranks]
+        _SEQ[ranks] += 1
         self.name = name or f"dtf{seq}"
         rt = _native.runtime()
         uid = ctypes.create_string_buffer(128)
-        key = f"dtf_rccl/{self.name}/{seq}/uid"
+        key = f"dtf_rccl/{'-'.join(map(str, ranks))}/{seq}/uid"
         store = dist.distributed_c10d._get_default_store()
         if self.rank == 0:
             _check(rt.dtfrt_rccl_unique_id(uid), "unique id")
@@ -92,8 +108,14 @@ class RcclCommunicator:
                                               self.name.encode(), ctypes.byref(err))
         if not self._h:
             _check(err.value or -1, "communicator init")
+        _LIVE.add(self)
         if self_check:
-            self._self_check()
+            self._self_check()  # a collective: every rank has read the id once it returns
+            if self.rank == 0:
+                try:
+                    store.delete_key(key)
+                except (RuntimeError, AttributeError):  # a store without deletion: the key only lingers
+                    pass
 
     def _self_check(self):
         t = torch.full((64,), float(self.rank + 1), device=self.device)
@@ -158,9 +180,18 @@ class RcclCommunicator:
         return int(_native.runtime().dtfrt_rccl_async_error(self._h))
 
     def destroy(self, abort=False):
+        """Release the communicator (abort=False: finalize = wait for its outstanding collectives, which needs the
+        peers alive; abort=True: local teardown). Idempotent."""
         h, self._h = getattr(self, "_h", None), None
+        _LIVE.discard(self)
         if h:
             _native.runtime().dtfrt_rccl_comm_destroy(h, int(bool(abort)))
+
+    def __del__(self):
+        try:
+            self.destroy(abort=True)
+        except Exception:
+            pass
 
 
 def wanted(implementation=None):

@@ -348,7 +348,8 @@ class MultiWorkerMirroredStrategy(Strategy):
         if not isinstance(b, collective.ShardedGradientBucketer):
             return Strategy.apply_gradients(self, optimizer, arena)
         optimizer.set_grad_scale(self.grad_scale())
-        optimizer.apply_segments(arena, b.segments(), reduce_sumsq=lambda t: dist.all_reduce(t))
+        red = (lambda t: b.rccl.all_reduce_(t)) if getattr(b, "rccl", None) is not None else (lambda t: dist.all_reduce(t))
+        optimizer.apply_segments(arena, b.segments(), reduce_sumsq=red)
         b.gather_params()
 
     def sync_optimizer_state(self, optimizer):
@@ -399,27 +400,63 @@ def _spawn_replicas(devices):
     """The parent side of MirroredStrategy(devices=[GPU...]): run this same program once per device, each copy a
     replica of a multi-process MirroredStrategy (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* for the process group,
     DTF_DEVICE_ORDINAL for its GPU), wait for them and exit with the worst status. The parent touches no GPU: the
-    children are started as plain subprocesses (no exec of the running program)."""
+    children are started as plain subprocesses (no exec of the running program).
+
+    Refused (ValueError / RuntimeError) when the program cannot be re-run as-is: ``python -c``, a host test runner
+    (pytest would re-run the whole session once per device), or a parent that already initialised HIP. The parent
+    polls all children: the first one to fail terminates its siblings (which would otherwise sit in rendezvous or
+    RCCL init until their timeout), and SIGINT / SIGTERM sent to the parent are forwarded to every child."""
+    import signal
     import socket
     import subprocess
     import sys
+    import time
     argv = list(getattr(sys, "orig_argv", []))[1:] or list(sys.argv)
     if not argv or argv[0] == "-c":
         raise ValueError("MirroredStrategy over several GPUs re-runs the program once per GPU: it needs a script or "
                          "module (python script.py / python -m module), not python -c")
+    if "pytest" in sys.modules:
+        raise ValueError("MirroredStrategy over several GPUs re-runs the program once per GPU; under a test runner "
+                         "that would re-run the whole session: start the replicas with cli.launch / torchrun instead")
+    if torch.cuda.is_initialized():
+        raise RuntimeError("MirroredStrategy over several GPUs must be constructed before the program touches a GPU: "
+                           "this process initialised HIP already, and it starts one child process per device")
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     procs = []
-    for r, d in enumerate(devices):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(len(devices)), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DTF_DEVICE_ORDINAL=str(d.index or 0))
-        env[_MIRRORED_CHILD] = "1"
-        procs.append(subprocess.Popen([sys.executable] + argv, env=env))
-    rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
+
+    def _forward(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+
+    prev = {sig: signal.signal(sig, _forward) for sig in (signal.SIGINT, signal.SIGTERM)}
+    try:
+        for r, d in enumerate(devices):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(len(devices)), LOCAL_RANK=str(r),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DTF_DEVICE_ORDINAL=str(d.index or 0))
+            env[_MIRRORED_CHILD] = "1"
+            procs.append(subprocess.Popen([sys.executable] + argv, env=env))
+        rc = 0
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0:
+                    rc = max(rc, abs(code))
+                    for q in live:  # a dead replica leaves its peers blocked in collectives: stop them
+                        q.terminate()
+            time.sleep(0.05)
+        for p in procs:
+            p.wait()
+    finally:
+        for sig, h in prev.items():
+            signal.signal(sig, h)
     raise SystemExit(rc)
 
 

@@ -16,7 +16,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sys.path.insert(0, ROOT)
     import bench
-    out = bench._allreduce_sweep(dist, torch.device("cpu"), world, sizes_mb=(1, 2), iters=2)
+    out = bench._allreduce_sweep(dist, torch.device("cpu"), world, [], sizes_mb=(1, 2), iters=2)
     q.put((rank, out))
     dist.destroy_process_group()
 
@@ -36,8 +36,10 @@ def test_allreduce_sweep_gloo_world2():
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    assert set(res[0]) == {"1MB", "2MB"} and res[0] == res[1]
-    assert all(v > 0 for v in res[0].values())
+    # no GPU communicator here: only the process-group row (the native rows need the nccl backend)
+    assert set(res[0]) == {"torch_process_group"} and res[0] == res[1]
+    pg = res[0]["torch_process_group"]
+    assert set(pg) == {"1MB", "2MB"} and all(v > 0 for v in pg.values())
 
 
 @pytest.mark.gpu
@@ -60,5 +62,6 @@ def test_bench_multirank_path_on_one_gpu(tmp_path):
     assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["process_group_backend"] == "gloo"
     assert out["replicas_identical"] is True
     assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "dp2"
-    assert isinstance(out["allreduce_busbw_GBps"], dict) and len(out["allreduce_busbw_GBps"]) == 6
+    sweep = out["allreduce_busbw_GBps"]
+    assert isinstance(sweep, dict) and len(sweep["torch_process_group"]) == 6
     assert out["value"] > 0 and out["steps"] == 2 and out["warmup"] == 1

@@ -164,7 +164,8 @@ def _worker_rccl1(port, jit, wire, q, zero=False, impl="AUTO"):
         losses = [float(fn((x, y))["loss"]) for x, y in _batches("gpt2", s.device, steps=5)]
         torch.cuda.synchronize()
         b = s._bucketers[id(m._arena)]
-        q.put((type(fn).__name__, [w.detach().float().cpu().numpy() for w in m.trainable_variables], losses,
+        kind = type(fn).__name__ + (":captured" if getattr(fn, "captured", False) else "")
+        q.put((kind, [w.detach().float().cpu().numpy() for w in m.trainable_variables], losses,
                len(b.buckets), dict(b.paths)))
         dist.destroy_process_group()
     except Exception:
@@ -172,12 +173,16 @@ def _worker_rccl1(port, jit, wire, q, zero=False, impl="AUTO"):
 
 
 @pytest.mark.parametrize("jit,wire,zero,impl", [(False, "f32", False, "AUTO"), (True, "f32", False, "AUTO"),
-                                                (False, "bf16", False, "AUTO"), (False, "f32", True, "AUTO"),
+                                                (False, "bf16", False, "AUTO"), (True, "bf16", False, "AUTO"),
+                                                (False, "f32", True, "AUTO"), (True, "f32", True, "AUTO"),
+                                                (False, "f32", True, "RING"),
                                                 (False, "f32", False, "RING"), (True, "f32", False, "RING")])
 def test_rccl_bucketer_world1_matches_single_process(cuda, jit, wire, zero, impl):
-    """zero=True: ZeRO-1 on RCCL (reduce_scatter_tensor into the compact shard gradient, segment-wise fused
-    AdamW, in-place all_gather_into_tensor of the masters, bf16 refresh). impl AUTO: the buckets go through the
-    framework's own RCCL communicator (parallel/rccl.py) on the communication stream; RING: torch's process group."""
+    """zero=True: ZeRO-1 on RCCL (reduce-scatter into the compact shard gradient, segment-wise fused AdamW, in-place
+    all-gather of the masters, bf16 refresh). impl AUTO: the buckets go through the framework's own RCCL communicator
+    (parallel/rccl.py) on the communication stream; RING: torch's process group. jit: the multi-rank step is captured
+    as per-stream hipGraphs when the collectives are the native communicator's (the default), and stays eager on
+    torch's process group."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker_rccl1, args=(_port(), jit, wire, q, zero, impl))
@@ -189,10 +194,10 @@ def test_rccl_bucketer_world1_matches_single_process(cuda, jit, wire, zero, impl
         if p.is_alive():
             p.kill()
     assert ws is not None, losses
-    assert nb > 3 and kind == ("CapturedStep" if jit else "method")
-    if not zero:  # which communicator carried the buckets
-        native = impl == "AUTO"
-        assert (paths["rccl_native"] > 0) == native and (paths["rccl"] > 0) == (not native), paths
+    want = "method" if not jit else ("CapturedStep:captured" if impl == "AUTO" else "CapturedStep")
+    assert nb > 3 and kind == want, kind
+    native = impl == "AUTO"  # which communicator carried the buckets
+    assert (paths["rccl_native"] > 0) == native and (paths["rccl"] > 0) == (not native), paths
     m = _gpt2(100)
     ref = [float(m.train_step((x, y))["loss"]) for x, y in _batches("gpt2", cuda, steps=5)]
     torch.cuda.synchronize()

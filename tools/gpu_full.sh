@@ -2,7 +2,7 @@
 # benches. Each step under its own time limit; stops at the first failure.
 set -o pipefail
 mkdir -p gpurun_out
-tag=${1:-r5}
+tag=${1:-r6}
 timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/${tag}_gputests.log 2>&1 || { tail -40 gpurun_out/${tag}_gputests.log; exit 1; }
 tail -n 3 gpurun_out/${tag}_gputests.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1 || { tail -20 gpurun_out/${tag}_smoke.log; exit 1; }

@@ -1,7 +1,7 @@
-# rocprofv3 kernel trace of one model's bench step (steady-state stats): bash tools/gpu_r5_prof.sh <model> <tag> [bench args]
+# rocprofv3 kernel trace of one model's bench step (steady-state stats): bash tools/gpu_prof.sh <model> <tag> [bench args]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-m=${1:-gpt2_medium}; tag=${2:-r5}; shift 2
+m=${1:-resnet50}; tag=${2:-r6}; shift 2
 mkdir -p gpurun_out/prof_$tag
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_$tag -o kt -- python3 -u bench.py --model $m --steps 6 --warmup 2 "$@" > gpurun_out/prof_$tag/bench.log 2>&1 || exit 1
 f=$(find gpurun_out/prof_$tag -name "*kernel_trace.csv" | head -1)
