@@ -93,6 +93,10 @@ _KERNEL_SIGS = {
     "dtf_colsum": [P, L, I, P, I, P, L, P],
     "dtf_embed_fwd": [P, P, P, P, P, P, P, L, I, I, P],
     "dtf_embed_bwd_sorted": [P, P, P, P, L, I, P],
+    "dtf_sort_keys": [P, L, I, P, P, P, L, P],
+    "dtf_gather_rows": [P, P, P, L, I, P],
+    "dtf_gather_cols": [P, I, L, L, P, L, P, P],
+    "dtf_gather_rows_bwd": [P, P, P, L, P, L, I, P],
     "dtf_embed_bwd_small": [P, P, P, L, I, I, I, P, L, P],
     "dtf_softmax_ce": [P, I, P, P, P, I, L, I, F, F, P],
     "dtf_softmax_fwd": [P, P, L, I, I, F, I, P, P],

@@ -132,7 +132,7 @@ class BertModel(Model):
         if mpos is not None:  # gather the masked positions only (BERT pretraining)
             B, S, Hd = h.shape
             idx = (mpos + torch.arange(B, device=mpos.device)[:, None] * S).reshape(-1)
-            h = h.reshape(B * S, Hd).index_select(0, idx).reshape(B, -1, Hd)
+            h = ops.gather_rows(h.reshape(B * S, Hd), idx).reshape(B, -1, Hd)
         return self.mlm_logits(h)
 
     def nsp_logits(self, h):

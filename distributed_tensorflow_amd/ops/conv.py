@@ -532,13 +532,24 @@ def _s2d_index(Cp, device):
     return _S2D_IDX[key]
 
 
+def _gather_cols(m, idx, ncols):
+    """out[:, j] = m[:, idx[j]] of a row-major 2-D matrix, 0 where idx[j] == m.shape[1] (sort.hip dtf_gather_cols on
+    the GPU: one launch, no zero-column concatenation)."""
+    rows, cols = m.shape
+    if on_gpu(m) and m.element_size() in (2, 4):
+        m = m.contiguous()
+        out = torch.empty((rows, ncols), dtype=m.dtype, device=m.device)
+        call("dtf_gather_cols", ptr(m), m.element_size(), rows, cols, ptr(idx), ncols, ptr(out), stream())
+        return out
+    return torch.cat([m, m.new_zeros(rows, 1)], 1).index_select(1, idx)
+
+
 def stem_s2d_filter(w):
     """[K, 7, 7, Cp] -> [K, 4, 4, 16]: the 7x7/2 pad-3 filter as a 4x4/1 filter over image_to_s2d_bf16 output."""
     K, R, S, Cp = w.shape
     assert (R, S) == (7, 7)
     fwd, _ = _s2d_index(Cp, w.device)
-    wz = torch.cat([w.reshape(K, -1), w.new_zeros(K, 1)], 1)
-    return wz.index_select(1, fwd).reshape(K, 4, 4, 16).contiguous()
+    return _gather_cols(w.reshape(K, -1), fwd, fwd.numel()).reshape(K, 4, 4, 16)
 
 
 def stem_s2d_filter_grad(dw2, shape):
@@ -546,8 +557,7 @@ def stem_s2d_filter_grad(dw2, shape):
     colour channels c >= 4 get zero)."""
     K, R, S, Cp = shape
     _, back = _s2d_index(Cp, dw2.device)
-    dz = torch.cat([dw2.reshape(K, -1), dw2.new_zeros(K, 1)], 1)
-    return dz.index_select(1, back).reshape(K, R, S, Cp)
+    return _gather_cols(dw2.reshape(K, -1), back, back.numel()).reshape(K, R, S, Cp)
 
 
 def image_to_s2d_bf16(x_nchw):

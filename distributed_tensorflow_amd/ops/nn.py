@@ -266,6 +266,57 @@ class _AddFn(torch.autograd.Function):
         return dy, dy
 
 
+# ------------------------------------------------------------------ sort / indexed rows
+def sort_keys(keys, key_bits=None):
+    """(sorted keys, permutation) of a 1-D int64 tensor of non-negative keys < 2^key_bits — a stable sort: equal keys
+    keep their input order (csrc/kernels/sort.hip radix sort on GPU; torch.sort(stable=True) on the CPU)."""
+    keys = keys.reshape(-1).long().contiguous()
+    if not on_gpu(keys):
+        return torch.sort(keys, stable=True)
+    n = keys.numel()
+    if key_bits is None:
+        raise ValueError("sort_keys on the GPU needs key_bits (the key range), read from no device value")
+    sk = torch.empty_like(keys)
+    perm = torch.empty_like(keys)
+    ws_bytes = 2 * n * 8 + 256 * ((n + 1023) // 1024) * 4 + 64
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=keys.device)
+    call("dtf_sort_keys", ptr(keys), n, int(key_bits), ptr(sk), ptr(perm), ptr(ws), ws_bytes, stream())
+    return sk, perm
+
+
+def _bits(n):
+    return max(1, int(n - 1).bit_length())
+
+
+class _GatherRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, idx):
+        src, idx = src.contiguous(), idx.reshape(-1).long().contiguous()
+        R, D = src.shape
+        out = torch.empty((idx.numel(), D), dtype=src.dtype, device=src.device)
+        call("dtf_gather_rows", ptr(src), ptr(idx), ptr(out), idx.numel(), D, stream())
+        ctx.save_for_backward(idx)
+        ctx.R = R
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, = ctx.saved_tensors
+        dy = dy.to(BF16).contiguous()
+        sidx, perm = sort_keys(idx, _bits(ctx.R))
+        ds = torch.empty((ctx.R, dy.shape[1]), dtype=BF16, device=dy.device)
+        call("dtf_gather_rows_bwd", ptr(dy), ptr(sidx), ptr(perm), idx.numel(), ptr(ds), ctx.R, dy.shape[1], stream())
+        return ds, None
+
+
+def gather_rows(src, idx):
+    """src[idx] for a 2-D bf16 src and 1-D row indices (the masked-LM gather); its gradient sums the rows gathered
+    more than once in a fixed order and writes zeros elsewhere (deterministic, no fill pass, no atomics)."""
+    if on_gpu(src) and src.dtype == BF16 and src.dim() == 2 and src.shape[1] % 8 == 0:
+        return _GatherRowsFn.apply(src, idx)
+    return src.index_select(0, idx.reshape(-1).long())
+
+
 # ------------------------------------------------------------------ embeddings
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
@@ -301,7 +352,7 @@ class _EmbedFn(torch.autograd.Function):
         direct = [direct_grad(t) for t in tables]
         # word table: sort the ids once, then one deterministic segment-sum per distinct id (no atomics)
         dt = direct[0] if direct[0] is not None else torch.zeros(tshape, dtype=F32, device=dy.device)
-        sid, perm = torch.sort(ids.reshape(-1))
+        sid, perm = sort_keys(ids, _bits(tshape[0]))
         call("dtf_embed_bwd_sorted", ptr(dy), ptr(sid), ptr(perm), ptr(dt), T, D, stream())
         dp = dy_ = None
         if pshape is not None:  # positions: dp[s] = sum over the batch of dy[b, s]  (a column sum)
@@ -316,7 +367,7 @@ class _EmbedFn(torch.autograd.Function):
                 call("dtf_embed_bwd_small", ptr(dy), ptr(tid), ptr(dy_), T, D, yshape[0], acc, ptr(ws), ws.numel(),
                      stream())
             elif tid is not None:
-                sid2, perm2 = torch.sort(tid.reshape(-1))
+                sid2, perm2 = sort_keys(tid, _bits(yshape[0]))
                 call("dtf_embed_bwd_sorted", ptr(dy), ptr(sid2), ptr(perm2), ptr(dy_), T, D, stream())
             else:  # no type ids: every token uses row 0
                 call("dtf_colsum", ptr(dy), T, D, ptr(dy_), acc, ptr(ws), ws.numel(), stream())

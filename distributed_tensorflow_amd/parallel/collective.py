@@ -320,8 +320,8 @@ class ShardedGradientBucketer(GradientBucketer):
     SURVEY §2.6 "Reduce-scatter / all-gather (ZeRO-1, optional)".
     """
 
-    def __init__(self, arena, group=None, bucket_mb=None, wire_dtype=None):
-        super().__init__(arena, group=group, bucket_mb=bucket_mb, wire_dtype=wire_dtype)
+    def __init__(self, arena, group=None, bucket_mb=None, wire_dtype=None, implementation=None):
+        super().__init__(arena, group=group, bucket_mb=bucket_mb, wire_dtype=wire_dtype, implementation=implementation)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.shards = []   # per bucket: (chunk s, own_lo, own_hi, compact offset)

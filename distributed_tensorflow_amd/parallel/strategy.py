@@ -313,7 +313,8 @@ class MultiWorkerMirroredStrategy(Strategy):
         bump_weights_epoch()
         if self.shard_optimizer:
             b = collective.ShardedGradientBucketer(arena, bucket_mb=self.bucket_mb,
-                                                   wire_dtype=getattr(self, "wire_dtype", None)).install()
+                                                   wire_dtype=getattr(self, "wire_dtype", None),
+                                                   implementation=getattr(self, "implementation", None)).install()
         elif arena.grad.device.type == "cpu" and os.environ.get("DTF_CPU_ALLREDUCE", "shm") == "shm":
             # one node, CPU arenas: shared-memory reduce-scatter/all-gather instead of gloo TCP
             name = f"ar{os.environ.get('MASTER_PORT', '0')}_{len(self._bucketers)}"
