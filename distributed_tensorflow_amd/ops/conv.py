@@ -544,12 +544,33 @@ def _gather_cols(m, idx, ncols):
     return torch.cat([m, m.new_zeros(rows, 1)], 1).index_select(1, idx)
 
 
-def stem_s2d_filter(w):
-    """[K, 7, 7, Cp] -> [K, 4, 4, 16]: the 7x7/2 pad-3 filter as a 4x4/1 filter over image_to_s2d_bf16 output."""
+class _S2DFilterFn(torch.autograd.Function):
+    """stem_s2d_filter as an autograd node (the native column gather has no autograd of its own): the backward is the
+    inverse gather stem_s2d_filter_grad. Used where the s2d filter feeds an autograd conv (the frozen-BN stem path)."""
+
+    @staticmethod
+    def forward(ctx, w):
+        ctx.shape = tuple(w.shape)
+        return _s2d_filter_raw(w)
+
+    @staticmethod
+    def backward(ctx, g):
+        return stem_s2d_filter_grad(g.contiguous(), ctx.shape)
+
+
+def _s2d_filter_raw(w):
     K, R, S, Cp = w.shape
     assert (R, S) == (7, 7)
     fwd, _ = _s2d_index(Cp, w.device)
     return _gather_cols(w.reshape(K, -1), fwd, fwd.numel()).reshape(K, 4, 4, 16)
+
+
+def stem_s2d_filter(w):
+    """[K, 7, 7, Cp] -> [K, 4, 4, 16]: the 7x7/2 pad-3 filter as a 4x4/1 filter over image_to_s2d_bf16 output
+    (differentiable: gradients flow back to the 7x7 filter)."""
+    if torch.is_grad_enabled() and w.requires_grad:
+        return _S2DFilterFn.apply(w)
+    return _s2d_filter_raw(w)
 
 
 def stem_s2d_filter_grad(dw2, shape):
