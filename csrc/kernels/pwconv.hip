@@ -13,6 +13,13 @@
 //    unconditionally — rows past M go to an out-of-range buffer offset — so the count is exact);
 //  * the epilogue stores bf16 straight from the accumulators and keeps the BN sum / sum-of-squares of the
 //    stored (bf16) values in registers across ALL of the block's tiles: one partial row per block (<= 256 rows).
+// Two-pass ConvBN forward (MODE 1 then MODE 2, dtf_conv_bn_apply_fwd): the layer writes 4x the bytes it reads, so
+// recomputing the product is cheaper than storing it and reading it back for the BatchNorm apply. MODE 1 keeps only
+// the statistics (no stores); after the finalize, MODE 2 recomputes the same tiles (bitwise the same bf16 values:
+// same MFMA sequence) and its epilogue applies the BatchNorm, adds the residual (optionally itself a deferred
+// BatchNorm: res * rscale + rshift), applies the ReLU and stores the block output with its 1-bit ReLU mask (and the
+// conv output yc only when the backward still needs it) — the standalone apply pass (read yc + res, write out) and
+// the yc write/read disappear (ResNet-50 bottleneck c3: 17 -> 14 activation-widths of traffic, 10 without yc).
 // Reference op: the Conv2D + FusedBatchNorm pair of the model trainer/task.py:62-71 builds.
 #include "gemm_core.h"
 
@@ -25,13 +32,22 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 struct PwArgs {
   const bf16_t* X;  // [M][C] activations
   const bf16_t* W;  // [K][C] filters
-  bf16_t* Y;        // [M][K]
+  bf16_t* Y;        // [M][K] (MODE 2: optional conv output)
   float* stats;     // [nslots][2K] partial rows (sum | sum of squares)
   int M, K;
   int tiles_m, tiles_n, nslots;
+  // MODE 2 (BatchNorm apply epilogue): out = [relu](yc * scale + shift [+ res | + res * rscale + rshift])
+  const float* scale;
+  const float* shift;
+  const bf16_t* res;
+  const float* rscale;
+  const float* rshift;
+  bf16_t* out;
+  uint8_t* mbits;  // 1-bit ReLU mask of out (relu only)
+  int relu;
 };
 
-template <int C, int WMW, bool STG = false>
+template <int C, int WMW, bool STG = false, int MODE = 0>
 struct PwGeo {
   static constexpr int NTH = 256 * WMW;        // 4 column waves x WMW row waves
   static constexpr int BM = 64 * WMW;          // rows per tile (64 per row wave)
@@ -47,11 +63,15 @@ struct PwGeo {
   static constexpr int ST = STG ? BM * 32 / NTH : 16;
   static constexpr int SROW = 256 + 8;         // staged row (bf16 elements): 16-B pad
   static constexpr int SMEM = NBUF * IMG + (STG ? BM * SROW * 2 : 0);
+  // vector-memory ops per thread per tile after the DMA: MODE 0 the stores, MODE 1 none, MODE 2 the out (+ yc)
+  // stores and the mask bytes (counted for the vmcnt waits; the yc stores only when requested: see SW)
+  static constexpr int STM = MODE == 1 ? 0 : ST;
 };
 
-template <int C, int WMW, bool STG>
+template <int C, int WMW, bool STG, int MODE>
 __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
-  using G = PwGeo<C, WMW, STG>;
+  static_assert(MODE != 2 || STG, "the apply epilogue works on the LDS-staged tile");
+  using G = PwGeo<C, WMW, STG, MODE>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wn = wave & 3, wm = wave >> 2;
@@ -102,16 +122,64 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) cs[j][r] = cq[j][r] = 0.f;
 
+  // MODE 2: this thread's 8-channel chunk of the tile row is fixed (NTH % 32 == 0): its BN coefficients live in
+  // registers for the whole kernel
+  const int ch = t & 31;
+  const int nch = tile_n * 256 + ch * 8;
+  float bsc[8], bsh[8], rsc[8], rsh[8];
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.res, (short)0, (MODE == 2 && a.res) ? (int)((long)a.M * a.K * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.out, (short)0, MODE == 2 ? (int)((long)a.M * a.K * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.mbits, (short)0, (MODE == 2 && a.mbits) ? (int)((long)a.M * a.K / 8) : 0, 0x00020000);
+  if constexpr (MODE == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bsc[j] = a.scale[nch + j];
+      bsh[j] = a.shift[nch + j];
+      rsc[j] = a.rscale ? a.rscale[nch + j] : 1.f;
+      rsh[j] = a.rscale ? a.rshift[nch + j] : 0.f;
+    }
+  }
+
   for (int it = 0; it < n_mine; ++it) {
-    // tile `it` landed: the ops this thread issued after it are tile it+1's DMA (if any) and tile it-1's stores
-    if (it + 1 < n_mine) {
-      if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD + G::ST) : "memory");
+    // tile `it` landed. MODE 0: the ops this thread issued after it are tile it+1's DMA (if any) and tile it-1's
+    // stores. MODE 1: only tile it+1's DMA. MODE 2: tile `it` is older than tile it-1's residual loads, which
+    // iteration it-1 waited for — only the first tile needs a wait here.
+    if constexpr (MODE == 0) {
+      if (it + 1 < n_mine) {
+        if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD + G::ST) : "memory");
+      } else {
+        if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::ST) : "memory");
+      }
+    } else if constexpr (MODE == 1) {
+      if (it + 1 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-      if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::ST) : "memory");
+      if (it == 0) {
+        if (n_mine > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     __syncthreads();  // every wave's DMA share landed; every wave is done with the buffer tile it+2 reuses
+    const int mt = first + it * step;
+    // MODE 2: this tile's residual chunks, in flight under the MFMAs (issued before tile it+2's DMA, so waiting for
+    // them leaves that DMA in flight)
+    uint4 rv[G::ST];
+    if constexpr (MODE == 2) {
+      if (a.res) {
+#pragma unroll
+        for (int k = 0; k < G::ST; ++k) {
+          const int row = (t + k * G::NTH) >> 5;
+          const int m = mt * G::BM + row;
+          const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)nch) * 2u : 0x80000000u;
+          rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+        }
+      }
+    }
     if (it + 2 < n_mine) issue(first + (it + 2) * step, (it + 2) % G::NBUF);
     const char* img = smem + (it % G::NBUF) * G::IMG;
 
@@ -137,7 +205,6 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
     // ---- epilogue: bf16 stores straight from the accumulators (lane: row (lane&15), 4 consecutive columns), or
     // (STG) through an LDS stage as 16-B row-contiguous chunks; rows past M store to an out-of-range offset (dropped
     // by the range check) so every thread issues ST stores
-    const int mt = first + it * step;
     char* stg = smem + G::NBUF * G::IMG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -149,22 +216,26 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
         o.x = pack2bf(acc[i][j][0], acc[i][j][1]);
         o.y = pack2bf(acc[i][j][2], acc[i][j][3]);
         if constexpr (STG) {
-          const int ml = wm * 64 + 16 * i + (lane & 15), nl = wn * 64 + 16 * j + 4 * (lane >> 4);
-          *reinterpret_cast<uint2*>(stg + (ml * G::SROW + nl) * 2) = o;
-        } else {
+          if constexpr (MODE != 1) {
+            const int ml = wm * 64 + 16 * i + (lane & 15), nl = wn * 64 + 16 * j + 4 * (lane >> 4);
+            *reinterpret_cast<uint2*>(stg + (ml * G::SROW + nl) * 2) = o;
+          }
+        } else if constexpr (MODE != 1) {
           const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)n) * 2u : 0x80000000u;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, o), yr, off, 0, 0);
         }
-        // statistics of the stored values (rows past M hold exact zeros: they add nothing)
-        const float v0 = __uint_as_float(o.x << 16), v1 = __uint_as_float(o.x & 0xffff0000u);
-        const float v2 = __uint_as_float(o.y << 16), v3 = __uint_as_float(o.y & 0xffff0000u);
-        cs[j][0] += v0; cq[j][0] = fmaf(v0, v0, cq[j][0]);
-        cs[j][1] += v1; cq[j][1] = fmaf(v1, v1, cq[j][1]);
-        cs[j][2] += v2; cq[j][2] = fmaf(v2, v2, cq[j][2]);
-        cs[j][3] += v3; cq[j][3] = fmaf(v3, v3, cq[j][3]);
+        if constexpr (MODE != 2) {
+          // statistics of the stored values (rows past M hold exact zeros: they add nothing)
+          const float v0 = __uint_as_float(o.x << 16), v1 = __uint_as_float(o.x & 0xffff0000u);
+          const float v2 = __uint_as_float(o.y << 16), v3 = __uint_as_float(o.y & 0xffff0000u);
+          cs[j][0] += v0; cq[j][0] = fmaf(v0, v0, cq[j][0]);
+          cs[j][1] += v1; cq[j][1] = fmaf(v1, v1, cq[j][1]);
+          cs[j][2] += v2; cq[j][2] = fmaf(v2, v2, cq[j][2]);
+          cs[j][3] += v3; cq[j][3] = fmaf(v3, v3, cq[j][3]);
+        }
       }
     }
-    if constexpr (STG) {
+    if constexpr (STG && MODE == 0) {
       __syncthreads();  // the tile is staged (the next tile's staging writes come after the next top barrier)
 #pragma unroll
       for (int k = 0; k < G::ST; ++k) {
@@ -176,7 +247,50 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), yr, off, 0, 0);
       }
     }
+    if constexpr (MODE == 2) {
+      __syncthreads();  // the tile is staged
+      // the residual chunks are in: everything but tile it+2's DMA (issued after them) has completed
+      if (it + 2 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) {
+        const int row = (t + k * G::NTH) >> 5;
+        const int m = mt * G::BM + row;
+        const uint4 yv = *reinterpret_cast<const uint4*>(stg + (row * G::SROW + ch * 8) * 2);
+        const uint32_t e = (uint32_t)m * (uint32_t)a.K + (uint32_t)nch;  // element index (valid rows)
+        const uint32_t off = m < a.M ? e * 2u : 0x80000000u;
+        if (a.Y) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, yv), yr, off, 0, 0);
+        // bn_apply_row's arithmetic, operation for operation (bitwise the same block output)
+        const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+        const uint32_t rw[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+        float o[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = 2 * q + h;
+            const float f = __uint_as_float(h ? (yw[q] & 0xffff0000u) : (yw[q] << 16));
+            float v = fmaf(f, bsc[j], bsh[j]);
+            if (a.res) {
+              const float r = __uint_as_float(h ? (rw[q] & 0xffff0000u) : (rw[q] << 16));
+              v += a.rscale ? fmaf(r, rsc[j], rsh[j]) : r;
+            }
+            if (a.relu) v = fmaxf(v, 0.f);
+            o[j] = v;
+          }
+        const uint4 ov = make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]),
+                                    pack2bf(o[6], o[7]));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, ov), orr, off, 0, 0);
+        if (a.mbits) {
+          uint32_t bits = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bits |= (uint32_t)(f2bf(o[j]) != 0 && o[j] > 0.f) << j;
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, mr, m < a.M ? e >> 3 : 0x80000000u, 0, 0);
+        }
+      }
+    }
   }
+  if constexpr (MODE == 2) return;  // (no statistics)
 
   // ---- one partial row per block: the 16 row lanes by DPP, the WMW row waves through LDS (fixed order)
   __syncthreads();  // the ring is free (every wave's last tile is multiplied)
@@ -203,9 +317,41 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
   }
 }
 
-template <int C, int WMW, bool STG = false>
+template <int C, int WMW, bool STG, int MODE>
 void launch_pw(const PwArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((pw_conv_kernel<C, WMW, STG>), dim3(grid), dim3(256 * WMW), 0, st, a);
+  hipLaunchKernelGGL((pw_conv_kernel<C, WMW, STG, MODE>), dim3(grid), dim3(256 * WMW), 0, st, a);
+}
+
+template <int MODE>
+void launch_pw_c(const PwArgs& a, int C, int grid, hipStream_t st) {
+  if (C == 64) launch_pw<64, 2, true, MODE>(a, grid, st);
+  else if (C == 128) launch_pw<128, 1, true, MODE>(a, grid, st);
+  else launch_pw<256, 1, true, MODE>(a, grid, st);
+}
+
+// grid / row-slot plan shared by every mode (the same tile -> block assignment in both passes of the two-pass form)
+bool pw_plan(PwArgs& a, long M, int C, int K, int& grid) {
+  if (!(C == 64 || C == 128 || C == 256) || (K % 256)) return false;
+  const int tiles_n = K / 256;
+  if (tiles_n != 1 && tiles_n != 2 && tiles_n != 4 && tiles_n != 8) return false;
+  if (M * C * 2 >= (1l << 31) || M * K * 2 >= (1l << 31)) return false;
+  // C 128 / 256: one row wave per block (the 128-VGPR filter slice; for C 128 the 3-deep ring plus the LDS store
+  // stage of a 128-row tile would exceed the LDS); C 64: two row waves per block. Every tile is stored through an
+  // LDS stage as row-contiguous 16-B chunks. (Measured alternatives, removed: several one-row-wave blocks per CU
+  // for C 64, direct fragment stores: profiles/r4_pointwise_conv_bw_probe.txt, r4_negative_results.txt.)
+  const int wmw = C == 64 ? 2 : 1;
+  const int bm = 64 * wmw;
+  a.M = (int)M; a.K = K;
+  a.tiles_m = (int)((M + bm - 1) / bm);
+  a.tiles_n = tiles_n;
+  if (a.tiles_m < 8) return false;
+  // one block per CU (or bpc); fewer when there are fewer tiles (grid stays a multiple of 8 * tiles_n, and the
+  // partial rows (one per row slot) never outnumber the M-tiles: the caller's scratch holds ceil(M/64) rows)
+  grid = 256;
+  while (grid > 8 * tiles_n && grid / tiles_n > a.tiles_m) grid /= 2;
+  a.nslots = grid / tiles_n;
+  if (a.nslots > a.tiles_m && a.nslots > 8) return false;
+  return true;
 }
 
 }  // namespace
@@ -214,37 +360,56 @@ void launch_pw(const PwArgs& a, int grid, hipStream_t st) {
 // K a multiple of 256 with K/256 in {1, 2, 4, 8}. Returns the number of partial rows written (> 0) or 0 when the
 // shape is not handled (the caller uses the general kernel).
 int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int C, int K, hipStream_t st) {
-  if (!(C == 64 || C == 128 || C == 256) || (K % 256) || !stats) return 0;
-  const int tiles_n = K / 256;
-  if (tiles_n != 1 && tiles_n != 2 && tiles_n != 4 && tiles_n != 8) return 0;
-  if (M * C * 2 >= (1l << 31) || M * K * 2 >= (1l << 31)) return 0;
+  if (!stats) return 0;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 15)) return 0;
-  // C 128 / 256: one row wave per block (the 128-VGPR filter slice; for C 128 the 3-deep ring plus the LDS store
-  // stage of a 128-row tile would exceed the LDS); C 64: two row waves per block. Every tile is stored through an
-  // LDS stage as row-contiguous 16-B chunks. (Measured alternatives, removed: several one-row-wave blocks per CU
-  // for C 64, direct fragment stores: profiles/r4_pointwise_conv_bw_probe.txt, r4_negative_results.txt.)
-  const int wmw = C == 64 ? 2 : 1;
-  const int bm = 64 * wmw;
   PwArgs a{};
+  int grid = 0;
+  if (!pw_plan(a, M, C, K, grid)) return 0;
   a.X = (const bf16_t*)X; a.W = (const bf16_t*)W; a.Y = (bf16_t*)Y; a.stats = stats;
-  a.M = (int)M; a.K = K;
-  a.tiles_m = (int)((M + bm - 1) / bm);
-  a.tiles_n = tiles_n;
-  if (a.tiles_m < 8) return 0;
-  // one block per CU (or bpc); fewer when there are fewer tiles (grid stays a multiple of 8 * tiles_n, and the
-  // partial rows (one per row slot) never outnumber the M-tiles: the caller's scratch holds ceil(M/64) rows)
-  int grid = 256;
-  while (grid > 8 * tiles_n && grid / tiles_n > a.tiles_m) grid /= 2;
-  a.nslots = grid / tiles_n;
-  if (a.nslots > a.tiles_m && a.nslots > 8) return 0;
-  if (C == 64) launch_pw<64, 2, true>(a, grid, st);
-  else if (C == 128) launch_pw<128, 1, true>(a, grid, st);
-  else launch_pw<256, 1, true>(a, grid, st);
+  launch_pw_c<0>(a, C, grid, st);
   return hipGetLastError() == hipSuccess ? a.nslots : 0;
 }
 
-
 }  // namespace dtf
+
+DTF_API int dtf_bn_finalize(float* part, int T, const float* gamma, const float* beta, float* running_mean,
+                            float* running_var, long M, int C, float momentum, float eps, float* scale,
+                            float* shift, float* mean_out, float* invstd_out, void* stream);  // norm.hip
+
+// Two-pass training ConvBN forward of a channel-expanding 1x1 conv (see the MODE notes at the top):
+//   pass 1: statistics of yc = X W^T (nothing stored) -> part;  finalize -> scale/shift/mean/invstd + running stats;
+//   pass 2: out = [relu](yc * scale + shift [+ res | + res * rscale + rshift]) with its ReLU mask mbits (relu only),
+//           and yc itself only when Y != nullptr.
+// part: >= ceil(M/64) * 2K floats of scratch. Returns 0, or -1 when the shape is not handled (nothing launched).
+DTF_API int dtf_conv_bn_apply_fwd(const void* X, const void* W, void* Y, void* out, void* mbits, const void* res,
+                                  const float* rscale, const float* rshift, long M, int C, int K, int relu,
+                                  float* part, const float* gamma, const float* beta, float* rmean, float* rvar,
+                                  float momentum, float eps, float* scale, float* shift, float* mean, float* invstd,
+                                  void* stream) {
+  using namespace dtf;
+  hipStream_t st = (hipStream_t)stream;
+  if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 15) || ((uintptr_t)out & 15) ||
+      ((uintptr_t)res & 15) || !out || !part || ((rscale == nullptr) != (rshift == nullptr)))
+    return -1;
+  PwArgs a{};
+  int grid = 0;
+  if (!pw_plan(a, M, C, K, grid)) return -1;
+  a.X = (const bf16_t*)X; a.W = (const bf16_t*)W; a.stats = part;
+  launch_pw_c<1>(a, C, grid, st);
+  int rc = dtf_bn_finalize(part, a.nslots, gamma, beta, rmean, rvar, M, K, momentum, eps, scale, shift, mean, invstd,
+                           stream);
+  if (rc) return rc;
+  a.Y = (bf16_t*)Y;
+  a.scale = scale; a.shift = shift;
+  a.res = (const bf16_t*)res;
+  a.rscale = res ? rscale : nullptr;
+  a.rshift = res ? rshift : nullptr;
+  a.out = (bf16_t*)out;
+  a.mbits = relu ? (uint8_t*)mbits : nullptr;
+  a.relu = relu;
+  launch_pw_c<2>(a, C, grid, st);
+  return (int)hipGetLastError();
+}
 
 // Test / tuning entry: the pointwise forward on its own (stats: [nslots][2K] floats, nslots <= ceil(M/64)).
 DTF_API int dtf_pwconv_fwd(const void* X, const void* W, void* Y, float* stats, int* rows, long M, int C, int K,
