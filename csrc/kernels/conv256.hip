@@ -322,7 +322,6 @@ bool conv256_on() { return true; }
 // large enough to fill the chip with 1-block/CU tiles (at least ~256 blocks). bn: 64 or 128 (0: by N).
 // Returns 0 if launched, 1 if not eligible (the caller falls back to gemm_core's kernels).
 int conv256_try(GemmArgs& a, int amode, int bmode, int cfg, hipStream_t st, bool force) {
-  if (a.cat) return 1;  // (concatenated A operands: gemm_core.h / gemm_w4.hip only)
   if ((!conv256_on() && !force) || a.atomic_out) return 1;
   // pointwise convolutions (K-contiguous x K-contiguous) stay on gemm_core.h's LDS-DMA tiles: measured slower here
   // on every ResNet-50 1x1 layer it was eligible for (fwd 49.5 vs 43 us stage-3 c1, 96-101 vs 71-73 us stage-4

@@ -1031,70 +1031,3 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   dtf_sum_rows(ws, mn, splitk, mn, dW, accumulate, st);
   return (int)hipGetLastError();
 }
-
-// ---- linear BatchNorm backward of a 1x1 conv (ops.conv _lbb) -------------------------------------------------------
-// With yc = X W^T (X [M][C] the conv input, W [K][C]) the BN backward dyc = a*dz + b*yc + c (per output channel) never
-// needs yc or dyc: dX = dyc W = [dz | X] . [diag(a) W ; W^T diag(b) W] + c^T W and dW = dyc^T X = diag(a) (dz^T X) +
-// diag(b) W (X^T X) + c (1^T X), the BN reduction sum dz*yc = rowdot(W, dz^T X). Two GEMMs over the concatenated
-// operand [dz | X] (GemmArgs::cat) replace the BN apply pass and its reads of yc.
-
-// dX[M][C] = [dZ | X] . Bd^T + bias (Bd [C][K + C] bf16), with the BN-backward statistics of dX for the BatchNorm
-// whose output X is (bnx = its input, bnmask, bnmean -> bnpart rows [tiles][2C], *bnrows), on the LDS-DMA tiles.
-DTF_API int dtf_conv1x1_dgrad_cat(const void* dZ, const void* X, const void* Bd, const float* bias, void* dX, long M,
-                                  int K, int C, const void* bnx, const void* bnmask, const float* bnmean, float* bnpart,
-                                  int* bnrows, void* stream) {
-  if ((K & 63) || (C & 63) || M * (long)K * 2 >= (1l << 31) || M * (long)C * 2 >= (1l << 31)) return -1;
-  if (bnx && (!bnpart || !bnmean || !bnrows)) return -9;
-  GemmArgs a{};
-  a.A = (const bf16_t*)dZ; a.lda = K;
-  a.A2 = (const bf16_t*)X; a.lda2 = C; a.K1 = K; a.cat = 1;
-  a.B = (const bf16_t*)Bd; a.ldb = K + C;
-  a.C = dX; a.ldc = C; a.bias = bias;
-  a.M = (int)M; a.N = C; a.K = K + C;
-  a.batch = 1; a.splitk = 1; a.kchunk = K + C; a.alpha = 1.f; a.beta = 0.f;
-  if (bnx) {
-    a.stats = bnpart;
-    a.bnx = (const bf16_t*)bnx;
-    a.bnmask = (const uint8_t*)bnmask;
-    a.bnmean = bnmean;
-  }
-  const int tile = pick_glds_tile(a, OP_KCONTIG, OP_KCONTIG);
-  if (tile < 0) return -2;
-  dispatch(a, OP_KCONTIG, OP_KCONTIG, tile, (hipStream_t)stream);
-  if (bnrows) *bnrows = bnx ? a.tiles_m : 0;
-  return (int)hipGetLastError();
-}
-
-// out[K + C][C] (f32) = [dZ | X]^T . X over the M pixels (rows < K: dZ^T X, rows >= K: the Gram matrix X^T X) and
-// rsum[K + C] = the row sums of [dZ | X]^T (sum dz per channel, then the column sums of X), on the 4-wave kernel
-// (row-split A: GemmArgs::cat 2, row sums: the fused bias-gradient path), split-K into f32 slabs in ws.
-DTF_API int dtf_conv1x1_wgrad_cat(const void* dZ, const void* X, float* out, float* rsum, long M, int K, int C,
-                                  float* ws, long ws_elems, void* stream) {
-  if ((K % 256) || (C & 63) || (M % BK) || M >= (1l << 31) || M * (long)K * 2 >= (1l << 31) || !ws || !rsum) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  GemmArgs a{};
-  a.A = (const bf16_t*)dZ; a.lda = K;
-  a.A2 = (const bf16_t*)X; a.lda2 = C; a.K1 = K; a.cat = 2;
-  a.B = (const bf16_t*)X; a.ldb = C;
-  a.M = K + C; a.N = C; a.K = (int)M; a.ldc = C;
-  a.batch = 1; a.alpha = 1.f; a.beta = 0.f; a.out_f32 = 1;
-  const int bn = C > 128 ? 256 : 128;
-  const long tiles = (long)cdiv(a.M, 256) * cdiv(a.N, bn);
-  const long kt = M / BK;
-  const long mn = (long)a.M * a.N;
-  // ~2 rounds of one block per CU, >= 16 K-tiles per split, slabs + row sums within the scratch
-  long s = std::max<long>(1, std::min<long>((512 + tiles - 1) / tiles, kt / 16));
-  s = std::min<long>(s, 256);
-  while (s > 1 && s * (mn + a.M) > ws_elems) --s;
-  if (s * (mn + a.M) > ws_elems) return -3;
-  a.splitk = (int)s;
-  a.kchunk = (int)(((M + s - 1) / s + BK - 1) / BK * BK);
-  a.C = ws;
-  a.slab = mn;
-  a.rowsum = ws + s * mn;
-  if (gemm_w4_try(a, OP_KOUTER, OP_KOUTER, st, bn)) return -2;
-  count_launch(LC_SPLITK);
-  dtf_sum_rows(ws, mn, (int)s, mn, out, 0, stream);
-  dtf_sum_rows(a.rowsum, a.M, (int)s, a.M, rsum, 0, stream);
-  return (int)hipGetLastError();
-}

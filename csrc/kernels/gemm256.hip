@@ -496,7 +496,6 @@ void launch256(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8) {
 
 // Used by dtf_gemm for eligible problems; returns 0 if launched, 1 if not eligible. bn: 256 or 128 (tile width).
 int gemm256_try(GemmArgs& a, int amode, int bmode, hipStream_t st, int fp8, int bn) {
-  if (a.cat) return 1;  // (concatenated A operands: gemm_core.h / gemm_w4.hip only)
   if (a.kchunk % BK || a.kchunk < 2 * BK || (a.lda & 7) || (a.ldb & 7) || a.stats || a.atomic_out || a.crm ||
       a.betamask || a.bsrc)
     return 1;

@@ -122,14 +122,6 @@ struct GemmArgs {
   // optional row sums of A over each split's K range (gemm_w4.hip, K-outer A, f32 out): rowsum[split][M] — the bias
   // gradient of a weight-gradient GEMM dW = dY^T X is the row sum of its A operand dY^T (written by the N-tile-0 blocks)
   float* rowsum;
-  // optional second A operand (the linear BatchNorm backward of a 1x1 conv, ops.conv _lbb): cat 1 = K-split: the
-  // K-tiles at k >= K1 read A2 (row stride lda2) at column k - K1 (K-contiguous A on the LDS-DMA tiles only); cat 2 =
-  // row split: the output rows m >= K1 read A2 (stride lda2) as its rows m - K1 (the kernel switches the operand per
-  // M-tile: K1 % BM == 0; K-outer A on gemm_kernel / gemm_w4). Host-checked; 0 = off.
-  const bf16_t* A2;
-  long lda2;
-  int K1;
-  int cat;
 };
 
 // 4 floats -> 4 packed OCP fp8 bytes (fmt 0 e4m3, 1 e5m2), values already scaled and clamped
@@ -587,21 +579,10 @@ struct GldsLoader {
   uint32_t tmask[L];  // KCONTIG: ~0 for valid rows; gathers: in-image tap mask
   int coff[L];        // byte offset of this lane's logical chunk in the 64-wide K-tile (the same for every i:
                       // rows 32 i + (t >> 3) share (row >> 1) & 7)
-  // K-split second operand (GemmArgs::cat 1): K-tiles from k1 on come from rsrc2 (row stride ld2 elements)
-  __amdgpu_buffer_rsrc_t rsrc2;
-  int k1, ld2, rb;
-
-  __device__ __forceinline__ void init_cat(const bf16_t* p2, long ld2_, int K1, int r0, int Rtot) {
-    rsrc2 = __builtin_amdgcn_make_buffer_rsrc((void*)p2, (short)0, (int)((long)Rtot * ld2_ * 2), 0x00020000);
-    k1 = K1;
-    ld2 = (int)ld2_;
-    rb = r0;
-  }
 
   __device__ __forceinline__ void init(const GemmArgs& a, const bf16_t* p, long ld, int r0, int Rtot) {
     const int t = threadIdx.x;
     const ConvGeom& g = a.g;
-    k1 = 0x7fffffff;
     uint32_t bytes;
     if constexpr (MODE == OP_KCONTIG) bytes = (uint32_t)((long)Rtot * ld * 2);  // host: < 2 GiB
     else if constexpr (MODE == OP_IM2COL_T) bytes = (uint32_t)((long)g.N * g.H * g.W * g.C * 2);
@@ -658,19 +639,6 @@ struct GldsLoader {
     int toff;
     uint32_t tap = 0, c0 = (uint32_t)k0;
     if constexpr (MODE == OP_KCONTIG) {
-      if (k0 >= k1) {  // K-split second operand (wave-uniform): row r at column k0 - k1 of A2
-        const int t = threadIdx.x;
-#pragma unroll
-        for (int i = 0; i < L; ++i) {
-          const bool ok = tmask[i] != 0u && k0 + (coff[i] >> 1) < Kend;
-          const uint32_t off =
-              ok ? (uint32_t)((rb + 32 * i + (t >> 3)) * ld2 * 2 + (k0 - k1) * 2 + coff[i]) : 0x80000000u;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc2, (__attribute__((address_space(3))) void*)(lds + i * 4096 +
-                                                                                                  wave * 1024),
-                                                   16, off, 0, 0, 0);
-        }
-        return;
-      }
       toff = k0 * 2;
     } else {
       const ConvGeom& g = a.g;
@@ -1160,15 +1128,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmArgs a) {
 
   typename std::conditional<GLDS, GldsFor<BM, AM>, LoaderFor<BM, AM>>::type la;
   typename std::conditional<GLDS, GldsFor<BN, BMODE>, LoaderFor<BN, BMODE>>::type lb;
-  if (a.cat == 2) {  // row split: this M-tile reads A (rows < K1) or A2 (rows >= K1) — see GemmArgs::cat
-    if (m0 >= a.K1) la.init(a, a.A2, a.lda2, m0 - a.K1, a.M - a.K1);
-    else la.init(a, Ap, a.lda, m0, a.K1);
-  } else {
-    la.init(a, Ap, a.lda, m0, a.M);
-  }
-  if constexpr (GLDS && AM == OP_KCONTIG) {
-    if (a.cat == 1) la.init_cat(a.A2, a.lda2, a.K1, m0, a.M);
-  }
+  la.init(a, Ap, a.lda, m0, a.M);
   lb.init(a, Bp, a.ldb, n0, a.N);
 
   v4f acc[TM][TN];

@@ -327,12 +327,7 @@ __global__ void __launch_bounds__(W4_THREADS, 1) gemm_w4_kernel(GemmArgs a) {
 
   W4LoaderFor<256, AM> la;
   W4Loader<BN, BMODE> lb;
-  if (a.cat == 2) {  // row split (GemmArgs::cat): this M-tile reads A (rows < K1) or A2 (rows >= K1)
-    if (m0 >= a.K1) la.init(a, a.A2, a.lda2, m0 - a.K1, a.M - a.K1, threadIdx.x);
-    else la.init(a, a.A + (long)bz * a.sA, a.lda, m0, a.K1, threadIdx.x);
-  } else {
-    la.init(a, a.A + (long)bz * a.sA, a.lda, m0, a.M, threadIdx.x);
-  }
+  la.init(a, a.A + (long)bz * a.sA, a.lda, m0, a.M, threadIdx.x);
   lb.init(a, a.B + (long)bz * a.sB, a.ldb, n0, a.N, threadIdx.x);
   // LDS byte address of this wave's 1 KiB slot of piece 0 in stage 0 (wave-uniform: a scalar)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem +
@@ -521,7 +516,6 @@ void w4_launch(GemmArgs& a, int amode, int bmode, hipStream_t st) {
 // True if the 4-wave kernel can run C = A . B^T with these arguments: K % 64 == 0 per split, 16-B aligned operand
 // rows, K-outer operands with row counts % 8 == 0, operands < 2 GiB, and only the epilogue features w4_epilogue has.
 bool gemm_w4_ok(const GemmArgs& a, int amode, int bmode) {
-  if (a.cat == 1 || (a.cat == 2 && (amode != OP_KOUTER || a.batch > 1 || (a.K1 % 256)))) return false;
   if (a.atomic_out || a.crm || a.bsrc || a.betamask || a.scales || a.q8 || a.q8T || a.q8col || a.zero_slot)
     return false;
   // BN statistics: convolution forward (IM2COL_T) or the BN-backward reduction of a data gradient (DGRAD_T + bnx);

@@ -291,16 +291,13 @@ __device__ __forceinline__ void relu_mask8(float* d, const bf16_t* ymask, const 
 
 // Backward reduce: dz = dy * (y > 0 if relu-mask given); partial rows [gridDim.x][2C]:
 // [0,C) sum dz, [C,2C) sum dz*xhat. No atomics; bn_bwd_finalize sums the rows.
-// DZ: also store the masked dz (dz_out), and x may be null (then [C,2C) is 0): the mask pass of the linear BatchNorm
-// backward of a 1x1 conv (ops.conv _lbb), which needs dz itself and sum dz (+ a deferred projection BN's reduction).
-template <bool DZ>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
                                                             const bf16_t* __restrict__ ymask,
                                                             const uint8_t* __restrict__ mbits,
                                                             const bf16_t* __restrict__ x,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long M, int C,
-                                                            float* __restrict__ part, bf16_t* __restrict__ dz_out) {
+                                                            float* __restrict__ part) {
   __shared__ float red[4096];
   ColGeo g = colgeo(C);
   const int t = threadIdx.x;
@@ -309,8 +306,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
     const int cc = cc0 + t % g.TPR;
     float s[8] = {0}, q[8] = {0};
     if (t < g.TPR * g.RPB && cc < g.cols8) {
-      float mu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (x) load_coef8(mean + cc * 8, mu);
+      float mu[8];
+      load_coef8(mean + cc * 8, mu);
       // sum dz*(x - mean) here; the invstd factor is applied once per channel in bn_bwd_finalize
       const long rstep = (long)gridDim.x * g.RPB;
       long r = (long)blockIdx.x * g.RPB + rsub;
@@ -320,29 +317,27 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
         for (int u = 0; u < EU; ++u) {
           const long i8 = (r + u * rstep) * g.cols8 + cc;
           load8(dy + i8 * 8, d[u]);
-          if (!DZ || x) load8(x + i8 * 8, xv[u]);
+          load8(x + i8 * 8, xv[u]);
           relu_mask8(d[u], ymask, mbits, i8);
-          if constexpr (DZ) store8(dz_out + i8 * 8, d[u]);
         }
 #pragma unroll
         for (int u = 0; u < EU; ++u)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             s[j] += d[u][j];
-            if (!DZ || x) q[j] = fmaf(d[u][j], xv[u][j] - mu[j], q[j]);
+            q[j] = fmaf(d[u][j], xv[u][j] - mu[j], q[j]);
           }
       }
       for (; r < M; r += rstep) {
         float d[8], xv[8];
         const long i8 = r * g.cols8 + cc;
         load8(dy + i8 * 8, d);
-        if (!DZ || x) load8(x + i8 * 8, xv);
+        load8(x + i8 * 8, xv);
         relu_mask8(d, ymask, mbits, i8);
-        if constexpr (DZ) store8(dz_out + i8 * 8, d);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           s[j] += d[j];
-          if (!DZ || x) q[j] = fmaf(d[j], xv[j] - mu[j], q[j]);
+          q[j] = fmaf(d[j], xv[j] - mu[j], q[j]);
         }
       }
     }
@@ -1029,25 +1024,10 @@ DTF_API int dtf_bn_bwd(const void* dy, const void* ymask, const void* mbits, con
   float* coef = work;
   float* part = work + 3 * C;
   int G = red_grid(M, C);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(G), dim3(256), 0, st, (const bf16_t*)dy,
-                     (const bf16_t*)ymask, (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part,
-                     (bf16_t*)nullptr);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(G), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)ymask,
+                     (const uint8_t*)mbits, (const bf16_t*)x, mean, invstd, M, C, part);
   return bn_bwd_tail(dy, ymask, mbits, x, mean, invstd, gamma, M, C, dx, dz_out, dgamma, dbeta, accumulate, part, G,
                      coef, st, &sc);
-}
-
-// Mask pass of the linear BatchNorm backward (ops.conv _lbb): dz = dy * relu mask (mbits) stored to dz, with partial
-// rows [G][2C] of sum dz and (x2 given: a deferred projection BatchNorm's input with mean2) sum dz * (x2 - mean2);
-// part: capacity 1024 * 2C floats; *rows = G.
-DTF_API int dtf_bn_mask_reduce(const void* dy, const void* mbits, const void* x2, const float* mean2, long M, int C,
-                               void* dz, float* part, int* rows, void* stream) {
-  if ((C & 7) || !dz || !part || !rows) return -1;
-  const int G = red_grid(M, C);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(G), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)dy,
-                     (const bf16_t*)nullptr, (const uint8_t*)mbits, (const bf16_t*)x2, mean2, (const float*)nullptr, M,
-                     C, part, (bf16_t*)dz);
-  *rows = G;
-  return (int)hipGetLastError();
 }
 
 // Backward with the reduction already done by the GEMM that produced dy (dtf_conv_dgrad's fused BN-backward

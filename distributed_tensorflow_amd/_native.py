@@ -26,10 +26,6 @@ _KERNEL_SIGS = {
     "dtf_gemm": [P, P, P, P, P, P, P, I, I, I, L, L, L, I, I, I, L, L, L, F, F, I, I, I, I, P, L, P],
     "dtf_conv_fwd": [P, P, P, P, P, P] + [I] * 15 + [I, I, I, P],
     "dtf_pwconv_fwd": [P, P, P, P, P, L, I, I, P],
-    "dtf_bn_mask_reduce": [P, P, P, P, L, I, P, P, P, P],
-    "dtf_conv1x1_wgrad_cat": [P, P, P, P, L, I, I, P, L, P],
-    "dtf_conv1x1_dgrad_cat": [P, P, P, P, P, L, I, I, P, P, P, P, P, P],
-    "dtf_lbb_finalize": [P, P, P, P, P, P, L, I, I, P, P, I, P, I, P, P, P, P],
     "dtf_conv_bn_apply_fwd": [P, P, P, P, P, P, P, P, L, I, I, I, P, P, P, P, P, F, F, P, P, P, P, P],
     "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P, L, P, P, P, P, P, P, P],
     "dtf_conv_dgrad_addsub2": [P, P, P, P, I, I, I, I, I, I, P, L, P, P, P, P, P, P],

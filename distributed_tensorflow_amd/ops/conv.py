@@ -14,7 +14,7 @@ import os
 import torch
 
 from ._util import (BF16, F32, SIDE_STREAM_ON, IntOut, K as K_, before_overwrite, bf16_shadow, call, crsk_shadow,
-                    direct_grad, fork_side, mark_parked, on_gpu, ptr, stream, workspace)  # noqa: F401
+                    direct_grad, fork_side, mark_parked, on_gpu, ptr, stream, workspace)
 
 
 def out_size(h, k, s, p, d=1):
@@ -246,21 +246,6 @@ _COMPACT_PROJ = True
 # Two-pass forward of the channel-expanding 1x1 ConvBN (statistics pass + recomputed product with the BN apply in its
 # epilogue, pwconv.hip dtf_conv_bn_apply_fwd) instead of conv(+stats) -> finalize -> standalone apply pass.
 _TWO_PASS_PW = os.environ.get("DTF_PW2", "1") != "0"
-# Linear BatchNorm backward of the bottleneck's expanding 1x1 ConvBN (csrc/kernels/bn_linear.hip): the BN backward
-# through yc = X W^T by two GEMMs over [dz | X] — yc is never stored, the BN apply pass and its dyc never exist.
-_LINEAR_BN_BWD = os.environ.get("DTF_LBB", "0") != "0"
-
-
-def _lbb_ok(g, relu, role, training):
-    """The ConvBNs whose backward runs linear (_ConvBNFn._backward_lbb): training 1x1 stride-1 unpadded with ReLU,
-    not a projection shortcut; K_out % 256, C_in % 64, pixels % 64 (the concatenated GEMMs' tile seams), < 2 GiB."""
-    if not (_LINEAR_BN_BWD and training and relu and role != "proj"):
-        return False
-    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
-    if (R, S, sh, sw, ph, pw) != (1, 1, 1, 1, 0, 0) or K % 256 or C % 64:
-        return False
-    M = N * P * Q
-    return M % 64 == 0 and M * K * 2 < (1 << 31)
 
 
 def _two_pass_ok(g):
@@ -297,13 +282,11 @@ class _ConvBNFn(torch.autograd.Function):
         raff = getattr(res, "_dtf_affine", None) if res is not None else None
         deferred = role == "proj" and not relu and _DEFER_PROJ_BN
         out = mbits = None
-        lbb = _lbb_ok(g, relu, role, training) and any(ctx.needs_input_grad)
         if training and not deferred and _TWO_PASS_PW and _two_pass_ok(g):
             # channel-expanding 1x1 (bottleneck c3): statistics pass, finalize, then the recomputed product with the
-            # BatchNorm / residual / ReLU applied in the epilogue (pwconv.hip MODE 1 / 2) — no standalone apply pass;
-            # with the linear BN backward the conv output itself is never stored
-            yc = None if lbb else torch.empty((N, P, Q, K), dtype=BF16, device=dev)
-            out = torch.empty((N, P, Q, K), dtype=BF16, device=dev)
+            # BatchNorm / residual / ReLU applied in the epilogue (pwconv.hip MODE 1 / 2) — no standalone apply pass
+            yc = torch.empty((N, P, Q, K), dtype=BF16, device=dev)
+            out = torch.empty_like(yc)
             mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if relu else None
             part = torch.empty(((M + 63) // 64) * 2 * K, dtype=F32, device=dev)
             rc_ = res.contiguous() if res is not None else None
@@ -338,9 +321,6 @@ class _ConvBNFn(torch.autograd.Function):
             out = torch.empty_like(yc)
             call("dtf_bn_apply", ptr(yc), ptr(scale), ptr(shift), ptr(res), ptr(out), M, K, int(relu), ptr(mbits),
                  ptr(raff[0]) if raff else None, ptr(raff[1]) if raff else None, stream())
-        ctx.lbb = lbb
-        if lbb:
-            yc = None  # (the linear backward never reads the conv output)
         # backward needs the conv output and a 1-bit ReLU mask, not the bf16 BN output
         ctx.save_for_backward(x, w, gamma, yc, mbits, mean, invstd)
         ctx.bn_params = (gamma, beta)
@@ -352,8 +332,7 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.in_src = in_src if (ctx.needs_input_grad[0] and _FUSE_BN_BWD) else None
         ctx.res_src = res_src if (training and _FUSE_BN_BWD) else None
         ctx.src = None
-        ctx.out_shape = tuple(out.shape)
-        if training and _FUSE_BN_BWD and any(ctx.needs_input_grad) and not lbb:
+        if training and _FUSE_BN_BWD and any(ctx.needs_input_grad):
             src = _BNSource(yc, mbits, mean, invstd, gamma, (gamma, beta))
             out._dtf_bnsrc = src
             ctx.src = src
@@ -364,10 +343,8 @@ class _ConvBNFn(torch.autograd.Function):
         x, w, gamma, yc, mbits, mean, invstd = ctx.saved_tensors
         g = ctx.g
         K = g[4]
-        dout = dout.to(BF16).contiguous()
-        if ctx.lbb:
-            return _ConvBNFn._backward_lbb(ctx, dout, x, w, gamma, mbits, mean, invstd)
         M = yc.numel() // K
+        dout = dout.to(BF16).contiguous()
         if not ctx.training:
             return _ConvBNFn._backward_frozen(ctx, dout, x, w, gamma, yc, mbits, mean, invstd)
         dyc = torch.empty_like(yc)
@@ -439,68 +416,6 @@ class _ConvBNFn(torch.autograd.Function):
             dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
-
-    @staticmethod
-    def _backward_lbb(ctx, dout, x, w, gamma, mbits, mean, invstd):
-        """Linear BatchNorm backward of a training 1x1 ConvBN with ReLU (csrc/kernels/bn_linear.hip): the mask pass
-        dz = dout * relu' (+ sum dz, + the deferred projection BN's reduction), one GEMM over the pixels giving dz^T X,
-        X^T X and the row sums, the per-channel / per-filter finalize (dgamma, dbeta, dW, the dgrad operand), and the
-        data gradient [dz | X] . Bd^T + bias with the input BatchNorm's backward reduction in its epilogue. The conv
-        output yc and its gradient dyc are never materialised."""
-        g = ctx.g
-        N, H, W, C, K = g[:5]
-        M = N * H * W
-        dev = dout.device
-        link, role = ctx.link, ctx.role
-        rsrc = ctx.res_src  # a deferred projection shortcut BN: its reduction rides on the mask pass
-        ctx.res_src = ctx.src = None
-        dz = torch.empty_like(dout)
-        part = torch.empty(1024 * 2 * K, dtype=F32, device=dev)
-        rows = IntOut()
-        call("dtf_bn_mask_reduce", ptr(dout), ptr(mbits), ptr(rsrc.yc) if rsrc is not None else None,
-             ptr(rsrc.mean) if rsrc is not None else None, M, K, ptr(dz), ptr(part), rows.addr, stream())
-        if rsrc is not None:
-            rsrc.provide(dz, part, rows.value)
-        dres = None
-        if ctx.has_res:  # d(residual) = the masked gradient itself (parked for the first conv's epilogue when linked)
-            dres = link.park(dz) if (link is not None and role == "res") else dz
-        ws = workspace(dev)
-        p2 = torch.empty((K + C) * C, dtype=F32, device=dev)
-        rsum = torch.empty(K + C, dtype=F32, device=dev)
-        call("dtf_conv1x1_wgrad_cat", ptr(dz), ptr(x), ptr(p2), ptr(rsum), M, K, C, ptr(ws), ws.numel(), stream())
-        gamma_p, beta_p = ctx.bn_params
-        tg, tb = direct_grad(gamma_p), direct_grad(beta_p)
-        direct_bn = tg is not None and tb is not None
-        dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=dev)
-        dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=dev)
-        tw = direct_grad(w) if ctx.needs_input_grad[1] else None
-        dw = tw if tw is not None else torch.empty((K, 1, 1, C), dtype=F32, device=dev)
-        coef = torch.empty(3 * K, dtype=F32, device=dev)
-        bd = torch.empty(C * (K + C), dtype=BF16, device=dev)
-        bias = torch.empty(C, dtype=F32, device=dev)
-        call("dtf_lbb_finalize", ptr(p2), ptr(rsum), ptr(bf16_shadow(w)), ptr(gamma), ptr(mean), ptr(invstd), M, K, C,
-             ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(dw), int(tw is not None), ptr(coef), ptr(bd), ptr(bias),
-             stream())
-        dx = None
-        if ctx.needs_input_grad[0]:
-            src = ctx.in_src
-            complete = src is not None and src.consumers == 1
-            dx = torch.empty((N, H, W, C), dtype=BF16, device=dev)
-            bpart = brows = None
-            if complete:
-                bpart = torch.empty(((M + 63) // 64 + 1) * 2 * C, dtype=F32, device=dev)
-                brows = IntOut()
-            call("dtf_conv1x1_dgrad_cat", ptr(dz), ptr(x), ptr(bd), ptr(bias), ptr(dx), M, K, C,
-                 ptr(src.yc) if complete else None, ptr(src.mbits) if complete else None,
-                 ptr(src.mean) if complete else None, ptr(bpart), brows.addr if complete else None, stream())
-            if complete:
-                src.provide(dx, bpart, brows.value)
-            ctx.in_src = None
-        if tw is not None or not ctx.needs_input_grad[1]:
-            dw = None
-        if direct_bn:
-            dgamma = dbeta = None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
     @staticmethod
     def _backward_frozen(ctx, dout, x, w, gamma, yc, mbits, mean, invstd):
