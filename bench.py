@@ -117,12 +117,13 @@ def main():
                          "default: per model from the interleaved A/B (profiles/r5_hipgraph_default.txt)")
     ap.add_argument("--ar-sweep", type=int, default=1,
                     help="N>1: after the timed steps, time f32 all-reduces of 1-128 MB and report RCCL bus bandwidth")
-    ap.add_argument("--hiprio", type=int, default=1,
-                    help="1 (default): issue the train step on a high-priority HIP stream (the weight-gradient side "
-                         "stream keeps normal priority, so the dgrad critical path wins block dispatch whenever a CU "
-                         "frees up — the 4-wave GEMM blocks of the side stream hold a whole CU's registers); interleaved "
-                         "on one MI355X: ResNet-50 13,386 / 13,459 vs 13,317 / 13,337 img/s, GPT-2 +0.3%, BERT +-0 "
-                         "(profiles/r5_hipgraph_default.txt)")
+    ap.add_argument("--hiprio", type=int, default=None,
+                    help="1: issue the train step on a high-priority HIP stream (the weight-gradient side stream keeps "
+                         "normal priority, so the dgrad critical path wins block dispatch whenever a CU frees up); "
+                         "single replica, interleaved on one MI355X: ResNet-50 13,386 / 13,459 vs 13,317 / 13,337 "
+                         "img/s, GPT-2 +0.3%%, BERT +-0 (profiles/r5_hipgraph_default.txt). Default: 1 for a single "
+                         "replica, 0 on the collective path, where the high-priority main stream costs 11%% "
+                         "(forced-collective ResNet-50: 11,943 vs 13,436 img/s, profiles/r6_forced_collective.txt)")
     ap.add_argument("--ps", type=int, default=None, help="resnet50_ps: parameter-server tasks (default: see ps_bench)")
     ap.add_argument("--trainers", type=int, default=None, help="resnet50_ps: trainer tasks")
     ap.add_argument("--ps-cpu", action="store_true", help="resnet50_ps: PS shards in host shared memory")
@@ -140,6 +141,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world == 1 and "RANK" not in os.environ:
         return _relaunch(args)  # before anything touches the GPU
+    if args.hiprio is None:  # (see --hiprio: a win for one replica, a loss with the collectives)
+        args.hiprio = int(world == 1 and os.environ.get("DTF_FORCE_COLLECTIVE", "0") != "1")
 
     import torch
     import torch.distributed as dist
