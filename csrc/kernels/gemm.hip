@@ -743,6 +743,25 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
                            const void* bsrc2, void* stream);
 
+namespace dtf {
+int pwconv_dgrad_try(const void* dY, const void* Wck, void* dX, float beta, const void* betamask, const void* bnx,
+                     const void* bnmask, const float* bnmean, float* part, long M, int Kc, int N, const void* bsrc2,
+                     int H, int W, hipStream_t st);
+}
+// DTF_PW_DGRAD=0 (or dtf_set_pw_dgrad(0)) keeps the pointwise data gradients on the general GEMM tiles (A/B switch)
+static int g_pw_dgrad = -1;
+static bool pwdgrad_enabled() {
+  if (g_pw_dgrad < 0) {
+    const char* e = getenv("DTF_PW_DGRAD");
+    g_pw_dgrad = !(e && e[0] == '0');
+  }
+  return g_pw_dgrad != 0;
+}
+DTF_API int dtf_set_pw_dgrad(int on) {
+  g_pw_dgrad = on ? 1 : 0;
+  return 0;
+}
+
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
@@ -821,6 +840,16 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
     const int am = pointwise ? OP_KCONTIG
                    : (sh == 1 && sw == 1 && tap_uniform(K, R * S, (long)N * P * Q * K)) ? OP_DGRAD_T : OP_DGRAD;
     int t = tile;
+    // channel-reducing pointwise data gradients (ResNet-50 bottleneck c1: dY width 64..256 -> 4x the channels): the
+    // persistent pointwise kernel (filter in registers, beta accumulate + BN-backward partials in its store pass)
+    if (pointwise && t < 0 && !out_f32 && pwdgrad_enabled()) {
+      const int rows = pwconv_dgrad_try(dY, Wcrsk, dX, beta, betamask, bnx, bnmask, bnmean, bnx ? bnpart : nullptr,
+                                        a.M, K, C, bsrc2, H, W, st);
+      if (rows > 0) {
+        if (bnrows) *bnrows = bnx ? rows : 0;
+        return (int)hipGetLastError();
+      }
+    }
     // stride-1 3x3 data gradients into >= 256 channels (ResNet-50 stages 3-4): the 4-wave kernel with the dY gather
     // loader and the BN-backward statistics epilogue (profiles/r5_conv3x3_w4.txt)
     if (am == OP_DGRAD_T && R * S > 1 && t < 0 && C >= 256 && !out_f32 && beta == 0.f && !betamask && !bsrc2) {

@@ -45,6 +45,19 @@ struct PwArgs {
   bf16_t* out;
   uint8_t* mbits;  // 1-bit ReLU mask of out (relu only)
   int relu;
+  // MODE 3 (the data gradient of a channel-REDUCING 1x1 conv, X = dY [M][C], W = its filter as [K][C], Y = dX):
+  // Y = bf16(X W^T) (+ beta * cin, the old values zeroed where betamask's bit is clear: the residual gradient parked
+  // for this conv, gemm_core.h's staged beta path operation for operation); with bnmean the BatchNorm-backward
+  // partial rows of the stored values: [slot][0, K) sum dz, [K, 2K) sum dz * (bnx - bnmean), dz = value * bnmask bit
+  const bf16_t* cin;
+  const uint8_t* betamask;
+  float beta;
+  const bf16_t* bnx;
+  const uint8_t* bnmask;
+  const float* bnmean;
+  // MODE 3 with bW > 0: cin is the compact [N][bH/2][bW/2][K] data gradient of a stride-2 1x1 projection of the same
+  // input, added at the even pixels of the [N][bH][bW] grid only (beta 1, no mask)
+  int bH, bW;
 };
 
 template <int C, int WMW, bool STG = false, int MODE = 0>
@@ -68,9 +81,24 @@ struct PwGeo {
   static constexpr int STM = MODE == 1 ? 0 : ST;
 };
 
+// One 8-B fragment into the LDS store stage. Inline asm on purpose: the compiler cannot tell the stage from the DMA
+// ring (LDS-DMA writes carry no alias information), so before a plain LDS store it waits for EVERY outstanding
+// vector-memory op — draining the DMA of the tile two ahead before each epilogue and leaving one tile of prefetch.
+// The stage never overlaps the ring; tile_barrier() waits for these writes before it publishes the tile.
+__device__ __forceinline__ void stage_write(char* p, uint2 v) {
+  const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)p;
+  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
+// Workgroup barrier for the tile loop: this thread's LDS ops done, then s_barrier, as one asm statement (a compiler
+// memory barrier too). __syncthreads()' fence makes the compiler drain every outstanding vector-memory op first (it
+// counts the in-flight LDS-DMA of the next tiles as pending LDS writes); the loop orders its DMA with explicit vmcnt
+// waits instead.
+__device__ __forceinline__ void tile_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <int C, int WMW, bool STG, int MODE>
 __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
-  static_assert(MODE != 2 || STG, "the apply epilogue works on the LDS-staged tile");
+  static_assert(MODE < 2 || STG, "the apply / data-gradient epilogues work on the LDS-staged tile");
   using G = PwGeo<C, WMW, STG, MODE>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -133,6 +161,23 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
       (void*)a.out, (short)0, MODE == 2 ? (int)((long)a.M * a.K * 2) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.mbits, (short)0, (MODE == 2 && a.mbits) ? (int)((long)a.M * a.K / 8) : 0, 0x00020000);
+  // MODE 3: the old values (beta source), the BN input and its mask, the batch mean of this thread's 8 channels, and the
+  // thread's running sums of dz and dz * (x - mean) over all of its rows
+  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.cin, (short)0, (MODE == 3 && a.cin) ? (int)((long)(a.bW ? a.M / 4 : a.M) * a.K * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xbr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bnx, (short)0, (MODE == 3 && a.bnmean) ? (int)((long)a.M * a.K * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t bmr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.betamask, (short)0, (MODE == 3 && a.betamask) ? (int)((long)a.M * a.K / 8) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xmr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bnmask, (short)0, (MODE == 3 && a.bnmask) ? (int)((long)a.M * a.K / 8) : 0, 0x00020000);
+  const uint32_t bm_or = a.betamask ? 0u : 0xFFu, xm_or = a.bnmask ? 0u : 0xFFu;  // absent mask: every bit set
+  float mu3[8], s3[8], q3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s3[j] = q3[j] = 0.f;
+    mu3[j] = (MODE == 3 && a.bnmean) ? a.bnmean[nch + j] : 0.f;
+  }
   if constexpr (MODE == 2) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -158,17 +203,52 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
     } else if constexpr (MODE == 1) {
       if (it + 1 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
+    } else {  // MODE 2 / 3
       if (it == 0) {
         if (n_mine > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    __syncthreads();  // every wave's DMA share landed; every wave is done with the buffer tile it+2 reuses
+    tile_barrier();  // every wave's DMA share landed; every wave is done with the buffer tile it+2 reuses
     const int mt = first + it * step;
     // MODE 2: this tile's residual chunks, in flight under the MFMAs (issued before tile it+2's DMA, so waiting for
     // them leaves that DMA in flight)
     uint4 rv[G::ST];
+    // MODE 3: this tile's old values (beta source), BN input chunks and mask bytes, likewise in flight under the
+    // MFMAs (rows past M read as zeros through the range check: no beta term, dz = 0)
+    uint4 xv[MODE == 3 ? G::ST : 1];
+    uint32_t bmb[MODE == 3 ? G::ST : 1], xmb[MODE == 3 ? G::ST : 1];
+    if constexpr (MODE == 3) {
+      // addresses first (the compact source's pixel decomposition is all ALU), then the loads back to back
+      uint32_t off[G::ST], boff[G::ST], coff[G::ST], cbits[G::ST];
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) {
+        const int row = (t + k * G::NTH) >> 5;
+        const int m = mt * G::BM + row;
+        const uint32_t e = (uint32_t)m * (uint32_t)a.K + (uint32_t)nch;
+        off[k] = m < a.M ? e * 2u : 0x80000000u;
+        boff[k] = m < a.M ? e >> 3 : 0x80000000u;
+        coff[k] = off[k];
+        cbits[k] = 0xFFu;
+        if (a.bW) {  // compact stride-2 source: even pixels only
+          const uint32_t hw = (uint32_t)m % (uint32_t)(a.bH * a.bW), img = (uint32_t)m / (uint32_t)(a.bH * a.bW);
+          const uint32_t h = hw / (uint32_t)a.bW, w = hw % (uint32_t)a.bW;
+          const bool even = m < a.M && !((h | w) & 1u);
+          coff[k] = even ? (((img * (uint32_t)(a.bH / 2) + (h >> 1)) * (uint32_t)(a.bW / 2) + (w >> 1)) *
+                                (uint32_t)a.K + (uint32_t)nch) * 2u
+                         : 0x80000000u;
+          cbits[k] = even ? 0xFFu : 0u;
+        }
+      }
+      // (unconditional: a null operand has a zero-size range, its loads return zeros without touching memory)
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) {
+        rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cr, coff[k], 0, 0));
+        xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbr, off[k], 0, 0));
+        bmb[k] = ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(bmr, boff[k], 0, 0) | bm_or) & cbits[k];
+        xmb[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(xmr, boff[k], 0, 0) | xm_or;
+      }
+    }
     if constexpr (MODE == 2) {
       if (a.res) {
 #pragma unroll
@@ -218,13 +298,13 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
         if constexpr (STG) {
           if constexpr (MODE != 1) {
             const int ml = wm * 64 + 16 * i + (lane & 15), nl = wn * 64 + 16 * j + 4 * (lane >> 4);
-            *reinterpret_cast<uint2*>(stg + (ml * G::SROW + nl) * 2) = o;
+            stage_write(stg + (ml * G::SROW + nl) * 2, o);
           }
         } else if constexpr (MODE != 1) {
           const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)n) * 2u : 0x80000000u;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, o), yr, off, 0, 0);
         }
-        if constexpr (MODE != 2) {
+        if constexpr (MODE < 2) {
           // statistics of the stored values (rows past M hold exact zeros: they add nothing)
           const float v0 = __uint_as_float(o.x << 16), v1 = __uint_as_float(o.x & 0xffff0000u);
           const float v2 = __uint_as_float(o.y << 16), v3 = __uint_as_float(o.y & 0xffff0000u);
@@ -236,7 +316,7 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
       }
     }
     if constexpr (STG && MODE == 0) {
-      __syncthreads();  // the tile is staged (the next tile's staging writes come after the next top barrier)
+      tile_barrier();  // the tile is staged (the next tile's staging writes come after the next top barrier)
 #pragma unroll
       for (int k = 0; k < G::ST; ++k) {
         const int c = t + k * G::NTH, row = c >> 5, ch = c & 31;
@@ -248,7 +328,7 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
       }
     }
     if constexpr (MODE == 2) {
-      __syncthreads();  // the tile is staged
+      tile_barrier();  // the tile is staged
       // the residual chunks are in: everything but tile it+2's DMA (issued after them) has completed
       if (it + 2 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -289,8 +369,73 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
         }
       }
     }
+    if constexpr (MODE == 3) {
+      tile_barrier();  // the tile is staged
+      // the tile's loads are in: everything but tile it+2's DMA (issued after them) has completed
+      if (it + 2 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) {
+        const int row = (t + k * G::NTH) >> 5;
+        const int m = mt * G::BM + row;
+        uint4 val = *reinterpret_cast<const uint4*>(stg + (row * G::SROW + ch * 8) * 2);
+        if (a.cin) {  // gemm_epilogue's staged beta path, operation for operation
+          const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, ow[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
+          float f[8], g[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f[2 * q] = __uint_as_float(vw[q] << 16); f[2 * q + 1] = __uint_as_float(vw[q] & 0xffff0000u);
+            g[2 * q] = __uint_as_float(ow[q] << 16); g[2 * q + 1] = __uint_as_float(ow[q] & 0xffff0000u);
+          }
+#pragma unroll
+          for (int r = 0; r < 8; ++r) f[r] = ((bmb[k] >> r) & 1u) ? fmaf(a.beta, g[r], f[r]) : f[r];
+          val = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7]));
+        }
+        const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)nch) * 2u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, val), yr, off, 0, 0);
+        {  // (unconditional: with no bnmean the sums are of zeros and never written; a branch here leaves the xv
+           // loads unconsumed on one path, and the compiler then drains every load before the next tile's)
+          const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int r = 2 * q + h;
+              const float dv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
+              const float xx = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
+              const float dz = ((xmb[k] >> r) & 1u) ? dv : 0.f;
+              s3[r] += dz;
+              q3[r] = fmaf(dz, xx - mu3[r], q3[r]);
+            }
+        }
+      }
+    }
   }
   if constexpr (MODE == 2) return;  // (no statistics)
+  if constexpr (MODE == 3) {
+    if (!a.bnmean) return;
+    // one partial row per block: the NTH / 32 threads of each 8-channel chunk folded through LDS in a fixed order
+    __syncthreads();  // the ring is free
+    float* red = reinterpret_cast<float*>(smem);  // [thread][sum 8 | sq 8]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[t * 16 + j] = s3[j];
+      red[t * 16 + 8 + j] = q3[j];
+    }
+    __syncthreads();
+    if (t < 256) {  // column t of this block's 256: chunk t >> 3, channel t & 7
+      const int c8 = t >> 3, j = t & 7;
+      float sv = 0.f, qv = 0.f;
+      for (int u = c8; u < G::NTH; u += 32) {
+        sv += red[u * 16 + j];
+        qv += red[u * 16 + 8 + j];
+      }
+      float* prow = a.stats + (long)slot * 2 * a.K;
+      prow[tile_n * 256 + t] = sv;
+      prow[a.K + tile_n * 256 + t] = qv;
+    }
+    return;
+  }
 
   // ---- one partial row per block: the 16 row lanes by DPP, the WMW row waves through LDS (fixed order)
   __syncthreads();  // the ring is free (every wave's last tile is multiplied)
@@ -324,13 +469,17 @@ void launch_pw(const PwArgs& a, int grid, hipStream_t st) {
 
 template <int MODE>
 void launch_pw_c(const PwArgs& a, int C, int grid, hipStream_t st) {
-  if (C == 64) launch_pw<64, 2, true, MODE>(a, grid, st);
-  else if (C == 128) launch_pw<128, 1, true, MODE>(a, grid, st);
+  // (MODE 3 keeps one row wave for C 64 too: its epilogue holds four operands per chunk in flight, which needs the
+  // one-wave-per-SIMD register budget — two row waves spill)
+  if (C == 64) {
+    if constexpr (MODE == 3) launch_pw<64, 1, true, MODE>(a, grid, st);
+    else launch_pw<64, 2, true, MODE>(a, grid, st);
+  } else if (C == 128) launch_pw<128, 1, true, MODE>(a, grid, st);
   else launch_pw<256, 1, true, MODE>(a, grid, st);
 }
 
 // grid / row-slot plan shared by every mode (the same tile -> block assignment in both passes of the two-pass form)
-bool pw_plan(PwArgs& a, long M, int C, int K, int& grid) {
+bool pw_plan(PwArgs& a, long M, int C, int K, int& grid, bool one_row_wave = false) {
   if (!(C == 64 || C == 128 || C == 256) || (K % 256)) return false;
   const int tiles_n = K / 256;
   if (tiles_n != 1 && tiles_n != 2 && tiles_n != 4 && tiles_n != 8) return false;
@@ -339,7 +488,7 @@ bool pw_plan(PwArgs& a, long M, int C, int K, int& grid) {
   // stage of a 128-row tile would exceed the LDS); C 64: two row waves per block. Every tile is stored through an
   // LDS stage as row-contiguous 16-B chunks. (Measured alternatives, removed: several one-row-wave blocks per CU
   // for C 64, direct fragment stores: profiles/r4_pointwise_conv_bw_probe.txt, r4_negative_results.txt.)
-  const int wmw = C == 64 ? 2 : 1;
+  const int wmw = (C == 64 && !one_row_wave) ? 2 : 1;
   const int bm = 64 * wmw;
   a.M = (int)M; a.K = K;
   a.tiles_m = (int)((M + bm - 1) / bm);
@@ -367,6 +516,37 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
   if (!pw_plan(a, M, C, K, grid)) return 0;
   a.X = (const bf16_t*)X; a.W = (const bf16_t*)W; a.Y = (bf16_t*)Y; a.stats = stats;
   launch_pw_c<0>(a, C, grid, st);
+  return hipGetLastError() == hipSuccess ? a.nslots : 0;
+}
+
+// MODE 3: dX[M][N] = dY[M][Kc] . Wck^T (Wck: the conv filter as [N][Kc], i.e. [C][1][1][K]) for a channel-reducing
+// 1x1 conv's data gradient (Kc in {64, 128, 256}, N a multiple of 256 with N/256 in {1, 2, 4, 8}), optionally
+// accumulating beta * dX in place (betamask: the deferred ReLU bits of the old values) and with bnmean the
+// BatchNorm-backward partial rows of dX into part. Returns the number of partial rows (> 0), or 0 when not handled.
+// bsrc2 (with H, W even): instead of beta * dX, add the compact stride-2 shortcut gradient at the even pixels.
+int pwconv_dgrad_try(const void* dY, const void* Wck, void* dX, float beta, const void* betamask, const void* bnx,
+                     const void* bnmask, const float* bnmean, float* part, long M, int Kc, int N, const void* bsrc2,
+                     int H, int W, hipStream_t st) {
+  if (((uintptr_t)dY & 15) || ((uintptr_t)Wck & 15) || ((uintptr_t)dX & 15) || ((uintptr_t)bnx & 15) ||
+      ((uintptr_t)bsrc2 & 15))
+    return 0;
+  if ((bnmean != nullptr) != (part != nullptr) || (bnmean && !bnx) || (betamask && beta == 0.f)) return 0;
+  if (bsrc2 && (betamask || (H & 1) || (W & 1) || (long)H * W <= 0 || M % ((long)H * W))) return 0;
+  PwArgs a{};
+  int grid = 0;
+  if (!pw_plan(a, M, Kc, N, grid, true)) return 0;
+  a.X = (const bf16_t*)dY; a.W = (const bf16_t*)Wck; a.Y = (bf16_t*)dX; a.stats = part;
+  if (bsrc2) {
+    a.cin = (const bf16_t*)bsrc2;
+    a.bH = H; a.bW = W;
+    beta = 1.f;
+  } else {
+    a.cin = beta != 0.f ? (const bf16_t*)dX : nullptr;
+  }
+  a.beta = beta;
+  a.betamask = (const uint8_t*)betamask;
+  a.bnx = (const bf16_t*)bnx; a.bnmask = (const uint8_t*)bnmask; a.bnmean = bnmean;
+  launch_pw_c<3>(a, Kc, grid, st);
   return hipGetLastError() == hipSuccess ? a.nslots : 0;
 }
 
