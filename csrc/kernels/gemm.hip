@@ -761,6 +761,24 @@ DTF_API int dtf_set_pw_dgrad(int on) {
   g_pw_dgrad = on ? 1 : 0;
   return 0;
 }
+namespace dtf {
+int pw_wgrad_try(const void* X, const void* dY, float* dW, long P, int C, int K, int accumulate, float* ws,
+                 long ws_elems, hipStream_t st, bool split_out);
+}
+// DTF_PW_WGRAD=0 (or dtf_set_pw_wgrad(0)) keeps the 1x1 weight gradients on the general tiles (A/B switch)
+static int g_pw_wgrad = -1;
+static bool pwwgrad_enabled() {
+  if (g_pw_wgrad < 0) {
+    const char* e = getenv("DTF_PW_WGRAD");
+    g_pw_wgrad = e ? atoi(e) : 1;
+  }
+  return g_pw_wgrad != 0;
+}
+// 0 off, 1 single-tile filters, 2 also the two-tile ones
+DTF_API int dtf_set_pw_wgrad(int on) {
+  g_pw_wgrad = on;
+  return 0;
+}
 
 DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
@@ -924,6 +942,7 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int accumulate,
                            int splitk, int tile, float* ws, long ws_elems, void* stream) {
   if ((C & 7) || (K & 7)) return -1;
+  const int splitk_req = splitk;
   // the space-to-depth stem filter (4x4 x 16 channels -> 64): the register-staged 64-row tile beats the swapped
   // LDS-DMA default (tools/bench_stem.py: 251 vs 289 us at batch 256; round 1: 289 vs 309)
   if (tile < 0 && C == 16 && R == 4 && S == 4 && K == 64) tile = 3;
@@ -944,6 +963,10 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   a.splitk = splitk;
   a.kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;
   bool pointwise = R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0;
+  // small 1x1 filters over many pixels (ResNet-50 stages 1-2): the persistent kernel, whole filter tile per block
+  if (pointwise && tile < 0 && splitk_req <= 0 && pwwgrad_enabled() &&
+      pw_wgrad_try(X, dY, dW, (long)N * H * W, C, K, accumulate, ws, ws_elems, st, g_pw_wgrad == 2) == 0)
+    return 0;
   const bool small = (long)N * H * W * C * 2 < (1l << 31) && (long)N * P * Q * K * 2 < (1l << 31);
   // spatial filters: LDS-DMA staged 128x128 (measured best for every ResNet-50 3x3 filter); 1x1 filters keep
   // the register-staged kernels (tools/conv_roofline.py --only wgrad --tiles)
