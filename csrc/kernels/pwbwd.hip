@@ -1,0 +1,311 @@
+// Fused backward of a channel-REDUCING 1x1 stride-1 convolution (ResNet-50 stage-1 bottleneck c3 and stride-1
+// projection: K_out = 256 output channels from C_in = 64): ONE pass over dY computes both
+//   dX[p][c]  = sum_k dY[p][k] W[k][c]          (+ the BatchNorm-backward partial rows of dX, MODE 3 style), and
+//   dW[k][c] += sum_p dY[p][k] X[p][c]          (whole filter in the block's accumulators, one f32 partial per block).
+// The separate kernels read dY — the 4x-wide tensor, 4 of the 5 activation widths either of them reads — twice (the
+// dgrad on the main stream, the wgrad on the side stream: 1.64 GB each per layer at batch 1024). Here each 64-pixel
+// dY tile arrives once by LDS-DMA as a K-outer image that serves both products: the weight gradient reads it
+// transposed (ds_read_b64_tr_b16, frag_kouter's addressing), the data gradient row-wise (16-B reads at the same
+// swizzled chunks) against the filter held in registers. X (the layer input, 64 channels) rides in the same ring.
+// The dX tile is staged through LDS and stored as 16-B row chunks with the BN partials of the stored values.
+// Reference op: the Conv2D gradients of the model trainer/task.py:62-71 builds.
+#include "gemm_core.h"
+
+namespace dtf {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+struct PbArgs {
+  const bf16_t* dY;   // [P][K]
+  const bf16_t* X;    // [P][C]
+  const bf16_t* Wck;  // [C][K] (the conv filter as [C][1][1][K])
+  bf16_t* dX;         // [P][C]
+  const bf16_t* bnx;  // optional BN-backward partials of dX: BN input [P][C], its ReLU bits, batch mean
+  const uint8_t* bnmask;
+  const float* bnmean;
+  float* part;        // [slots][2C]
+  float* ws;          // [slots][K][C] weight-gradient partials
+  int P, tiles_p, slots;
+};
+
+template <int R>
+__device__ __forceinline__ v8bf tr_frag(const char* lds, int cb, int kk, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  v4s r[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = 32 * kk + 8 * G + 4 * h + q;
+    const int g = ((cb >> 2) + p) ^ (kouter_swz<R>(k) << 2);
+    const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, lds + k * (R * 2) + g * 8);
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r[h]) : "v"(addr));
+  }
+  v8s both = __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(v8bf, both);
+}
+
+// row fragment of the same K-outer image: pixel row pr + (lane & 15), channels 32 s + 8 (lane >> 4) .. +7
+template <int R>
+__device__ __forceinline__ v8bf row_frag(const char* lds, int pr, int s, int lane) {
+  const int row = pr + (lane & 15);
+  const int c16 = 4 * s + (lane >> 4);
+  const int pc = c16 ^ (kouter_swz<R>(row) << 1);
+  const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, lds + row * (R * 2) + pc * 16);
+  v4i r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return __builtin_bit_cast(v8bf, r);
+}
+
+template <int R>
+struct KoDma {  // LDS-DMA of a [64 pixel][R] slice into the K-outer image (pwwgrad.hip WgOperand)
+  static constexpr int L = R / 32;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int kr[L], coff[L];
+  __device__ __forceinline__ void init(const bf16_t* p, long rows) {
+    const int t = threadIdx.x;
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(rows * R * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int pb = i * 4096 + t * 16;
+      kr[i] = pb / (R * 2);
+      coff[i] = ((((pb % (R * 2)) >> 4) ^ (kouter_swz<R>(kr[i]) << 1)) * 16);
+    }
+  }
+  __device__ __forceinline__ void issue(int p0, int P, char* lds) {
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int p = p0 + kr[i];
+      const uint32_t off = p < P ? (uint32_t)(p * (R * 2) + coff[i]) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void*)(lds + i * 4096 + wave * 1024), 16, off, 0, 0, 0);
+    }
+  }
+};
+
+template <int K, int C>
+__global__ void __launch_bounds__(256, 1) pw_bwd_kernel(PbArgs a) {
+  static_assert(K == 256 && C == 64, "the stage-1 shape: 4 waves x 64 filter rows, 4 waves x 16 dX columns");
+  constexpr int IMG_Y = 64 * K * 2, IMG_X = 64 * C * 2, IMG = IMG_Y + IMG_X, NBUF = 3;
+  constexpr int LD = K / 32 + C / 32;     // DMA instructions per thread per tile
+  constexpr int SROW = C + 8;             // staged dX row (bf16), 16-B pad
+  constexpr int CH = C / 8;               // 16-B chunks per dX row
+  constexpr int ST = 64 * CH / 256;       // dX chunks per thread per tile
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * IMG + 64 * SROW * 2];
+  char* stg = smem + NBUF * IMG;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int slot = blockIdx.x;
+
+  // the wave's dgrad filter slice: W[c = 16 wave + (lane & 15)][k = 32 s + 8 (lane >> 4) .. +7]
+  v8bf fw[K / 32];
+#pragma unroll
+  for (int s = 0; s < K / 32; ++s)
+    fw[s] = *reinterpret_cast<const v8bf*>(a.Wck + (long)(16 * wave + (lane & 15)) * K + 32 * s + 8 * (lane >> 4));
+  // consume them here, before any DMA is in flight: otherwise the compiler places their vmcnt waits at the first
+  // MFMA inside the tile loop, where every iteration would then drain the prefetch
+#pragma unroll
+  for (int s = 0; s < K / 32; ++s) asm volatile("" ::"v"(fw[s]));
+
+  KoDma<K> dmy;
+  KoDma<C> dmx;
+  dmy.init(a.dY, a.P);
+  dmx.init(a.X, a.P);
+  auto issue = [&](int tile, int buf) {
+    char* img = smem + buf * IMG;
+    dmy.issue(tile * 64, a.P, img);
+    dmx.issue(tile * 64, a.P, img + IMG_Y);
+  };
+  const int step = a.slots;
+  const int n_mine = slot < a.tiles_p ? (a.tiles_p - slot + step - 1) / step : 0;
+  if (n_mine > 0) issue(slot, 0);
+  if (n_mine > 1) issue(slot + step, 1);
+
+  // BN partials of dX: this thread's 8-channel chunk is fixed (256 % CH == 0)
+  const int ch = t % CH, nch = ch * 8;
+  const __amdgpu_buffer_rsrc_t dxr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dX, (short)0, (int)((long)a.P * C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xbr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bnx, (short)0, a.bnmean ? (int)((long)a.P * C * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xmr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bnmask, (short)0, a.bnmask ? (int)((long)a.P * C / 8) : 0, 0x00020000);
+  const uint32_t xm_or = a.bnmask ? 0u : 0xFFu;
+  float mu[8], bs[8], bq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bs[j] = bq[j] = 0.f;
+    mu[j] = a.bnmean ? a.bnmean[nch + j] : 0.f;
+  }
+
+  v4f aw[4][4];  // weight gradient: wave rows k = 64 wave + 16 j, columns c = 16 i (acc[i][j]: lane 4 c of one k)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) aw[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+  for (int it = 0; it < n_mine; ++it) {
+    // tile `it` landed. Issued after it: tile it+1's DMA (a dummy one past the last tile; none when n_mine == 1 at
+    // it 0) and, from iteration 1 on, tile it-1's ST stores
+    if (it == 0) {
+      if (n_mine > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LD + ST) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int tile = slot + it * step;
+    // this tile's BN inputs and mask bytes, in flight under the MFMAs (issued before tile it+2's DMA)
+    uint4 xv[ST];
+    uint32_t xmb[ST];
+#pragma unroll
+    for (int k = 0; k < ST; ++k) {
+      const int p = tile * 64 + ((t + 256 * k) / CH);
+      const uint32_t e = (uint32_t)p * C + nch;
+      const bool ok = p < a.P;
+      xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbr, ok ? e * 2u : 0x80000000u, 0, 0));
+      xmb[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(xmr, ok ? e >> 3 : 0x80000000u, 0, 0);
+    }
+    // (issued unconditionally — past the last tile every row is out of range and the ring buffer no tile uses gets
+    // zeros — so the compiler's wait counts for the loads above stay the same on every iteration)
+    issue(it + 2 < n_mine ? slot + (it + 2) * step : a.tiles_p, (it + 2) % NBUF);
+    const char* img = smem + (it % NBUF) * IMG;
+
+    // ---- weight gradient: D[c][k] += X^T dY over this tile's 64 pixels
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8bf fx[4], fy[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fx[i] = tr_frag<C>(img + IMG_Y, 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fy[j] = tr_frag<K>(img, 64 * wave + 16 * j, kk, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(fx[i]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fy[j]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) aw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[i], fy[j], aw[i][j], 0, 0, 0);
+    }
+
+    // ---- data gradient: dX[p][16 wave ..] = dY[p][:] W[:][16 wave ..] (lane: pixel row, 4 consecutive c)
+    v4f ad[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ad[i] = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < K / 32; ++s) {
+      v8bf fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = row_frag<K>(img, 16 * i, s, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(fa[i]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ad[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[s], fa[i], ad[i], 0, 0, 0);
+    }
+    // stage the bf16 dX tile (inline-asm LDS stores: see pwconv.hip stage_write)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pl = 16 * i + (lane & 15), cl = 16 * wave + 4 * (lane >> 4);
+      uint2 o;
+      o.x = pack2bf(ad[i][0], ad[i][1]);
+      o.y = pack2bf(ad[i][2], ad[i][3]);
+      const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, stg + (pl * SROW + cl) * 2);
+      asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(o) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the tile is staged
+    // the BN loads are in: everything but tile it+2's DMA (issued after them) has completed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LD) : "memory");
+#pragma unroll
+    for (int k = 0; k < ST; ++k) {
+      const int pl = (t + 256 * k) / CH;
+      const int p = tile * 64 + pl;
+      uint4 val;
+      {
+        const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, stg + (pl * SROW + nch) * 2);
+        v4i r;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr) : "memory");
+        val = __builtin_bit_cast(uint4, r);
+      }
+      const uint32_t off = p < a.P ? ((uint32_t)p * C + nch) * 2u : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, val), dxr, off, 0, 0);
+      const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 2 * q + h;
+          const float dv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
+          const float xx = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
+          const float dz = (((xmb[k] | xm_or) >> r) & 1u) ? dv : 0.f;
+          bs[r] += dz;
+          bq[r] = fmaf(dz, xx - mu[r], bq[r]);
+        }
+    }
+  }
+
+  // ---- weight-gradient partial of this block: lane holds c = 16 i + 4 (lane >> 4) + r of k = 64 wave + 16 j + lane&15
+  float* slab = a.ws + (long)slot * K * C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 64 * wave + 16 * j + (lane & 15);
+      const int c = 16 * i + 4 * (lane >> 4);
+      *reinterpret_cast<float4*>(slab + (long)k * C + c) = make_float4(aw[i][j][0], aw[i][j][1], aw[i][j][2], aw[i][j][3]);
+    }
+  if (!a.bnmean) return;
+  // ---- one BN partial row per block: the 256 / CH threads of each chunk folded through LDS in a fixed order
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy DMA past the last tile has landed too
+  __syncthreads();  // every tile's reads of the ring are done
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[t * 16 + j] = bs[j];
+    red[t * 16 + 8 + j] = bq[j];
+  }
+  __syncthreads();
+  if (t < C) {
+    const int c8 = t >> 3, j = t & 7;
+    float sv = 0.f, qv = 0.f;
+    for (int u = c8; u < 256; u += CH) {
+      sv += red[u * 16 + j];
+      qv += red[u * 16 + 8 + j];
+    }
+    float* prow = a.part + (long)slot * 2 * C;
+    prow[t] = sv;
+    prow[C + t] = qv;
+  }
+}
+
+}  // namespace
+}  // namespace dtf
+
+// Fused data + weight gradient of a 1x1 stride-1 conv with K_out = 256, C_in = 64 over P pixels (see the top):
+// dX (bf16 [P][C]); dW (f32 [K][C]) = or += (accumulate) the weight gradient; with bnmean, the BatchNorm-backward
+// partial rows of dX (sum dz | sum dz (bnx - mean), dz = dX * bnmask bit) into part, *rows = their count.
+// ws: >= 256 * K * C floats. Returns 0, or -1 when the shape is not handled (nothing launched).
+DTF_API int dtf_pw_conv_bwd(const void* dY, const void* X, const void* Wck, void* dX, float* dW, int accumulate,
+                            const void* bnx, const void* bnmask, const float* bnmean, float* part, int* rows,
+                            float* ws, long ws_elems, long P, int K, int C, void* stream) {
+  using namespace dtf;
+  hipStream_t st = (hipStream_t)stream;
+  if (K != 256 || C != 64) return -1;
+  if (((uintptr_t)dY & 15) || ((uintptr_t)X & 15) || ((uintptr_t)Wck & 15) || ((uintptr_t)dX & 15) ||
+      ((uintptr_t)bnx & 15) || !ws || !dW)
+    return -1;
+  if (bnmean && (!bnx || !part)) return -1;
+  if (P * K * 2 >= (1l << 31) || P < 64 * 256) return -1;
+  PbArgs a{};
+  a.dY = (const bf16_t*)dY; a.X = (const bf16_t*)X; a.Wck = (const bf16_t*)Wck; a.dX = (bf16_t*)dX;
+  a.bnx = (const bf16_t*)bnx; a.bnmask = (const uint8_t*)bnmask; a.bnmean = bnmean; a.part = part; a.ws = ws;
+  a.P = (int)P;
+  a.tiles_p = (int)((P + 63) / 64);
+  a.slots = 256;
+  if ((long)a.slots * K * C > ws_elems) return -1;
+  hipLaunchKernelGGL((pw_bwd_kernel<256, 64>), dim3(a.slots), dim3(256), 0, st, a);
+  if (hipGetLastError() != hipSuccess) return -1;
+  dtf_sum_rows(ws, (long)K * C, a.slots, (long)K * C, dW, accumulate, st);
+  if (rows) *rows = bnmean ? a.slots : 0;
+  return (int)hipGetLastError();
+}

@@ -95,6 +95,36 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=N
     return dx
 
 
+def pw_bwd_ok(g, M_min=64 * 256):
+    """Shapes of the fused 1x1 data + weight gradient (pwbwd.hip): stride-1 unpadded 1x1, K_out 256 from C_in 64
+    (ResNet-50 stage-1 c3 and stride-1 projection), >= 256 pixel tiles, tensors < 2 GiB."""
+    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw = g[:13]
+    M = N * P * Q
+    return ((R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0) and K == 256 and C == 64 and M >= M_min
+            and M * K * 2 < (1 << 31))
+
+
+def conv_bwd_fused_raw(dy, x, w_master, g, dw_out, bn=None):
+    """dX (bf16) and dW += (into the f32 arena gradient dw_out) of a pw_bwd_ok conv in ONE pass over dy
+    (pwbwd.hip); with `bn` (the _BNSource of the BatchNorm that produced x, see conv_dgrad_raw) the BN-backward
+    partial rows of dX go to it."""
+    N, H, W, C, K = g[:5]
+    M = N * H * W
+    wc = crsk_shadow(w_master, K, 1, C)
+    dx = torch.empty((N, H, W, C), dtype=BF16, device=dy.device)
+    ws = workspace(dy.device)
+    part = rows = None
+    if bn is not None:
+        part = torch.empty(256 * 2 * C, dtype=F32, device=dy.device)
+        rows = IntOut()
+    bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
+    call("dtf_pw_conv_bwd", ptr(dy), ptr(x), ptr(wc), ptr(dx), ptr(dw_out), 1, *bn_ptrs, ptr(part),
+         rows.addr if rows else None, ptr(ws), ws.numel(), M, K, C, stream())
+    if bn is not None:
+        bn.provide(dx, part, rows.value)
+    return dx
+
+
 def conv_wgrad_raw(x, dy, g, out=None):
     """dW [K,R,S,C] f32; with `out` (an arena gradient view) the result is accumulated into it."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
@@ -246,6 +276,9 @@ _COMPACT_PROJ = True
 # Two-pass forward of the channel-expanding 1x1 ConvBN (statistics pass + recomputed product with the BN apply in its
 # epilogue, pwconv.hip dtf_conv_bn_apply_fwd) instead of conv(+stats) -> finalize -> standalone apply pass.
 _TWO_PASS_PW = os.environ.get("DTF_PW2", "1") != "0"
+# Fused data + weight gradient of the stage-1 channel-reducing 1x1 convs (pwbwd.hip): one read of dY for both,
+# the weight gradient on the main stream instead of the side stream.
+_FUSED_PW_BWD = os.environ.get("DTF_PW_BWD", "1") != "0"
 
 
 def _two_pass_ok(g):
@@ -384,8 +417,19 @@ class _ConvBNFn(torch.autograd.Function):
         elif link is not None and role == "res":
             dres = link.park(dres)
         dx = dw = None
+        tw = direct_grad(w) if ctx.needs_input_grad[1] else None
+        if (_FUSED_PW_BWD and tw is not None and ctx.needs_input_grad[0] and role != "acc" and pw_bwd_ok(g)
+                and x.is_contiguous() and x.dtype == BF16):
+            src = ctx.in_src
+            complete = src is not None and role != "proj" and src.consumers == 1
+            dx = conv_bwd_fused_raw(dyc, x, w, g, tw, bn=src if complete else None)
+            if link is not None and role == "proj":
+                dx = link.park(dx)
+            ctx.in_src = None
+            if direct_bn:
+                dgamma = dbeta = None
+            return dx, None, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
         if ctx.needs_input_grad[1]:
-            tw = direct_grad(w)
             if tw is not None and SIDE_STREAM_ON:
                 with fork_side(x.device, x, dyc):  # off the critical path: overlaps the dgrad chain
                     conv_wgrad_raw(x, dyc, g, out=tw)

@@ -1,0 +1,121 @@
+"""Fused data + weight gradient of the ResNet-50 stage-1 channel-reducing 1x1 conv (csrc/kernels/pwbwd.hip,
+dtf_pw_conv_bwd): one pass over dY gives dX (+ the BatchNorm-backward partial rows of dX) and dW.
+
+dX must equal, BITWISE, the separate data-gradient GEMM (same k order per MFMA chain); dW and the partial sums agree
+with the separate kernels to f32 summation order, and all three with a plain PyTorch fp32 reference. At block level
+the gradients of three stage-1 bottlenecks with the fused path on and off agree to that summation order. The
+reference's op is the gradient of the Conv2D the ResNet-50 trainer builds (trainer/task.py:62-71)."""
+import ctypes
+
+import pytest
+import torch
+
+from distributed_tensorflow_amd.ops import conv as OC
+from distributed_tensorflow_amd.ops._util import call, ptr, stream
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+F32 = torch.float32
+
+
+def _bits(b):
+    M, N = b.shape
+    w = (1 << torch.arange(8, device=b.device, dtype=torch.int32))
+    return (b.view(M, N // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8).view(-1)
+
+
+@pytest.mark.parametrize("P", [16384, 50000, 200003])
+@pytest.mark.parametrize("with_bn", [False, True])
+def test_pw_bwd_matches_separate_kernels(cuda, P, with_bn):
+    K, C = 256, 64
+    g = torch.Generator(device="cpu").manual_seed(P + int(with_bn))
+    dy = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    x = torch.relu(torch.randn(P, C, generator=g)).to(BF).to(cuda)
+    wck = (torch.randn(C, K, generator=g) * K ** -0.5).to(BF).to(cuda)  # [C][1][1][K]
+    dw0 = torch.randn(K, C, generator=g).to(cuda)
+    bnx = _bits(torch.rand(P, C, generator=g) > 0.5) if with_bn else None
+    bn = (torch.randn(P, C, generator=g).to(BF).to(cuda), bnx.to(cuda),
+          (torch.randn(C, generator=g) * 0.1).to(cuda)) if with_bn else (None, None, None)
+    ws = torch.empty(32 << 20, dtype=F32, device=cuda)
+    # fused
+    dx = torch.full((P, C), float("nan"), dtype=BF, device=cuda)
+    dw = dw0.clone()
+    part = torch.full((256 * 2 * C,), float("nan"), device=cuda) if with_bn else None
+    rows = ctypes.c_int(0)
+    call("dtf_pw_conv_bwd", ptr(dy), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1, ptr(bn[0]), ptr(bn[1]), ptr(bn[2]),
+         ptr(part), ctypes.addressof(rows), ptr(ws), ws.numel(), P, K, C, stream())
+    # separate: data gradient (general tile) and weight gradient
+    dx2 = torch.empty(P, C, dtype=BF, device=cuda)
+    part2 = torch.empty((((P + 63) // 64) + 1) * 2 * C, device=cuda) if with_bn else None
+    rows2 = ctypes.c_int(0)
+    call("dtf_set_pw_dgrad", 0)
+    try:
+        call("dtf_conv_dgrad_x", ptr(dy), ptr(wck), ptr(dx2), P, 1, 1, C, K, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0.0,
+             ptr(ws), 16, ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part2),
+             ctypes.addressof(rows2) if with_bn else None, None, None, stream())
+    finally:
+        call("dtf_set_pw_dgrad", 1)
+    dw2 = dw0.clone()
+    call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw2), P, 1, 1, C, K, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1, 0, -1,
+         ptr(ws), ws.numel(), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx.view(torch.int16), dx2.view(torch.int16)), "dX differs from the separate dgrad"
+    ref_dx = dy.float() @ wck.float().t()
+    assert torch.allclose(dx.float(), ref_dx, atol=3e-2, rtol=2e-2)
+    ref_dw = dw0 + dy.float().t() @ x.float()
+    scale = ref_dw.abs().max().item()
+    assert (dw - ref_dw).abs().max().item() <= 1e-4 * scale + 1e-3
+    assert (dw - dw2).abs().max().item() <= 1e-4 * scale + 1e-3
+    if with_bn:
+        assert rows.value == 256
+        s1 = part.view(256, 2 * C).sum(0)
+        s2 = part2[: rows2.value * 2 * C].view(rows2.value, 2 * C).sum(0)
+        sc = s2.abs().max().item() + 1.0
+        assert torch.allclose(s1, s2, atol=1e-4 * sc, rtol=1e-4)
+
+
+def test_pw_bwd_block_gradients(cuda, monkeypatch):
+    """Three stage-1 bottlenecks (the projection block and two identity blocks: every c3 and the stride-1 projection
+    take the fused path) trained the framework's way (arena gradients, direct accumulation): the gradients with the
+    fused path on and off agree to f32 summation order."""
+    from distributed_tensorflow_amd.keras import initializers
+    from distributed_tensorflow_amd.models import resnet as R
+    from distributed_tensorflow_amd.ops._util import direct_grads
+    from distributed_tensorflow_amd.variables import ParamArena
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(64, 16, 16, 64, generator=g).to(cuda).to(BF)
+    runs = {}
+    seen = {}
+    real_call = OC.call
+
+    def spy(name, *args):
+        seen[name] = seen.get(name, 0) + 1
+        return real_call(name, *args)
+
+    monkeypatch.setattr(OC, "call", spy)
+    for fused in (False, True):
+        monkeypatch.setattr(OC, "_FUSED_PW_BWD", fused)
+        initializers.set_seed(3)
+        blocks = [R.Bottleneck(64, stride=1, project=True), R.Bottleneck(64), R.Bottleneck(64)]
+        with torch.no_grad():
+            h = x
+            for b in blocks:
+                h = b(h, training=False)
+        params = [w for b in blocks for w in b.trainable_weights]
+        arena = ParamArena(params, device=cuda)
+        seen.clear()
+        xx = x.clone().requires_grad_(True)
+        h = xx
+        for b in blocks:
+            h = b(h, training=True)
+        loss = (h.float() * torch.linspace(-1, 1, h.shape[-1], device=cuda)).square().mean()
+        with direct_grads():
+            loss.backward()
+        torch.cuda.synchronize()
+        runs[fused] = [xx.grad.float(), arena.grad.clone()]
+        assert seen.get("dtf_pw_conv_bwd", 0) == (4 if fused else 0), seen
+    for a, b in zip(runs[False], runs[True]):
+        assert torch.isfinite(b).all()
+        err = (a - b).norm().item() / (a.norm().item() + 1e-12)
+        assert err < 1e-2, err
