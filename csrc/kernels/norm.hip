@@ -1064,6 +1064,15 @@ static void bn_bwd_finalize_launch(float* part, int G, const float* mean, const 
                      dgamma, dbeta, accumulate, coef);
 }
 
+// Finalize only: sum the T partial rows [T][2C] in `part` (scratch) into dgamma/dbeta and the apply coefficients
+// coef (3*C) — for a consumer that applies them itself (pwbwd.hip dtf_pw_conv_bwd_bn).
+DTF_API int dtf_bn_bwd_coef(float* part, int T, const float* mean, const float* invstd, const float* gamma, long M,
+                            int C, float* dgamma, float* dbeta, int accumulate, float* coef, void* stream) {
+  if ((C & 7) || T < 1 || !part || !coef) return -1;
+  bn_bwd_finalize_launch(part, T, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
 static int bn_bwd_tail(const void* dy, const void* ymask, const void* mbits, const void* x, const float* mean,
                        const float* invstd, const float* gamma, long M, int C, void* dx, void* dz_out, float* dgamma,
                        float* dbeta, int accumulate, float* part, int G, float* coef, hipStream_t st,

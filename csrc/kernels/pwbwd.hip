@@ -278,6 +278,259 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_kernel(PbArgs a) {
   }
 }
 
+// ---- the same with the BatchNorm(+ReLU) backward of the conv's output folded in: dY = a dz + b y + c per channel
+// (dz = dout where the ReLU bit is set, else 0; y the conv output; a, b, c from bn_bwd_finalize) is computed per
+// tile from dout / y / the mask bits in registers — bn_bwd_apply_row's arithmetic, bitwise the same bf16 dY — and
+// written into the K-outer image by this kernel, so the standalone apply pass (read dout + y, write dY) and this
+// kernel's read of dY disappear. The next tile's dout / y / mask chunks are loaded into registers while this tile
+// is multiplied; dY images are double-buffered, X keeps its 3-deep LDS-DMA ring.
+struct PbnArgs {
+  PbArgs b;
+  const bf16_t* dout;   // [P][K] gradient of the BN(+ReLU) output
+  const bf16_t* y;      // [P][K] BN input (the conv output)
+  const uint8_t* ymask; // [P][K] ReLU bits (nullptr: no ReLU)
+  const float* coef;    // [3][K]
+};
+
+template <int K, int C>
+__global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
+  static_assert(K == 256 && C == 64, "the stage-1 shape");
+  const PbArgs& a = A.b;
+  constexpr int IMG_Y = 64 * K * 2, IMG_X = 64 * C * 2;
+  constexpr int LDX = C / 32;             // X DMA instructions per thread per tile
+  constexpr int U = 64 * (K / 8) / 256;   // dY chunks per thread per tile (8)
+  constexpr int LR = 3 * U;               // register loads per thread per tile (dout, y, mask byte)
+  constexpr int SROW = C + 8, CH = C / 8, ST = 64 * CH / 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG_Y + 3 * IMG_X + 64 * SROW * 2];
+  char* ximg = smem + 2 * IMG_Y;
+  char* stg = ximg + 3 * IMG_X;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int slot = blockIdx.x;
+
+  v8bf fw[K / 32];
+#pragma unroll
+  for (int s = 0; s < K / 32; ++s)
+    fw[s] = *reinterpret_cast<const v8bf*>(a.Wck + (long)(16 * wave + (lane & 15)) * K + 32 * s + 8 * (lane >> 4));
+  // this thread's dY channel chunk (fixed) and its BN-backward coefficients
+  const int cy = t % (K / 8), ry = t / (K / 8);  // rows ry + 8 u
+  float ka[8], kb[8], kc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ka[j] = A.coef[cy * 8 + j];
+    kb[j] = A.coef[K + cy * 8 + j];
+    kc[j] = A.coef[2 * K + cy * 8 + j];
+  }
+#pragma unroll
+  for (int s = 0; s < K / 32; ++s) asm volatile("" ::"v"(fw[s]));  // (see pw_bwd_kernel)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(ka[j]), "v"(kb[j]), "v"(kc[j]));
+
+  const __amdgpu_buffer_rsrc_t dr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A.dout, (short)0, (int)((long)a.P * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A.y, (short)0, (int)((long)a.P * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)A.ymask, (short)0, A.ymask ? (int)((long)a.P * K / 8) : 0, 0x00020000);
+  const uint32_t ym_or = A.ymask ? 0u : 0xFFu;
+  uint4 dv[U], yv[U];
+  uint32_t mb[U];
+  auto load_tile = [&](int tile) {  // past the last tile (tile == tiles_p) every row is out of range: zeros
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = tile * 64 + ry + 8 * u;
+      const uint32_t e = (uint32_t)p * K + cy * 8;
+      const bool ok = p < a.P;
+      dv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? e * 2u : 0x80000000u, 0, 0));
+      yv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, ok ? e * 2u : 0x80000000u, 0, 0));
+      mb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mr, ok ? e >> 3 : 0x80000000u, 0, 0);
+    }
+  };
+  auto transform = [&](int tile, char* img) {  // dY = a dz + b y + c -> bf16 -> the K-outer image
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = ry + 8 * u;
+      const bool ok = tile * 64 + row < a.P;
+      const uint32_t dw_[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w}, yw[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
+      const uint32_t bits = mb[u] | ym_or;
+      float o[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * q + h;
+          float d = __uint_as_float(h ? (dw_[q] & 0xffff0000u) : (dw_[q] << 16));
+          const float yy = __uint_as_float(h ? (yw[q] & 0xffff0000u) : (yw[q] << 16));
+          if (!((bits >> j) & 1u)) d = 0.f;
+          o[j] = ok ? fmaf(ka[j], d, fmaf(kb[j], yy, kc[j])) : 0.f;
+        }
+      const v4i w4 = {(int)pack2bf(o[0], o[1]), (int)pack2bf(o[2], o[3]), (int)pack2bf(o[4], o[5]),
+                      (int)pack2bf(o[6], o[7])};
+      const int pc = cy ^ (kouter_swz<K>(row) << 1);
+      const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, img + row * (K * 2) + pc * 16);
+      asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(w4) : "memory");
+    }
+  };
+
+  KoDma<C> dmx;
+  dmx.init(a.X, a.P);
+  const int step = a.slots;
+  const int n_mine = slot < a.tiles_p ? (a.tiles_p - slot + step - 1) / step : 0;
+  auto tile_of = [&](int i) { return i < n_mine ? slot + i * step : a.tiles_p; };
+  // prologue, in this order: X tile 0, registers of tile 0, X tile 1
+  dmx.issue(tile_of(0) * 64, a.P, ximg);
+  load_tile(tile_of(0));
+  dmx.issue(tile_of(1) * 64, a.P, ximg + IMG_X);
+
+  const int ch = t % CH, nch = ch * 8;
+  const __amdgpu_buffer_rsrc_t dxr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dX, (short)0, (int)((long)a.P * C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xbr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bnx, (short)0, a.bnmean ? (int)((long)a.P * C * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xmr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bnmask, (short)0, a.bnmask ? (int)((long)a.P * C / 8) : 0, 0x00020000);
+  const uint32_t xm_or = a.bnmask ? 0u : 0xFFu;
+  float mu[8], bs[8], bq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bs[j] = bq[j] = 0.f;
+    mu[j] = a.bnmean ? a.bnmean[nch + j] : 0.f;
+  }
+  v4f aw[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) aw[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+  for (int it = 0; it < n_mine; ++it) {
+    // this tile's registers and X image are in. Issued after them: X of tile it+1 (LDX) and, from iteration 1 on,
+    // the ST dX stores of tile it-1
+    if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LDX) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LDX + ST) : "memory");
+    const int tile = slot + it * step;
+    char* yimg = smem + (it & 1) * IMG_Y;
+    const char* xim = ximg + (it % 3) * IMG_X;
+    transform(tile, yimg);
+    // every wave's dY share is written, every wave's X share landed; every wave is done with the dY image and the X
+    // buffer that this iteration's loads below refill
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    uint4 xv[ST];
+    uint32_t xmb[ST];
+#pragma unroll
+    for (int k = 0; k < ST; ++k) {
+      const int p = tile * 64 + ((t + 256 * k) / CH);
+      const uint32_t e = (uint32_t)p * C + nch;
+      const bool ok = p < a.P;
+      xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbr, ok ? e * 2u : 0x80000000u, 0, 0));
+      xmb[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(xmr, ok ? e >> 3 : 0x80000000u, 0, 0);
+    }
+    load_tile(tile_of(it + 1));
+    dmx.issue(tile_of(it + 2) * 64, a.P, ximg + ((it + 2) % 3) * IMG_X);
+
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v8bf fx[4], fy[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fx[i] = tr_frag<C>(xim, 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fy[j] = tr_frag<K>(yimg, 64 * wave + 16 * j, kk, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(fx[i]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fy[j]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) aw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[i], fy[j], aw[i][j], 0, 0, 0);
+    }
+    v4f ad[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ad[i] = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < K / 32; ++s) {
+      v8bf fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = row_frag<K>(yimg, 16 * i, s, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(fa[i]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ad[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[s], fa[i], ad[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pl = 16 * i + (lane & 15), cl = 16 * wave + 4 * (lane >> 4);
+      uint2 o;
+      o.x = pack2bf(ad[i][0], ad[i][1]);
+      o.y = pack2bf(ad[i][2], ad[i][3]);
+      const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, stg + (pl * SROW + cl) * 2);
+      asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(o) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the tile is staged
+    // the BN loads are in: issued after them, the next tile's registers (LR) and X image (LDX)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LR + LDX) : "memory");
+#pragma unroll
+    for (int k = 0; k < ST; ++k) {
+      const int pl = (t + 256 * k) / CH;
+      const int p = tile * 64 + pl;
+      uint4 val;
+      {
+        const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, stg + (pl * SROW + nch) * 2);
+        v4i r;
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr) : "memory");
+        val = __builtin_bit_cast(uint4, r);
+      }
+      const bool ok = p < a.P;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, val), dxr,
+                                             ok ? ((uint32_t)p * C + nch) * 2u : 0x80000000u, 0, 0);
+      const uint32_t bits = ok ? (xmb[k] | xm_or) : 0u;
+      const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, xw[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 2 * q + h;
+          const float dvv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
+          const float xx = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
+          const float dz = ((bits >> r) & 1u) ? dvv : 0.f;
+          bs[r] += dz;
+          bq[r] = fmaf(dz, xx - mu[r], bq[r]);
+        }
+    }
+  }
+
+  float* slab = a.ws + (long)slot * K * C;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 64 * wave + 16 * j + (lane & 15);
+      const int c = 16 * i + 4 * (lane >> 4);
+      *reinterpret_cast<float4*>(slab + (long)k * C + c) = make_float4(aw[i][j][0], aw[i][j][1], aw[i][j][2], aw[i][j][3]);
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy loads / DMA past the last tile have landed too
+  if (!a.bnmean) return;
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[t * 16 + j] = bs[j];
+    red[t * 16 + 8 + j] = bq[j];
+  }
+  __syncthreads();
+  if (t < C) {
+    const int c8 = t >> 3, j = t & 7;
+    float sv = 0.f, qv = 0.f;
+    for (int u = c8; u < 256; u += CH) {
+      sv += red[u * 16 + j];
+      qv += red[u * 16 + 8 + j];
+    }
+    float* prow = a.part + (long)slot * 2 * C;
+    prow[t] = sv;
+    prow[C + t] = qv;
+  }
+}
+
 }  // namespace
 }  // namespace dtf
 
@@ -304,6 +557,37 @@ DTF_API int dtf_pw_conv_bwd(const void* dY, const void* X, const void* Wck, void
   a.slots = 256;
   if ((long)a.slots * K * C > ws_elems) return -1;
   hipLaunchKernelGGL((pw_bwd_kernel<256, 64>), dim3(a.slots), dim3(256), 0, st, a);
+  if (hipGetLastError() != hipSuccess) return -1;
+  dtf_sum_rows(ws, (long)K * C, a.slots, (long)K * C, dW, accumulate, st);
+  if (rows) *rows = bnmean ? a.slots : 0;
+  return (int)hipGetLastError();
+}
+
+// dtf_pw_conv_bwd with the conv output's BatchNorm(+ReLU) backward applied on the fly (see pw_bwd_bn_kernel):
+// dY = a dz + b y + c from dout, y, the ReLU bits ymask (nullptr: none) and coef [3][K] (bn_bwd_finalize's
+// coefficients, dtf_bn_bwd_coef); dY itself is never stored.
+DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymask, const float* coef, const void* X,
+                               const void* Wck, void* dX, float* dW, int accumulate, const void* bnx,
+                               const void* bnmask, const float* bnmean, float* part, int* rows, float* ws,
+                               long ws_elems, long P, int K, int C, void* stream) {
+  using namespace dtf;
+  hipStream_t st = (hipStream_t)stream;
+  if (K != 256 || C != 64 || !coef) return -1;
+  if (((uintptr_t)dout & 15) || ((uintptr_t)y & 15) || ((uintptr_t)X & 15) || ((uintptr_t)Wck & 15) ||
+      ((uintptr_t)dX & 15) || ((uintptr_t)bnx & 15) || !ws || !dW)
+    return -1;
+  if (bnmean && (!bnx || !part)) return -1;
+  if (P * K * 2 >= (1l << 31) || P < 64 * 256) return -1;
+  PbnArgs A{};
+  PbArgs& a = A.b;
+  a.X = (const bf16_t*)X; a.Wck = (const bf16_t*)Wck; a.dX = (bf16_t*)dX;
+  a.bnx = (const bf16_t*)bnx; a.bnmask = (const uint8_t*)bnmask; a.bnmean = bnmean; a.part = part; a.ws = ws;
+  a.P = (int)P;
+  a.tiles_p = (int)((P + 63) / 64);
+  a.slots = 256;
+  A.dout = (const bf16_t*)dout; A.y = (const bf16_t*)y; A.ymask = (const uint8_t*)ymask; A.coef = coef;
+  if ((long)a.slots * K * C > ws_elems) return -1;
+  hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64>), dim3(a.slots), dim3(256), 0, st, A);
   if (hipGetLastError() != hipSuccess) return -1;
   dtf_sum_rows(ws, (long)K * C, a.slots, (long)K * C, dW, accumulate, st);
   if (rows) *rows = bnmean ? a.slots : 0;

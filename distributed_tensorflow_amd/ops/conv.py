@@ -125,6 +125,26 @@ def conv_bwd_fused_raw(dy, x, w_master, g, dw_out, bn=None):
     return dx
 
 
+def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None):
+    """conv_bwd_fused_raw with dy = a*dz + b*y + c (the BatchNorm(+ReLU) backward of y = conv output, coefficients
+    coef [3K] from dtf_bn_bwd_coef, dz = dout under the ReLU bits ymask) computed inside the kernel."""
+    N, H, W, C, K = g[:5]
+    M = N * H * W
+    wc = crsk_shadow(w_master, K, 1, C)
+    dx = torch.empty((N, H, W, C), dtype=BF16, device=dout.device)
+    ws = workspace(dout.device)
+    part = rows = None
+    if bn is not None:
+        part = torch.empty(256 * 2 * C, dtype=F32, device=dout.device)
+        rows = IntOut()
+    bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
+    call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ymask), ptr(coef), ptr(x), ptr(wc), ptr(dx), ptr(dw_out), 1,
+         *bn_ptrs, ptr(part), rows.addr if rows else None, ptr(ws), ws.numel(), M, K, C, stream())
+    if bn is not None:
+        bn.provide(dx, part, rows.value)
+    return dx
+
+
 def conv_wgrad_raw(x, dy, g, out=None):
     """dW [K,R,S,C] f32; with `out` (an arena gradient view) the result is accumulated into it."""
     N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
@@ -278,7 +298,9 @@ _COMPACT_PROJ = True
 _TWO_PASS_PW = os.environ.get("DTF_PW2", "1") != "0"
 # Fused data + weight gradient of the stage-1 channel-reducing 1x1 convs (pwbwd.hip): one read of dY for both,
 # the weight gradient on the main stream instead of the side stream.
-_FUSED_PW_BWD = os.environ.get("DTF_PW_BWD", "1") != "0"
+# Level 2 also folds the conv output's BatchNorm(+ReLU) backward into that pass when its reduction is already done
+# (identity blocks: dY = a dz + b y + c computed per tile, never stored: the standalone apply pass disappears).
+_FUSED_PW_BWD = int(os.environ.get("DTF_PW_BWD", "2"))
 
 
 def _two_pass_ok(g):
@@ -397,6 +419,26 @@ class _ConvBNFn(torch.autograd.Function):
         if rsrc is not None:  # projection shortcut BN: its backward reduction rides on our apply pass
             part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=yc.device), IntOut()
             sc = (ptr(rsrc.yc), ptr(rsrc.mean), ptr(part2), rows2.addr)
+        if (fused is not None and lazy_res and rsrc is None and _FUSED_PW_BWD >= 2 and ctx.needs_input_grad[0]
+                and ctx.needs_input_grad[1] and pw_bwd_ok(g) and x.is_contiguous() and x.dtype == BF16):
+            tw = direct_grad(w)
+            if tw is not None:
+                # identity-block c3: finalize the BN-backward reduction only, then ONE pass computes dY per tile from
+                # dout / yc / the ReLU bits and both conv gradients from it (dY is never stored)
+                coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+                call("dtf_bn_bwd_coef", ptr(fused[1]), fused[2], ptr(mean), ptr(invstd), ptr(gamma), M, K,
+                     ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(coef), stream())
+                src = ctx.in_src
+                complete = src is not None and src.consumers == 1
+                dx = conv_bwd_bn_fused_raw(dout, yc, mbits, coef, x, w, g, tw, bn=src if complete else None)
+                # the identity shortcut's gradient: dout parked with the ReLU mask (read above, in stream order, before
+                # the first conv's dgrad overwrites it)
+                link.park(dout, mask=mbits)
+                ctx.in_src = ctx.src = ctx.res_src = None
+                if direct_bn:
+                    dgamma = dbeta = None
+                return (dx, None, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None,
+                        None)
         if fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
             coef = torch.empty(3 * K, dtype=F32, device=yc.device)
             call("dtf_bn_bwd_partials", ptr(dout), ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
@@ -418,7 +460,7 @@ class _ConvBNFn(torch.autograd.Function):
             dres = link.park(dres)
         dx = dw = None
         tw = direct_grad(w) if ctx.needs_input_grad[1] else None
-        if (_FUSED_PW_BWD and tw is not None and ctx.needs_input_grad[0] and role != "acc" and pw_bwd_ok(g)
+        if (_FUSED_PW_BWD >= 1 and tw is not None and ctx.needs_input_grad[0] and role != "acc" and pw_bwd_ok(g)
                 and x.is_contiguous() and x.dtype == BF16):
             src = ctx.in_src
             complete = src is not None and role != "proj" and src.consumers == 1

@@ -75,10 +75,55 @@ def test_pw_bwd_matches_separate_kernels(cuda, P, with_bn):
         assert torch.allclose(s1, s2, atol=1e-4 * sc, rtol=1e-4)
 
 
-def test_pw_bwd_block_gradients(cuda, monkeypatch):
-    """Three stage-1 bottlenecks (the projection block and two identity blocks: every c3 and the stride-1 projection
-    take the fused path) trained the framework's way (arena gradients, direct accumulation): the gradients with the
-    fused path on and off agree to f32 summation order."""
+@pytest.mark.parametrize("P", [16384, 200003])
+def test_pw_bwd_bn_matches_apply_then_fused(cuda, P):
+    """dtf_pw_conv_bwd_bn (dY computed per tile from dout, y, the ReLU bits and the BN-backward coefficients) equals
+    the standalone apply pass (dtf_bn_bwd_apply_coef) followed by dtf_pw_conv_bwd: dX bitwise, dW and the partials
+    to f32 summation order."""
+    K, C = 256, 64
+    g = torch.Generator(device="cpu").manual_seed(P)
+    dout = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    y = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    ym = _bits(torch.rand(P, K, generator=g) > 0.3).to(cuda)
+    coef = torch.cat([torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1,
+                      torch.randn(K, generator=g) * 0.01]).to(cuda)
+    x = torch.relu(torch.randn(P, C, generator=g)).to(BF).to(cuda)
+    wck = (torch.randn(C, K, generator=g) * K ** -0.5).to(BF).to(cuda)
+    bn = (torch.randn(P, C, generator=g).to(BF).to(cuda), _bits(torch.rand(P, C, generator=g) > 0.5).to(cuda),
+          (torch.randn(C, generator=g) * 0.1).to(cuda))
+    ws = torch.empty(32 << 20, dtype=F32, device=cuda)
+    dx = torch.full((P, C), float("nan"), dtype=BF, device=cuda)
+    dw = torch.zeros(K, C, device=cuda)
+    part = torch.full((256 * 2 * C,), float("nan"), device=cuda)
+    rows = ctypes.c_int(0)
+    call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
+         ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part), ctypes.addressof(rows), ptr(ws), ws.numel(), P, K, C,
+         stream())
+    dyc = torch.empty(P, K, dtype=BF, device=cuda)
+    call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(ym), ptr(y), P, K, ptr(dyc), None, ptr(coef), None, None, None,
+         None, stream())
+    dx2 = torch.full((P, C), float("nan"), dtype=BF, device=cuda)
+    dw2 = torch.zeros(K, C, device=cuda)
+    part2 = torch.full((256 * 2 * C,), float("nan"), device=cuda)
+    rows2 = ctypes.c_int(0)
+    call("dtf_pw_conv_bwd", ptr(dyc), ptr(x), ptr(wck), ptr(dx2), ptr(dw2), 1, ptr(bn[0]), ptr(bn[1]), ptr(bn[2]),
+         ptr(part2), ctypes.addressof(rows2), ptr(ws), ws.numel(), P, K, C, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx.view(torch.int16), dx2.view(torch.int16))
+    assert torch.equal(dw, dw2)  # same dY bits, same kernel structure and reduction order
+    assert torch.equal(part, part2)
+    # and the dY the kernel used is the fp32 formula
+    bits = ((ym.view(-1, 1) >> torch.arange(8, device=cuda, dtype=torch.uint8)) & 1).view(P, K).float()
+    ref = (coef[:K] * dout.float() * bits + coef[K:2 * K] * y.float() + coef[2 * K:]).to(BF)
+    assert (ref.float() - dyc.float()).abs().max().item() <= 1e-2 * ref.float().abs().max().item()
+
+
+@pytest.mark.parametrize("level", [1, 2])
+def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
+    """Three stage-1 bottlenecks trained the framework's way (arena gradients, direct accumulation). Level 1: every c3
+    and the stride-1 projection take the fused data + weight gradient; level 2: the middle block's c3 (identity
+    block whose BN-backward reduction its consumer already took) also folds the BatchNorm backward in. Gradients agree
+    with the unfused path to f32 summation order."""
     from distributed_tensorflow_amd.keras import initializers
     from distributed_tensorflow_amd.models import resnet as R
     from distributed_tensorflow_amd.ops._util import direct_grads
@@ -94,8 +139,8 @@ def test_pw_bwd_block_gradients(cuda, monkeypatch):
         return real_call(name, *args)
 
     monkeypatch.setattr(OC, "call", spy)
-    for fused in (False, True):
-        monkeypatch.setattr(OC, "_FUSED_PW_BWD", fused)
+    for lv in (0, level):
+        monkeypatch.setattr(OC, "_FUSED_PW_BWD", lv)
         initializers.set_seed(3)
         blocks = [R.Bottleneck(64, stride=1, project=True), R.Bottleneck(64), R.Bottleneck(64)]
         with torch.no_grad():
@@ -113,9 +158,10 @@ def test_pw_bwd_block_gradients(cuda, monkeypatch):
         with direct_grads():
             loss.backward()
         torch.cuda.synchronize()
-        runs[fused] = [xx.grad.float(), arena.grad.clone()]
-        assert seen.get("dtf_pw_conv_bwd", 0) == (4 if fused else 0), seen
-    for a, b in zip(runs[False], runs[True]):
+        runs[lv] = [xx.grad.float(), arena.grad.clone()]
+        want = {0: (0, 0), 1: (4, 0), 2: (3, 1)}[lv]
+        assert (seen.get("dtf_pw_conv_bwd", 0), seen.get("dtf_pw_conv_bwd_bn", 0)) == want, seen
+    for a, b in zip(runs[0], runs[level]):
         assert torch.isfinite(b).all()
         err = (a - b).norm().item() / (a.norm().item() + 1e-12)
         assert err < 1e-2, err
