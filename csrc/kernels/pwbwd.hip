@@ -292,27 +292,39 @@ struct PbnArgs {
   const float* coef;    // [3][K]
 };
 
-template <int K, int C>
+// <K, C, BMP, CB>: BMP pixels per tile; each block owns CB of the C columns (C / CB blocks per pixel slot, on one XCD
+// and in step, so the second one's dout / y reads hit L2): dX[:, its CB] and dW[:, its CB]. Waves split dW by K/4
+// rows and dX by 16 columns.
+template <int K, int C, int BMP, int CB>
 __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
-  static_assert(K == 256 && C == 64, "the stage-1 shape");
-  const PbArgs& a = A.b;
-  constexpr int IMG_Y = 64 * K * 2, IMG_X = 64 * C * 2;
-  constexpr int LDX = C / 32;             // X DMA instructions per thread per tile
-  constexpr int U = 64 * (K / 8) / 256;   // dY chunks per thread per tile (8)
-  constexpr int LR = 3 * U;               // register loads per thread per tile (dout, y, mask byte)
-  constexpr int SROW = C + 8, CH = C / 8, ST = 64 * CH / 256;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG_Y + 3 * IMG_X + 64 * SROW * 2];
+  static_assert(CB == 64 && BMP % 32 == 0 && BMP <= 64 && C % CB == 0, "geometry");
+  constexpr int NH = C / CB;                   // blocks per pixel slot
+  constexpr int FK = K / 4 / 16;               // dW row fragments per wave
+  constexpr int FP = BMP / 16;                 // dX pixel fragments
+  constexpr int NKK = BMP / 32;                // 32-pixel MFMA k-substeps per tile
+  constexpr int IMG_Y = BMP * K * 2, IMG_X = BMP * CB * 2;
+  constexpr int LDX = IMG_X / 4096;            // X DMA instructions per thread per tile
+  constexpr int U = BMP * (K / 8) / 256;       // dY chunks per thread per tile
+  constexpr int RPT = 256 / (K / 8);           // rows covered by one pass of the 256 threads
+  constexpr int LR = 3 * U;                    // register loads per thread per tile (dout, y, mask byte)
+  constexpr int SROW = CB + 8, CH = CB / 8, ST = BMP * CH / 256;
+  static_assert(LDX >= 1 && ST >= 1 && U >= 1 && RPT >= 1, "geometry");
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG_Y + 3 * IMG_X + BMP * SROW * 2];
   char* ximg = smem + 2 * IMG_Y;
   char* stg = ximg + 3 * IMG_X;
+  const PbArgs& a = A.b;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int slot = blockIdx.x;
+  // block -> (pixel slot, column block h): the NH blocks of a slot are blockIdx b, b+8, ... (one XCD)
+  const int b = blockIdx.x, xcd = b & 7, j8 = b >> 3;
+  const int h = j8 % NH, slot = xcd + 8 * (j8 / NH);
+  const int c0 = h * CB;
 
-  v8bf fw[K / 32];
+  v8bf fw[K / 32];  // W[c = c0 + 16 wave + (lane & 15)][k = 32 s + 8 (lane >> 4) .. +7]
 #pragma unroll
   for (int s = 0; s < K / 32; ++s)
-    fw[s] = *reinterpret_cast<const v8bf*>(a.Wck + (long)(16 * wave + (lane & 15)) * K + 32 * s + 8 * (lane >> 4));
-  // this thread's dY channel chunk (fixed) and its BN-backward coefficients
-  const int cy = t % (K / 8), ry = t / (K / 8);  // rows ry + 8 u
+    fw[s] = *reinterpret_cast<const v8bf*>(a.Wck + (long)(c0 + 16 * wave + (lane & 15)) * K + 32 * s +
+                                           8 * (lane >> 4));
+  const int cy = t % (K / 8), ry = t / (K / 8);  // this thread's dY chunk (fixed) and first row (rows ry + RPT u)
   float ka[8], kb[8], kc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -320,8 +332,9 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     kb[j] = A.coef[K + cy * 8 + j];
     kc[j] = A.coef[2 * K + cy * 8 + j];
   }
+  // consume these loads before any DMA is in flight (else their waits land inside the tile loop)
 #pragma unroll
-  for (int s = 0; s < K / 32; ++s) asm volatile("" ::"v"(fw[s]));  // (see pw_bwd_kernel)
+  for (int s = 0; s < K / 32; ++s) asm volatile("" ::"v"(fw[s]));
 #pragma unroll
   for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(ka[j]), "v"(kb[j]), "v"(kc[j]));
 
@@ -337,7 +350,7 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
   auto load_tile = [&](int tile) {  // past the last tile (tile == tiles_p) every row is out of range: zeros
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = tile * 64 + ry + 8 * u;
+      const int p = tile * BMP + ry + RPT * u;
       const uint32_t e = (uint32_t)p * K + cy * 8;
       const bool ok = p < a.P;
       dv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? e * 2u : 0x80000000u, 0, 0));
@@ -348,18 +361,18 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
   auto transform = [&](int tile, char* img) {  // dY = a dz + b y + c -> bf16 -> the K-outer image
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int row = ry + 8 * u;
-      const bool ok = tile * 64 + row < a.P;
+      const int row = ry + RPT * u;
+      const bool ok = tile * BMP + row < a.P;
       const uint32_t dw_[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w}, yw[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
       const uint32_t bits = mb[u] | ym_or;
       float o[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = 2 * q + h;
-          float d = __uint_as_float(h ? (dw_[q] & 0xffff0000u) : (dw_[q] << 16));
-          const float yy = __uint_as_float(h ? (yw[q] & 0xffff0000u) : (yw[q] << 16));
+        for (int hh = 0; hh < 2; ++hh) {
+          const int j = 2 * q + hh;
+          float d = __uint_as_float(hh ? (dw_[q] & 0xffff0000u) : (dw_[q] << 16));
+          const float yy = __uint_as_float(hh ? (yw[q] & 0xffff0000u) : (yw[q] << 16));
           if (!((bits >> j) & 1u)) d = 0.f;
           o[j] = ok ? fmaf(ka[j], d, fmaf(kb[j], yy, kc[j])) : 0.f;
         }
@@ -371,17 +384,35 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     }
   };
 
-  KoDma<C> dmx;
-  dmx.init(a.X, a.P);
+  // X: the [BMP][CB] column block of rows with stride C, by LDS-DMA into a K-outer image (pwwgrad.hip's mapping)
+  const __amdgpu_buffer_rsrc_t xsr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.X, (short)0, (int)((long)a.P * C * 2), 0x00020000);
+  int xkr[LDX], xco[LDX];
+#pragma unroll
+  for (int i = 0; i < LDX; ++i) {
+    const int pb = i * 4096 + t * 16;
+    xkr[i] = pb / (CB * 2);
+    xco[i] = (c0 + ((((pb % (CB * 2)) >> 4) ^ (kouter_swz<CB>(xkr[i]) << 1)) * 8)) * 2;
+  }
+  auto x_issue = [&](int tile, char* img) {
+#pragma unroll
+    for (int i = 0; i < LDX; ++i) {
+      const int p = tile * BMP + xkr[i];
+      const uint32_t off = p < a.P ? (uint32_t)(p * (C * 2) + xco[i]) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xsr, (__attribute__((address_space(3))) void*)(img + i * 4096 + wave * 1024), 16, off, 0, 0, 0);
+    }
+  };
+
   const int step = a.slots;
   const int n_mine = slot < a.tiles_p ? (a.tiles_p - slot + step - 1) / step : 0;
   auto tile_of = [&](int i) { return i < n_mine ? slot + i * step : a.tiles_p; };
   // prologue, in this order: X tile 0, registers of tile 0, X tile 1
-  dmx.issue(tile_of(0) * 64, a.P, ximg);
+  x_issue(tile_of(0), ximg);
   load_tile(tile_of(0));
-  dmx.issue(tile_of(1) * 64, a.P, ximg + IMG_X);
+  x_issue(tile_of(1), ximg + IMG_X);
 
-  const int ch = t % CH, nch = ch * 8;
+  const int ch = t % CH, nch = c0 + ch * 8;
   const __amdgpu_buffer_rsrc_t dxr =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.dX, (short)0, (int)((long)a.P * C * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t xbr = __builtin_amdgcn_make_buffer_rsrc(
@@ -395,11 +426,11 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     bs[j] = bq[j] = 0.f;
     mu[j] = a.bnmean ? a.bnmean[nch + j] : 0.f;
   }
-  v4f aw[4][4];
+  v4f aw[4][FK];  // dW: rows k = (K/4) wave + 16 j, columns c0 + 16 i (lane: 4 consecutive c of one k)
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) aw[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FK; ++j) aw[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
 
   for (int it = 0; it < n_mine; ++it) {
     // this tile's registers and X image are in. Issued after them: X of tile it+1 (LDX) and, from iteration 1 on,
@@ -417,48 +448,50 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     uint32_t xmb[ST];
 #pragma unroll
     for (int k = 0; k < ST; ++k) {
-      const int p = tile * 64 + ((t + 256 * k) / CH);
+      const int p = tile * BMP + ((t + 256 * k) / CH);
       const uint32_t e = (uint32_t)p * C + nch;
       const bool ok = p < a.P;
       xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbr, ok ? e * 2u : 0x80000000u, 0, 0));
       xmb[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(xmr, ok ? e >> 3 : 0x80000000u, 0, 0);
     }
     load_tile(tile_of(it + 1));
-    dmx.issue(tile_of(it + 2) * 64, a.P, ximg + ((it + 2) % 3) * IMG_X);
+    x_issue(tile_of(it + 2), ximg + ((it + 2) % 3) * IMG_X);
 
+    // ---- dW[k][c] += sum over the tile's pixels of dY[p][k] X[p][c]
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      v8bf fx[4], fy[4];
+    for (int kk = 0; kk < NKK; ++kk) {
+      v8bf fx[4], fy[FK];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fx[i] = tr_frag<C>(xim, 16 * i, kk, lane);
+      for (int i = 0; i < 4; ++i) fx[i] = tr_frag<CB>(xim, 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fy[j] = tr_frag<K>(yimg, 64 * wave + 16 * j, kk, lane);
+      for (int j = 0; j < FK; ++j) fy[j] = tr_frag<K>(yimg, (K / 4) * wave + 16 * j, kk, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(fx[i]));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fy[j]));
+      for (int j = 0; j < FK; ++j) asm volatile("" : "+v"(fy[j]));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) aw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[i], fy[j], aw[i][j], 0, 0, 0);
+        for (int j = 0; j < FK; ++j) aw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[i], fy[j], aw[i][j], 0, 0, 0);
     }
-    v4f ad[4];
+    // ---- dX[p][c0 + 16 wave ..] = dY[p][:] W[:][..]
+    v4f ad[FP];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ad[i] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < FP; ++i) ad[i] = (v4f){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < K / 32; ++s) {
-      v8bf fa[4];
+      v8bf fa[FP];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = row_frag<K>(yimg, 16 * i, s, lane);
+      for (int i = 0; i < FP; ++i) fa[i] = row_frag<K>(yimg, 16 * i, s, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(fa[i]));
+      for (int i = 0; i < FP; ++i) asm volatile("" : "+v"(fa[i]));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ad[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[s], fa[i], ad[i], 0, 0, 0);
+      for (int i = 0; i < FP; ++i) ad[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[s], fa[i], ad[i], 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < FP; ++i) {
       const int pl = 16 * i + (lane & 15), cl = 16 * wave + 4 * (lane >> 4);
       uint2 o;
       o.x = pack2bf(ad[i][0], ad[i][1]);
@@ -472,10 +505,10 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
 #pragma unroll
     for (int k = 0; k < ST; ++k) {
       const int pl = (t + 256 * k) / CH;
-      const int p = tile * 64 + pl;
+      const int p = tile * BMP + pl;
       uint4 val;
       {
-        const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, stg + (pl * SROW + nch) * 2);
+        const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, stg + (pl * SROW + ch * 8) * 2);
         v4i r;
         asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr) : "memory");
         val = __builtin_bit_cast(uint4, r);
@@ -488,10 +521,10 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int r = 2 * q + h;
-          const float dvv = __uint_as_float(h ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
-          const float xx = __uint_as_float(h ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
+        for (int hh = 0; hh < 2; ++hh) {
+          const int r = 2 * q + hh;
+          const float dvv = __uint_as_float(hh ? (vw[q] & 0xffff0000u) : (vw[q] << 16));
+          const float xx = __uint_as_float(hh ? (xw[q] & 0xffff0000u) : (xw[q] << 16));
           const float dz = ((bits >> r) & 1u) ? dvv : 0.f;
           bs[r] += dz;
           bq[r] = fmaf(dz, xx - mu[r], bq[r]);
@@ -503,9 +536,9 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = 64 * wave + 16 * j + (lane & 15);
-      const int c = 16 * i + 4 * (lane >> 4);
+    for (int j = 0; j < FK; ++j) {
+      const int k = (K / 4) * wave + 16 * j + (lane & 15);
+      const int c = c0 + 16 * i + 4 * (lane >> 4);
       *reinterpret_cast<float4*>(slab + (long)k * C + c) = make_float4(aw[i][j][0], aw[i][j][1], aw[i][j][2], aw[i][j][3]);
     }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy loads / DMA past the last tile have landed too
@@ -518,7 +551,7 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     red[t * 16 + 8 + j] = bq[j];
   }
   __syncthreads();
-  if (t < C) {
+  if (t < CB) {
     const int c8 = t >> 3, j = t & 7;
     float sv = 0.f, qv = 0.f;
     for (int u = c8; u < 256; u += CH) {
@@ -526,8 +559,8 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
       qv += red[u * 16 + 8 + j];
     }
     float* prow = a.part + (long)slot * 2 * C;
-    prow[t] = sv;
-    prow[C + t] = qv;
+    prow[c0 + t] = sv;
+    prow[C + c0 + t] = qv;
   }
 }
 
@@ -572,22 +605,26 @@ DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymas
                                long ws_elems, long P, int K, int C, void* stream) {
   using namespace dtf;
   hipStream_t st = (hipStream_t)stream;
-  if (K != 256 || C != 64 || !coef) return -1;
+  // stage 1 (256 -> 64): one block per 64-pixel slot; stage 2 (512 -> 128): two column blocks per 32-pixel slot
+  const bool s1 = K == 256 && C == 64, s2 = K == 512 && C == 128;
+  if (!(s1 || s2) || !coef) return -1;
   if (((uintptr_t)dout & 15) || ((uintptr_t)y & 15) || ((uintptr_t)X & 15) || ((uintptr_t)Wck & 15) ||
       ((uintptr_t)dX & 15) || ((uintptr_t)bnx & 15) || !ws || !dW)
     return -1;
   if (bnmean && (!bnx || !part)) return -1;
-  if (P * K * 2 >= (1l << 31) || P < 64 * 256) return -1;
+  const int bmp = s1 ? 64 : 32, nh = C / 64;
   PbnArgs A{};
   PbArgs& a = A.b;
   a.X = (const bf16_t*)X; a.Wck = (const bf16_t*)Wck; a.dX = (bf16_t*)dX;
   a.bnx = (const bf16_t*)bnx; a.bnmask = (const uint8_t*)bnmask; a.bnmean = bnmean; a.part = part; a.ws = ws;
   a.P = (int)P;
-  a.tiles_p = (int)((P + 63) / 64);
-  a.slots = 256;
+  a.tiles_p = (int)((P + bmp - 1) / bmp);
+  a.slots = 256 / nh;
+  if (P * K * 2 >= (1l << 31) || a.tiles_p < a.slots) return -1;
   A.dout = (const bf16_t*)dout; A.y = (const bf16_t*)y; A.ymask = (const uint8_t*)ymask; A.coef = coef;
   if ((long)a.slots * K * C > ws_elems) return -1;
-  hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64>), dim3(a.slots), dim3(256), 0, st, A);
+  if (s1) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64>), dim3(256), dim3(256), 0, st, A);
+  else hipLaunchKernelGGL((pw_bwd_bn_kernel<512, 128, 32, 64>), dim3(256), dim3(256), 0, st, A);
   if (hipGetLastError() != hipSuccess) return -1;
   dtf_sum_rows(ws, (long)K * C, a.slots, (long)K * C, dW, accumulate, st);
   if (rows) *rows = bnmean ? a.slots : 0;

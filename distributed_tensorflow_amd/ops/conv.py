@@ -104,6 +104,16 @@ def pw_bwd_ok(g, M_min=64 * 256):
             and M * K * 2 < (1 << 31))
 
 
+def pw_bwd_bn_ok(g):
+    """Shapes of the BatchNorm-folded form (dtf_pw_conv_bwd_bn): stage 1 (K_out 256 from 64, >= 256 64-pixel tiles)
+    or stage 2 (K_out 512 from 128, >= 128 32-pixel tiles)."""
+    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw = g[:13]
+    M = N * P * Q
+    if (R, S, sh, sw, ph, pw) != (1, 1, 1, 1, 0, 0) or M * K * 2 >= (1 << 31):
+        return False
+    return (K, C) == (256, 64) and M >= 64 * 256 or (K, C) == (512, 128) and M >= 32 * 128
+
+
 def conv_bwd_fused_raw(dy, x, w_master, g, dw_out, bn=None):
     """dX (bf16) and dW += (into the f32 arena gradient dw_out) of a pw_bwd_ok conv in ONE pass over dy
     (pwbwd.hip); with `bn` (the _BNSource of the BatchNorm that produced x, see conv_dgrad_raw) the BN-backward
@@ -135,7 +145,7 @@ def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None)
     ws = workspace(dout.device)
     part = rows = None
     if bn is not None:
-        part = torch.empty(256 * 2 * C, dtype=F32, device=dout.device)
+        part = torch.empty(256 * 2 * C, dtype=F32, device=dout.device)  # (<= 256 pixel slots)
         rows = IntOut()
     bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ymask), ptr(coef), ptr(x), ptr(wc), ptr(dx), ptr(dw_out), 1,
@@ -420,7 +430,7 @@ class _ConvBNFn(torch.autograd.Function):
             part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=yc.device), IntOut()
             sc = (ptr(rsrc.yc), ptr(rsrc.mean), ptr(part2), rows2.addr)
         if (fused is not None and lazy_res and rsrc is None and _FUSED_PW_BWD >= 2 and ctx.needs_input_grad[0]
-                and ctx.needs_input_grad[1] and pw_bwd_ok(g) and x.is_contiguous() and x.dtype == BF16):
+                and ctx.needs_input_grad[1] and pw_bwd_bn_ok(g) and x.is_contiguous() and x.dtype == BF16):
             tw = direct_grad(w)
             if tw is not None:
                 # identity-block c3: finalize the BN-backward reduction only, then ONE pass computes dY per tile from

@@ -75,6 +75,58 @@ def test_pw_bwd_matches_separate_kernels(cuda, P, with_bn):
         assert torch.allclose(s1, s2, atol=1e-4 * sc, rtol=1e-4)
 
 
+@pytest.mark.parametrize("P", [8192, 100003])
+def test_pw_bwd_bn_stage2_matches_separate_kernels(cuda, P):
+    """Stage-2 shape (K_out 512 from C_in 128: two column blocks per 32-pixel slot): dX bitwise the apply pass +
+    general data-gradient tile, dW and the BN partial sums to f32 summation order, against fp32 references too."""
+    K, C = 512, 128
+    g = torch.Generator(device="cpu").manual_seed(P + 1)
+    dout = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    y = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    ym = _bits(torch.rand(P, K, generator=g) > 0.3).to(cuda)
+    coef = torch.cat([torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1,
+                      torch.randn(K, generator=g) * 0.01]).to(cuda)
+    x = torch.relu(torch.randn(P, C, generator=g)).to(BF).to(cuda)
+    wck = (torch.randn(C, K, generator=g) * K ** -0.5).to(BF).to(cuda)
+    bn = (torch.randn(P, C, generator=g).to(BF).to(cuda), _bits(torch.rand(P, C, generator=g) > 0.5).to(cuda),
+          (torch.randn(C, generator=g) * 0.1).to(cuda))
+    ws = torch.empty(32 << 20, dtype=F32, device=cuda)
+    dx = torch.full((P, C), float("nan"), dtype=BF, device=cuda)
+    dw0 = torch.randn(K, C, generator=g).to(cuda)
+    dw = dw0.clone()
+    part = torch.full((256 * 2 * C,), float("nan"), device=cuda)
+    rows = ctypes.c_int(0)
+    call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
+         ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part), ctypes.addressof(rows), ptr(ws), ws.numel(), P, K, C,
+         stream())
+    dyc = torch.empty(P, K, dtype=BF, device=cuda)
+    call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(ym), ptr(y), P, K, ptr(dyc), None, ptr(coef), None, None, None,
+         None, stream())
+    dx2 = torch.empty(P, C, dtype=BF, device=cuda)
+    part2 = torch.empty((((P + 63) // 64) + 1) * 2 * C, device=cuda)
+    rows2 = ctypes.c_int(0)
+    call("dtf_set_pw_dgrad", 0)
+    try:
+        call("dtf_conv_dgrad_x", ptr(dyc), ptr(wck), ptr(dx2), P, 1, 1, C, K, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0.0,
+             ptr(ws), 16, ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part2), ctypes.addressof(rows2), None, None,
+             stream())
+    finally:
+        call("dtf_set_pw_dgrad", 1)
+    torch.cuda.synchronize()
+    assert rows.value == 128
+    ref_dx = dyc.float() @ wck.float().t()
+    assert torch.allclose(dx.float(), ref_dx, atol=3e-2, rtol=2e-2)
+    nbad = (dx.view(torch.int16) != dx2.view(torch.int16)).sum().item()
+    assert nbad == 0, f"{nbad} dX elements differ from the general tile"
+    ref_dw = dw0 + dyc.float().t() @ x.float()
+    scale = ref_dw.abs().max().item()
+    assert (dw - ref_dw).abs().max().item() <= 1e-4 * scale + 1e-3
+    s1 = part[: rows.value * 2 * C].view(rows.value, 2 * C).sum(0)
+    s2 = part2[: rows2.value * 2 * C].view(rows2.value, 2 * C).sum(0)
+    sc = s2.abs().max().item() + 1.0
+    assert torch.allclose(s1, s2, atol=1e-4 * sc, rtol=1e-4)
+
+
 @pytest.mark.parametrize("P", [16384, 200003])
 def test_pw_bwd_bn_matches_apply_then_fused(cuda, P):
     """dtf_pw_conv_bwd_bn (dY computed per tile from dout, y, the ReLU bits and the BN-backward coefficients) equals
@@ -162,6 +214,51 @@ def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
         want = {0: (0, 0), 1: (4, 0), 2: (3, 1)}[lv]
         assert (seen.get("dtf_pw_conv_bwd", 0), seen.get("dtf_pw_conv_bwd_bn", 0)) == want, seen
     for a, b in zip(runs[0], runs[level]):
+        assert torch.isfinite(b).all()
+        err = (a - b).norm().item() / (a.norm().item() + 1e-12)
+        assert err < 1e-2, err
+
+
+def test_pw_bwd_bn_stage2_block_gradients(cuda, monkeypatch):
+    """Stage-2 bottlenecks (stride-2 projection block + two identity blocks, width 128): the middle block's c3 takes
+    the BatchNorm-folded fused path; gradients agree with the unfused path to f32 summation order."""
+    from distributed_tensorflow_amd.keras import initializers
+    from distributed_tensorflow_amd.models import resnet as R
+    from distributed_tensorflow_amd.ops._util import direct_grads
+    from distributed_tensorflow_amd.variables import ParamArena
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(32, 32, 32, 256, generator=g).to(cuda).to(BF)
+    runs = {}
+    seen = {}
+    real_call = OC.call
+
+    def spy(name, *args):
+        seen[name] = seen.get(name, 0) + 1
+        return real_call(name, *args)
+
+    monkeypatch.setattr(OC, "call", spy)
+    for lv in (0, 2):
+        monkeypatch.setattr(OC, "_FUSED_PW_BWD", lv)
+        initializers.set_seed(5)
+        blocks = [R.Bottleneck(128, stride=2, project=True), R.Bottleneck(128), R.Bottleneck(128)]
+        with torch.no_grad():
+            h = x
+            for b in blocks:
+                h = b(h, training=False)
+        params = [w for b in blocks for w in b.trainable_weights]
+        arena = ParamArena(params, device=cuda)
+        seen.clear()
+        xx = x.clone().requires_grad_(True)
+        h = xx
+        for b in blocks:
+            h = b(h, training=True)
+        loss = (h.float() * torch.linspace(-1, 1, h.shape[-1], device=cuda)).square().mean()
+        with direct_grads():
+            loss.backward()
+        torch.cuda.synchronize()
+        runs[lv] = [xx.grad.float(), arena.grad.clone()]
+        assert seen.get("dtf_pw_conv_bwd_bn", 0) == (1 if lv else 0), seen
+    for a, b in zip(runs[0], runs[2]):
         assert torch.isfinite(b).all()
         err = (a - b).norm().item() / (a.norm().item() + 1e-12)
         assert err < 1e-2, err
