@@ -290,14 +290,21 @@ struct PbnArgs {
   const bf16_t* y;      // [P][K] BN input (the conv output)
   const uint8_t* ymask; // [P][K] ReLU bits (nullptr: no ReLU)
   const float* coef;    // [3][K]
+  // SC: the BatchNorm-backward reduction of a projection shortcut whose (deferred) BN output was added as this
+  // layer's residual: its incoming gradient is the same masked dz, its BN input ysc [P][K] with batch mean msc;
+  // one partial row per block [slots][2K] (sum dz | sum dz (ysc - msc)) — bn_bwd_apply_kernel<true>'s sums
+  const bf16_t* ysc;
+  const float* msc;
+  float* psc;
 };
 
 // <K, C, BMP, CB>: BMP pixels per tile; each block owns CB of the C columns (C / CB blocks per pixel slot, on one XCD
 // and in step, so the second one's dout / y reads hit L2): dX[:, its CB] and dW[:, its CB]. Waves split dW by K/4
 // rows and dX by 16 columns.
-template <int K, int C, int BMP, int CB>
+template <int K, int C, int BMP, int CB, bool SC = false>
 __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
   static_assert(CB == 64 && BMP % 32 == 0 && BMP <= 64 && C % CB == 0, "geometry");
+  static_assert(!SC || C == CB, "the shortcut sums are taken by the only block of a pixel slot");
   constexpr int NH = C / CB;                   // blocks per pixel slot
   constexpr int FK = K / 4 / 16;               // dW row fragments per wave
   constexpr int FP = BMP / 16;                 // dX pixel fragments
@@ -345,8 +352,16 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
   const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)A.ymask, (short)0, A.ymask ? (int)((long)a.P * K / 8) : 0, 0x00020000);
   const uint32_t ym_or = A.ymask ? 0u : 0xFFu;
-  uint4 dv[U], yv[U];
+  uint4 dv[U], yv[U], sv_[SC ? U : 1];
   uint32_t mb[U];
+  const __amdgpu_buffer_rsrc_t scr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)A.ysc, (short)0, SC ? (int)((long)a.P * K * 2) : 0, 0x00020000);
+  float ssc[8], qsc[8], msc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ssc[j] = qsc[j] = 0.f;
+    msc[j] = SC ? A.msc[cy * 8 + j] : 0.f;
+  }
   auto load_tile = [&](int tile) {  // past the last tile (tile == tiles_p) every row is out of range: zeros
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -356,6 +371,8 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
       dv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? e * 2u : 0x80000000u, 0, 0));
       yv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, ok ? e * 2u : 0x80000000u, 0, 0));
       mb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mr, ok ? e >> 3 : 0x80000000u, 0, 0);
+      if constexpr (SC)
+        sv_[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(scr, ok ? e * 2u : 0x80000000u, 0, 0));
     }
   };
   auto transform = [&](int tile, char* img) {  // dY = a dz + b y + c -> bf16 -> the K-outer image
@@ -375,6 +392,11 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
           const float yy = __uint_as_float(hh ? (yw[q] & 0xffff0000u) : (yw[q] << 16));
           if (!((bits >> j) & 1u)) d = 0.f;
           o[j] = ok ? fmaf(ka[j], d, fmaf(kb[j], yy, kc[j])) : 0.f;
+          if constexpr (SC) {  // (rows past P: d is 0)
+            const uint32_t sw = hh ? (sv_[u][q] & 0xffff0000u) : (sv_[u][q] << 16);
+            ssc[j] += d;
+            qsc[j] = fmaf(d, __uint_as_float(sw) - msc[j], qsc[j]);
+          }
         }
       const v4i w4 = {(int)pack2bf(o[0], o[1]), (int)pack2bf(o[2], o[3]), (int)pack2bf(o[4], o[5]),
                       (int)pack2bf(o[6], o[7])};
@@ -542,6 +564,27 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
       *reinterpret_cast<float4*>(slab + (long)k * C + c) = make_float4(aw[i][j][0], aw[i][j][1], aw[i][j][2], aw[i][j][3]);
     }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy loads / DMA past the last tile have landed too
+  if constexpr (SC) {  // the shortcut's partial row: the RPT threads of each dY chunk folded in a fixed order
+    __syncthreads();
+    float* red2 = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red2[t * 16 + j] = ssc[j];
+      red2[t * 16 + 8 + j] = qsc[j];
+    }
+    __syncthreads();
+    for (int c = t; c < K; c += 256) {
+      const int c8 = c >> 3, j = c & 7;
+      float sv = 0.f, qv = 0.f;
+      for (int u = c8; u < 256; u += K / 8) {
+        sv += red2[u * 16 + j];
+        qv += red2[u * 16 + 8 + j];
+      }
+      float* prow = A.psc + (long)slot * 2 * K;
+      prow[c] = sv;
+      prow[K + c] = qv;
+    }
+  }
   if (!a.bnmean) return;
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);
@@ -599,10 +642,12 @@ DTF_API int dtf_pw_conv_bwd(const void* dY, const void* X, const void* Wck, void
 // dtf_pw_conv_bwd with the conv output's BatchNorm(+ReLU) backward applied on the fly (see pw_bwd_bn_kernel):
 // dY = a dz + b y + c from dout, y, the ReLU bits ymask (nullptr: none) and coef [3][K] (bn_bwd_finalize's
 // coefficients, dtf_bn_bwd_coef); dY itself is never stored.
+// ysc / msc / psc (stage-1 shape only): the projection shortcut's BN-backward partial rows (see PbnArgs), *rsc rows.
 DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymask, const float* coef, const void* X,
                                const void* Wck, void* dX, float* dW, int accumulate, const void* bnx,
                                const void* bnmask, const float* bnmean, float* part, int* rows, float* ws,
-                               long ws_elems, long P, int K, int C, void* stream) {
+                               long ws_elems, long P, int K, int C, const void* ysc, const float* msc, float* psc,
+                               int* rsc, void* stream) {
   using namespace dtf;
   hipStream_t st = (hipStream_t)stream;
   // stage 1 (256 -> 64): one block per 64-pixel slot; stage 2 (512 -> 128): two column blocks per 32-pixel slot
@@ -612,6 +657,8 @@ DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymas
       ((uintptr_t)dX & 15) || ((uintptr_t)bnx & 15) || !ws || !dW)
     return -1;
   if (bnmean && (!bnx || !part)) return -1;
+  const bool sc = ysc != nullptr;
+  if (sc && (!s1 || !msc || !psc || ((uintptr_t)ysc & 15))) return -1;
   const int bmp = s1 ? 64 : 32, nh = C / 64;
   PbnArgs A{};
   PbArgs& a = A.b;
@@ -623,10 +670,13 @@ DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymas
   if (P * K * 2 >= (1l << 31) || a.tiles_p < a.slots) return -1;
   A.dout = (const bf16_t*)dout; A.y = (const bf16_t*)y; A.ymask = (const uint8_t*)ymask; A.coef = coef;
   if ((long)a.slots * K * C > ws_elems) return -1;
-  if (s1) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64>), dim3(256), dim3(256), 0, st, A);
+  A.ysc = (const bf16_t*)ysc; A.msc = msc; A.psc = psc;
+  if (s1 && sc) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, true>), dim3(256), dim3(256), 0, st, A);
+  else if (s1) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64>), dim3(256), dim3(256), 0, st, A);
   else hipLaunchKernelGGL((pw_bwd_bn_kernel<512, 128, 32, 64>), dim3(256), dim3(256), 0, st, A);
   if (hipGetLastError() != hipSuccess) return -1;
   dtf_sum_rows(ws, (long)K * C, a.slots, (long)K * C, dW, accumulate, st);
   if (rows) *rows = bnmean ? a.slots : 0;
+  if (rsc) *rsc = sc ? a.slots : 0;
   return (int)hipGetLastError();
 }

@@ -35,7 +35,7 @@ _KERNEL_SIGS = {
     "dtf_set_ew_variant": [I],
     "dtf_set_pw_dgrad": [I],
     "dtf_pw_conv_bwd": [P, P, P, P, P, I, P, P, P, P, P, P, L, L, I, I, P],
-    "dtf_pw_conv_bwd_bn": [P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, L, L, I, I, P],
+    "dtf_pw_conv_bwd_bn": [P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P],
     "dtf_bn_bwd_coef": [P, I, P, P, P, L, I, P, P, I, P, P],
     "dtf_set_pw_wgrad": [I],
     "dtf_set_split_penalty": [I],

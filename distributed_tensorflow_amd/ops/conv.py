@@ -135,9 +135,11 @@ def conv_bwd_fused_raw(dy, x, w_master, g, dw_out, bn=None):
     return dx
 
 
-def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None):
+def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None, sc=None):
     """conv_bwd_fused_raw with dy = a*dz + b*y + c (the BatchNorm(+ReLU) backward of y = conv output, coefficients
-    coef [3K] from dtf_bn_bwd_coef, dz = dout under the ReLU bits ymask) computed inside the kernel."""
+    coef [3K] from dtf_bn_bwd_coef, dz = dout under the ReLU bits ymask) computed inside the kernel. With `sc` (the
+    _BNSource of a deferred projection-shortcut BN added as this layer's residual) the kernel also takes that BN's
+    backward reduction of dz and provides it to the source for `dout`."""
     N, H, W, C, K = g[:5]
     M = N * H * W
     wc = crsk_shadow(w_master, K, 1, C)
@@ -148,10 +150,17 @@ def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None)
         part = torch.empty(256 * 2 * C, dtype=F32, device=dout.device)  # (<= 256 pixel slots)
         rows = IntOut()
     bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
+    psc = rsc = None
+    if sc is not None:
+        psc, rsc = torch.empty(256 * 2 * K, dtype=F32, device=dout.device), IntOut()
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ymask), ptr(coef), ptr(x), ptr(wc), ptr(dx), ptr(dw_out), 1,
-         *bn_ptrs, ptr(part), rows.addr if rows else None, ptr(ws), ws.numel(), M, K, C, stream())
+         *bn_ptrs, ptr(part), rows.addr if rows else None, ptr(ws), ws.numel(), M, K, C,
+         ptr(sc.yc) if sc is not None else None, ptr(sc.mean) if sc is not None else None, ptr(psc),
+         rsc.addr if rsc else None, stream())
     if bn is not None:
         bn.provide(dx, part, rows.value)
+    if sc is not None:
+        sc.provide(dout, psc, rsc.value)
     return dx
 
 
@@ -409,7 +418,13 @@ class _ConvBNFn(torch.autograd.Function):
         g = ctx.g
         K = g[4]
         M = yc.numel() // K
+        # a deferred projection BN whose consumer handed over its raw incoming gradient with the ReLU bits to apply
+        # (see the projection-block branch below): dz = dout under that mask
+        dmask = getattr(dout, "_dtf_mask", None)
         dout = dout.to(BF16).contiguous()
+        if dmask is not None:
+            assert mbits is None and not ctx.relu
+            mbits = dmask
         if not ctx.training:
             return _ConvBNFn._backward_frozen(ctx, dout, x, w, gamma, yc, mbits, mean, invstd)
         dyc = torch.empty_like(yc)
@@ -444,6 +459,42 @@ class _ConvBNFn(torch.autograd.Function):
                 # the identity shortcut's gradient: dout parked with the ReLU mask (read above, in stream order, before
                 # the first conv's dgrad overwrites it)
                 link.park(dout, mask=mbits)
+                ctx.in_src = ctx.src = ctx.res_src = None
+                if direct_bn:
+                    dgamma = dbeta = None
+                return (dx, None, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None,
+                        None)
+        blk_ok = (_FUSED_PW_BWD >= 2 and fused is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+                  and x.is_contiguous() and x.dtype == BF16)
+        if blk_ok and rsrc is not None and not lazy_res and ctx.relu and pw_bwd_bn_ok(g) and g[4] == 256 and g[3] == 64:
+            tw = direct_grad(w)
+            if tw is not None:
+                # projection-block c3 (stage 1): the same one-pass form, also taking the shortcut BN's reduction of
+                # dz; the shortcut then receives the raw dout tagged with the ReLU bits instead of a materialised dz
+                coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+                call("dtf_bn_bwd_coef", ptr(fused[1]), fused[2], ptr(mean), ptr(invstd), ptr(gamma), M, K,
+                     ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(coef), stream())
+                src = ctx.in_src
+                complete = src is not None and role != "proj" and src.consumers == 1
+                dx = conv_bwd_bn_fused_raw(dout, yc, mbits, coef, x, w, g, tw, bn=src if complete else None,
+                                           sc=rsrc)
+                dout._dtf_mask = mbits
+                ctx.in_src = ctx.src = ctx.res_src = None
+                if direct_bn:
+                    dgamma = dbeta = None
+                return (dx, None, dgamma, dbeta, dout, None, None, None, None, None, None, None, None, None, None,
+                        None)
+        if (blk_ok and dmask is not None and role == "proj" and rsrc is None and pw_bwd_bn_ok(g)
+                and g[4] == 256 and g[3] == 64):
+            tw = direct_grad(w)
+            if tw is not None:
+                # the stride-1 projection of that block: its BN backward folded into its own gradient pass
+                coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+                call("dtf_bn_bwd_coef", ptr(fused[1]), fused[2], ptr(mean), ptr(invstd), ptr(gamma), M, K,
+                     ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(coef), stream())
+                dx = conv_bwd_bn_fused_raw(dout, yc, mbits, coef, x, w, g, tw)
+                if link is not None:
+                    dx = link.park(dx)
                 ctx.in_src = ctx.src = ctx.res_src = None
                 if direct_bn:
                     dgamma = dbeta = None

@@ -98,7 +98,7 @@ def test_pw_bwd_bn_stage2_matches_separate_kernels(cuda, P):
     rows = ctypes.c_int(0)
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
          ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part), ctypes.addressof(rows), ptr(ws), ws.numel(), P, K, C,
-         stream())
+         None, None, None, None, stream())
     dyc = torch.empty(P, K, dtype=BF, device=cuda)
     call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(ym), ptr(y), P, K, ptr(dyc), None, ptr(coef), None, None, None,
          None, stream())
@@ -150,7 +150,7 @@ def test_pw_bwd_bn_matches_apply_then_fused(cuda, P):
     rows = ctypes.c_int(0)
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
          ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part), ctypes.addressof(rows), ptr(ws), ws.numel(), P, K, C,
-         stream())
+         None, None, None, None, stream())
     dyc = torch.empty(P, K, dtype=BF, device=cuda)
     call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(ym), ptr(y), P, K, ptr(dyc), None, ptr(coef), None, None, None,
          None, stream())
@@ -174,7 +174,8 @@ def test_pw_bwd_bn_matches_apply_then_fused(cuda, P):
 def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
     """Three stage-1 bottlenecks trained the framework's way (arena gradients, direct accumulation). Level 1: every c3
     and the stride-1 projection take the fused data + weight gradient; level 2: the middle block's c3 (identity
-    block whose BN-backward reduction its consumer already took) also folds the BatchNorm backward in. Gradients agree
+    block whose BN-backward reduction its consumer already took), the projection block's c3 (with the shortcut BN
+    reduction) and its stride-1 projection also fold the BatchNorm backward in. Gradients agree
     with the unfused path to f32 summation order."""
     from distributed_tensorflow_amd.keras import initializers
     from distributed_tensorflow_amd.models import resnet as R
@@ -211,7 +212,7 @@ def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
             loss.backward()
         torch.cuda.synchronize()
         runs[lv] = [xx.grad.float(), arena.grad.clone()]
-        want = {0: (0, 0), 1: (4, 0), 2: (3, 1)}[lv]
+        want = {0: (0, 0), 1: (4, 0), 2: (1, 3)}[lv]
         assert (seen.get("dtf_pw_conv_bwd", 0), seen.get("dtf_pw_conv_bwd_bn", 0)) == want, seen
     for a, b in zip(runs[0], runs[level]):
         assert torch.isfinite(b).all()
@@ -262,3 +263,41 @@ def test_pw_bwd_bn_stage2_block_gradients(cuda, monkeypatch):
         assert torch.isfinite(b).all()
         err = (a - b).norm().item() / (a.norm().item() + 1e-12)
         assert err < 1e-2, err
+
+
+def test_pw_bwd_bn_shortcut_partials(cuda):
+    """The projection-shortcut BN-backward reduction taken inside the BN-folded pass equals the one the standalone
+    apply pass takes (bn_bwd_apply_kernel<true>): sum dz and sum dz (ysc - mean) per channel."""
+    P, K, C = 65536 + 37, 256, 64
+    g = torch.Generator(device="cpu").manual_seed(23)
+    dout = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    y = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    ysc = torch.randn(P, K, generator=g).to(BF).to(cuda)
+    msc = (torch.randn(K, generator=g) * 0.1).to(cuda)
+    ym = _bits(torch.rand(P, K, generator=g) > 0.3).to(cuda)
+    coef = torch.cat([torch.rand(K, generator=g) + 0.5, torch.randn(K, generator=g) * 0.1,
+                      torch.randn(K, generator=g) * 0.01]).to(cuda)
+    x = torch.relu(torch.randn(P, C, generator=g)).to(BF).to(cuda)
+    wck = (torch.randn(C, K, generator=g) * K ** -0.5).to(BF).to(cuda)
+    ws = torch.empty(32 << 20, dtype=F32, device=cuda)
+    dx = torch.empty(P, C, dtype=BF, device=cuda)
+    dw = torch.zeros(K, C, device=cuda)
+    psc = torch.full((256 * 2 * K,), float("nan"), device=cuda)
+    rsc = ctypes.c_int(0)
+    call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
+         None, None, None, None, None, ptr(ws), ws.numel(), P, K, C, ptr(ysc), ptr(msc), ptr(psc),
+         ctypes.addressof(rsc), stream())
+    dyc = torch.empty(P, K, dtype=BF, device=cuda)
+    dz = torch.empty(P, K, dtype=BF, device=cuda)
+    part2 = torch.empty(4096 * 2 * K, device=cuda)
+    rows2 = ctypes.c_int(0)
+    call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(ym), ptr(y), P, K, ptr(dyc), ptr(dz), ptr(coef), ptr(ysc), ptr(msc),
+         ptr(part2), ctypes.addressof(rows2), stream())
+    torch.cuda.synchronize()
+    assert rsc.value == 256 and rows2.value > 0
+    s1 = psc.view(256, 2 * K).sum(0)
+    s2 = part2[: rows2.value * 2 * K].view(rows2.value, 2 * K).sum(0)
+    ref = torch.cat([dz.float().sum(0), (dz.float() * (ysc.float() - msc)).sum(0)])
+    sc = ref.abs().max().item() + 1.0
+    assert torch.allclose(s1, s2, atol=1e-4 * sc, rtol=1e-4)
+    assert torch.allclose(s1, ref, atol=1e-3 * sc, rtol=1e-3)
