@@ -741,12 +741,12 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream);
+                           const void* bsrc2, void* stream, const void* bnrx = nullptr, const void* bnrw = nullptr);
 
 namespace dtf {
 int pwconv_dgrad_try(const void* dY, const void* Wck, void* dX, float beta, const void* betamask, const void* bnx,
                      const void* bnmask, const float* bnmean, float* part, long M, int Kc, int N, const void* bsrc2,
-                     int H, int W, hipStream_t st);
+                     int H, int W, hipStream_t st, const void* bnrx, const void* bnrw);
 }
 // DTF_PW_DGRAD=0 (or dtf_set_pw_dgrad(0)) keeps the pointwise data gradients on the general GEMM tiles (A/B switch)
 static int g_pw_dgrad = -1;
@@ -795,17 +795,21 @@ DTF_API int dtf_conv_dgrad(const void* dY, const void* Wcrsk, void* dX, int N, i
 // The general bf16 data gradient of the ConvBN path: optional beta accumulate (+ deferred ReLU mask betamask), the
 // compact stride-2 shortcut gradient bsrc2 (pointwise stride-1 convs, H and W even), and the BN-backward statistics
 // of dX (bnx/bnmask/bnmean -> bnpart/bnrows).
+// bnrx / bnrw: the BN input is not stored but is bf16(bnrx bnrw^T) (a 64-channel-input 1x1 conv's output, pwconv.hip
+// RX): only the persistent pointwise route recomputes it; any other route returns -12 with nothing launched (the
+// caller then materialises it and passes bnx).
 DTF_API int dtf_conv_dgrad_x(const void* dY, const void* Wcrsk, void* dX, int N, int H, int W, int C, int K, int R,
                              int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, float beta, void* ws,
                              long ws_bf16, const void* bnx, const void* bnmask, const float* bnmean, float* bnpart,
-                             int* bnrows, const void* betamask, const void* bsrc2, void* stream) {
+                             int* bnrows, const void* betamask, const void* bsrc2, const void* bnrx, const void* bnrw,
+                             void* stream) {
   if (bsrc2) {
     if ((H & 1) || (W & 1) || R != 1 || S != 1 || sh != 1 || sw != 1 || ph != 0 || pw != 0) return -11;
     return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, 1, 1, H, W, 1, 1, 0, 0, 1, 1, 0, 1.f, -1, ws, ws_bf16, bnx,
-                           bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream);
+                           bnmask, bnmean, bnpart, bnrows, nullptr, bsrc2, stream, bnrx, bnrw);
   }
   return conv_dgrad_impl(dY, Wcrsk, dX, N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, 0, beta, -1, ws, ws_bf16,
-                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream);
+                         bnx, bnmask, bnmean, bnpart, bnrows, betamask, nullptr, stream, bnrx, bnrw);
 }
 
 DTF_API int dtf_conv_dgrad_addsub2(const void* dY, const void* Wcrsk, void* dX, const void* bsrc2, int N, int H, int W,
@@ -821,8 +825,9 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
                            int S, int P, int Q, int sh, int sw, int ph, int pw, int dh, int dw, int out_f32,
                            float beta, int tile, void* ws, long ws_bf16, const void* bnx, const void* bnmask,
                            const float* bnmean, float* bnpart, int* bnrows, const void* betamask,
-                           const void* bsrc2, void* stream) {
+                           const void* bsrc2, void* stream, const void* bnrx, const void* bnrw) {
   if ((C & 3) || (K & 7)) return -1;
+  if (bnrx && (bnx || !bnrw || !bnpart || !bnmean || !bnrows)) return -9;
   if (bnx && (out_f32 || (C & 7) || !bnpart || !bnmean || !bnrows)) return -9;
   if (betamask && (out_f32 || beta == 0.f || (C & 7) || sh > 1 || sw > 1)) return -10;
   hipStream_t st = (hipStream_t)stream;
@@ -844,6 +849,7 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
   };
   const bool phased = (sh > 1 || sw > 1) && dh == 1 && dw == 1 && ws != nullptr &&
                       ws_bf16 >= (long)C * R * S * K && !(C & 7);
+  if (bnrx && phased) return -12;
   if (!phased) {
     GemmArgs a{};
     a.g = make_geom(N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw);
@@ -861,13 +867,14 @@ static int conv_dgrad_impl(const void* dY, const void* Wcrsk, void* dX, int N, i
     // channel-reducing pointwise data gradients (ResNet-50 bottleneck c1: dY width 64..256 -> 4x the channels): the
     // persistent pointwise kernel (filter in registers, beta accumulate + BN-backward partials in its store pass)
     if (pointwise && t < 0 && !out_f32 && pwdgrad_enabled()) {
-      const int rows = pwconv_dgrad_try(dY, Wcrsk, dX, beta, betamask, bnx, bnmask, bnmean, bnx ? bnpart : nullptr,
-                                        a.M, K, C, bsrc2, H, W, st);
+      const int rows = pwconv_dgrad_try(dY, Wcrsk, dX, beta, betamask, bnx, bnmask, bnmean,
+                                        (bnx || bnrx) ? bnpart : nullptr, a.M, K, C, bsrc2, H, W, st, bnrx, bnrw);
       if (rows > 0) {
-        if (bnrows) *bnrows = bnx ? rows : 0;
+        if (bnrows) *bnrows = (bnx || bnrx) ? rows : 0;
         return (int)hipGetLastError();
       }
     }
+    if (bnrx) return -12;  // (nothing launched: the caller materialises the BN input)
     // stride-1 3x3 data gradients into >= 256 channels (ResNet-50 stages 3-4): the 4-wave kernel with the dY gather
     // loader and the BN-backward statistics epilogue (profiles/r5_conv3x3_w4.txt)
     if (am == OP_DGRAD_T && R * S > 1 && t < 0 && C >= 256 && !out_f32 && beta == 0.f && !betamask && !bsrc2) {

@@ -296,15 +296,19 @@ struct PbnArgs {
   const bf16_t* ysc;
   const float* msc;
   float* psc;
+  // YR: y is not stored — recompute it per tile as bf16(X W^T) from the X tile already in LDS and wy [K][C] (the
+  // layer's forward filter), the forward pwconv's MFMA sequence (bitwise its stored values)
+  const bf16_t* wy;
 };
 
 // <K, C, BMP, CB>: BMP pixels per tile; each block owns CB of the C columns (C / CB blocks per pixel slot, on one XCD
 // and in step, so the second one's dout / y reads hit L2): dX[:, its CB] and dW[:, its CB]. Waves split dW by K/4
 // rows and dX by 16 columns.
-template <int K, int C, int BMP, int CB, bool SC = false>
+template <int K, int C, int BMP, int CB, bool SC = false, bool YR = false>
 __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
   static_assert(CB == 64 && BMP % 32 == 0 && BMP <= 64 && C % CB == 0, "geometry");
   static_assert(!SC || C == CB, "the shortcut sums are taken by the only block of a pixel slot");
+  static_assert(!YR || (C == CB && BMP == 64 && K == 256), "y recompute: the stage-1 shape (one block per slot)");
   constexpr int NH = C / CB;                   // blocks per pixel slot
   constexpr int FK = K / 4 / 16;               // dW row fragments per wave
   constexpr int FP = BMP / 16;                 // dX pixel fragments
@@ -313,12 +317,14 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
   constexpr int LDX = IMG_X / 4096;            // X DMA instructions per thread per tile
   constexpr int U = BMP * (K / 8) / 256;       // dY chunks per thread per tile
   constexpr int RPT = 256 / (K / 8);           // rows covered by one pass of the 256 threads
-  constexpr int LR = 3 * U;                    // register loads per thread per tile (dout, y, mask byte)
+  constexpr int LR = (3 + (SC ? 1 : 0) - (YR ? 1 : 0)) * U;  // register loads per thread per tile (dout, y, mask, ysc)
+  constexpr int YROW = K + 8;                  // YR: staged y row (bf16), 16-B pad
   constexpr int SROW = CB + 8, CH = CB / 8, ST = BMP * CH / 256;
   static_assert(LDX >= 1 && ST >= 1 && U >= 1 && RPT >= 1, "geometry");
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG_Y + 3 * IMG_X + BMP * SROW * 2];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG_Y + 3 * IMG_X + BMP * SROW * 2 + (YR ? BMP * YROW * 2 : 0)];
   char* ximg = smem + 2 * IMG_Y;
   char* stg = ximg + 3 * IMG_X;
+  char* ystg = stg + BMP * SROW * 2;
   const PbArgs& a = A.b;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   // block -> (pixel slot, column block h): the NH blocks of a slot are blockIdx b, b+8, ... (one XCD)
@@ -338,6 +344,18 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     ka[j] = A.coef[cy * 8 + j];
     kb[j] = A.coef[K + cy * 8 + j];
     kc[j] = A.coef[2 * K + cy * 8 + j];
+  }
+  // YR: the wave's forward-filter slice wy[k = 64 wave + 16 j + (lane & 15)][c = 32 kk + 8 (lane >> 4) .. +7]
+  v8bf wyf[YR ? 4 : 1][2];
+  if constexpr (YR) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        wyf[j][kk] = *reinterpret_cast<const v8bf*>(A.wy + (long)(64 * wave + 16 * j + (lane & 15)) * CB + 32 * kk +
+                                                     8 * (lane >> 4));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(wyf[j][0]), "v"(wyf[j][1]));
   }
   // consume these loads before any DMA is in flight (else their waits land inside the tile loop)
 #pragma unroll
@@ -369,13 +387,28 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
       const uint32_t e = (uint32_t)p * K + cy * 8;
       const bool ok = p < a.P;
       dv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, ok ? e * 2u : 0x80000000u, 0, 0));
-      yv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, ok ? e * 2u : 0x80000000u, 0, 0));
+      if constexpr (!YR)
+        yv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, ok ? e * 2u : 0x80000000u, 0, 0));
       mb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(mr, ok ? e >> 3 : 0x80000000u, 0, 0);
       if constexpr (SC)
         sv_[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(scr, ok ? e * 2u : 0x80000000u, 0, 0));
     }
   };
   auto transform = [&](int tile, char* img) {  // dY = a dz + b y + c -> bf16 -> the K-outer image
+    if constexpr (YR) {  // this tile's y chunks from the LDS stage
+      v4i yr4[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, ystg + ((ry + RPT * u) * YROW + cy * 8) * 2);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(yr4[u]) : "v"(addr));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        asm volatile("" : "+v"(yr4[u]));
+        yv[u] = __builtin_bit_cast(uint4, yr4[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int row = ry + RPT * u;
@@ -462,6 +495,40 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     const int tile = slot + it * step;
     char* yimg = smem + (it & 1) * IMG_Y;
     const char* xim = ximg + (it % 3) * IMG_X;
+    if constexpr (YR) {
+      // every wave's X share landed; every wave is done with the previous tile's y stage
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      v4f ay[4][4];  // y[p = 16 i + (lane & 15)][k = 64 wave + 16 j + 4 (lane >> 4) + r]
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ay[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        v8bf xa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xa[i] = row_frag<CB>(xim, 16 * i, kk, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(xa[i]));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ay[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wyf[j][kk], xa[i], ay[i][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint2 o;
+          o.x = pack2bf(ay[i][j][0], ay[i][j][1]);
+          o.y = pack2bf(ay[i][j][2], ay[i][j][3]);
+          const int pl = 16 * i + (lane & 15), kl = 64 * wave + 16 * j + 4 * (lane >> 4);
+          const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, ystg + (pl * YROW + kl) * 2);
+          asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(o) : "memory");
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // y staged
+    }
     transform(tile, yimg);
     // every wave's dY share is written, every wave's X share landed; every wave is done with the dY image and the X
     // buffer that this iteration's loads below refill
@@ -643,11 +710,12 @@ DTF_API int dtf_pw_conv_bwd(const void* dY, const void* X, const void* Wck, void
 // dY = a dz + b y + c from dout, y, the ReLU bits ymask (nullptr: none) and coef [3][K] (bn_bwd_finalize's
 // coefficients, dtf_bn_bwd_coef); dY itself is never stored.
 // ysc / msc / psc (stage-1 shape only): the projection shortcut's BN-backward partial rows (see PbnArgs), *rsc rows.
+// wy (stage-1 shape only, y == nullptr): recompute y from X and the forward filter wy [K][C] instead of reading it.
 DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymask, const float* coef, const void* X,
                                const void* Wck, void* dX, float* dW, int accumulate, const void* bnx,
                                const void* bnmask, const float* bnmean, float* part, int* rows, float* ws,
                                long ws_elems, long P, int K, int C, const void* ysc, const float* msc, float* psc,
-                               int* rsc, void* stream) {
+                               int* rsc, const void* wy, void* stream) {
   using namespace dtf;
   hipStream_t st = (hipStream_t)stream;
   // stage 1 (256 -> 64): one block per 64-pixel slot; stage 2 (512 -> 128): two column blocks per 32-pixel slot
@@ -671,7 +739,12 @@ DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymas
   A.dout = (const bf16_t*)dout; A.y = (const bf16_t*)y; A.ymask = (const uint8_t*)ymask; A.coef = coef;
   if ((long)a.slots * K * C > ws_elems) return -1;
   A.ysc = (const bf16_t*)ysc; A.msc = msc; A.psc = psc;
-  if (s1 && sc) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, true>), dim3(256), dim3(256), 0, st, A);
+  A.wy = (const bf16_t*)wy;
+  // (y recompute with the shortcut sums: 49 VGPRs spill — not offered; the projection block stores its y)
+  if (wy && (!s1 || sc || y || ((uintptr_t)wy & 15))) return -1;
+  if (!wy && !y) return -1;
+  if (s1 && wy) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, false, true>), dim3(256), dim3(256), 0, st, A);
+  else if (s1 && sc) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, true>), dim3(256), dim3(256), 0, st, A);
   else if (s1) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64>), dim3(256), dim3(256), 0, st, A);
   else hipLaunchKernelGGL((pw_bwd_bn_kernel<512, 128, 32, 64>), dim3(256), dim3(256), 0, st, A);
   if (hipGetLastError() != hipSuccess) return -1;

@@ -58,6 +58,10 @@ struct PwArgs {
   // MODE 3 with bW > 0: cin is the compact [N][bH/2][bW/2][K] data gradient of a stride-2 1x1 projection of the same
   // input, added at the even pixels of the [N][bH][bW] grid only (beta 1, no mask)
   int bH, bW;
+  // MODE 3, RX: the BN input bnx is not stored — it is the bf16 output of a 64-channel-input 1x1 conv, recomputed per
+  // tile as bf16(rx rw^T) (rx [M][64], rw [K][64]) with that forward's MFMA sequence (bitwise its values)
+  const bf16_t* rx;
+  const bf16_t* rw;
 };
 
 template <int C, int WMW, bool STG = false, int MODE = 0>
@@ -96,11 +100,37 @@ __device__ __forceinline__ void stage_write(char* p, uint2 v) {
 // waits instead.
 __device__ __forceinline__ void tile_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int C, int WMW, bool STG, int MODE>
+// N 16-B chunks of the LDS store stage (byte offsets off[i] from base), by inline asm for the same reason as
+// stage_write: a plain LDS load here makes hipcc drain the DMA of the tile two ahead ("s_waitcnt vmcnt(0)") before the
+// store pass of every tile. One wait for all N reads; each result is tied to it.
+template <int N>
+__device__ __forceinline__ void stage_read(uint4 (&v)[N], const char* base, const int (&off)[N]) {
+  v4i r[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)(base + off[i]);
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r[i]) : "v"(addr));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    asm volatile("" : "+v"(r[i]));
+    v[i] = __builtin_bit_cast(uint4, r[i]);
+  }
+}
+
+template <int C, int WMW, bool STG, int MODE, bool RX = false>
 __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
   static_assert(MODE < 2 || STG, "the apply / data-gradient epilogues work on the LDS-staged tile");
+  static_assert(!RX || (MODE == 3 && WMW == 1), "bnx recompute: the data-gradient mode, one row wave");
   using G = PwGeo<C, WMW, STG, MODE>;
-  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  constexpr int RIMG = G::BM * 128;                 // RX: one [BM][64] rx sub-image
+  constexpr int LRX = RX ? G::BM / G::RPI : 0;      // RX: its DMA instructions per thread per tile
+  constexpr int LDT = G::LD + LRX;                  // DMA instructions per thread per tile
+  constexpr int YROW = 256 + 8;                     // RX: staged y row (bf16), 16-B pad
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM + (RX ? 3 * RIMG + G::BM * YROW * 2 : 0)];
+  char* rximg = smem + G::SMEM;
+  char* ystg = rximg + 3 * RIMG;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int wn = wave & 3, wm = wave >> 2;
   // block -> (column tile, row slot): the blocks of one row slot (all column tiles) are on one XCD
@@ -139,10 +169,41 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
     }
   };
 
+  // RX: the recompute operands — the wave's rw slice in registers (rows n0 + 16 j + (lane & 15)), rx tiles by DMA
+  v8bf fr[RX ? 4 : 1][2];
+  const __amdgpu_buffer_rsrc_t rxr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.rx, (short)0, RX ? (int)((long)a.M * 128) : 0, 0x00020000);
+  if constexpr (RX) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        fr[j][kk] = *reinterpret_cast<const v8bf*>(a.rw + (long)(n0 + 16 * j + (lane & 15)) * 64 + 32 * kk +
+                                                   8 * (lane >> 4));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(fr[j][0]), "v"(fr[j][1]));  // (waited for before any DMA)
+  }
+  auto issue_rx = [&](int mt, int buf) {
+    if constexpr (RX) {
+      char* img = rximg + buf * RIMG;
+#pragma unroll
+      for (int i = 0; i < LRX; ++i) {
+        const int row = G::RPI * i + (t >> 3);
+        const int r = mt * G::BM + row;
+        const uint32_t base =
+            r < a.M ? (uint32_t)r * 128u + (uint32_t)(((t & 7) ^ ((row >> 1) & 7)) * 16) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rxr, (__attribute__((address_space(3))) void*)(img + i * (G::RPI * 128) + wave * 1024), 16, base, 0, 0, 0);
+      }
+    }
+  };
+
   const int first = slot, step = a.nslots;
   const int n_mine = first < a.tiles_m ? (a.tiles_m - first + step - 1) / step : 0;
-  if (n_mine > 0) issue(first, 0);
-  if (n_mine > 1) issue(first + step, 1);
+  // every DMA is issued, past the block's last tile as a dummy one (every row out of range: zeros into a ring buffer no
+  // tile uses), so each wait count below is the same on every iteration — and so are hipcc's own counts for the loads
+  // issued before a DMA (with a conditional DMA it assumes the no-DMA path and drains it)
+  auto tile_of = [&](int i) { return i < n_mine ? first + i * step : a.tiles_m; };
 
   float cs[4][4], cq[4][4];
 #pragma unroll
@@ -166,7 +227,7 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
   const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.cin, (short)0, (MODE == 3 && a.cin) ? (int)((long)(a.bW ? a.M / 4 : a.M) * a.K * 2) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t xbr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.bnx, (short)0, (MODE == 3 && a.bnmean) ? (int)((long)a.M * a.K * 2) : 0, 0x00020000);
+      (void*)a.bnx, (short)0, (MODE == 3 && a.bnmean && !RX) ? (int)((long)a.M * a.K * 2) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t bmr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.betamask, (short)0, (MODE == 3 && a.betamask) ? (int)((long)a.M * a.K / 8) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t xmr = __builtin_amdgcn_make_buffer_rsrc(
@@ -187,26 +248,35 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
       rsh[j] = a.rscale ? a.rshift[nch + j] : 0.f;
     }
   }
+  // consume every per-kernel register operand loaded above (filter slices, coefficients, means) BEFORE the first DMA:
+  // hipcc otherwise places their vmcnt waits at their first use inside the tile loop, where on every later iteration
+  // those waits hold up the in-flight DMA and stores instead
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < C / 32; ++s) asm volatile("" ::"v"(fb[j][s]));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if constexpr (MODE == 2) asm volatile("" ::"v"(bsc[j]), "v"(bsh[j]), "v"(rsc[j]), "v"(rsh[j]));
+    if constexpr (MODE == 3) asm volatile("" ::"v"(mu3[j]));
+  }
+  issue(tile_of(0), 0);
+  issue_rx(tile_of(0), 0);
+  issue(tile_of(1), 1);
+  issue_rx(tile_of(1), 1);
 
   for (int it = 0; it < n_mine; ++it) {
-    // tile `it` landed. MODE 0: the ops this thread issued after it are tile it+1's DMA (if any) and tile it-1's
-    // stores. MODE 1: only tile it+1's DMA. MODE 2: tile `it` is older than tile it-1's residual loads, which
-    // iteration it-1 waited for — only the first tile needs a wait here.
+    // tile `it` landed. MODE 0: the ops this thread issued after it are tile it+1's DMA (a dummy past the last tile)
+    // and tile it-1's stores. MODE 1: only tile it+1's DMA. MODE 2 / 3: tile `it` is older than tile it-1's loads,
+    // which iteration it-1 waited for — only the first tile needs a wait here.
     if constexpr (MODE == 0) {
-      if (it + 1 < n_mine) {
-        if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD + G::ST) : "memory");
-      } else {
-        if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::ST) : "memory");
-      }
+      if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD + G::ST) : "memory");
     } else if constexpr (MODE == 1) {
-      if (it + 1 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
     } else {  // MODE 2 / 3
       if (it == 0) {
-        if (n_mine > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LDT) : "memory");
       }
     }
     tile_barrier();  // every wave's DMA share landed; every wave is done with the buffer tile it+2 reuses
@@ -244,23 +314,23 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
 #pragma unroll
       for (int k = 0; k < G::ST; ++k) {
         rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cr, coff[k], 0, 0));
-        xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbr, off[k], 0, 0));
+        if constexpr (!RX) xv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xbr, off[k], 0, 0));
         bmb[k] = ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(bmr, boff[k], 0, 0) | bm_or) & cbits[k];
         xmb[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(xmr, boff[k], 0, 0) | xm_or;
       }
     }
-    if constexpr (MODE == 2) {
-      if (a.res) {
+    if constexpr (MODE == 2) {  // (unconditional: without a residual the range is empty and the loads return zeros;
+                                 // a branch here makes hipcc wait for them at the join)
 #pragma unroll
-        for (int k = 0; k < G::ST; ++k) {
-          const int row = (t + k * G::NTH) >> 5;
-          const int m = mt * G::BM + row;
-          const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)nch) * 2u : 0x80000000u;
-          rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
-        }
+      for (int k = 0; k < G::ST; ++k) {
+        const int row = (t + k * G::NTH) >> 5;
+        const int m = mt * G::BM + row;
+        const uint32_t off = m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)nch) * 2u : 0x80000000u;
+        rv[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
       }
     }
-    if (it + 2 < n_mine) issue(first + (it + 2) * step, (it + 2) % G::NBUF);
+    issue(tile_of(it + 2), (it + 2) % G::NBUF);
+    issue_rx(tile_of(it + 2), (it + 2) % G::NBUF);
     const char* img = smem + (it % G::NBUF) * G::IMG;
 
     v4f acc[4][4];
@@ -317,11 +387,16 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
     }
     if constexpr (STG && MODE == 0) {
       tile_barrier();  // the tile is staged (the next tile's staging writes come after the next top barrier)
+      uint4 sv[G::ST];
+      int so[G::ST];
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) so[k] = (((t + k * G::NTH) >> 5) * G::SROW + ((t + k * G::NTH) & 31) * 8) * 2;
+      stage_read(sv, stg, so);
 #pragma unroll
       for (int k = 0; k < G::ST; ++k) {
         const int c = t + k * G::NTH, row = c >> 5, ch = c & 31;
         const int m = mt * G::BM + row;
-        const uint4 v = *reinterpret_cast<const uint4*>(stg + (row * G::SROW + ch * 8) * 2);
+        const uint4 v = sv[k];
         const uint32_t off =
             m < a.M ? ((uint32_t)m * (uint32_t)a.K + (uint32_t)(tile_n * 256 + ch * 8)) * 2u : 0x80000000u;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), yr, off, 0, 0);
@@ -330,13 +405,17 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
     if constexpr (MODE == 2) {
       tile_barrier();  // the tile is staged
       // the residual chunks are in: everything but tile it+2's DMA (issued after them) has completed
-      if (it + 2 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
+      uint4 sv[G::ST];
+      int so[G::ST];
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) so[k] = (((t + k * G::NTH) >> 5) * G::SROW + ch * 8) * 2;
+      stage_read(sv, stg, so);
 #pragma unroll
       for (int k = 0; k < G::ST; ++k) {
         const int row = (t + k * G::NTH) >> 5;
         const int m = mt * G::BM + row;
-        const uint4 yv = *reinterpret_cast<const uint4*>(stg + (row * G::SROW + ch * 8) * 2);
+        const uint4 yv = sv[k];
         const uint32_t e = (uint32_t)m * (uint32_t)a.K + (uint32_t)nch;  // element index (valid rows)
         const uint32_t off = m < a.M ? e * 2u : 0x80000000u;
         if (a.Y) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, yv), yr, off, 0, 0);
@@ -370,15 +449,53 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
       }
     }
     if constexpr (MODE == 3) {
-      tile_barrier();  // the tile is staged
+      if constexpr (RX) {
+        // the BN input of this tile: y = bf16(rx rw^T) for the wave's 64 columns, the producing pwconv forward's MFMA
+        // sequence (fragments in the same k order, kk 0 then 1), staged for the store pass
+        const char* rimg = rximg + (it % G::NBUF) * RIMG;
+        v4f ay[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ay[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          v8bf fa[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fa[i] = frag_kcontig(rimg, 16 * i, kk, lane);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ay[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[j][kk], fa[i], ay[i][j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            uint2 o;
+            o.x = pack2bf(ay[i][j][0], ay[i][j][1]);
+            o.y = pack2bf(ay[i][j][2], ay[i][j][3]);
+            stage_write(ystg + ((16 * i + (lane & 15)) * YROW + wn * 64 + 16 * j + 4 * (lane >> 4)) * 2, o);
+          }
+      }
+      tile_barrier();  // the tile is staged (RX: and its BN input)
       // the tile's loads are in: everything but tile it+2's DMA (issued after them) has completed
-      if (it + 2 < n_mine) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LD) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LDT) : "memory");
+      uint4 sv[G::ST];
+      int so[G::ST];
+#pragma unroll
+      for (int k = 0; k < G::ST; ++k) so[k] = (((t + k * G::NTH) >> 5) * G::SROW + ch * 8) * 2;
+      stage_read(sv, stg, so);
+      if constexpr (RX) {
+#pragma unroll
+        for (int k = 0; k < G::ST; ++k) so[k] = (((t + k * G::NTH) >> 5) * YROW + ch * 8) * 2;
+        stage_read(xv, ystg, so);
+      }
 #pragma unroll
       for (int k = 0; k < G::ST; ++k) {
         const int row = (t + k * G::NTH) >> 5;
         const int m = mt * G::BM + row;
-        uint4 val = *reinterpret_cast<const uint4*>(stg + (row * G::SROW + ch * 8) * 2);
+        uint4 val = sv[k];
         if (a.cin) {  // gemm_epilogue's staged beta path, operation for operation
           const uint32_t vw[4] = {val.x, val.y, val.z, val.w}, ow[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
           float f[8], g[8];
@@ -411,6 +528,9 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
       }
     }
   }
+  // the dummy DMA past the last tile (and, for blocks without tiles, both prologue ones) lands in the ring before it
+  // is reused below
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (MODE == 2) return;  // (no statistics)
   if constexpr (MODE == 3) {
     if (!a.bnmean) return;
@@ -462,15 +582,19 @@ __global__ void __launch_bounds__(256 * WMW, 1) pw_conv_kernel(PwArgs a) {
   }
 }
 
-template <int C, int WMW, bool STG, int MODE>
+template <int C, int WMW, bool STG, int MODE, bool RX = false>
 void launch_pw(const PwArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((pw_conv_kernel<C, WMW, STG, MODE>), dim3(grid), dim3(256 * WMW), 0, st, a);
+  hipLaunchKernelGGL((pw_conv_kernel<C, WMW, STG, MODE, RX>), dim3(grid), dim3(256 * WMW), 0, st, a);
 }
 
 template <int MODE>
 void launch_pw_c(const PwArgs& a, int C, int grid, hipStream_t st) {
   // (MODE 3 keeps one row wave for C 64 too: its epilogue holds four operands per chunk in flight, which needs the
   // one-wave-per-SIMD register budget — two row waves spill)
+  if constexpr (MODE == 3) {  // (RX: the stage-1 BN inputs, consumed by the C 64 / 128 data gradients only)
+    if (a.rx && C == 64) return launch_pw<64, 1, true, MODE, true>(a, grid, st);
+    if (a.rx && C == 128) return launch_pw<128, 1, true, MODE, true>(a, grid, st);
+  }
   if (C == 64) {
     if constexpr (MODE == 3) launch_pw<64, 1, true, MODE>(a, grid, st);
     else launch_pw<64, 2, true, MODE>(a, grid, st);
@@ -526,11 +650,14 @@ int pwconv_try(const void* X, const void* W, void* Y, float* stats, long M, int 
 // bsrc2 (with H, W even): instead of beta * dX, add the compact stride-2 shortcut gradient at the even pixels.
 int pwconv_dgrad_try(const void* dY, const void* Wck, void* dX, float beta, const void* betamask, const void* bnx,
                      const void* bnmask, const float* bnmean, float* part, long M, int Kc, int N, const void* bsrc2,
-                     int H, int W, hipStream_t st) {
+                     int H, int W, hipStream_t st, const void* bnrx, const void* bnrw) {
   if (((uintptr_t)dY & 15) || ((uintptr_t)Wck & 15) || ((uintptr_t)dX & 15) || ((uintptr_t)bnx & 15) ||
       ((uintptr_t)bsrc2 & 15))
     return 0;
-  if ((bnmean != nullptr) != (part != nullptr) || (bnmean && !bnx) || (betamask && beta == 0.f)) return 0;
+  if ((bnmean != nullptr) != (part != nullptr) || (bnmean && !bnx && !bnrx) || (betamask && beta == 0.f)) return 0;
+  if (bnrx && (bnx || !bnmean || !bnrw || N != 256 || (Kc != 64 && Kc != 128) || ((uintptr_t)bnrx & 15) ||
+               ((uintptr_t)bnrw & 15) || M * 128 >= (1l << 31)))
+    return 0;
   if (bsrc2 && (betamask || (H & 1) || (W & 1) || (long)H * W <= 0 || M % ((long)H * W))) return 0;
   PwArgs a{};
   int grid = 0;
@@ -546,6 +673,7 @@ int pwconv_dgrad_try(const void* dY, const void* Wck, void* dX, float beta, cons
   a.beta = beta;
   a.betamask = (const uint8_t*)betamask;
   a.bnx = (const bf16_t*)bnx; a.bnmask = (const uint8_t*)bnmask; a.bnmean = bnmean;
+  a.rx = (const bf16_t*)bnrx; a.rw = (const bf16_t*)bnrw;
   launch_pw_c<3>(a, Kc, grid, st);
   return hipGetLastError() == hipSuccess ? a.nslots : 0;
 }

@@ -30,12 +30,12 @@ _KERNEL_SIGS = {
     "dtf_conv_dgrad": [P, P, P] + [I] * 15 + [I, F, I, P, L, P, P, P, P, P, P, P],
     "dtf_conv_dgrad_addsub2": [P, P, P, P, I, I, I, I, I, I, P, L, P, P, P, P, P, P],
     "dtf_conv_fwd_bn": [P, P, P, P] + [I] * 15 + [I, P, P, P, P, F, F, P, P, P, P, P, P],
-    "dtf_conv_dgrad_x": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P],
+    "dtf_conv_dgrad_x": [P, P, P] + [I] * 15 + [F, P, L, P, P, P, P, P, P, P, P, P, P],
     "dtf_bn_bwd_apply_coef": [P, P, P, L, I, P, P, P, P, P, P, P, P],
     "dtf_set_ew_variant": [I],
     "dtf_set_pw_dgrad": [I],
     "dtf_pw_conv_bwd": [P, P, P, P, P, I, P, P, P, P, P, P, L, L, I, I, P],
-    "dtf_pw_conv_bwd_bn": [P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P],
+    "dtf_pw_conv_bwd_bn": [P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P, P],
     "dtf_bn_bwd_coef": [P, I, P, P, P, L, I, P, P, I, P, P],
     "dtf_set_pw_wgrad": [I],
     "dtf_set_split_penalty": [I],

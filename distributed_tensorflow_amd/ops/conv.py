@@ -87,12 +87,32 @@ def conv_dgrad_raw(dy, w_master, g, acc=None, bn=None, acc_mask=None, acc_sub2=N
     bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
     if acc_sub2 is not None:  # + the compact gradient of a stride-2 1x1 shortcut at the even pixels
         assert acc is None and (R, S, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0)
-    call("dtf_conv_dgrad_x", ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
-         1.0 if (acc is not None or acc_sub2 is not None) else 0.0, ptr(ws), 2 * ws.numel(), *bn_ptrs, ptr(part),
-         rows.addr if rows else None, ptr(acc_mask) if acc is not None else None, ptr(acc_sub2), stream())
+    rx = (ptr(bn.rx), ptr(bf16_shadow(bn.rw))) if (bn is not None and bn.yc is None) else (None, None)
+    args = (ptr(dy), ptr(wc), ptr(dx), N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw,
+            1.0 if (acc is not None or acc_sub2 is not None) else 0.0, ptr(ws), 2 * ws.numel())
+    tail = (ptr(part), rows.addr if rows else None, ptr(acc_mask) if acc is not None else None, ptr(acc_sub2))
+    rc = K_().dtf_conv_dgrad_x(*args, None, ptr(bn.mbits), ptr(bn.mean), *tail, *rx, stream()) if rx[0] else -12
+    if rc == -12:  # (the BN input is stored, or only the persistent pointwise route can recompute it)
+        if bn is not None:
+            bn_ptrs = (ptr(bn.materialize()), ptr(bn.mbits), ptr(bn.mean))
+        call("dtf_conv_dgrad_x", *args, *bn_ptrs, *tail, None, None, stream())
+    elif rc != 0:
+        raise RuntimeError(f"dtf_conv_dgrad_x failed with status {rc}")
     if bn is not None:
         bn.provide(dx, part, rows.value)
     return dx
+
+
+def _recompute_y(x, w, g):
+    """bf16(x w^T) of a stage-1 channel-expanding 1x1 conv whose output was not stored, with the pointwise forward
+    kernel the two-pass forward used (the same MFMA sequence: bitwise its values)."""
+    N, H, W, C, K = g[:5]
+    M = N * H * W
+    y = torch.empty((N, H, W, K), dtype=BF16, device=x.device)
+    stats = torch.empty(((M + 63) // 64) * 2 * K, dtype=F32, device=x.device)
+    rows = IntOut()
+    call("dtf_pwconv_fwd", ptr(x), ptr(bf16_shadow(w)), ptr(y), ptr(stats), rows.addr, M, C, K, stream())
+    return y
 
 
 def pw_bwd_ok(g, M_min=64 * 256):
@@ -127,7 +147,7 @@ def conv_bwd_fused_raw(dy, x, w_master, g, dw_out, bn=None):
     if bn is not None:
         part = torch.empty(256 * 2 * C, dtype=F32, device=dy.device)
         rows = IntOut()
-    bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
+    bn_ptrs = ((ptr(bn.materialize()), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
     call("dtf_pw_conv_bwd", ptr(dy), ptr(x), ptr(wc), ptr(dx), ptr(dw_out), 1, *bn_ptrs, ptr(part),
          rows.addr if rows else None, ptr(ws), ws.numel(), M, K, C, stream())
     if bn is not None:
@@ -135,11 +155,12 @@ def conv_bwd_fused_raw(dy, x, w_master, g, dw_out, bn=None):
     return dx
 
 
-def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None, sc=None):
+def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None, sc=None, wy=None):
     """conv_bwd_fused_raw with dy = a*dz + b*y + c (the BatchNorm(+ReLU) backward of y = conv output, coefficients
     coef [3K] from dtf_bn_bwd_coef, dz = dout under the ReLU bits ymask) computed inside the kernel. With `sc` (the
     _BNSource of a deferred projection-shortcut BN added as this layer's residual) the kernel also takes that BN's
-    backward reduction of dz and provides it to the source for `dout`."""
+    backward reduction of dz and provides it to the source for `dout`. With `wy` (the layer's bf16 forward filter) and
+    y None, y is recomputed per tile from x (it was not stored).""" 
     N, H, W, C, K = g[:5]
     M = N * H * W
     wc = crsk_shadow(w_master, K, 1, C)
@@ -149,14 +170,14 @@ def conv_bwd_bn_fused_raw(dout, y, ymask, coef, x, w_master, g, dw_out, bn=None,
     if bn is not None:
         part = torch.empty(256 * 2 * C, dtype=F32, device=dout.device)  # (<= 256 pixel slots)
         rows = IntOut()
-    bn_ptrs = ((ptr(bn.yc), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
+    bn_ptrs = ((ptr(bn.materialize()), ptr(bn.mbits), ptr(bn.mean)) if bn is not None else (None, None, None))
     psc = rsc = None
     if sc is not None:
         psc, rsc = torch.empty(256 * 2 * K, dtype=F32, device=dout.device), IntOut()
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ymask), ptr(coef), ptr(x), ptr(wc), ptr(dx), ptr(dw_out), 1,
          *bn_ptrs, ptr(part), rows.addr if rows else None, ptr(ws), ws.numel(), M, K, C,
          ptr(sc.yc) if sc is not None else None, ptr(sc.mean) if sc is not None else None, ptr(psc),
-         rsc.addr if rsc else None, stream())
+         rsc.addr if rsc else None, ptr(wy), stream())
     if bn is not None:
         bn.provide(dx, part, rows.value)
     if sc is not None:
@@ -280,14 +301,23 @@ class _BNSource:
     backward then skips its reduction pass (bn_bwd_reduce), provided the gradient it receives is exactly the
     tensor that dgrad wrote (same storage: autograd added nothing else to it)."""
     __slots__ = ("yc", "mbits", "mean", "invstd", "gamma", "gamma_p", "beta_p", "consumers", "part", "rows", "dx",
-                 "ver", "__weakref__")
+                 "ver", "rx", "rw", "g", "__weakref__")
 
-    def __init__(self, yc, mbits, mean, invstd=None, gamma=None, params=(None, None)):
+    def __init__(self, yc, mbits, mean, invstd=None, gamma=None, params=(None, None), recompute=None):
         self.yc, self.mbits, self.mean = yc, mbits, mean
         self.invstd, self.gamma = invstd, gamma
         self.gamma_p, self.beta_p = params
         self.consumers = 0
         self.part = self.rows = self.dx = self.ver = None
+        # yc not stored: it is bf16(rx rw^T), the producing 1x1 conv's output (input rx, filter parameter rw, geometry
+        # g), recomputed by the consumers that can (pwconv.hip RX, pwbwd.hip YR) or materialised on demand
+        self.rx, self.rw, self.g = recompute if recompute is not None else (None, None, None)
+
+    def materialize(self):
+        """The BN input yc, recomputed once (bitwise the forward's values) if it was not stored."""
+        if self.yc is None:
+            self.yc = _recompute_y(self.rx, self.rw, self.g)
+        return self.yc
 
     def provide(self, dx, part, rows):
         # dx itself is held (not its address), with its version: see nn.same_unmodified
@@ -319,7 +349,9 @@ _TWO_PASS_PW = os.environ.get("DTF_PW2", "1") != "0"
 # the weight gradient on the main stream instead of the side stream.
 # Level 2 also folds the conv output's BatchNorm(+ReLU) backward into that pass when its reduction is already done
 # (identity blocks: dY = a dz + b y + c computed per tile, never stored: the standalone apply pass disappears).
-_FUSED_PW_BWD = int(os.environ.get("DTF_PW_BWD", "2"))
+# Level 3 (default) stops storing the stage-1 identity blocks' c3 output y at all: the folded pass and the next
+# block's c1 data gradient recompute it per tile from the c3 input (bitwise the forward's values).
+_FUSED_PW_BWD = int(os.environ.get("DTF_PW_BWD", "3"))
 
 
 def _two_pass_ok(g):
@@ -359,8 +391,12 @@ class _ConvBNFn(torch.autograd.Function):
         if training and not deferred and _TWO_PASS_PW and _two_pass_ok(g):
             # channel-expanding 1x1 (bottleneck c3): statistics pass, finalize, then the recomputed product with the
             # BatchNorm / residual / ReLU applied in the epilogue (pwconv.hip MODE 1 / 2) — no standalone apply pass
-            yc = torch.empty((N, P, Q, K), dtype=BF16, device=dev)
-            out = torch.empty_like(yc)
+            # level 3: an identity block's stage-1 c3 output is not stored at all — its consumers (this layer's
+            # BatchNorm-folded backward, the next block's c1 data gradient) recompute it from x and w
+            keep_y = not (_FUSED_PW_BWD >= 3 and (C, K) == (64, 256) and relu and res is not None and raff is None
+                          and link is not None and role == "res" and M >= 64 * 256 and any(ctx.needs_input_grad))
+            yc = torch.empty((N, P, Q, K), dtype=BF16, device=dev) if keep_y else None
+            out = torch.empty((N, P, Q, K), dtype=BF16, device=dev)
             mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if relu else None
             part = torch.empty(((M + 63) // 64) * 2 * K, dtype=F32, device=dev)
             rc_ = res.contiguous() if res is not None else None
@@ -407,7 +443,8 @@ class _ConvBNFn(torch.autograd.Function):
         ctx.res_src = res_src if (training and _FUSE_BN_BWD) else None
         ctx.src = None
         if training and _FUSE_BN_BWD and any(ctx.needs_input_grad):
-            src = _BNSource(yc, mbits, mean, invstd, gamma, (gamma, beta))
+            src = _BNSource(yc, mbits, mean, invstd, gamma, (gamma, beta),
+                            recompute=(x, w, g) if yc is None else None)
             out._dtf_bnsrc = src
             ctx.src = src
         return out
@@ -417,7 +454,8 @@ class _ConvBNFn(torch.autograd.Function):
         x, w, gamma, yc, mbits, mean, invstd = ctx.saved_tensors
         g = ctx.g
         K = g[4]
-        M = yc.numel() // K
+        M = g[0] * g[7] * g[8]
+        yshape, dev = (g[0], g[7], g[8], K), x.device
         # a deferred projection BN whose consumer handed over its raw incoming gradient with the ReLU bits to apply
         # (see the projection-block branch below): dz = dout under that mask
         dmask = getattr(dout, "_dtf_mask", None)
@@ -427,35 +465,37 @@ class _ConvBNFn(torch.autograd.Function):
             mbits = dmask
         if not ctx.training:
             return _ConvBNFn._backward_frozen(ctx, dout, x, w, gamma, yc, mbits, mean, invstd)
-        dyc = torch.empty_like(yc)
+        dyc = torch.empty(yshape, dtype=BF16, device=dev)
         link, role = ctx.link, ctx.role
         # identity shortcut with ReLU: park dout + the ReLU mask instead of writing the masked residual gradient
         lazy_res = (ctx.has_res and ctx.relu and link is not None and role == "res" and not link.closed
                     and _LAZY_RES and mbits is not None)
-        dres = torch.empty_like(yc) if (ctx.has_res and ctx.relu and not lazy_res) else None
+        dres = torch.empty(yshape, dtype=BF16, device=dev) if (ctx.has_res and ctx.relu and not lazy_res) else None
         gamma_p, beta_p = ctx.bn_params
         tg, tb = direct_grad(gamma_p), direct_grad(beta_p)
         direct_bn = tg is not None and tb is not None  # accumulate dgamma/dbeta into the arena grads
-        dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
-        dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
+        dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=dev)
+        dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=dev)
         fused = ctx.src.take(dout) if ctx.src is not None else None
         rsrc = ctx.res_src if dres is not None else None
         sc = (None, None, None, None)
         if rsrc is not None:  # projection shortcut BN: its backward reduction rides on our apply pass
-            part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=yc.device), IntOut()
+            part2, rows2 = torch.empty(2048 * 2 * K, dtype=F32, device=dev), IntOut()
             sc = (ptr(rsrc.yc), ptr(rsrc.mean), ptr(part2), rows2.addr)
         if (fused is not None and lazy_res and rsrc is None and _FUSED_PW_BWD >= 2 and ctx.needs_input_grad[0]
-                and ctx.needs_input_grad[1] and pw_bwd_bn_ok(g) and x.is_contiguous() and x.dtype == BF16):
+                and ctx.needs_input_grad[1] and pw_bwd_bn_ok(g) and x.is_contiguous() and x.dtype == BF16
+                and (yc is not None or (g[4], g[3]) == (256, 64))):
             tw = direct_grad(w)
             if tw is not None:
                 # identity-block c3: finalize the BN-backward reduction only, then ONE pass computes dY per tile from
                 # dout / yc / the ReLU bits and both conv gradients from it (dY is never stored)
-                coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+                coef = torch.empty(3 * K, dtype=F32, device=dev)
                 call("dtf_bn_bwd_coef", ptr(fused[1]), fused[2], ptr(mean), ptr(invstd), ptr(gamma), M, K,
                      ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(coef), stream())
                 src = ctx.in_src
                 complete = src is not None and src.consumers == 1
-                dx = conv_bwd_bn_fused_raw(dout, yc, mbits, coef, x, w, g, tw, bn=src if complete else None)
+                dx = conv_bwd_bn_fused_raw(dout, yc, mbits, coef, x, w, g, tw, bn=src if complete else None,
+                                           wy=bf16_shadow(w) if yc is None else None)
                 # the identity shortcut's gradient: dout parked with the ReLU mask (read above, in stream order, before
                 # the first conv's dgrad overwrites it)
                 link.park(dout, mask=mbits)
@@ -466,12 +506,13 @@ class _ConvBNFn(torch.autograd.Function):
                         None)
         blk_ok = (_FUSED_PW_BWD >= 2 and fused is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
                   and x.is_contiguous() and x.dtype == BF16)
-        if blk_ok and rsrc is not None and not lazy_res and ctx.relu and pw_bwd_bn_ok(g) and g[4] == 256 and g[3] == 64:
+        if (blk_ok and yc is not None and rsrc is not None and not lazy_res and ctx.relu and pw_bwd_bn_ok(g)
+                and g[4] == 256 and g[3] == 64):
             tw = direct_grad(w)
             if tw is not None:
                 # projection-block c3 (stage 1): the same one-pass form, also taking the shortcut BN's reduction of
                 # dz; the shortcut then receives the raw dout tagged with the ReLU bits instead of a materialised dz
-                coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+                coef = torch.empty(3 * K, dtype=F32, device=dev)
                 call("dtf_bn_bwd_coef", ptr(fused[1]), fused[2], ptr(mean), ptr(invstd), ptr(gamma), M, K,
                      ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(coef), stream())
                 src = ctx.in_src
@@ -484,12 +525,12 @@ class _ConvBNFn(torch.autograd.Function):
                     dgamma = dbeta = None
                 return (dx, None, dgamma, dbeta, dout, None, None, None, None, None, None, None, None, None, None,
                         None)
-        if (blk_ok and dmask is not None and role == "proj" and rsrc is None and pw_bwd_bn_ok(g)
+        if (blk_ok and yc is not None and dmask is not None and role == "proj" and rsrc is None and pw_bwd_bn_ok(g)
                 and g[4] == 256 and g[3] == 64):
             tw = direct_grad(w)
             if tw is not None:
                 # the stride-1 projection of that block: its BN backward folded into its own gradient pass
-                coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+                coef = torch.empty(3 * K, dtype=F32, device=dev)
                 call("dtf_bn_bwd_coef", ptr(fused[1]), fused[2], ptr(mean), ptr(invstd), ptr(gamma), M, K,
                      ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(coef), stream())
                 dx = conv_bwd_bn_fused_raw(dout, yc, mbits, coef, x, w, g, tw)
@@ -500,13 +541,15 @@ class _ConvBNFn(torch.autograd.Function):
                     dgamma = dbeta = None
                 return (dx, None, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None,
                         None)
+        if yc is None:  # (not stored by the forward and not recomputed inside a fused pass above)
+            yc = _recompute_y(x, w, g)
         if fused is not None:  # the consumer's dgrad epilogue already reduced this gradient
-            coef = torch.empty(3 * K, dtype=F32, device=yc.device)
+            coef = torch.empty(3 * K, dtype=F32, device=dev)
             call("dtf_bn_bwd_partials", ptr(dout), ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
                  ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(fused[1]), fused[2], ptr(coef),
                  *sc, stream())
         else:
-            work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
+            work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=dev)
             call("dtf_bn_bwd", ptr(dout), None, ptr(mbits), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), M, K,
                  ptr(dyc), ptr(dres), ptr(dgamma), ptr(dbeta), int(direct_bn), ptr(work), *sc, stream())
         if rsrc is not None and rows2.value > 0:

@@ -53,7 +53,7 @@ def test_pw_bwd_matches_separate_kernels(cuda, P, with_bn):
     try:
         call("dtf_conv_dgrad_x", ptr(dy), ptr(wck), ptr(dx2), P, 1, 1, C, K, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0.0,
              ptr(ws), 16, ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part2),
-             ctypes.addressof(rows2) if with_bn else None, None, None, stream())
+             ctypes.addressof(rows2) if with_bn else None, None, None, None, None, stream())
     finally:
         call("dtf_set_pw_dgrad", 1)
     dw2 = dw0.clone()
@@ -98,7 +98,7 @@ def test_pw_bwd_bn_stage2_matches_separate_kernels(cuda, P):
     rows = ctypes.c_int(0)
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
          ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part), ctypes.addressof(rows), ptr(ws), ws.numel(), P, K, C,
-         None, None, None, None, stream())
+         None, None, None, None, None, stream())
     dyc = torch.empty(P, K, dtype=BF, device=cuda)
     call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(ym), ptr(y), P, K, ptr(dyc), None, ptr(coef), None, None, None,
          None, stream())
@@ -109,7 +109,7 @@ def test_pw_bwd_bn_stage2_matches_separate_kernels(cuda, P):
     try:
         call("dtf_conv_dgrad_x", ptr(dyc), ptr(wck), ptr(dx2), P, 1, 1, C, K, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 0.0,
              ptr(ws), 16, ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part2), ctypes.addressof(rows2), None, None,
-             stream())
+             None, None, stream())
     finally:
         call("dtf_set_pw_dgrad", 1)
     torch.cuda.synchronize()
@@ -150,7 +150,7 @@ def test_pw_bwd_bn_matches_apply_then_fused(cuda, P):
     rows = ctypes.c_int(0)
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
          ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), ptr(part), ctypes.addressof(rows), ptr(ws), ws.numel(), P, K, C,
-         None, None, None, None, stream())
+         None, None, None, None, None, stream())
     dyc = torch.empty(P, K, dtype=BF, device=cuda)
     call("dtf_bn_bwd_apply_coef", ptr(dout), ptr(ym), ptr(y), P, K, ptr(dyc), None, ptr(coef), None, None, None,
          None, stream())
@@ -170,13 +170,15 @@ def test_pw_bwd_bn_matches_apply_then_fused(cuda, P):
     assert (ref.float() - dyc.float()).abs().max().item() <= 1e-2 * ref.float().abs().max().item()
 
 
-@pytest.mark.parametrize("level", [1, 2])
+@pytest.mark.parametrize("level", [1, 2, 3])
 def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
     """Three stage-1 bottlenecks trained the framework's way (arena gradients, direct accumulation). Level 1: every c3
     and the stride-1 projection take the fused data + weight gradient; level 2: the middle block's c3 (identity
     block whose BN-backward reduction its consumer already took), the projection block's c3 (with the shortcut BN
     reduction) and its stride-1 projection also fold the BatchNorm backward in. Gradients agree
-    with the unfused path to f32 summation order."""
+    with the unfused path to f32 summation order. Level 3: the identity blocks' c3 outputs are not stored; the middle
+    block's fold recomputes y per tile, the last block's c1 data gradient recomputes its BN input, the last c3
+    (no fused reduction: the loss consumes it) materialises it."""
     from distributed_tensorflow_amd.keras import initializers
     from distributed_tensorflow_amd.models import resnet as R
     from distributed_tensorflow_amd.ops._util import direct_grads
@@ -212,7 +214,7 @@ def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
             loss.backward()
         torch.cuda.synchronize()
         runs[lv] = [xx.grad.float(), arena.grad.clone()]
-        want = {0: (0, 0), 1: (4, 0), 2: (1, 3)}[lv]
+        want = {0: (0, 0), 1: (4, 0), 2: (1, 3), 3: (1, 3)}[lv]
         assert (seen.get("dtf_pw_conv_bwd", 0), seen.get("dtf_pw_conv_bwd_bn", 0)) == want, seen
     for a, b in zip(runs[0], runs[level]):
         assert torch.isfinite(b).all()
@@ -286,7 +288,7 @@ def test_pw_bwd_bn_shortcut_partials(cuda):
     rsc = ctypes.c_int(0)
     call("dtf_pw_conv_bwd_bn", ptr(dout), ptr(y), ptr(ym), ptr(coef), ptr(x), ptr(wck), ptr(dx), ptr(dw), 1,
          None, None, None, None, None, ptr(ws), ws.numel(), P, K, C, ptr(ysc), ptr(msc), ptr(psc),
-         ctypes.addressof(rsc), stream())
+         ctypes.addressof(rsc), None, stream())
     dyc = torch.empty(P, K, dtype=BF, device=cuda)
     dz = torch.empty(P, K, dtype=BF, device=cuda)
     part2 = torch.empty(4096 * 2 * K, device=cuda)
@@ -301,3 +303,41 @@ def test_pw_bwd_bn_shortcut_partials(cuda):
     sc = ref.abs().max().item() + 1.0
     assert torch.allclose(s1, s2, atol=1e-4 * sc, rtol=1e-4)
     assert torch.allclose(s1, ref, atol=1e-3 * sc, rtol=1e-3)
+
+
+def test_pw_dgrad_recomputes_bn_input(cuda):
+    """pwconv.hip MODE 3 with the BN input recomputed per tile (RX: bf16(rx rw^T), the stage-1 c3 output the forward
+    did not store) equals MODE 3 reading the materialised BN input: dX and the partial rows bitwise (same values,
+    same order); plain and compact-shortcut forms."""
+    from distributed_tensorflow_amd.ops._util import bf16_shadow
+    for imgs, H, W, Kc, sub2 in ((16, 32, 32, 64, False), (16, 32, 32, 128, True)):
+        M, N = imgs * H * W, 256
+        g = torch.Generator(device="cpu").manual_seed(Kc)
+        dy = torch.randn(M, Kc, generator=g).to(BF).to(cuda)
+        wck = (torch.randn(N, Kc, generator=g) * Kc ** -0.5).to(BF).to(cuda)
+        rx = torch.relu(torch.randn(M, 64, generator=g)).to(BF).to(cuda)
+        rw = (torch.randn(N, 64, generator=g) * 0.125).to(BF).to(cuda)
+        y = OC._recompute_y(rx, rw, (imgs, H, W, 64, N))
+        ref_y = (rx.float() @ rw.float().t()).to(BF)
+        assert (y.view(M, N).float() - ref_y.float()).abs().max().item() <= 1e-2 * ref_y.float().abs().max().item()
+        mask = _bits(torch.rand(M, N, generator=g) > 0.5).to(cuda)
+        mean = (torch.randn(N, generator=g) * 0.1).to(cuda)
+        s2 = torch.randn(imgs, H // 2, W // 2, N, generator=g).to(BF).to(cuda) if sub2 else None
+        acc = None if sub2 else torch.randn(M, N, generator=g).to(BF).to(cuda)
+        outs = []
+        for mode in ("stored", "rx"):
+            dx = acc.clone() if acc is not None else torch.empty(M, N, dtype=BF, device=cuda)
+            part = torch.full(((M + 63) // 64 * 2 * N,), float("nan"), device=cuda)
+            rows = ctypes.c_int(0)
+            ws = torch.empty(16, dtype=BF, device=cuda)
+            bnx = y if mode == "stored" else None
+            rr = (ptr(rx), ptr(rw)) if mode == "rx" else (None, None)
+            call("dtf_conv_dgrad_x", ptr(dy), ptr(wck), ptr(dx), imgs, H, W, N, Kc, 1, 1, H, W, 1, 1, 0, 0, 1, 1,
+                 1.0 if acc is not None else 0.0, ptr(ws), 16, ptr(bnx), ptr(mask), ptr(mean), ptr(part),
+                 ctypes.addressof(rows), None, ptr(s2), *rr, stream())
+            torch.cuda.synchronize()
+            outs.append((dx, part[: rows.value * 2 * N].clone(), rows.value))
+        (a, pa, ra), (b, pb, rb) = outs
+        assert ra == rb and ra <= 256
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+        assert torch.equal(pa, pb)

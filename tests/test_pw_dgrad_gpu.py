@@ -31,7 +31,8 @@ def _dgrad(cuda, dy, wck, M, Kc, N, acc=None, amask=None, bn=None, pw=True, sub2
         H, W = hw if hw else (1, 1)
         call("dtf_conv_dgrad_x", ptr(dy), ptr(wck), ptr(dx), M // (H * W), H, W, N, Kc, 1, 1, H, W, 1, 1, 0, 0, 1, 1,
              1.0 if acc is not None else 0.0, ptr(ws), 16, *bnp, ptr(part),
-             ctypes.addressof(rows) if bn else None, ptr(amask) if acc is not None else None, ptr(sub2), stream())
+             ctypes.addressof(rows) if bn else None, ptr(amask) if acc is not None else None, ptr(sub2), None, None,
+             stream())
         torch.cuda.synchronize()
         sums = part[: rows.value * 2 * N].view(rows.value, 2 * N).sum(0) if bn else None
         return dx, sums, rows.value
