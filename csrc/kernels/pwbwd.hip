@@ -498,35 +498,40 @@ __global__ void __launch_bounds__(256, 1) pw_bwd_bn_kernel(PbnArgs A) {
     if constexpr (YR) {
       // every wave's X share landed; every wave is done with the previous tile's y stage
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      v4f ay[4][4];  // y[p = 16 i + (lane & 15)][k = 64 wave + 16 j + 4 (lane >> 4) + r]
+      // (in two halves of 32 pixels: half the accumulators)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int hp = 0; hp < 2; ++hp) {
+        v4f ay[2][4];  // y[p = 32 hp + 16 i + (lane & 15)][k = 64 wave + 16 j + 4 (lane >> 4) + r]
 #pragma unroll
-        for (int j = 0; j < 4; ++j) ay[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        v8bf xa[4];
+          for (int j = 0; j < 4; ++j) ay[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) xa[i] = row_frag<CB>(xim, 16 * i, kk, lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int kk = 0; kk < 2; ++kk) {
+          v8bf xa[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(xa[i]));
+          for (int i = 0; i < 2; ++i) xa[i] = row_frag<CB>(xim, 32 * hp + 16 * i, kk, lane);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 2; ++i) asm volatile("" : "+v"(xa[i]));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) ay[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wyf[j][kk], xa[i], ay[i][j], 0, 0, 0);
-      }
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint2 o;
-          o.x = pack2bf(ay[i][j][0], ay[i][j][1]);
-          o.y = pack2bf(ay[i][j][2], ay[i][j][3]);
-          const int pl = 16 * i + (lane & 15), kl = 64 * wave + 16 * j + 4 * (lane >> 4);
-          const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, ystg + (pl * YROW + kl) * 2);
-          asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(o) : "memory");
+            for (int j = 0; j < 4; ++j)
+              ay[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wyf[j][kk], xa[i], ay[i][j], 0, 0, 0);
         }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            uint2 o;
+            o.x = pack2bf(ay[i][j][0], ay[i][j][1]);
+            o.y = pack2bf(ay[i][j][2], ay[i][j][3]);
+            const int pl = 32 * hp + 16 * i + (lane & 15), kl = 64 * wave + 16 * j + 4 * (lane >> 4);
+            const uint32_t addr = (uint32_t)(uintptr_t)LDS_PTR(char, ystg + (pl * YROW + kl) * 2);
+            asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(o) : "memory");
+          }
+      }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // y staged
     }
     transform(tile, yimg);
@@ -740,10 +745,10 @@ DTF_API int dtf_pw_conv_bwd_bn(const void* dout, const void* y, const void* ymas
   if ((long)a.slots * K * C > ws_elems) return -1;
   A.ysc = (const bf16_t*)ysc; A.msc = msc; A.psc = psc;
   A.wy = (const bf16_t*)wy;
-  // (y recompute with the shortcut sums: 49 VGPRs spill — not offered; the projection block stores its y)
-  if (wy && (!s1 || sc || y || ((uintptr_t)wy & 15))) return -1;
+  if (wy && (!s1 || y || ((uintptr_t)wy & 15))) return -1;
   if (!wy && !y) return -1;
-  if (s1 && wy) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, false, true>), dim3(256), dim3(256), 0, st, A);
+  if (s1 && wy && sc) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, true, true>), dim3(256), dim3(256), 0, st, A);
+  else if (s1 && wy) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, false, true>), dim3(256), dim3(256), 0, st, A);
   else if (s1 && sc) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64, true>), dim3(256), dim3(256), 0, st, A);
   else if (s1) hipLaunchKernelGGL((pw_bwd_bn_kernel<256, 64, 64, 64>), dim3(256), dim3(256), 0, st, A);
   else hipLaunchKernelGGL((pw_bwd_bn_kernel<512, 128, 32, 64>), dim3(256), dim3(256), 0, st, A);

@@ -349,9 +349,10 @@ _TWO_PASS_PW = os.environ.get("DTF_PW2", "1") != "0"
 # the weight gradient on the main stream instead of the side stream.
 # Level 2 also folds the conv output's BatchNorm(+ReLU) backward into that pass when its reduction is already done
 # (identity blocks: dY = a dz + b y + c computed per tile, never stored: the standalone apply pass disappears).
-# Level 3 (default) stops storing the stage-1 identity blocks' c3 output y at all: the folded pass and the next
-# block's c1 data gradient recompute it per tile from the c3 input (bitwise the forward's values).
-_FUSED_PW_BWD = int(os.environ.get("DTF_PW_BWD", "3"))
+# Level 3 stops storing the stage-1 identity blocks' c3 output y at all: the folded pass and the next
+# block's c1 data gradient recompute it per tile from the c3 input (bitwise the forward's values); level 4 (default) also the
+# projection block's.
+_FUSED_PW_BWD = int(os.environ.get("DTF_PW_BWD", "4"))
 
 
 def _two_pass_ok(g):
@@ -393,8 +394,10 @@ class _ConvBNFn(torch.autograd.Function):
             # BatchNorm / residual / ReLU applied in the epilogue (pwconv.hip MODE 1 / 2) — no standalone apply pass
             # level 3: an identity block's stage-1 c3 output is not stored at all — its consumers (this layer's
             # BatchNorm-folded backward, the next block's c1 data gradient) recompute it from x and w
-            keep_y = not (_FUSED_PW_BWD >= 3 and (C, K) == (64, 256) and relu and res is not None and raff is None
-                          and link is not None and role == "res" and M >= 64 * 256 and any(ctx.needs_input_grad))
+            keep_y = not (_FUSED_PW_BWD >= 3 and (C, K) == (64, 256) and relu and res is not None
+                          and M >= 64 * 256 and any(ctx.needs_input_grad)
+                          and ((raff is None and link is not None and role == "res")
+                               or (_FUSED_PW_BWD >= 4 and raff is not None)))
             yc = torch.empty((N, P, Q, K), dtype=BF16, device=dev) if keep_y else None
             out = torch.empty((N, P, Q, K), dtype=BF16, device=dev)
             mbits = torch.empty(M * K // 8, dtype=torch.uint8, device=dev) if relu else None
@@ -506,7 +509,7 @@ class _ConvBNFn(torch.autograd.Function):
                         None)
         blk_ok = (_FUSED_PW_BWD >= 2 and fused is not None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
                   and x.is_contiguous() and x.dtype == BF16)
-        if (blk_ok and yc is not None and rsrc is not None and not lazy_res and ctx.relu and pw_bwd_bn_ok(g)
+        if (blk_ok and rsrc is not None and not lazy_res and ctx.relu and pw_bwd_bn_ok(g)
                 and g[4] == 256 and g[3] == 64):
             tw = direct_grad(w)
             if tw is not None:
@@ -518,7 +521,7 @@ class _ConvBNFn(torch.autograd.Function):
                 src = ctx.in_src
                 complete = src is not None and role != "proj" and src.consumers == 1
                 dx = conv_bwd_bn_fused_raw(dout, yc, mbits, coef, x, w, g, tw, bn=src if complete else None,
-                                           sc=rsrc)
+                                           sc=rsrc, wy=bf16_shadow(w) if yc is None else None)
                 dout._dtf_mask = mbits
                 ctx.in_src = ctx.src = ctx.res_src = None
                 if direct_bn:

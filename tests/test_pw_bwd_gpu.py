@@ -170,7 +170,7 @@ def test_pw_bwd_bn_matches_apply_then_fused(cuda, P):
     assert (ref.float() - dyc.float()).abs().max().item() <= 1e-2 * ref.float().abs().max().item()
 
 
-@pytest.mark.parametrize("level", [1, 2, 3])
+@pytest.mark.parametrize("level", [1, 2, 3, 4])
 def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
     """Three stage-1 bottlenecks trained the framework's way (arena gradients, direct accumulation). Level 1: every c3
     and the stride-1 projection take the fused data + weight gradient; level 2: the middle block's c3 (identity
@@ -214,7 +214,7 @@ def test_pw_bwd_block_gradients(cuda, monkeypatch, level):
             loss.backward()
         torch.cuda.synchronize()
         runs[lv] = [xx.grad.float(), arena.grad.clone()]
-        want = {0: (0, 0), 1: (4, 0), 2: (1, 3), 3: (1, 3)}[lv]
+        want = {0: (0, 0), 1: (4, 0), 2: (1, 3), 3: (1, 3), 4: (1, 3)}[lv]
         assert (seen.get("dtf_pw_conv_bwd", 0), seen.get("dtf_pw_conv_bwd_bn", 0)) == want, seen
     for a, b in zip(runs[0], runs[level]):
         assert torch.isfinite(b).all()
