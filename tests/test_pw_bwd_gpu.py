@@ -341,3 +341,54 @@ def test_pw_dgrad_recomputes_bn_input(cuda):
         assert ra == rb and ra <= 256
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
         assert torch.equal(pa, pb)
+
+
+def test_unstored_y_falls_back_when_the_consumer_cannot_recompute(cuda, monkeypatch):
+    """Level 4 with the persistent pointwise data gradient switched off: the next block's c1 data gradient cannot
+    recompute the unstored c3 output (dtf_conv_dgrad_x returns -12, nothing launched), so it is materialised once
+    (_BNSource.materialize) — gradients equal the level-0 path's to f32 summation order."""
+    from distributed_tensorflow_amd.keras import initializers
+    from distributed_tensorflow_amd.models import resnet as R
+    from distributed_tensorflow_amd.ops._util import direct_grads
+    from distributed_tensorflow_amd.variables import ParamArena
+    g = torch.Generator().manual_seed(29)
+    x = torch.randn(64, 16, 16, 64, generator=g).to(cuda).to(BF)
+    runs = {}
+    mats = []
+    real = OC._recompute_y
+
+    def spy(*a):
+        mats.append(1)
+        return real(*a)
+
+    monkeypatch.setattr(OC, "_recompute_y", spy)
+    call("dtf_set_pw_dgrad", 0)
+    try:
+        for lv in (0, 4):
+            monkeypatch.setattr(OC, "_FUSED_PW_BWD", lv)
+            mats.clear()
+            initializers.set_seed(3)
+            blocks = [R.Bottleneck(64, stride=1, project=True), R.Bottleneck(64), R.Bottleneck(64)]
+            with torch.no_grad():
+                h = x
+                for b in blocks:
+                    h = b(h, training=False)
+            params = [w for b in blocks for w in b.trainable_weights]
+            arena = ParamArena(params, device=cuda)
+            xx = x.clone().requires_grad_(True)
+            h = xx
+            for b in blocks:
+                h = b(h, training=True)
+            loss = (h.float() * torch.linspace(-1, 1, h.shape[-1], device=cuda)).square().mean()
+            with direct_grads():
+                loss.backward()
+            torch.cuda.synchronize()
+            runs[lv] = [xx.grad.float(), arena.grad.clone()]
+            if lv == 4:
+                assert len(mats) >= 2, mats  # b1 / b2 c1 dgrads materialised the unstored BN inputs
+    finally:
+        call("dtf_set_pw_dgrad", 1)
+    for a, b in zip(runs[0], runs[4]):
+        assert torch.isfinite(b).all()
+        err = (a - b).norm().item() / (a.norm().item() + 1e-12)
+        assert err < 1e-2, err
