@@ -8,6 +8,10 @@
 // transposed (ds_read_b64_tr_b16, frag_kouter's addressing), the data gradient row-wise (16-B reads at the same
 // swizzled chunks) against the filter held in registers. X (the layer input, 64 channels) rides in the same ring.
 // The dX tile is staged through LDS and stored as 16-B row chunks with the BN partials of the stored values.
+// pw_bwd_bn_kernel (below) goes further: dY itself is never stored — it is the BatchNorm(+ReLU) backward of the conv
+// output y, computed per tile from dout, y and the ReLU bits (stage 1 and stage 2 shapes); optionally y is not stored
+// either and is recomputed from the X tile (YR), and the same pass takes a projection shortcut's BN-backward sums (SC).
+// Measured effects: profiles/r6_fused_1x1_backward.txt.
 // Reference op: the Conv2D gradients of the model trainer/task.py:62-71 builds.
 #include "gemm_core.h"
 
