@@ -195,6 +195,23 @@ def conv_wgrad_raw(x, dy, g, out=None):
     return dw_
 
 
+_STEM_WGRAD = os.environ.get("DTF_STEM_WGRAD", "1") != "0"  # A/B switch: 0 keeps the general wgrad tiles
+
+
+def stem_wgrad_raw(x, dy, g):
+    """dW [64, 4, 4, 16] f32 of the space-to-depth stem conv (valid 4x4/1 over the s2d image x [N, Hs, Ws, 16]): the
+    persistent stem kernel (csrc/kernels/stemwgrad.hip: the filter gradient resident in the accumulators, one dY row
+    image and a ring of s2d rows in LDS, taps as pixel shifts), or the general tiles when it does not take the shape."""
+    N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw = g
+    if (_STEM_WGRAD and on_gpu(x) and (C, K, R, S, sh, sw, ph, pw, dh, dw) == (16, 64, 4, 4, 1, 1, 0, 0, 1, 1)
+            and x.is_contiguous() and dy.is_contiguous()):
+        dw_ = torch.empty((K, R, S, C), dtype=F32, device=x.device)
+        ws = workspace(x.device)
+        if K_().dtf_stem_wgrad(ptr(x), ptr(dy), ptr(dw_), N, H, W, 0, ptr(ws), ws.numel(), stream()) == 0:
+            return dw_
+    return conv_wgrad_raw(x, dy, g)
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, dil, act):
@@ -720,7 +737,7 @@ class _ConvBNPoolFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             tw = direct_grad(w)
             if ctx.s2d:
-                dw = stem_s2d_filter_grad(conv_wgrad_raw(x, dyc, g), w.shape)
+                dw = stem_s2d_filter_grad(stem_wgrad_raw(x, dyc, g), w.shape)
                 if tw is not None:
                     tw.add_(dw)
             else:

@@ -3,6 +3,7 @@ same conv as a 4x4/1 conv over the 2x2 space-to-depth image [N, 115, 115, 16] (3
 2/1 rows of zero padding baked in). Times forward (with BN statistics) and weight gradient per tile.
 
   python tools/bench_stem.py
+  python tools/bench_stem.py --wgrad-s2d [BATCH]   # s2d weight gradient: persistent stem kernel vs the general tiles
 """
 import os
 import sys
@@ -50,7 +51,31 @@ def run(name, H, Cin, R, s, p):
         print(line, flush=True)
 
 
+def wgrad_s2d(nb):
+    dev = torch.device("cuda")
+    x = torch.randn(nb, 115, 115, 16, device=dev).to(BF)
+    dy = torch.randn(nb, 112, 112, 64, device=dev).to(BF)
+    g = (nb, 115, 115, 16, 64, 4, 4, 112, 112, 1, 1, 0, 0, 1, 1)
+    ws = workspace(dev)
+    dw = torch.zeros(64, 4, 4, 16, device=dev)
+    fl = 2.0 * nb * 112 * 112 * 64 * 256
+    gb = (x.numel() + dy.numel()) * 2 / 1e9
+    stem = lambda: call("dtf_stem_wgrad", ptr(x), ptr(dy), ptr(dw), nb, 115, 115, 0, ptr(ws), ws.numel(), stream())
+    gen = lambda: call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw), nb, 115, 115, 16, 64, 4, 4, 112, 112, 1, 1, 0, 0,
+                       1, 1, 0, 0, -1, ptr(ws), ws.numel(), stream())
+    for name, fn in (("stem kernel", stem), ("general", gen), ("stem kernel", stem)):
+        tt = timeit(fn)
+        print(f"s2d wgrad batch {nb} {name:12s} {tt * 1e6:8.1f}us  {fl / tt / 1e12:5.0f} TF  {gb / tt / 1e3:5.2f} TB/s "
+              f"(x + dY = {gb:.2f} GB)", flush=True)
+    a = C.stem_wgrad_raw(x, dy, g)
+    b = C.conv_wgrad_raw(x, dy, g)
+    print(f"max |stem - general| = {(a - b).abs().max().item():.3e} (max |dW| {b.abs().max().item():.3e})")
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
-    run("stem7x7", 224, 8, 7, 2, 3)
-    run("stem_s2d", 115, 16, 4, 1, 0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--wgrad-s2d":
+        wgrad_s2d(int(sys.argv[2]) if len(sys.argv) > 2 else 1024)
+    else:
+        run("stem7x7", 224, 8, 7, 2, 3)
+        run("stem_s2d", 115, 16, 4, 1, 0)
