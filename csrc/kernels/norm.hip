@@ -1158,6 +1158,7 @@ DTF_API int dtf_maxpool_bn_bwd(const void* dy, const void* arg, const void* x, c
     hipLaunchKernelGGL((maxpool_bn_bwd_reduce_kernel<false>), dim3(G), dim3(256), 0, st, (const bf16_t*)dy,
                        (const uint8_t*)arg, (const bf16_t*)x, mean, pg, part);
   bn_bwd_finalize_launch(part, G, mean, invstd, gamma, M, C, dgamma, dbeta, accumulate, coef, st);
+  if (!dx) return (int)hipGetLastError();  // coefficients only: the consumer applies them (dtf_stem_wgrad_fused)
   if (b2)
     hipLaunchKernelGGL((maxpool_bn_bwd_apply_kernel<true>), dim3(ew_grid(rows, C)), dim3(256), 0, st,
                        (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)x, coef, pg, (bf16_t*)dx);

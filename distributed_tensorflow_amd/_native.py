@@ -43,6 +43,7 @@ _KERNEL_SIGS = {
     "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P],
     "dtf_conv_wgrad": [P, P, P] + [I] * 15 + [I, I, I, P, L, P],
     "dtf_stem_wgrad": [P, P, P, I, I, I, I, P, L, P],
+    "dtf_stem_wgrad_fused": [P, P, P, P, P, P, I, I, I, I, P, L, P],
     "dtf_bn_stats": [P, L, I, P, P, P],
     "dtf_bn_finalize": [P, I, P, P, P, P, L, I, F, F, P, P, P, P, P],
     "dtf_bn_infer_coeff": [P, P, P, P, I, F, P, P, P],

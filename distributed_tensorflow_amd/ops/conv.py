@@ -196,6 +196,8 @@ def conv_wgrad_raw(x, dy, g, out=None):
 
 
 _STEM_WGRAD = os.environ.get("DTF_STEM_WGRAD", "1") != "0"  # A/B switch: 0 keeps the general wgrad tiles
+# 1: the s2d stem's BN + ReLU + MaxPool backward is applied inside the stem wgrad kernel (dtf_stem_wgrad_fused)
+_STEM_WGRAD_FUSED = _STEM_WGRAD and os.environ.get("DTF_STEM_WGRAD_FUSED", "1") != "0"
 
 
 def stem_wgrad_raw(x, dy, g):
@@ -719,17 +721,34 @@ class _ConvBNPoolFn(torch.autograd.Function):
         N, H, W, C, K, R, S, P, Q = g[:9]
         P2, Q2, pk, ps, pp = ctx.pool
         dy = dy.to(BF16).contiguous()
-        dyc = torch.empty_like(yc)
         gamma_p, beta_p = ctx.bn_params
         tg, tb = direct_grad(gamma_p), direct_grad(beta_p)
         direct_bn = tg is not None and tb is not None
         dgamma = tg if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
         dbeta = tb if direct_bn else torch.empty(K, dtype=F32, device=yc.device)
         work = torch.empty((2 * 1024 + 3) * K, dtype=F32, device=yc.device)
+        # s2d stem, filter gradient only: the BN + ReLU + pool backward is applied inside the stem wgrad kernel
+        # (dtf_stem_wgrad_fused) from the coefficients the reduce pass leaves in work[:3K]; dyc is never formed
+        fused = (ctx.s2d and _STEM_WGRAD_FUSED and ctx.needs_input_grad[1] and (K, pk, ps, pp) == (
+            64, (3, 3), (2, 2), (1, 1)) and P == 2 * P2 and Q == 2 * Q2 and W <= 128 and C == 16 and R == 4)
+        dyc = None if fused else torch.empty_like(yc)
         call("dtf_maxpool_bn_bwd", ptr(dy), ptr(arg), ptr(yc), ptr(mean), ptr(invstd), ptr(gamma), N, P, Q, K, P2,
-             Q2, pk[0], pk[1], ps[0], ps[1], pp[0], pp[1], ptr(dyc), ptr(dgamma), ptr(dbeta), int(direct_bn),
-             ptr(work), stream())
+             Q2, pk[0], pk[1], ps[0], ps[1], pp[0], pp[1], None if fused else ptr(dyc), ptr(dgamma), ptr(dbeta),
+             int(direct_bn), ptr(work), stream())
         dx = dw = None
+        if fused:
+            dw2 = torch.empty((K, R, S, C), dtype=F32, device=x.device)
+            ws = workspace(x.device)
+            call("dtf_stem_wgrad_fused", ptr(x), ptr(yc), ptr(dy), ptr(arg), ptr(work), ptr(dw2), N, H, W, 0, ptr(ws),
+                 ws.numel(), stream())
+            dw = stem_s2d_filter_grad(dw2, w.shape)
+            tw = direct_grad(w)
+            if tw is not None:
+                tw.add_(dw)
+                dw = None
+            if direct_bn:
+                dgamma = dbeta = None
+            return None, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
         if ctx.needs_input_grad[0]:
             if ctx.s2d:
                 raise NotImplementedError("no input gradient through the space-to-depth stem (image input)")

@@ -87,3 +87,28 @@ def test_stem_wgrad_raw_routes_and_falls_back(cuda):
     dw = C.stem_wgrad_raw(x, dy, _geom(2, 115, 115))
     ref = _ref(x, dy)
     assert (dw - ref).abs().max().item() <= 2e-5 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("B,H", [(3, 224), (5, 60)])
+def test_stem_wgrad_fused_is_bitwise_the_unfused_path(cuda, B, H, monkeypatch):
+    """The stem's BN + ReLU + MaxPool backward applied inside the wgrad kernel (dtf_stem_wgrad_fused; the stem's dY
+    is never stored) against the unfused path (maxpool_bn_bwd_apply writes dY, then the stem kernel): the dY values
+    and the kernel's summation order are the same, so dW, dgamma and dbeta are bitwise equal."""
+    from distributed_tensorflow_amd import ops
+    g = torch.Generator().manual_seed(H + B)
+    img = torch.randn(B, 3, H, H, generator=g).to(cuda)
+    w = (torch.randn(64, 7, 7, 4, generator=g) * 0.05).to(cuda)
+    gamma = (torch.rand(64, generator=g) + 0.5).to(cuda)
+    beta = (torch.randn(64, generator=g) * 0.1).to(cuda)
+    dyv = torch.randn(B, H // 4, H // 4, 64, generator=g).to(cuda)
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(C, "_STEM_WGRAD_FUSED", fused)
+        wd, gd, bd = (t.clone().requires_grad_(True) for t in (w, gamma, beta))
+        rm, rv = torch.zeros(64, device=cuda), torch.ones(64, device=cuda)
+        y = ops.conv_bn_maxpool(ops.image_to_s2d_bf16(img), wd, gd, bd, rm, rv, stride=(2, 2), pad=(3, 3), s2d=True)
+        outs.append(torch.autograd.grad((y.float() * dyv).sum(), [wd, gd, bd]))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert outs[1][0].abs().max().item() > 0
