@@ -765,6 +765,23 @@ namespace dtf {
 int pw_wgrad_try(const void* X, const void* dY, float* dW, long P, int C, int K, int accumulate, float* ws,
                  long ws_elems, hipStream_t st, bool split_out);
 }
+namespace dtf {
+int c3_wgrad_try(const void* X, const void* dY, float* dW, int N, int H, int W, int accumulate, float* ws,
+                 long ws_elems, hipStream_t st);
+}
+// DTF_C3_WGRAD=0 (or dtf_set_c3_wgrad(0)) keeps the 64-channel 3x3 weight gradients on the general tiles
+static int g_c3_wgrad = -1;
+static bool c3wgrad_enabled() {
+  if (g_c3_wgrad < 0) {
+    const char* e = getenv("DTF_C3_WGRAD");
+    g_c3_wgrad = !(e && e[0] == '0');
+  }
+  return g_c3_wgrad != 0;
+}
+DTF_API int dtf_set_c3_wgrad(int on) {
+  g_c3_wgrad = on ? 1 : 0;
+  return 0;
+}
 // DTF_PW_WGRAD=0 (or dtf_set_pw_wgrad(0)) keeps the 1x1 weight gradients on the general tiles (A/B switch)
 static int g_pw_wgrad = -1;
 static bool pwwgrad_enabled() {
@@ -973,6 +990,11 @@ DTF_API int dtf_conv_wgrad(const void* X, const void* dY, float* dW, int N, int 
   // small 1x1 filters over many pixels (ResNet-50 stages 1-2): the persistent kernel, whole filter tile per block
   if (pointwise && tile < 0 && splitk_req <= 0 && pwwgrad_enabled() &&
       pw_wgrad_try(X, dY, dW, (long)N * H * W, C, K, accumulate, ws, ws_elems, st, g_pw_wgrad == 2) == 0)
+    return 0;
+  // 64 -> 64 channel 3x3 / stride 1 / pad 1 (ResNet-50 stage 1): the persistent kernel (c3wgrad.hip)
+  if (tile < 0 && splitk_req <= 0 && C == 64 && K == 64 && R == 3 && S == 3 && sh == 1 && sw == 1 && ph == 1 &&
+      pw == 1 && dh == 1 && dw == 1 && P == H && Q == W && c3wgrad_enabled() &&
+      c3_wgrad_try(X, dY, dW, N, H, W, accumulate, ws, ws_elems, st) == 0)
     return 0;
   const bool small = (long)N * H * W * C * 2 < (1l << 31) && (long)N * P * Q * K * 2 < (1l << 31);
   // spatial filters: LDS-DMA staged 128x128 (measured best for every ResNet-50 3x3 filter); 1x1 filters keep

@@ -38,6 +38,7 @@ _KERNEL_SIGS = {
     "dtf_pw_conv_bwd_bn": [P, P, P, P, P, P, P, P, I, P, P, P, P, P, P, L, L, I, I, P, P, P, P, P, P],
     "dtf_bn_bwd_coef": [P, I, P, P, P, L, I, P, P, I, P, P],
     "dtf_set_pw_wgrad": [I],
+    "dtf_set_c3_wgrad": [I],
     "dtf_set_split_penalty": [I],
     "dtf_set_ew_apply_nu": [I],
     "dtf_bn_bwd_partials": [P, P, P, P, P, P, L, I, P, P, P, P, I, P, I, P, P, P, P, P, P],

@@ -4,6 +4,7 @@ same conv as a 4x4/1 conv over the 2x2 space-to-depth image [N, 115, 115, 16] (3
 
   python tools/bench_stem.py
   python tools/bench_stem.py --wgrad-s2d [BATCH]   # s2d weight gradient: persistent stem kernel vs the general tiles
+  python tools/bench_stem.py --wgrad-3x3 [BATCH]   # stage-1 3x3 (64 -> 64, 56 x 56) weight gradient, c3wgrad.hip vs tiles
 """
 import os
 import sys
@@ -72,9 +73,29 @@ def wgrad_s2d(nb):
     print(f"max |stem - general| = {(a - b).abs().max().item():.3e} (max |dW| {b.abs().max().item():.3e})")
 
 
+def wgrad_3x3(nb):
+    dev = torch.device("cuda")
+    x = torch.randn(nb, 56, 56, 64, device=dev).to(BF)
+    dy = torch.randn(nb, 56, 56, 64, device=dev).to(BF)
+    ws = workspace(dev)
+    dw = torch.zeros(64, 3, 3, 64, device=dev)
+    fl = 2.0 * nb * 56 * 56 * 64 * 576
+    gb = (x.numel() + dy.numel()) * 2 / 1e9
+    run = lambda: call("dtf_conv_wgrad", ptr(x), ptr(dy), ptr(dw), nb, 56, 56, 64, 64, 3, 3, 56, 56, 1, 1, 1, 1, 1, 1,
+                       0, 0, -1, ptr(ws), ws.numel(), stream())
+    for on in (1, 0, 1):
+        call("dtf_set_c3_wgrad", on)
+        tt = timeit(run)
+        print(f"3x3 wgrad batch {nb} {'c3wgrad' if on else 'general':8s} {tt * 1e6:8.1f}us  {fl / tt / 1e12:5.0f} TF  "
+              f"{gb / tt / 1e3:5.2f} TB/s", flush=True)
+    call("dtf_set_c3_wgrad", 1)
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
-    if len(sys.argv) > 1 and sys.argv[1] == "--wgrad-s2d":
+    if len(sys.argv) > 1 and sys.argv[1] == "--wgrad-3x3":
+        wgrad_3x3(int(sys.argv[2]) if len(sys.argv) > 2 else 1024)
+    elif len(sys.argv) > 1 and sys.argv[1] == "--wgrad-s2d":
         wgrad_s2d(int(sys.argv[2]) if len(sys.argv) > 2 else 1024)
     else:
         run("stem7x7", 224, 8, 7, 2, 3)
