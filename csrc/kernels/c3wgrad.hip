@@ -150,25 +150,31 @@ __global__ void __launch_bounds__(256, 1) c3_wgrad_kernel(C3Args a) {
     const char* xr[3];
 #pragma unroll
     for (int ta = 0; ta < 3; ++ta) xr[ta] = xs + ((n * VH + h + ta) & (C3_NS - 1)) * C3_SLOT;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      v8bf fx[9], fy[4];
+    // fragments double-buffered across the row's 2 pixel k-steps: k-step 1's reads land under k-step 0's MFMAs
+    v8bf fx[2][9], fy[2][4];
+    auto load = [&](int ks, v8bf(&x)[9], v8bf(&y)[4]) {
 #pragma unroll
       for (int ta = 0; ta < 3; ++ta)
 #pragma unroll
-        for (int tb = 0; tb < 3; ++tb) fx[ta * 3 + tb] = c3_frag(xr[ta], 16 * wave, tb, ks, lane);
+        for (int tb = 0; tb < 3; ++tb) x[ta * 3 + tb] = c3_frag(xr[ta], 16 * wave, tb, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fy[j] = c3_frag(img, 16 * j, 0, ks, lane);
+      for (int j = 0; j < 4; ++j) y[j] = c3_frag(img, 16 * j, 0, ks, lane);
+    };
+    load(0, fx[0], fy[0]);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int u = 0; u < 9; ++u) asm volatile("" : "+v"(fx[u]));
+      for (int u = 0; u < 9; ++u) asm volatile("" : "+v"(fx[ks][u]));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fy[j]));
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fy[ks][j]));
+      if (ks == 0) load(1, fx[1], fy[1]);
       // D[c][k]: src0 = X^T (rows c), src1 = dY (columns k)
 #pragma unroll
       for (int u = 0; u < 9; ++u)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[u], fy[j], acc[u][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+          acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[ks][u], fy[ks][j], acc[u][j], 0, 0, 0);
     }
     next(n, h);
   }
